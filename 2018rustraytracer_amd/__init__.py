@@ -1,0 +1,14 @@
+"""rtm — MI355X-native per-pixel ray-trace / ray-march renderer.
+
+Drop-in for the CPU render loop of PtrMan/2018RustRayTracer (src/main.rs):
+orthographic ray generation, ray-sphere front/back hits, fixed-step implicit
+surface marching into a shadow map, Lambert + specular shading, RGBA
+framebuffer write — as hand-written gfx950 HIP kernels behind a C ABI
+(include/rtm.h, librtm.so).  The package name starts with a digit, so import it
+with importlib.import_module("2018rustraytracer_amd").
+"""
+from . import abi, scenes  # noqa: F401
+from .abi import RtmError, load_library  # noqa: F401
+from .scenes import (Bilinear, Camera, EnumFace, Linear, PrimitiveSphere, Scene, Shading,  # noqa: F401
+                     eye_camera, shadow_camera)
+from .renderer import Context, Viewport, device_count, renderColorImage, render_frame  # noqa: F401

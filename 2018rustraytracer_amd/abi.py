@@ -1,0 +1,140 @@
+"""ctypes mirror of include/rtm.h and the loader for the HIP library (librtm.so).
+
+The structs are byte-for-byte the C ABI; the loader fails loudly when the
+library is missing (there is no CPU fallback on the product path).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_PKG_DIR, "librtm.so")
+
+RTM_ABI_VERSION = 1
+RTM_MAX_SPHERES = 16
+RTM_MAX_PATCHES = 4
+RTM_MAX_DIM = 32768
+
+RTM_OK = 0
+RTM_ERR_INVALID = -1
+RTM_ERR_UNSUPPORTED = -2
+RTM_ERR_HIP = -3
+RTM_ERR_NO_DEVICE = -4
+RTM_ERR_OOM = -5
+
+RTM_CAMERA_ORTHOGONAL = 0
+RTM_CAMERA_PERSPECTIVE = 1
+RTM_FACE_FRONT = 0
+RTM_FACE_BACK = 1
+
+RTM_FLAG_NO_MARCH = 0x1
+RTM_FLAG_NO_SHADOW_RASTER = 0x2
+RTM_FLAG_FUSED_SHADOW = 0x4
+
+
+class rtm_sphere(C.Structure):
+    _fields_ = [("id", C.c_int64), ("pos", C.c_double * 3), ("r", C.c_double),
+                ("color", C.c_double * 3)]
+
+
+class rtm_patch(C.Structure):
+    _fields_ = [("a0", C.c_double), ("b0", C.c_double), ("a1", C.c_double), ("b1", C.c_double)]
+
+
+class rtm_camera(C.Structure):
+    _fields_ = [("type", C.c_int32), ("reserved", C.c_int32), ("pos", C.c_double * 3),
+                ("dir", C.c_double * 3), ("up", C.c_double * 3), ("side", C.c_double * 3)]
+
+
+class rtm_scene(C.Structure):
+    _fields_ = [("spheres", C.POINTER(rtm_sphere)), ("patches", C.POINTER(rtm_patch)),
+                ("n_spheres", C.c_int32), ("n_patches", C.c_int32)]
+
+
+class rtm_stats(C.Structure):
+    _fields_ = [("eye_hits", C.c_int64 * RTM_MAX_SPHERES), ("eye_hit_pixels", C.c_int64),
+                ("lit_pixels", C.c_int64), ("eye_sphere_tests", C.c_int64),
+                ("shadow_sphere_tests", C.c_int64), ("march_iterations", C.c_int64),
+                ("march_hits", C.c_int64), ("march_in_range", C.c_int64)]
+
+    def as_dict(self) -> dict:
+        d = {name: getattr(self, name) for name, _ in self._fields_ if name != "eye_hits"}
+        d["eye_hits"] = list(self.eye_hits)
+        return d
+
+
+assert C.sizeof(rtm_sphere) == 64
+assert C.sizeof(rtm_patch) == 32
+assert C.sizeof(rtm_camera) == 104
+assert C.sizeof(rtm_scene) == 24
+assert C.sizeof(rtm_stats) == 8 * (RTM_MAX_SPHERES + 7)
+
+# (name, restype, argtypes) for every symbol include/rtm.h declares.
+_P = C.c_void_p
+_I32 = C.c_int32
+ABI_SYMBOLS = [
+    ("rtm_abi_version", C.c_int32, []),
+    ("rtm_last_error", C.c_char_p, []),
+    ("rtm_device_count", C.c_int32, []),
+    ("rtm_ctx_create", C.c_int, [_I32, C.POINTER(_P)]),
+    ("rtm_ctx_destroy", None, [_P]),
+    ("rtm_ctx_stream", _P, [_P]),
+    ("rtm_ctx_synchronize", C.c_int, [_P]),
+    ("rtm_ctx_last_kernel_ms", C.c_int, [_P, C.POINTER(C.c_float), C.POINTER(C.c_float)]),
+    ("rtm_ctx_set_timing_capacity", C.c_int, [_P, _I32]),
+    ("rtm_ctx_kernel_ms_history", C.c_int, [_P, C.POINTER(C.c_float), C.POINTER(C.c_float), _I32,
+                                            C.POINTER(_I32)]),
+    ("rtm_render", C.c_int, [C.POINTER(rtm_scene), C.POINTER(rtm_camera), C.POINTER(rtm_camera),
+                             _I32, _I32, _I32, _I32, C.POINTER(C.c_float)]),
+    ("rtm_render_async", C.c_int, [_P, C.POINTER(rtm_scene), C.POINTER(rtm_camera),
+                                   C.POINTER(rtm_camera), _I32, _I32, _I32, _I32, _I32, _I32, _P]),
+    ("rtm_ctx_shadow_map", _P, [_P]),
+    ("rtm_render_stats", C.c_int, [_P, C.POINTER(rtm_scene), C.POINTER(rtm_camera),
+                                   C.POINTER(rtm_camera), _I32, _I32, _I32, _I32,
+                                   C.POINTER(rtm_stats)]),
+    ("rtm_viewport_create", C.c_int, [_P, _I32, _I32, _I32, C.POINTER(rtm_camera), C.POINTER(_P)]),
+    ("rtm_viewport_destroy", None, [_P]),
+    ("rtm_viewport_rasterize", C.c_int, [_P, C.POINTER(rtm_scene)]),
+    ("rtm_viewport_process_raymarching_rays", C.c_int, [_P, C.POINTER(rtm_patch), _I32, _I32]),
+    ("rtm_render_color_image", C.c_int, [C.POINTER(rtm_scene), _P, _P, C.POINTER(C.c_float)]),
+    ("rtm_viewport_read_zbuffer", C.c_int, [_P, C.POINTER(C.c_double)]),
+]
+
+
+class RtmError(RuntimeError):
+    def __init__(self, code: int, where: str, msg: str = ""):
+        super().__init__(f"{where} failed with {code}: {msg}")
+        self.code = code
+
+
+_lib = None
+
+
+def load_library(path: str | None = None) -> C.CDLL:
+    """Load librtm.so (the HIP build).  Raises if it is missing: the product
+    path has no CPU fallback."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise FileNotFoundError(
+            f"{p} not built: run `python -c 'import __graft_entry__ as g; g.build()'` "
+            "(the HIP library is the only render path)")
+    lib = C.CDLL(p)
+    for name, res, args in ABI_SYMBOLS:
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.rtm_abi_version() != RTM_ABI_VERSION:
+        raise RuntimeError("librtm ABI version mismatch")
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def check(lib, code: int, where: str) -> None:
+    if code != RTM_OK:
+        msg = lib.rtm_last_error()
+        raise RtmError(code, where, msg.decode() if msg else "")

@@ -1,0 +1,553 @@
+// rtm_api.cpp — the C ABI (include/rtm.h) over the HIP kernels.
+//
+// Host responsibilities: validate the reference-shaped inputs, precompute the
+// per-(camera, sphere) constants in the reference's f64 operation order
+// (compiled with -ffp-contract=off), own device buffers / stream / events per
+// context, and return status codes instead of panicking (main.rs:700, 1949).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "rtm_kernels.h"
+
+#pragma clang fp contract(off)
+
+using namespace rtm;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+int fail(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_last_error = buf;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                    \
+    do {                                                                                 \
+        hipError_t e_ = (expr);                                                          \
+        if (e_ != hipSuccess) return fail(RTM_ERR_HIP, "%s: %s", #expr, hipGetErrorString(e_)); \
+    } while (0)
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    int device = 0;
+    ~DevBuf() {
+        if (p) {
+            int cur = 0;
+            (void)hipGetDevice(&cur);
+            (void)hipSetDevice(device);
+            (void)hipFree(p);
+            (void)hipSetDevice(cur);
+        }
+    }
+    int ensure(size_t need, int dev) {
+        if (need <= bytes) return RTM_OK;
+        if (p) {
+            (void)hipFree(p);
+            p = nullptr;
+            bytes = 0;
+        }
+        device = dev;
+        if (hipMalloc(&p, need) != hipSuccess) return fail(RTM_ERR_OOM, "hipMalloc(%zu) failed", need);
+        bytes = need;
+        return RTM_OK;
+    }
+};
+
+// ---- host-side precompute, reference op order ----
+inline double dot3(const double a[3], const double b[3]) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+
+// Viewport::rasterize ORTHOGONAL projection of one sphere (main.rs:449-470) and the
+// axis normalisation of calcEllipseDistToCenter (main.rs:2849-2850).
+RasterSphereK project_sphere(const rtm_camera& c, const rtm_sphere& s) {
+    RasterSphereK k{};
+    double diff[3] = {s.pos[0] - c.pos[0], s.pos[1] - c.pos[1], s.pos[2] - c.pos[2]};
+    k.z = dot3(c.dir, diff);  // calcDepthOfProjectedPoint: dot(dir, p - pos)
+    k.cx = dot3(diff, c.side);  // Camera::project: dot(diff, side)
+    k.cy = dot3(diff, c.up);
+    k.r = s.r;
+    const double m = std::sqrt(s.r * s.r + 0.0 * 0.0);  // Vec2::magnitude of (r, 0)
+    const double inv = 1.0 / m;                          // Vec2::normalized: scale(1.0/m)
+    k.n = s.r * inv;
+    k.z0 = 0.0 * inv;
+    k.m = m;
+    // Cull radius: a covered pixel has |rel.x|, |rel.y| < m*(1+4 ulp); 1e-9 relative margin.
+    k.R = std::fabs(m) * (1.0 + 1e-9) + 1e-300;
+    if (!(k.R == k.R)) k.R = INFINITY;  // NaN m: let the exact test decide (it yields NaN -> no hit)
+    k.id = s.id;
+    return k;
+}
+
+ShadeSphereK shade_sphere(const rtm_sphere& s) {
+    ShadeSphereK k{};
+    k.px = s.pos[0];
+    k.py = s.pos[1];
+    k.pz = s.pos[2];
+    k.r = s.r;
+    k.inv_r = 1.0 / s.r;
+    k.cr = s.color[0];
+    k.cg = s.color[1];
+    k.cb = s.color[2];
+    return k;
+}
+
+CamK cam_k(const rtm_camera& c) {
+    CamK k{};
+    for (int i = 0; i < 3; ++i) {
+        k.pos[i] = c.pos[i];
+        k.dir[i] = c.dir[i];
+        k.up[i] = c.up[i];
+        k.side[i] = c.side[i];
+    }
+    k.type = c.type;
+    return k;
+}
+
+PatchK patch_k(const rtm_patch& p) {
+    PatchK k{};
+    k.a0 = p.a0;
+    k.d0 = p.b0 - p.a0;  // linear(): diff = b - a (main.rs:2067)
+    k.a1 = p.a1;
+    k.d1 = p.b1 - p.a1;
+    return k;
+}
+
+int validate_scene(const rtm_scene* scene) {
+    if (!scene) return fail(RTM_ERR_INVALID, "scene is NULL");
+    if (scene->n_spheres < 0 || scene->n_spheres > RTM_MAX_SPHERES)
+        return fail(RTM_ERR_INVALID, "n_spheres=%d outside [0,%d]", scene->n_spheres, RTM_MAX_SPHERES);
+    if (scene->n_patches < 0 || scene->n_patches > RTM_MAX_PATCHES)
+        return fail(RTM_ERR_INVALID, "n_patches=%d outside [0,%d]", scene->n_patches, RTM_MAX_PATCHES);
+    if (scene->n_spheres > 0 && !scene->spheres) return fail(RTM_ERR_INVALID, "spheres is NULL");
+    if (scene->n_patches > 0 && !scene->patches) return fail(RTM_ERR_INVALID, "patches is NULL");
+    for (int i = 0; i < scene->n_spheres; ++i) {
+        int64_t id = scene->spheres[i].id;
+        // the reference indexes scene.spherePrimitives[id] (main.rs:158, 748): out of range panics there
+        if (id < 0 || id >= scene->n_spheres)
+            return fail(RTM_ERR_INVALID, "sphere %d has id %lld outside [0,%d)", i, (long long)id, scene->n_spheres);
+    }
+    return RTM_OK;
+}
+
+int validate_camera(const rtm_camera* c, const char* what) {
+    if (!c) return fail(RTM_ERR_INVALID, "%s camera is NULL", what);
+    if (c->type != RTM_CAMERA_ORTHOGONAL && c->type != RTM_CAMERA_PERSPECTIVE)
+        return fail(RTM_ERR_INVALID, "%s camera type %d", what, c->type);
+    return RTM_OK;
+}
+
+int validate_dims(int32_t w, int32_t h) {
+    if (w <= 0 || h <= 0 || w > RTM_MAX_DIM || h > RTM_MAX_DIM)
+        return fail(RTM_ERR_INVALID, "image size %dx%d outside [1,%d]", w, h, RTM_MAX_DIM);
+    return RTM_OK;
+}
+
+int build_frame(FrameArgs& a, const rtm_scene* scene, const rtm_camera* eye, const rtm_camera* shadow, int32_t W,
+                int32_t H, int32_t steps, int32_t flags) {
+    int rc;
+    if ((rc = validate_scene(scene)) || (rc = validate_camera(eye, "eye")) || (rc = validate_camera(shadow, "shadow")) ||
+        (rc = validate_dims(W, H)))
+        return rc;
+    if (steps < 0) return fail(RTM_ERR_INVALID, "march_steps=%d < 0", steps);
+    if (flags & ~(RTM_FLAG_NO_MARCH | RTM_FLAG_NO_SHADOW_RASTER | RTM_FLAG_FUSED_SHADOW))
+        return fail(RTM_ERR_INVALID, "unknown flags 0x%x", flags);
+    // The frame path rasterizes both viewports: orthographic only (perspective
+    // projectSphere is BASELINE "next" row f-3); Camera::project asserts ORTHO (main.rs:1949).
+    if (eye->type != RTM_CAMERA_ORTHOGONAL || shadow->type != RTM_CAMERA_ORTHOGONAL)
+        return fail(RTM_ERR_UNSUPPORTED, "frame path needs ORTHOGONAL eye and shadow cameras");
+    std::memset(&a, 0, sizeof a);
+    for (int i = 0; i < scene->n_spheres; ++i) {
+        a.esph[i] = project_sphere(*eye, scene->spheres[i]);
+        a.ssph[i] = project_sphere(*shadow, scene->spheres[i]);
+        a.shade[i] = shade_sphere(scene->spheres[i]);
+    }
+    for (int i = 0; i < scene->n_patches; ++i) a.patch[i] = patch_k(scene->patches[i]);
+    a.eye = cam_k(*eye);
+    a.shadow = cam_k(*shadow);
+    a.W = W;
+    a.H = H;
+    a.Ws = W;
+    a.Hs = H;
+    a.n_spheres = scene->n_spheres;
+    a.n_patches = scene->n_patches;
+    a.steps = steps;
+    a.flags = flags;
+    a.row_begin = 0;
+    a.row_end = H;
+    return RTM_OK;
+}
+
+}  // namespace
+
+struct TimingSlot {
+    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};  // shadow start/stop, eye start/stop
+    bool shadow = false;
+};
+
+struct rtm_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::vector<TimingSlot> ring;  // per-render kernel events (capacity = ring.size())
+    int64_t renders = 0;           // renders recorded into the ring
+    bool have_shadow_pass = false;
+    DevBuf smap;    // shadow map, W*H f64
+    DevBuf out;     // staging for rtm_render's host output
+    DevBuf stats;
+    int32_t smap_w = 0, smap_h = 0;
+};
+
+struct rtm_viewport {
+    rtm_ctx* ctx = nullptr;
+    int32_t W = 0, H = 0, face = 0;
+    rtm_camera cam{};
+    DevBuf zbuf, gh, gz, gid;
+};
+
+namespace {
+
+struct DeviceGuard {
+    int prev = 0;
+    explicit DeviceGuard(int dev) {
+        (void)hipGetDevice(&prev);
+        if (prev != dev) (void)hipSetDevice(dev);
+    }
+    ~DeviceGuard() {
+        int cur = 0;
+        (void)hipGetDevice(&cur);
+        if (cur != prev) (void)hipSetDevice(prev);
+    }
+};
+
+int enqueue_frame(rtm_ctx* ctx, FrameArgs& a, float* out_dev, StatsK* stats) {
+    int rc;
+    const bool fused = (a.flags & RTM_FLAG_FUSED_SHADOW) != 0;
+    hipStream_t s = ctx->stream;
+    double* smap = nullptr;
+    TimingSlot* slot = ctx->ring.empty() ? nullptr : &ctx->ring[(size_t)(ctx->renders % (int64_t)ctx->ring.size())];
+    if (!fused) {
+        if ((rc = ctx->smap.ensure(sizeof(double) * (size_t)a.Ws * (size_t)a.Hs, ctx->device))) return rc;
+        smap = (double*)ctx->smap.p;
+        ctx->smap_w = a.Ws;
+        ctx->smap_h = a.Hs;
+        if (slot) HIP_TRY(hipEventRecord(slot->ev[0], s));
+        if ((rc = launch_shadow_pass(a, smap, s, stats))) return fail(rc, "shadow pass launch failed");
+        if (slot) HIP_TRY(hipEventRecord(slot->ev[1], s));
+        ctx->have_shadow_pass = true;
+    } else {
+        ctx->have_shadow_pass = false;
+    }
+    if (slot) HIP_TRY(hipEventRecord(slot->ev[2], s));
+    if ((rc = launch_eye_pass(a, smap, out_dev, s, stats))) return fail(rc, "eye pass launch failed");
+    if (slot) {
+        HIP_TRY(hipEventRecord(slot->ev[3], s));
+        slot->shadow = !fused;
+        ctx->renders++;
+    }
+    return RTM_OK;
+}
+
+rtm_ctx* default_ctx(int* rc) {
+    thread_local std::unique_ptr<rtm_ctx, void (*)(rtm_ctx*)> c(nullptr, rtm_ctx_destroy);
+    if (!c) {
+        rtm_ctx* p = nullptr;
+        *rc = rtm_ctx_create(0, &p);
+        if (*rc) return nullptr;
+        c.reset(p);
+    }
+    *rc = RTM_OK;
+    return c.get();
+}
+
+int check_ortho_raster(const rtm_camera& c) {
+    if (c.type != RTM_CAMERA_ORTHOGONAL)
+        return fail(RTM_ERR_UNSUPPORTED, "rasterize: perspective projectSphere (main.rs:473-530) is not on this path");
+    return RTM_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int32_t rtm_abi_version(void) { return RTM_ABI_VERSION; }
+
+const char* rtm_last_error(void) { return g_last_error.c_str(); }
+
+int32_t rtm_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+int rtm_ctx_create(int32_t device, rtm_ctx** out) {
+    if (!out) return fail(RTM_ERR_INVALID, "out is NULL");
+    *out = nullptr;
+    int n = rtm_device_count();
+    if (n <= 0) return fail(RTM_ERR_NO_DEVICE, "no HIP device visible");
+    if (device < 0 || device >= n) return fail(RTM_ERR_INVALID, "device %d outside [0,%d)", device, n);
+    hipDeviceProp_t prop;
+    HIP_TRY(hipGetDeviceProperties(&prop, device));
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return fail(RTM_ERR_NO_DEVICE, "device %d is %s, this library is built for gfx950", device, prop.gcnArchName);
+    std::unique_ptr<rtm_ctx> c(new rtm_ctx);
+    c->device = device;
+    DeviceGuard g(device);
+    HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    *out = c.release();
+    int rc = rtm_ctx_set_timing_capacity(*out, 1);
+    if (rc) {
+        rtm_ctx_destroy(*out);
+        *out = nullptr;
+        return rc;
+    }
+    return RTM_OK;
+}
+
+void rtm_ctx_destroy(rtm_ctx* ctx) {
+    if (!ctx) return;
+    {
+        DeviceGuard g(ctx->device);
+        if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+        for (auto& sl : ctx->ring)
+            for (auto& e : sl.ev)
+                if (e) (void)hipEventDestroy(e);
+        if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    }
+    delete ctx;
+}
+
+void* rtm_ctx_stream(rtm_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
+
+int rtm_ctx_synchronize(rtm_ctx* ctx) {
+    if (!ctx) return fail(RTM_ERR_INVALID, "ctx is NULL");
+    DeviceGuard g(ctx->device);
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    return RTM_OK;
+}
+
+int rtm_ctx_set_timing_capacity(rtm_ctx* ctx, int32_t capacity) {
+    if (!ctx || capacity < 0 || capacity > (1 << 20)) return fail(RTM_ERR_INVALID, "ctx NULL or capacity %d", capacity);
+    DeviceGuard g(ctx->device);
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    for (auto& sl : ctx->ring)
+        for (auto& e : sl.ev)
+            if (e) (void)hipEventDestroy(e);
+    ctx->ring.assign((size_t)capacity, TimingSlot{});
+    ctx->renders = 0;
+    for (auto& sl : ctx->ring)
+        for (auto& e : sl.ev) HIP_TRY(hipEventCreate(&e));
+    return RTM_OK;
+}
+
+int rtm_ctx_kernel_ms_history(rtm_ctx* ctx, float* shadow_ms, float* eye_ms, int32_t max, int32_t* count) {
+    if (!ctx || max < 0 || !count) return fail(RTM_ERR_INVALID, "bad arguments");
+    DeviceGuard g(ctx->device);
+    const int64_t cap = (int64_t)ctx->ring.size();
+    int64_t n = ctx->renders < cap ? ctx->renders : cap;
+    if (n > max) n = max;
+    for (int64_t i = 0; i < n; ++i) {
+        const TimingSlot& sl = ctx->ring[(size_t)((ctx->renders - n + i) % cap)];
+        float sm = 0.0f, em = 0.0f;
+        if (sl.shadow) HIP_TRY(hipEventElapsedTime(&sm, sl.ev[0], sl.ev[1]));
+        HIP_TRY(hipEventElapsedTime(&em, sl.ev[2], sl.ev[3]));
+        if (shadow_ms) shadow_ms[i] = sm;
+        if (eye_ms) eye_ms[i] = em;
+    }
+    *count = (int32_t)n;
+    return RTM_OK;
+}
+
+int rtm_ctx_last_kernel_ms(rtm_ctx* ctx, float* shadow_ms, float* eye_ms) {
+    if (!ctx) return fail(RTM_ERR_INVALID, "ctx is NULL");
+    if (ctx->renders == 0 || ctx->ring.empty()) return fail(RTM_ERR_INVALID, "no timed render yet");
+    int32_t n = 0;
+    float sm = 0.0f, em = 0.0f;
+    int rc = rtm_ctx_kernel_ms_history(ctx, &sm, &em, 1, &n);
+    if (rc) return rc;
+    if (shadow_ms) *shadow_ms = sm;
+    if (eye_ms) *eye_ms = em;
+    return RTM_OK;
+}
+
+int rtm_render_async(rtm_ctx* ctx, const rtm_scene* scene, const rtm_camera* eye, const rtm_camera* shadow,
+                     int32_t width, int32_t height, int32_t march_steps, int32_t flags, int32_t row_begin,
+                     int32_t row_end, float* out_rgba_dev) {
+    if (!ctx) return fail(RTM_ERR_INVALID, "ctx is NULL");
+    if (!out_rgba_dev) return fail(RTM_ERR_INVALID, "out_rgba_dev is NULL");
+    FrameArgs a;
+    int rc = build_frame(a, scene, eye, shadow, width, height, march_steps, flags);
+    if (rc) return rc;
+    if (row_begin < 0 || row_end > height || row_begin >= row_end)
+        return fail(RTM_ERR_INVALID, "row range [%d,%d) outside [0,%d)", row_begin, row_end, height);
+    a.row_begin = row_begin;
+    a.row_end = row_end;
+    DeviceGuard g(ctx->device);
+    return enqueue_frame(ctx, a, out_rgba_dev, nullptr);
+}
+
+const double* rtm_ctx_shadow_map(rtm_ctx* ctx) {
+    if (!ctx || !ctx->have_shadow_pass) return nullptr;
+    return (const double*)ctx->smap.p;
+}
+
+int rtm_render(const rtm_scene* scene, const rtm_camera* eye, const rtm_camera* shadow, int32_t width,
+               int32_t height, int32_t march_steps, int32_t flags, float* out_rgba) {
+    if (!out_rgba) return fail(RTM_ERR_INVALID, "out_rgba is NULL");
+    FrameArgs a;
+    int rc = build_frame(a, scene, eye, shadow, width, height, march_steps, flags);
+    if (rc) return rc;
+    rtm_ctx* ctx = default_ctx(&rc);
+    if (!ctx) return rc;
+    DeviceGuard g(ctx->device);
+    const size_t bytes = sizeof(float) * 4 * (size_t)width * (size_t)height;
+    if ((rc = ctx->out.ensure(bytes, ctx->device))) return rc;
+    if ((rc = enqueue_frame(ctx, a, (float*)ctx->out.p, nullptr))) return rc;
+    HIP_TRY(hipMemcpyAsync(out_rgba, ctx->out.p, bytes, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    return RTM_OK;
+}
+
+int rtm_render_stats(rtm_ctx* ctx, const rtm_scene* scene, const rtm_camera* eye, const rtm_camera* shadow,
+                     int32_t width, int32_t height, int32_t march_steps, int32_t flags, rtm_stats* out) {
+    if (!ctx || !out) return fail(RTM_ERR_INVALID, "ctx/out is NULL");
+    FrameArgs a;
+    int rc = build_frame(a, scene, eye, shadow, width, height, march_steps, flags);
+    if (rc) return rc;
+    DeviceGuard g(ctx->device);
+    const size_t bytes = sizeof(float) * 4 * (size_t)width * (size_t)height;
+    if ((rc = ctx->out.ensure(bytes, ctx->device))) return rc;
+    if ((rc = ctx->stats.ensure(sizeof(StatsK), ctx->device))) return rc;
+    HIP_TRY(hipMemsetAsync(ctx->stats.p, 0, sizeof(StatsK), ctx->stream));
+    if ((rc = enqueue_frame(ctx, a, (float*)ctx->out.p, (StatsK*)ctx->stats.p))) return rc;
+    HIP_TRY(hipMemcpyAsync(out, ctx->stats.p, sizeof(StatsK), hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    return RTM_OK;
+}
+
+// ---- reference-seam API ----
+
+int rtm_viewport_create(rtm_ctx* ctx, int32_t width, int32_t height, int32_t face, const rtm_camera* camera,
+                        rtm_viewport** out) {
+    if (!ctx || !out) return fail(RTM_ERR_INVALID, "ctx/out is NULL");
+    *out = nullptr;
+    int rc;
+    if ((rc = validate_dims(width, height)) || (rc = validate_camera(camera, "viewport"))) return rc;
+    if (face != RTM_FACE_FRONT && face != RTM_FACE_BACK) return fail(RTM_ERR_INVALID, "face %d", face);
+    std::unique_ptr<rtm_viewport> v(new rtm_viewport);
+    v->ctx = ctx;
+    v->W = width;
+    v->H = height;
+    v->face = face;
+    v->cam = *camera;
+    DeviceGuard g(ctx->device);
+    const size_t n = (size_t)width * (size_t)height;
+    if ((rc = v->zbuf.ensure(n * sizeof(double), ctx->device)) || (rc = v->gh.ensure(n * sizeof(double), ctx->device)) ||
+        (rc = v->gz.ensure(n * sizeof(double), ctx->device)) || (rc = v->gid.ensure(n * sizeof(int32_t), ctx->device)))
+        return rc;
+    // zBuffer: Map2d::new(.., INFINITY); rasterized: vec![None; ..] (main.rs:1534-1536)
+    if ((rc = launch_fill((double*)v->zbuf.p, (int64_t)n, INFINITY, (int32_t*)v->gid.p, -1, ctx->stream)))
+        return fail(rc, "viewport init launch failed");
+    *out = v.release();
+    return RTM_OK;
+}
+
+void rtm_viewport_destroy(rtm_viewport* vp) {
+    if (!vp) return;
+    {
+        DeviceGuard g(vp->ctx->device);
+        (void)hipStreamSynchronize(vp->ctx->stream);
+    }
+    delete vp;
+}
+
+int rtm_viewport_rasterize(rtm_viewport* vp, const rtm_scene* scene) {
+    if (!vp) return fail(RTM_ERR_INVALID, "viewport is NULL");
+    int rc;
+    if ((rc = validate_scene(scene)) || (rc = check_ortho_raster(vp->cam))) return rc;
+    RasterArgs a;
+    std::memset(&a, 0, sizeof a);
+    for (int i = 0; i < scene->n_spheres; ++i) a.sph[i] = project_sphere(vp->cam, scene->spheres[i]);
+    a.n_spheres = scene->n_spheres;
+    a.face = vp->face;
+    a.W = vp->W;
+    a.H = vp->H;
+    DeviceGuard g(vp->ctx->device);
+    if ((rc = launch_vp_rasterize(a, (double*)vp->zbuf.p, (double*)vp->gh.p, (double*)vp->gz.p, (int32_t*)vp->gid.p,
+                                  vp->ctx->stream)))
+        return fail(rc, "rasterize launch failed");
+    return RTM_OK;
+}
+
+int rtm_viewport_process_raymarching_rays(rtm_viewport* vp, const rtm_patch* patches, int32_t n_patches,
+                                          int32_t steps) {
+    if (!vp) return fail(RTM_ERR_INVALID, "viewport is NULL");
+    if (n_patches < 0 || n_patches > RTM_MAX_PATCHES) return fail(RTM_ERR_INVALID, "n_patches=%d", n_patches);
+    if (n_patches > 0 && !patches) return fail(RTM_ERR_INVALID, "patches is NULL");
+    if (steps < 0) return fail(RTM_ERR_INVALID, "steps=%d", steps);
+    MarchArgs a;
+    std::memset(&a, 0, sizeof a);
+    for (int i = 0; i < n_patches; ++i) a.patch[i] = patch_k(patches[i]);
+    a.cam = cam_k(vp->cam);
+    a.n_patches = n_patches;
+    a.steps = steps;
+    a.W = vp->W;
+    a.H = vp->H;
+    DeviceGuard g(vp->ctx->device);
+    int rc = launch_vp_march(a, (double*)vp->zbuf.p, vp->ctx->stream);
+    if (rc) return fail(rc, "march launch failed");
+    return RTM_OK;
+}
+
+int rtm_render_color_image(const rtm_scene* scene, const rtm_viewport* vp, const rtm_viewport* shadow_vp,
+                           float* out_rgba) {
+    if (!vp || !shadow_vp || !out_rgba) return fail(RTM_ERR_INVALID, "viewport/out is NULL");
+    if (vp->ctx != shadow_vp->ctx) return fail(RTM_ERR_INVALID, "viewports belong to different contexts");
+    int rc;
+    if ((rc = validate_scene(scene))) return rc;
+    if (shadow_vp->cam.type != RTM_CAMERA_ORTHOGONAL)
+        return fail(RTM_ERR_UNSUPPORTED, "Camera::project is orthographic only (main.rs:1949)");
+    ShadeArgs a;
+    std::memset(&a, 0, sizeof a);
+    for (int i = 0; i < scene->n_spheres; ++i) a.shade[i] = shade_sphere(scene->spheres[i]);
+    a.eye = cam_k(vp->cam);
+    a.shadow = cam_k(shadow_vp->cam);
+    a.W = vp->W;
+    a.H = vp->H;
+    a.Ws = shadow_vp->W;
+    a.Hs = shadow_vp->H;
+    a.n_spheres = scene->n_spheres;
+    rtm_ctx* ctx = vp->ctx;
+    DeviceGuard g(ctx->device);
+    const size_t bytes = sizeof(float) * 4 * (size_t)vp->W * (size_t)vp->H;
+    if ((rc = ctx->out.ensure(bytes, ctx->device))) return rc;
+    if ((rc = launch_vp_shade(a, (const double*)shadow_vp->zbuf.p, (const double*)vp->gh.p, (const double*)vp->gz.p,
+                              (const int32_t*)vp->gid.p, (float*)ctx->out.p, ctx->stream)))
+        return fail(rc, "shade launch failed");
+    HIP_TRY(hipMemcpyAsync(out_rgba, ctx->out.p, bytes, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    return RTM_OK;
+}
+
+int rtm_viewport_read_zbuffer(const rtm_viewport* vp, double* out) {
+    if (!vp || !out) return fail(RTM_ERR_INVALID, "viewport/out is NULL");
+    DeviceGuard g(vp->ctx->device);
+    HIP_TRY(hipMemcpyAsync(out, vp->zbuf.p, sizeof(double) * (size_t)vp->W * (size_t)vp->H, hipMemcpyDeviceToHost,
+                           vp->ctx->stream));
+    HIP_TRY(hipStreamSynchronize(vp->ctx->stream));
+    return RTM_OK;
+}
+
+}  // extern "C"

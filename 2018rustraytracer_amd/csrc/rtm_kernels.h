@@ -1,0 +1,99 @@
+// rtm_kernels.h — kernel-argument structs shared by the host library and the
+// HIP kernels.  Every scene constant the reference recomputes per pixel but
+// that depends only on (camera, sphere) is evaluated once on the host, in the
+// reference's floating-point operation order, and travels to the GPU as a
+// kernel argument (constant memory, read through the scalar cache into SGPRs).
+#pragma once
+
+#include <stdint.h>
+
+#include "../../include/rtm.h"
+
+namespace rtm {
+
+// One sphere as seen by one ORTHOGONAL camera (Viewport::rasterize, main.rs:449-470).
+// For axisA=(r,0), axisB=(0,r): axisA.normalized()=(n,z0), axisB.normalized()=(z0,n),
+// |axisA|=|axisB|=m (main.rs:2849-2850, 2098-2109).
+struct RasterSphereK {
+    double cx, cy;  // Camera::project(pos).xy (main.rs:455, 464)
+    double z;       // calcDepthOfProjectedPoint(pos) (main.rs:450)
+    double r;       // the r rasterizeSphere multiplies relativeHeight by (main.rs:541, 316)
+    double n, z0;   // r*(1/m), 0*(1/m)
+    double m;       // sqrt(r*r + 0*0)
+    double R;       // cull radius: |rel.x|>R or |rel.y|>R implies d>=1 (pure cull)
+    int64_t id;     // PrimitiveSphere.id -> G-buffer (main.rs:189)
+};
+
+// Per-sphere shading constants, indexed by id (renderColorImage, main.rs:748-759).
+struct ShadeSphereK {
+    double px, py, pz;  // pos
+    double r;           // calcDepth's primitiveSphere.r (main.rs:160)
+    double inv_r;       // 1.0/r (main.rs:752)
+    double cr, cg, cb;  // shading
+};
+
+struct CamK {  // ORTHOGONAL or PERSPECTIVE camera (main.rs:1887-1898)
+    double pos[3], dir[3], up[3], side[3];
+    int32_t type;
+    int32_t pad;
+};
+
+// Bilinear patch with the linear() differences b-a precomputed (main.rs:2066-2068).
+struct PatchK {
+    double a0, d0;  // _0.a, _0.b - _0.a
+    double a1, d1;  // _1.a, _1.b - _1.a
+};
+
+// Everything one frame's kernels read.  Kept < 4 KiB (kernarg limit).
+struct FrameArgs {
+    RasterSphereK esph[RTM_MAX_SPHERES];  // eye camera projection
+    RasterSphereK ssph[RTM_MAX_SPHERES];  // shadow camera projection
+    ShadeSphereK shade[RTM_MAX_SPHERES];
+    PatchK patch[RTM_MAX_PATCHES];
+    CamK eye, shadow;
+    int32_t W, H;            // eye image
+    int32_t Ws, Hs;          // shadow map (== W, H)
+    int32_t n_spheres, n_patches;
+    int32_t steps, flags;
+    int32_t row_begin, row_end;
+};
+static_assert(sizeof(FrameArgs) <= 4096, "FrameArgs must fit the 4 KiB kernarg segment");
+
+// Reference-seam kernels (one per reference function).
+struct RasterArgs {
+    RasterSphereK sph[RTM_MAX_SPHERES];
+    int32_t n_spheres, face, W, H;
+};
+
+struct MarchArgs {
+    PatchK patch[RTM_MAX_PATCHES];
+    CamK cam;
+    int32_t n_patches, steps, W, H;
+};
+
+struct ShadeArgs {
+    ShadeSphereK shade[RTM_MAX_SPHERES];
+    CamK eye, shadow;
+    int32_t W, H, Ws, Hs;
+    int32_t n_spheres, pad;
+};
+
+// Device counters for rtm_render_stats (layout == rtm_stats).
+struct StatsK {
+    unsigned long long eye_hits[RTM_MAX_SPHERES];
+    unsigned long long eye_hit_pixels, lit_pixels, eye_sphere_tests, shadow_sphere_tests;
+    unsigned long long march_iterations, march_hits, march_in_range;
+};
+static_assert(sizeof(StatsK) == sizeof(rtm_stats), "StatsK layout");
+
+// Launchers (rtm_kernels.hip).  All asynchronous on `stream`.
+int launch_shadow_pass(const FrameArgs& a, double* smap, void* stream, StatsK* stats);
+int launch_eye_pass(const FrameArgs& a, const double* smap, float* out, void* stream, StatsK* stats);
+int launch_vp_rasterize(const RasterArgs& a, double* zbuf, double* gh, double* gz, int32_t* gid,
+                        void* stream);
+int launch_vp_march(const MarchArgs& a, double* zbuf, void* stream);
+int launch_vp_shade(const ShadeArgs& a, const double* szbuf, const double* gh, const double* gz,
+                    const int32_t* gid, float* out, void* stream);
+int launch_fill(double* p, int64_t n, double v, int32_t* ip, int32_t iv, void* stream);
+
+}  // namespace rtm

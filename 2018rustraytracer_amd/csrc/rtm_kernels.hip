@@ -1,0 +1,492 @@
+// rtm_kernels.hip — CDNA4 (gfx950) kernels for the per-pixel hot path of
+// PtrMan/2018RustRayTracer src/main.rs.
+//
+// Numerics: IEEE f64 in the reference's operation order, FMA contraction off
+// (file pragma + -ffp-contract=off), correctly-rounded f64 div/sqrt (the
+// AMDGPU default lowering).  Results are bit-identical to the CPU oracle.
+//
+// Work mapping: one work-item per pixel; a 256-thread workgroup is a 64x4
+// pixel tile, so each wave owns 64 consecutive pixels of one row: the RGBA f32
+// store is one contiguous 1 KiB global_store_dwordx4 per wave and the f64
+// shadow-map store 512 B.  Scene constants are kernel arguments (uniform,
+// scalar-cache/SGPR operands).  No MFMA: this is scalar per-pixel math.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+#include "rtm_kernels.h"
+
+#pragma clang fp contract(off)
+
+namespace rtm {
+
+namespace {
+
+constexpr int TILE_X = 64;  // one wave per tile row
+constexpr int TILE_Y = 4;   // four waves per workgroup
+constexpr int BLOCK = TILE_X * TILE_Y;
+
+// main.rs:306-307 / 1903-1907: ((i as f64) / (res as f64)) * 2.0 - 1.0
+__device__ __forceinline__ double ndc(int i, int res) { return ((double)i / (double)res) * 2.0 - 1.0; }
+
+// Rust f64::signum (used by raymarchPatch, main.rs:2244, 2261)
+__device__ __forceinline__ double rsignum(double v) { return v != v ? v : copysign(1.0, v); }
+
+// inRange01 (main.rs:2282-2284)
+__device__ __forceinline__ bool in01(double v) { return fabs(v - 0.5) <= 0.5; }
+
+// calcDepthBilinear -> bilinear -> linear (main.rs:2146, 2073-2080, 2066-2069)
+__device__ __forceinline__ double bil(const PatchK& p, double x, double y) {
+    double d0 = p.a0 + p.d0 * x;
+    double d1 = p.a1 + p.d1 * x;
+    double dd = d1 - d0;
+    return d0 + dd * y;
+}
+
+// Rust `as i64` followed by `(W/2) +`; only membership in [0,W) matters downstream,
+// so magnitudes >= 4e18 map to an out-of-range sentinel (the reference's saturate+wrap
+// is out of range as well).  NaN -> 0 exactly as Rust.
+__device__ __forceinline__ int64_t tex_index(int64_t half, double v) {
+    int64_t t;
+    if (v != v) t = 0;
+    else if (fabs(v) < 4.0e18) t = (int64_t)v;
+    else t = v > 0.0 ? (int64_t)1 << 62 : -((int64_t)1 << 62);
+    return half + t;
+}
+
+// Sphere coverage of one pixel (projectSphereAtZBuffer, main.rs:176-195):
+// calcOthoDistanceByAbsPosition + calcHeightOfSphereOnUnit.
+__device__ __forceinline__ bool cover(const RasterSphereK& s, double x, double y, double& h) {
+    double relx = x - s.cx;
+    double rely = y - s.cy;
+    if (!(fabs(relx) <= s.R && fabs(rely) <= s.R)) return false;  // pure cull (reference bbox, main.rs:256-300)
+    double pa = (relx * s.n + rely * s.z0) / s.m;
+    double pb = (relx * s.z0 + rely * s.n) / s.m;
+    double d = sqrt(pa * pa + pb * pb);
+    if (d < 1.0) {
+        h = sqrt(1.0 - d * d);
+        return true;
+    }
+    return false;
+}
+
+struct MarchResult {
+    bool hit;
+    double t;
+    int iters;  // loop iterations executed (stats only)
+    bool in_range;
+};
+
+// raymarchPatchDomainM11 + raymarchPatch (main.rs:2179-2278).
+// When the ray has no x/y motion (step.x == step.y == 0, every axis-aligned
+// orthographic shadow camera) p.x, p.y and therefore inRange01 and the surface
+// depth are loop-invariant: the loop is unswitched and only p.z and t advance.
+// The sequential accumulation p.z += step.z, t += 0.03 is kept exactly.
+template <bool COUNT>
+__device__ __forceinline__ MarchResult march(double ox, double oy, double oz, double dx, double dy,
+                                             double dz, const PatchK& p, int steps) {
+    MarchResult r{false, 0.0, 0, false};
+    double px = (ox + 1.0) * 0.5;
+    double py = (oy + 1.0) * 0.5;
+    double pz = oz;
+    const double mstep = 0.03;
+    double sx = dx * mstep, sy = dy * mstep, sz = dz * mstep;
+    double t = 0.0;
+    double entry = rsignum(pz - bil(p, px, py));
+    if (COUNT) r.in_range = in01(px) && in01(py);
+    if (sx == 0.0 && sy == 0.0) {
+        // (px is never -0.0 here, so px + (+-0.0) == px bit for bit)
+        if (!(in01(px) && in01(py))) {
+            if (COUNT) r.iters = steps;
+            return r;
+        }
+        const double D = bil(p, px, py);
+        for (int k = 0; k < steps; ++k) {
+            if (rsignum(pz - D) != entry) {
+                r.hit = true;
+                r.t = t;
+                if (COUNT) r.iters = k + 1;
+                return r;
+            }
+            pz = pz + sz;
+            t = t + mstep;
+        }
+        if (COUNT) r.iters = steps;
+        return r;
+    }
+    for (int k = 0; k < steps; ++k) {
+        if (!in01(px) || !in01(py)) {
+            px = px + sx;
+            py = py + sy;
+            pz = pz + sz;
+            t = t + mstep;
+            continue;
+        }
+        if (rsignum(pz - bil(p, px, py)) != entry) {
+            r.hit = true;
+            r.t = t;
+            if (COUNT) r.iters = k + 1;
+            return r;
+        }
+        px = px + sx;
+        py = py + sy;
+        pz = pz + sz;
+        t = t + mstep;
+    }
+    if (COUNT) r.iters = steps;
+    return r;
+}
+
+// Camera::calcRayOriginAndDirection (main.rs:1902-1942); s, u are the [-1,1] scales.
+__device__ __forceinline__ void cam_ray(const CamK& c, double s, double u, double o[3], double d[3]) {
+    if (c.type == RTM_CAMERA_ORTHOGONAL) {
+        for (int k = 0; k < 3; ++k) {
+            o[k] = (c.pos[k] + c.side[k] * s) + c.up[k] * u;
+            d[k] = c.dir[k];
+        }
+    } else {
+        double v[3];
+        for (int k = 0; k < 3; ++k) v[k] = (c.dir[k] + c.side[k] * (s * 1.0)) + c.up[k] * (u * 1.0);
+        double m = sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
+        double inv = 1.0 / m;
+        for (int k = 0; k < 3; ++k) {
+            o[k] = c.pos[k];
+            d[k] = v[k] * inv;
+        }
+    }
+}
+
+// ---- statistics (rtm_render_stats only; never in the timed kernels) ----
+__device__ __forceinline__ unsigned long long wave_sum(unsigned long long v) {
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+__device__ __forceinline__ void stat_add(unsigned long long* ctr, unsigned long long v) {
+    v = wave_sum(v);
+    if ((threadIdx.x & 63) == 0 && v) atomicAdd(ctr, v);
+}
+
+// One shadow-map texel: shadow viewport rasterize (face BACK, main.rs:1569) then
+// processRaymarchingRays (main.rs:1571) with a strict-min update (main.rs:559).
+template <bool COUNT>
+__device__ __forceinline__ double shadow_texel(const FrameArgs& a, int xi, int yi, unsigned long long* n_tests,
+                                               unsigned long long* n_iters, unsigned long long* n_hits,
+                                               unsigned long long* n_inrange) {
+    const double x = ndc(xi, a.Ws);
+    const double y = ndc(yi, a.Hs);
+    double zb = INFINITY;
+    if (!(a.flags & RTM_FLAG_NO_SHADOW_RASTER)) {
+        for (int i = 0; i < a.n_spheres; ++i) {
+            double h;
+            if (cover(a.ssph[i], x, y, h)) {
+                if (COUNT) ++*n_tests;
+                double depth = a.ssph[i].z + h * a.ssph[i].r;  // EnumFace::BACK (main.rs:243)
+                if (depth < zb) zb = depth;
+            }
+        }
+    }
+    if (!(a.flags & RTM_FLAG_NO_MARCH)) {
+        double o[3], d[3];
+        cam_ray(a.shadow, x, y, o, d);
+        for (int k = 0; k < a.n_patches; ++k) {
+            MarchResult m = march<COUNT>(o[0], o[1], o[2], d[0], d[1], d[2], a.patch[k], a.steps);
+            if (COUNT) {
+                *n_iters += m.iters;
+                *n_hits += m.hit;
+                *n_inrange += m.in_range;
+            }
+            if (m.hit && m.t < zb) zb = m.t;
+        }
+    }
+    return zb;
+}
+
+template <bool COUNT>
+__global__ __launch_bounds__(BLOCK) void shadow_pass_kernel(const FrameArgs a, double* __restrict__ smap,
+                                                            StatsK* __restrict__ st) {
+    const int xi = blockIdx.x * TILE_X + (threadIdx.x & (TILE_X - 1));
+    const int yi = blockIdx.y * TILE_Y + (threadIdx.x >> 6);
+    const bool live = xi < a.Ws && yi < a.Hs;
+    unsigned long long nt = 0, ni = 0, nh = 0, nr = 0;
+    if (live) {
+        double zb = shadow_texel<COUNT>(a, xi, yi, &nt, &ni, &nh, &nr);
+        smap[(int64_t)yi * a.Ws + xi] = zb;
+    }
+    if (COUNT) {
+        stat_add(&st->shadow_sphere_tests, nt);
+        stat_add(&st->march_iterations, ni);
+        stat_add(&st->march_hits, nh);
+        stat_add(&st->march_in_range, nr);
+    }
+}
+
+// Eye pixel: eye viewport rasterize (face FRONT, main.rs:1616) + renderColorImage
+// (main.rs:714-898).  FUSED evaluates the looked-up shadow texel on demand.
+template <bool FUSED, bool COUNT>
+__global__ __launch_bounds__(BLOCK) void eye_pass_kernel(const FrameArgs a, const double* __restrict__ smap,
+                                                         float4* __restrict__ out, StatsK* __restrict__ st) {
+    const int xi = blockIdx.x * TILE_X + (threadIdx.x & (TILE_X - 1));
+    const int yl = blockIdx.y * TILE_Y + (threadIdx.x >> 6);
+    const int yi = a.row_begin + yl;
+    const bool live = xi < a.W && yi < a.row_end;
+    unsigned long long n_tests = 0, n_hit = 0, n_lit = 0, n_it = 0, n_mh = 0, n_ir = 0, n_st = 0;
+    int hit_id = -1;
+    if (live) {
+        const double x = ndc(xi, a.W);
+        const double y = ndc(yi, a.H);
+        // z-test over spheres in scene order, strict '<' against +INF init (main.rs:318)
+        double best = INFINITY, bh = 0.0, bz = 0.0;
+        int bid = -1;
+        for (int i = 0; i < a.n_spheres; ++i) {
+            double h;
+            if (cover(a.esph[i], x, y, h)) {
+                if (COUNT) ++n_tests;
+                double depth = a.esph[i].z - h * a.esph[i].r;  // EnumFace::FRONT (main.rs:239)
+                if (depth < best) {
+                    best = depth;
+                    bh = h;
+                    bz = a.esph[i].z;
+                    bid = (int)a.esph[i].id;
+                }
+            }
+        }
+        float4 c = make_float4(0.0f, 0.2f, 0.2f, 1.0f);  // (0.0, 0.2, 0.2) as f32 (main.rs:718-720)
+        if (bid >= 0) {
+            const ShadeSphereK& s = a.shade[bid];
+            // calcDepth (main.rs:160-162)
+            const double depth = bz - bh * s.r;
+            double o[3], d[3];
+            cam_ray(a.eye, x, y, o, d);
+            // world position and normal (main.rs:744-752)
+            const double wx = o[0] + d[0] * depth, wy = o[1] + d[1] * depth, wz = o[2] + d[2] * depth;
+            const double nx = (wx - s.px) * s.inv_r, ny = (wy - s.py) * s.inv_r, nz = (wz - s.pz) * s.inv_r;
+            // light (1,0,0).scale(-1.0) (main.rs:810-813)
+            const double Lx = 1.0 * -1.0, Ly = 0.0 * -1.0, Lz = 0.0 * -1.0;
+            double diffuse = fmax(nx * Lx + ny * Ly + nz * Lz, 0.0);
+            // reflect(L, n) = L - n*(-2 dot(L,n))  (main.rs:2872-2875, sign as written)
+            const double k2 = -2.0 * (Lx * nx + Ly * ny + Lz * nz);
+            const double Rx = Lx - nx * k2, Ry = Ly - ny * k2, Rz = Lz - nz * k2;
+            // retViewDirOfPixel, ORTHOGONAL (main.rs:1984)
+            const double vx = a.eye.dir[0] * -1.0, vy = a.eye.dir[1] * -1.0, vz = a.eye.dir[2] * -1.0;
+            double sp = fmax(vx * Rx + vy * Ry + vz * Rz, 0.0);
+            sp = sp * sp;  // powi(32): five squarings (compiler-rt __powidf2)
+            sp = sp * sp;
+            sp = sp * sp;
+            sp = sp * sp;
+            sp = sp * sp;
+            // shadow mapping (main.rs:836-856)
+            const double dfx = wx - a.shadow.pos[0], dfy = wy - a.shadow.pos[1], dfz = wz - a.shadow.pos[2];
+            const double qx = dfx * a.shadow.side[0] + dfy * a.shadow.side[1] + dfz * a.shadow.side[2];
+            const double qy = dfx * a.shadow.up[0] + dfy * a.shadow.up[1] + dfz * a.shadow.up[2];
+            const double qz = dfx * a.shadow.dir[0] + dfy * a.shadow.dir[1] + dfz * a.shadow.dir[2];
+            const int64_t hw = a.Ws / 2, hh = a.Hs / 2;
+            const int64_t tx = tex_index(hw, qx * (double)hw);
+            const int64_t ty = tex_index(hh, qy * (double)hh);
+            double dsm = INFINITY;
+            if (ty >= 0 && ty < a.Hs && tx >= 0 && tx < a.Ws) {
+                if (FUSED)
+                    dsm = shadow_texel<COUNT>(a, (int)tx, (int)ty, &n_st, &n_it, &n_mh, &n_ir);
+                else
+                    dsm = smap[ty * a.Ws + tx];
+            }
+            const bool lit = dsm > qz - 0.0;
+            const double lm = lit ? 1.0 : 0.25;
+            const double base = diffuse + sp;
+            c.x = (float)((base * lm) * s.cr);
+            c.y = (float)((base * lm) * s.cg);
+            c.z = (float)((base * lm) * s.cb);
+            if (COUNT) {
+                n_hit = 1;
+                n_lit = lit;
+                hit_id = bid;
+            }
+        }
+        out[(int64_t)yl * a.W + xi] = c;
+    }
+    if (COUNT) {
+        stat_add(&st->eye_sphere_tests, n_tests);
+        stat_add(&st->eye_hit_pixels, n_hit);
+        stat_add(&st->lit_pixels, n_lit);
+        for (int i = 0; i < a.n_spheres; ++i) stat_add(&st->eye_hits[i], hit_id == i);
+        if (FUSED) {
+            stat_add(&st->shadow_sphere_tests, n_st);
+            stat_add(&st->march_iterations, n_it);
+            stat_add(&st->march_hits, n_mh);
+            stat_add(&st->march_in_range, n_ir);
+        }
+    }
+}
+
+// ---- reference-seam kernels ----
+
+// Viewport::rasterize (main.rs:445-547): spheres in order against the viewport's
+// current zBuffer / G-buffer (rasterizeSphere, main.rs:304-330).
+__global__ __launch_bounds__(BLOCK) void vp_rasterize_kernel(const RasterArgs a, double* __restrict__ zbuf,
+                                                             double* __restrict__ gh, double* __restrict__ gz,
+                                                             int32_t* __restrict__ gid) {
+    const int xi = blockIdx.x * TILE_X + (threadIdx.x & (TILE_X - 1));
+    const int yi = blockIdx.y * TILE_Y + (threadIdx.x >> 6);
+    if (xi >= a.W || yi >= a.H) return;
+    const int64_t idx = (int64_t)yi * a.W + xi;
+    const double x = ndc(xi, a.W), y = ndc(yi, a.H);
+    double zb = zbuf[idx];
+    bool wrote = false;
+    double wh = 0.0, wz = 0.0;
+    int32_t wid = 0;
+    for (int i = 0; i < a.n_spheres; ++i) {
+        double h;
+        if (cover(a.sph[i], x, y, h)) {
+            double hr = h * a.sph[i].r;
+            double depth = a.face == RTM_FACE_FRONT ? a.sph[i].z - hr : a.sph[i].z + hr;
+            if (depth < zb) {
+                zb = depth;
+                wrote = true;
+                wh = h;
+                wz = a.sph[i].z;
+                wid = (int32_t)a.sph[i].id;
+            }
+        }
+    }
+    if (wrote) {
+        zbuf[idx] = zb;
+        gh[idx] = wh;
+        gz[idx] = wz;
+        gid[idx] = wid;
+    }
+}
+
+// Viewport::processRaymarchingRays (main.rs:551-565)
+__global__ __launch_bounds__(BLOCK) void vp_march_kernel(const MarchArgs a, double* __restrict__ zbuf) {
+    const int xi = blockIdx.x * TILE_X + (threadIdx.x & (TILE_X - 1));
+    const int yi = blockIdx.y * TILE_Y + (threadIdx.x >> 6);
+    if (xi >= a.W || yi >= a.H) return;
+    const int64_t idx = (int64_t)yi * a.W + xi;
+    double o[3], d[3];
+    cam_ray(a.cam, ndc(xi, a.W), ndc(yi, a.H), o, d);
+    double zb = zbuf[idx];
+    const double z0 = zb;
+    for (int k = 0; k < a.n_patches; ++k) {
+        MarchResult m = march<false>(o[0], o[1], o[2], d[0], d[1], d[2], a.patch[k], a.steps);
+        if (m.hit && m.t < zb) zb = m.t;
+    }
+    if (!(zb == z0)) zbuf[idx] = zb;
+}
+
+// renderColorImage (main.rs:710-902) from a G-buffer.
+__global__ __launch_bounds__(BLOCK) void vp_shade_kernel(const ShadeArgs a, const double* __restrict__ szbuf,
+                                                         const double* __restrict__ gh,
+                                                         const double* __restrict__ gz,
+                                                         const int32_t* __restrict__ gid, float4* __restrict__ out) {
+    const int xi = blockIdx.x * TILE_X + (threadIdx.x & (TILE_X - 1));
+    const int yi = blockIdx.y * TILE_Y + (threadIdx.x >> 6);
+    if (xi >= a.W || yi >= a.H) return;
+    const int64_t idx = (int64_t)yi * a.W + xi;
+    float4 c = make_float4(0.0f, 0.2f, 0.2f, 1.0f);
+    const int32_t id = gid[idx];
+    if (id >= 0) {
+        const ShadeSphereK& s = a.shade[id];
+        const double s01 = ndc(xi, a.W), u01 = ndc(yi, a.H);
+        double o[3], d[3];
+        cam_ray(a.eye, s01, u01, o, d);
+        double view[3];
+        if (a.eye.type == RTM_CAMERA_ORTHOGONAL) {
+            for (int k = 0; k < 3; ++k) view[k] = a.eye.dir[k] * -1.0;
+        } else {
+            for (int k = 0; k < 3; ++k) view[k] = d[k] * -1.0;  // retViewDirOfPixel == -ray dir
+        }
+        const double depth = gz[idx] - gh[idx] * s.r;
+        const double wx = o[0] + d[0] * depth, wy = o[1] + d[1] * depth, wz = o[2] + d[2] * depth;
+        const double nx = (wx - s.px) * s.inv_r, ny = (wy - s.py) * s.inv_r, nz = (wz - s.pz) * s.inv_r;
+        const double Lx = 1.0 * -1.0, Ly = 0.0 * -1.0, Lz = 0.0 * -1.0;
+        double diffuse = fmax(nx * Lx + ny * Ly + nz * Lz, 0.0);
+        const double k2 = -2.0 * (Lx * nx + Ly * ny + Lz * nz);
+        const double Rx = Lx - nx * k2, Ry = Ly - ny * k2, Rz = Lz - nz * k2;
+        double sp = fmax(view[0] * Rx + view[1] * Ry + view[2] * Rz, 0.0);
+        sp = sp * sp;
+        sp = sp * sp;
+        sp = sp * sp;
+        sp = sp * sp;
+        sp = sp * sp;
+        const double dfx = wx - a.shadow.pos[0], dfy = wy - a.shadow.pos[1], dfz = wz - a.shadow.pos[2];
+        const double qx = dfx * a.shadow.side[0] + dfy * a.shadow.side[1] + dfz * a.shadow.side[2];
+        const double qy = dfx * a.shadow.up[0] + dfy * a.shadow.up[1] + dfz * a.shadow.up[2];
+        const double qz = dfx * a.shadow.dir[0] + dfy * a.shadow.dir[1] + dfz * a.shadow.dir[2];
+        const int64_t hw = a.Ws / 2, hh = a.Hs / 2;
+        const int64_t tx = tex_index(hw, qx * (double)hw);
+        const int64_t ty = tex_index(hh, qy * (double)hh);
+        double dsm = INFINITY;
+        if (ty >= 0 && ty < a.Hs && tx >= 0 && tx < a.Ws) dsm = szbuf[ty * a.Ws + tx];
+        const double lm = (dsm > qz - 0.0) ? 1.0 : 0.25;
+        const double base = diffuse + sp;
+        c.x = (float)((base * lm) * s.cr);
+        c.y = (float)((base * lm) * s.cg);
+        c.z = (float)((base * lm) * s.cb);
+    }
+    out[idx] = c;
+}
+
+__global__ void fill_kernel(double* __restrict__ p, int64_t n, double v, int32_t* __restrict__ ip, int32_t iv) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        if (p) p[i] = v;
+        if (ip) ip[i] = iv;
+    }
+}
+
+inline dim3 grid_for(int w, int h) { return dim3((unsigned)((w + TILE_X - 1) / TILE_X), (unsigned)((h + TILE_Y - 1) / TILE_Y)); }
+
+inline int launched() { return hipGetLastError() == hipSuccess ? 0 : RTM_ERR_HIP; }
+
+}  // namespace
+
+int launch_shadow_pass(const FrameArgs& a, double* smap, void* stream, StatsK* stats) {
+    hipStream_t s = (hipStream_t)stream;
+    if (stats)
+        hipLaunchKernelGGL(shadow_pass_kernel<true>, grid_for(a.Ws, a.Hs), dim3(BLOCK), 0, s, a, smap, stats);
+    else
+        hipLaunchKernelGGL(shadow_pass_kernel<false>, grid_for(a.Ws, a.Hs), dim3(BLOCK), 0, s, a, smap, stats);
+    return launched();
+}
+
+int launch_eye_pass(const FrameArgs& a, const double* smap, float* out, void* stream, StatsK* stats) {
+    hipStream_t s = (hipStream_t)stream;
+    dim3 g = grid_for(a.W, a.row_end - a.row_begin);
+    float4* o = reinterpret_cast<float4*>(out);
+    const bool fused = (a.flags & RTM_FLAG_FUSED_SHADOW) != 0;
+    if (fused && stats)
+        hipLaunchKernelGGL((eye_pass_kernel<true, true>), g, dim3(BLOCK), 0, s, a, smap, o, stats);
+    else if (fused)
+        hipLaunchKernelGGL((eye_pass_kernel<true, false>), g, dim3(BLOCK), 0, s, a, smap, o, stats);
+    else if (stats)
+        hipLaunchKernelGGL((eye_pass_kernel<false, true>), g, dim3(BLOCK), 0, s, a, smap, o, stats);
+    else
+        hipLaunchKernelGGL((eye_pass_kernel<false, false>), g, dim3(BLOCK), 0, s, a, smap, o, stats);
+    return launched();
+}
+
+int launch_vp_rasterize(const RasterArgs& a, double* zbuf, double* gh, double* gz, int32_t* gid, void* stream) {
+    hipLaunchKernelGGL(vp_rasterize_kernel, grid_for(a.W, a.H), dim3(BLOCK), 0, (hipStream_t)stream, a, zbuf, gh,
+                       gz, gid);
+    return launched();
+}
+
+int launch_vp_march(const MarchArgs& a, double* zbuf, void* stream) {
+    hipLaunchKernelGGL(vp_march_kernel, grid_for(a.W, a.H), dim3(BLOCK), 0, (hipStream_t)stream, a, zbuf);
+    return launched();
+}
+
+int launch_vp_shade(const ShadeArgs& a, const double* szbuf, const double* gh, const double* gz, const int32_t* gid,
+                    float* out, void* stream) {
+    hipLaunchKernelGGL(vp_shade_kernel, grid_for(a.W, a.H), dim3(BLOCK), 0, (hipStream_t)stream, a, szbuf, gh, gz,
+                       gid, reinterpret_cast<float4*>(out));
+    return launched();
+}
+
+int launch_fill(double* p, int64_t n, double v, int32_t* ip, int32_t iv, void* stream) {
+    if (n <= 0) return 0;
+    int64_t blocks = (n + 255) / 256;
+    if (blocks > 2048) blocks = 2048;
+    hipLaunchKernelGGL(fill_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, p, n, v, ip, iv);
+    return launched();
+}
+
+}  // namespace rtm

@@ -1,0 +1,171 @@
+"""Host-side mirror of the reference's render interface over the HIP C ABI.
+
+Reference surface (src/main.rs) -> this module:
+    Viewport{rasterized, zBuffer, face, camera}   main.rs:426-439  -> Viewport
+    Viewport::rasterize(&Scene)                   main.rs:445      -> Viewport.rasterize
+    Viewport::processRaymarchingRays()            main.rs:551      -> Viewport.processRaymarchingRays
+    renderColorImage(&Scene,&Viewport,&Viewport)  main.rs:710      -> renderColorImage
+    the whole two-viewport frame of a scene script (main.rs:1533-1628) -> render_frame / Context.render_async
+
+Errors surface as abi.RtmError (the reference panics).  There is no CPU
+fallback: every call goes through librtm.so.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import abi
+from .scenes import EnumFace, REFERENCE_MARCH_STEPS, REFERENCE_PATCH, Camera, Scene  # noqa: F401
+
+
+def _lib():
+    return abi.load_library()
+
+
+def device_count() -> int:
+    return int(_lib().rtm_device_count())
+
+
+class Context:
+    """One device: stream, shadow map, events (rtm_ctx)."""
+
+    def __init__(self, device: int = 0):
+        self.device = device
+        self._h = C.c_void_p()
+        lib = _lib()
+        abi.check(lib, lib.rtm_ctx_create(device, C.byref(self._h)), "rtm_ctx_create")
+
+    @property
+    def handle(self):
+        return self._h
+
+    @property
+    def stream(self) -> int:
+        return _lib().rtm_ctx_stream(self._h) or 0
+
+    def synchronize(self):
+        lib = _lib()
+        abi.check(lib, lib.rtm_ctx_synchronize(self._h), "rtm_ctx_synchronize")
+
+    def last_kernel_ms(self):
+        s, e = C.c_float(), C.c_float()
+        lib = _lib()
+        abi.check(lib, lib.rtm_ctx_last_kernel_ms(self._h, C.byref(s), C.byref(e)), "rtm_ctx_last_kernel_ms")
+        return float(s.value), float(e.value)
+
+    def set_timing_capacity(self, n: int):
+        lib = _lib()
+        abi.check(lib, lib.rtm_ctx_set_timing_capacity(self._h, n), "rtm_ctx_set_timing_capacity")
+
+    def kernel_ms_history(self, n: int):
+        """Per-render (shadow_pass_ms, eye_pass_ms) from HIP events, oldest first."""
+        sm = (C.c_float * max(n, 1))()
+        em = (C.c_float * max(n, 1))()
+        cnt = C.c_int32()
+        lib = _lib()
+        abi.check(lib, lib.rtm_ctx_kernel_ms_history(self._h, sm, em, n, C.byref(cnt)), "rtm_ctx_kernel_ms_history")
+        return [float(v) for v in sm[:cnt.value]], [float(v) for v in em[:cnt.value]]
+
+    def render_async(self, scene: Scene, eye: Camera, shadow: Camera, width: int, height: int,
+                     steps: int, flags: int, out_ptr: int, row_begin: int = 0, row_end: int | None = None):
+        """Enqueue one frame; out_ptr is a device pointer (e.g. tensor.data_ptr())
+        to (row_end-row_begin)*width*4 floats."""
+        row_end = height if row_end is None else row_end
+        sc, keep = scene.to_c()
+        e, s = eye.to_c(), shadow.to_c()
+        lib = _lib()
+        abi.check(lib, lib.rtm_render_async(self._h, C.byref(sc), C.byref(e), C.byref(s), width, height,
+                                            steps, flags, row_begin, row_end, C.c_void_p(out_ptr)),
+                  "rtm_render_async")
+
+    def shadow_map_ptr(self) -> int:
+        return _lib().rtm_ctx_shadow_map(self._h) or 0
+
+    def stats(self, scene: Scene, eye: Camera, shadow: Camera, width: int, height: int, steps: int,
+              flags: int = 0) -> dict:
+        sc, keep = scene.to_c()
+        e, s = eye.to_c(), shadow.to_c()
+        st = abi.rtm_stats()
+        lib = _lib()
+        abi.check(lib, lib.rtm_render_stats(self._h, C.byref(sc), C.byref(e), C.byref(s), width, height,
+                                            steps, flags, C.byref(st)), "rtm_render_stats")
+        return st.as_dict()
+
+    def close(self):
+        if self._h:
+            _lib().rtm_ctx_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def render_frame(scene: Scene, eye: Camera, shadow: Camera, width: int, height: int, steps: int,
+                 flags: int = 0) -> np.ndarray:
+    """rtm_render: the full frame into host memory, (height, width, 4) f32."""
+    out = np.empty((height, width, 4), np.float32)
+    sc, keep = scene.to_c()
+    e, s = eye.to_c(), shadow.to_c()
+    lib = _lib()
+    abi.check(lib, lib.rtm_render(C.byref(sc), C.byref(e), C.byref(s), width, height, steps, flags,
+                                  out.ctypes.data_as(C.POINTER(C.c_float))), "rtm_render")
+    return out
+
+
+class Viewport:
+    """Reference Viewport (main.rs:426-439) with device-resident zBuffer / G-buffer."""
+
+    def __init__(self, ctx: Context, width: int, height: int, face: int, camera: Camera):
+        self.ctx, self.width, self.height, self.face, self.camera = ctx, width, height, face, camera
+        self._h = C.c_void_p()
+        c = camera.to_c()
+        lib = _lib()
+        abi.check(lib, lib.rtm_viewport_create(ctx.handle, width, height, face, C.byref(c), C.byref(self._h)),
+                  "rtm_viewport_create")
+
+    def rasterize(self, scene: Scene):  # main.rs:445
+        sc, keep = scene.to_c()
+        lib = _lib()
+        abi.check(lib, lib.rtm_viewport_rasterize(self._h, C.byref(sc)), "rtm_viewport_rasterize")
+
+    def processRaymarchingRays(self, patches=(REFERENCE_PATCH,), steps: int = REFERENCE_MARCH_STEPS):  # main.rs:551
+        arr = (abi.rtm_patch * max(len(patches), 1))()
+        for i, p in enumerate(patches):
+            arr[i].a0, arr[i].b0, arr[i].a1, arr[i].b1 = p._0.a, p._0.b, p._1.a, p._1.b
+        lib = _lib()
+        abi.check(lib, lib.rtm_viewport_process_raymarching_rays(self._h, arr, len(patches), steps),
+                  "rtm_viewport_process_raymarching_rays")
+
+    def zBuffer(self) -> np.ndarray:
+        out = np.empty((self.height, self.width), np.float64)
+        lib = _lib()
+        abi.check(lib, lib.rtm_viewport_read_zbuffer(self._h, out.ctypes.data_as(C.POINTER(C.c_double))),
+                  "rtm_viewport_read_zbuffer")
+        return out
+
+    def close(self):
+        if self._h:
+            _lib().rtm_viewport_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def renderColorImage(scene: Scene, viewport: Viewport, viewportShadowmapping: Viewport) -> np.ndarray:
+    """main.rs:710 — returns the (height, width, 4) f32 image (Color32 + alpha 1)."""
+    out = np.empty((viewport.height, viewport.width, 4), np.float32)
+    sc, keep = scene.to_c()
+    lib = _lib()
+    abi.check(lib, lib.rtm_render_color_image(C.byref(sc), viewport._h, viewportShadowmapping._h,
+                                              out.ctypes.data_as(C.POINTER(C.c_float))),
+              "rtm_render_color_image")
+    return out

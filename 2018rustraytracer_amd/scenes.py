@@ -1,0 +1,176 @@
+"""Scene description (reference main.rs:334-422) and the reference's test scenes.
+
+Plain-Python mirror of the reference's scene types so host code reads like the
+reference's scene scripts (testscene_*, main.rs:910-1633).  Trigonometry for
+animated spheres is evaluated here on the host (libm, as Rust's f64::sin/cos
+are on Linux) and passed to the device as data.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+from dataclasses import dataclass, field
+from typing import List
+
+from . import abi
+
+
+@dataclass
+class Shading:  # main.rs:336-340
+    colorR: float
+    colorG: float
+    colorB: float
+
+
+@dataclass
+class PrimitiveSphere:  # main.rs:343-349
+    id: int
+    shading: Shading
+    pos: tuple
+    r: float
+
+
+@dataclass
+class Linear:  # main.rs:2134-2137
+    a: float
+    b: float
+
+
+@dataclass
+class Bilinear:  # main.rs:2139-2142
+    _0: Linear
+    _1: Linear
+
+
+# rayEntry_ShadowRay_testing's hard-coded patch and step count (main.rs:2024-2031)
+REFERENCE_PATCH = Bilinear(Linear(0.1, 0.1), Linear(0.1, 0.1))
+REFERENCE_MARCH_STEPS = 500
+
+ORTHOGONAL = abi.RTM_CAMERA_ORTHOGONAL
+PERSPECTIVE = abi.RTM_CAMERA_PERSPECTIVE
+
+
+class EnumFace:  # main.rs:225-228
+    FRONT = abi.RTM_FACE_FRONT
+    BACK = abi.RTM_FACE_BACK
+
+
+@dataclass
+class Camera:  # main.rs:1887-1898 (resolution comes from the viewport)
+    type_: int
+    position: tuple
+    dirNormalized: tuple
+    upNormalized: tuple
+    sideNormalized: tuple
+
+    def to_c(self) -> abi.rtm_camera:
+        c = abi.rtm_camera()
+        c.type = self.type_
+        c.pos[:] = [float(v) for v in self.position]
+        c.dir[:] = [float(v) for v in self.dirNormalized]
+        c.up[:] = [float(v) for v in self.upNormalized]
+        c.side[:] = [float(v) for v in self.sideNormalized]
+        return c
+
+
+@dataclass
+class Scene:  # main.rs:404-410 (spheres + implicit patches: the hot path's primitives)
+    spherePrimitives: List[PrimitiveSphere] = field(default_factory=list)
+    patches: List[Bilinear] = field(default_factory=list)
+
+    def to_c(self):
+        """Returns (rtm_scene, keepalive) — keep the second value alive while
+        the first is in use."""
+        ns, npch = len(self.spherePrimitives), len(self.patches)
+        sph = (abi.rtm_sphere * max(ns, 1))()
+        for i, s in enumerate(self.spherePrimitives):
+            sph[i].id = int(s.id)
+            sph[i].pos[:] = [float(v) for v in s.pos]
+            sph[i].r = float(s.r)
+            sph[i].color[:] = [float(s.shading.colorR), float(s.shading.colorG), float(s.shading.colorB)]
+        pat = (abi.rtm_patch * max(npch, 1))()
+        for i, p in enumerate(self.patches):
+            pat[i].a0, pat[i].b0 = float(p._0.a), float(p._0.b)
+            pat[i].a1, pat[i].b1 = float(p._1.a), float(p._1.b)
+        sc = abi.rtm_scene()
+        sc.spheres = C.cast(sph, C.POINTER(abi.rtm_sphere))
+        sc.patches = C.cast(pat, C.POINTER(abi.rtm_patch))
+        sc.n_spheres = ns
+        sc.n_patches = npch
+        return sc, (sph, pat)
+
+
+# ---- cameras of the orthographic test scenes ----
+def shadow_camera() -> Camera:
+    """Shadow-map camera: the sun shines along +z (main.rs:1552-1563)."""
+    return Camera(ORTHOGONAL, (0.0, 0.0, 0.0), (0.0, 0.0, 1.0), (0.0, 1.0, 0.0), (1.0, 0.0, 0.0))
+
+
+def eye_camera() -> Camera:
+    """Eye camera at (-1,0,0) looking along +x (main.rs:1598-1609)."""
+    return Camera(ORTHOGONAL, (-1.0, 0.0, 0.0), (1.0, 0.0, 0.0), (0.0, 1.0, 0.0), (0.0, 0.0, 1.0))
+
+
+# ---- scenes ----
+def closely_orbiting_sphere(frame: int, patches=None) -> Scene:
+    """testscene_closelyOrbitingSphere frame `frame` (main.rs:1468-1522).
+    Default patches: the reference's hard-coded one (Scene A-ref)."""
+    f = float(frame)
+    spheres = [
+        PrimitiveSphere(0, Shading(0.02, 0.02, 1.0), (0.0, 0.0, 0.5), 0.2),
+        PrimitiveSphere(1, Shading(0.02, 0.02, 1.0), (0.0, 0.0, 0.5 + 0.2 * 2.0), 0.2),
+        PrimitiveSphere(2, Shading(0.9, 0.2, 0.2),
+                        (-0.0, math.sin(f * 0.025) * 0.7, math.cos(f * 0.025) * 0.7), 0.1),
+    ]
+    return Scene(spheres, list(patches) if patches is not None else [REFERENCE_PATCH])
+
+
+BENCH_PATCH = Bilinear(Linear(0.3, 2.1), Linear(0.9, 2.7))  # SURVEY.md §8d-2 Scene A-bench
+SCENE_B_PATCH2 = Bilinear(Linear(0.5, 1.5), Linear(1.2, 3.3))
+
+
+def scene_a_bench(frame: int = 100) -> Scene:
+    """Scene A-bench: frame 100 with a tilted patch so texels cross at 10..90
+    steps and the march bound K actually limits work."""
+    return closely_orbiting_sphere(frame, [BENCH_PATCH])
+
+
+_COLORS_B = [(0.02, 0.02, 1.0), (0.9, 0.2, 0.2), (0.2, 0.9, 0.2), (0.9, 0.9, 0.2)]
+
+
+def scene_b() -> Scene:
+    """Scene B: 16 spheres + 2 implicit patches (BASELINE config 5)."""
+    spheres = []
+    for i in range(16):
+        a = 2.0 * math.pi * i / 16.0
+        spheres.append(PrimitiveSphere(
+            i, Shading(*_COLORS_B[i % 4]),
+            (-0.5 + 0.0625 * i, 0.6 * math.sin(a), 0.6 + 0.6 * math.cos(a)),
+            0.08 + 0.01 * (i % 4)))
+    return Scene(spheres, [BENCH_PATCH, SCENE_B_PATCH2])
+
+
+def overlapping_spheres() -> Scene:
+    """testscene_overlappingSpheres (main.rs:1322-1458): two spheres, shadow pass
+    commented out (render with RTM_FLAG_NO_MARCH | RTM_FLAG_NO_SHADOW_RASTER)."""
+    return Scene([
+        PrimitiveSphere(0, Shading(0.02, 0.02, 1.0), (0.0, 0.0, 0.0), 0.5),
+        PrimitiveSphere(1, Shading(1.0, 1.0, 1.0), (0.0, 0.0, 0.5), 0.5),
+    ], [])
+
+
+OVERLAPPING_FLAGS = abi.RTM_FLAG_NO_MARCH | abi.RTM_FLAG_NO_SHADOW_RASTER
+
+# BASELINE.json configs -> (width, height, march_steps, scene factory, flags)
+CONFIGS = {
+    1: dict(width=256, height=256, steps=0, scene=lambda: closely_orbiting_sphere(100),
+            flags=abi.RTM_FLAG_NO_MARCH, desc="256x256, 3 spheres, no ray-march (CPU plumbing)"),
+    2: dict(width=1920, height=1080, steps=32, scene=scene_a_bench, flags=0,
+            desc="1920x1080, 3 spheres + 1 implicit, 32 march steps"),
+    3: dict(width=3840, height=2160, steps=64, scene=scene_a_bench, flags=0,
+            desc="3840x2160, 3 spheres + 1 implicit, 64 march steps"),
+    4: dict(width=7680, height=4320, steps=64, scene=scene_a_bench, flags=0,
+            desc="7680x4320, 3 spheres + 1 implicit, 64 march steps"),
+    5: dict(width=7680, height=4320, steps=128, scene=scene_b, flags=0,
+            desc="7680x4320, 16 spheres + 2 implicits, 128 march steps"),
+}

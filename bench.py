@@ -1,0 +1,216 @@
+#!/usr/bin/env python3
+"""Benchmark: Mpixels/s of the full two-pass frame (shadow viewport rasterize +
+march, eye viewport rasterize + shade) at BASELINE config 3 — 3840x2160,
+3 spheres + 1 implicit patch, 64 march steps.
+
+One process per GPU (torch.distributed.run); prints ONE JSON line on rank 0.
+
+Modes (--mode):
+  frames       (default) frame-parallel: rank r renders animation frames
+               r, r+N, ... of the orbiting-sphere sequence; each frame is
+               independent, no data-path collective ("scaling": "weak").
+  tile-gather  one frame per step, rows split into N bands, each rank renders
+               its band, then ONE RCCL gather assembles the RGBA f32 frame on
+               rank 0 ("scaling": "strong").
+"""
+from __future__ import annotations
+
+import argparse
+import glob
+import importlib
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "Mpixels/s at 3840×2160, 64 march steps; 1/2/4/8-GPU scaling"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--config", type=int, default=3)
+    ap.add_argument("--mode", choices=["frames", "tile-gather"], default="frames")
+    ap.add_argument("--fused", action="store_true", help="evaluate shadow texels on demand (same image)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=1)
+    return ap.parse_args()
+
+
+def _latest_traffic(cfg_id: int, kernel: str):
+    """HBM bytes per launch from the newest committed PMC summary (tools/profile.sh)."""
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")))
+    for f in reversed(files):
+        try:
+            d = json.load(open(f))
+        except Exception:
+            continue
+        if d.get("config") == cfg_id and kernel in d.get("kernels", {}):
+            return d["kernels"][kernel].get("hbm_bytes_per_launch")
+    return None
+
+
+def cpu_baseline(scene, eye, shadow, w, h, k, flags, threads):
+    """The CPU oracle (f64 C restatement of main.rs) on the host cores, rank 0 only."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle  # checker / CPU baseline only
+
+    oracle.lib()
+    best = None
+    for _ in range(2):
+        t0 = time.perf_counter()
+        oracle.render(scene, eye, shadow, w, h, k, flags, nthreads=threads)
+        dt = time.perf_counter() - t0
+        best = dt if best is None else min(best, dt)
+    return dict(value=round(w * h / best / 1e6, 3), unit="Mpixels/s", cores=threads, kind="port",
+                sample=f"full {w}x{h} frame, K={k}, Scene A-bench frame 100, best of 2, {threads} thread(s)",
+                seconds_per_frame=round(best, 3))
+
+
+def main():
+    a = parse()
+    import torch
+    import torch.distributed as dist
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    rtm = importlib.import_module("2018rustraytracer_amd")
+    sc = importlib.import_module("2018rustraytracer_amd.scenes")
+    metrics = importlib.import_module("2018rustraytracer_amd.metrics")
+    cfg = sc.CONFIGS[a.config]
+    W, H, K = cfg["width"], cfg["height"], cfg["steps"]
+    flags = cfg["flags"] | (rtm.abi.RTM_FLAG_FUSED_SHADOW if a.fused else 0)
+    eye, shadow = sc.eye_camera(), sc.shadow_camera()
+    ctx = rtm.Context(local)
+    ctx.set_timing_capacity(a.steps)
+
+    def scene_for(frame_index: int):
+        if a.config == 5:
+            return sc.scene_b()
+        if a.config == 1:
+            return sc.closely_orbiting_sphere(100 + frame_index)
+        return sc.scene_a_bench(100 + frame_index)
+
+    total = a.warmup + a.steps
+    if a.mode == "frames":
+        # inputs prepared before the timed region: one scene per frame this rank renders
+        scenes = [scene_for(i * world + rank) for i in range(total)]
+        c_scenes = [s.to_c() for s in scenes]
+        out = torch.empty((H, W, 4), dtype=torch.float32, device=f"cuda:{local}")
+        rows = (0, H)
+    else:
+        band = (H + world - 1) // world
+        r0, r1 = min(H, rank * band), min(H, (rank + 1) * band)
+        rows = (r0, r1)
+        scenes = [scene_for(i) for i in range(total)]
+        c_scenes = [s.to_c() for s in scenes]
+        bufs = [torch.zeros((band, W, 4), dtype=torch.float32, device=f"cuda:{local}") for _ in range(2)]
+        gathered = ([torch.empty((band, W, 4), dtype=torch.float32, device=f"cuda:{local}")
+                     for _ in range(world)] if rank == 0 else None)
+        ext = torch.cuda.ExternalStream(ctx.stream, device=torch.device("cuda", local))
+
+    lib = rtm.load_library()
+    import ctypes as C
+    e_c, s_c = eye.to_c(), shadow.to_c()
+    pending = [None, None]
+
+    def step(i: int):
+        sc_c = c_scenes[i][0]
+        if a.mode == "frames":
+            rc = lib.rtm_render_async(ctx.handle, C.byref(sc_c), C.byref(e_c), C.byref(s_c), W, H, K, flags,
+                                      0, H, C.c_void_p(out.data_ptr()))
+            rtm.abi.check(lib, rc, "rtm_render_async")
+            return
+        b = i % 2
+        with torch.cuda.stream(ext):
+            if pending[b] is not None:
+                pending[b].wait()  # the ctx stream waits until the gather reading bufs[b] is done
+            if rows[1] > rows[0]:
+                rc = lib.rtm_render_async(ctx.handle, C.byref(sc_c), C.byref(e_c), C.byref(s_c), W, H, K,
+                                          flags, rows[0], rows[1], C.c_void_p(bufs[b].data_ptr()))
+                rtm.abi.check(lib, rc, "rtm_render_async")
+            if world > 1:
+                pending[b] = dist.gather(bufs[b], gathered, dst=0, async_op=True)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    for i in range(a.warmup):
+        step(i)
+    barrier()
+    t0 = time.perf_counter()
+    for i in range(a.warmup, total):
+        step(i)
+    for p in pending:
+        if p is not None:
+            p.wait()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # per-kernel HIP-event durations over the timed region (ctx stream)
+    sh_ms, eye_ms = ctx.kernel_ms_history(a.steps)
+    if rows[1] <= rows[0]:
+        sh_ms, eye_ms = [0.0], [0.0]
+    avg_sh = sum(sh_ms) / max(len(sh_ms), 1)
+    avg_eye = sum(eye_ms) / max(len(eye_ms), 1)
+
+    if rank == 0:
+        pixels = W * H * a.steps * (world if a.mode == "frames" else 1)
+        value = pixels / elapsed / 1e6
+        s0 = scenes[a.warmup]
+        band_h = rows[1] - rows[0]
+        st = ctx.stats(s0, eye, shadow, W, H, K, flags)
+        work = metrics.frame_work(st, W, H, len(s0.spherePrimitives), len(s0.patches), flags, fused=a.fused)
+        dom = "eye_pass" if (a.fused or avg_eye >= avg_sh) else "shadow_pass"
+        dom_ms = avg_eye if dom == "eye_pass" else avg_sh
+        roof = metrics.roofline(dom, work, dom_ms, _latest_traffic(a.config, dom))
+        res = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "Mpixels/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(elapsed / a.steps * 1e3, 5),
+            "higher_is_better": True,
+            "scaling": "weak" if a.mode == "frames" else "strong",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic: Scene A-bench (SURVEY.md §8d-2) animation frames 100+i, f64 scene built on host"
+                    if a.config in (2, 3, 4) else "synthetic: SURVEY.md §8d-2 scene",
+            "config": {"workload": cfg["desc"], "config_id": a.config, "width": W, "height": H,
+                       "march_steps": K, "mode": a.mode, "shadow": "fused" if a.fused else "two-pass",
+                       "parallelism": (f"frame-parallel x{world}" if a.mode == "frames"
+                                       else f"row-bands x{world} + rccl gather"),
+                       "rows_rank0": band_h},
+            "kernels": {"shadow_pass_ms": round(avg_sh, 5), "eye_pass_ms": round(avg_eye, 5),
+                        "frame_kernel_ms": round(avg_sh + avg_eye, 5)},
+            "roofline": roof,
+            "parity": "bit-exact vs CPU oracle (tests/test_gpu_parity.py)",
+        }
+        if world == 1 and not a.no_cpu_baseline:
+            res["cpu_baseline"] = cpu_baseline(s0, eye, shadow, W, H, K, flags, a.cpu_threads)
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()

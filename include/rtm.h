@@ -1,0 +1,194 @@
+/*
+ * rtm.h — C ABI of the MI355X-native ray-trace / ray-march renderer ("rtm").
+ *
+ * Drop-in boundary for the CPU render loop of PtrMan/2018RustRayTracer
+ * (reference: src/main.rs).  The reference has no FFI; the seams this ABI
+ * replaces are the three Rust calls its scene drivers make
+ * (testscene_closelyOrbitingSphere, main.rs:1568-1628):
+ *
+ *   Viewport::rasterize(&mut self, &Scene)              main.rs:445-547
+ *   Viewport::processRaymarchingRays(&mut self)         main.rs:551-565
+ *   renderColorImage(&Scene, &Viewport, &Viewport)      main.rs:710-902
+ *
+ * Two API levels:
+ *   1. rtm_render / rtm_render_async — the whole two-viewport frame
+ *      (shadow viewport rasterize + march, eye viewport rasterize + shade) in
+ *      two HIP kernels; output RGBA f32.
+ *   2. rtm_viewport_* / rtm_render_color_image — one call per reference seam,
+ *      for callers that drive the passes themselves as the reference does.
+ *
+ * Conventions
+ *   - All geometry is IEEE f64 (reference Vec3 is f64, main.rs:59-63); the
+ *     framebuffer is RGBA f32 row-major, index y*width+x (Map2d, main.rs:2351-2373;
+ *     Color32 main.rs:647-651; alpha is always 1.0).
+ *   - Every entry point returns 0 (RTM_OK) or a negative RTM_ERR_* code; no
+ *     exceptions or aborts cross the ABI (the reference panics instead,
+ *     main.rs:700, 1949).  rtm_last_error() gives a thread-local message.
+ *   - The caller owns every pointer it passes.  Host-pointer calls block until
+ *     the output is written.  A context is not reentrant.
+ *   - The 512x512 resolution the reference hard-codes (main.rs:306-307, 553-554,
+ *     711-716, 840-841) is generalised to width x height for both viewports;
+ *     at 512x512 the output is the reference's.
+ */
+#ifndef RTM_H
+#define RTM_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RTM_ABI_VERSION 1
+
+/* ---- limits: scene constants travel as kernel arguments (SGPR path) ---- */
+#define RTM_MAX_SPHERES 16
+#define RTM_MAX_PATCHES 4
+#define RTM_MAX_DIM 32768
+
+/* ---- status codes ---- */
+#define RTM_OK 0
+#define RTM_ERR_INVALID -1     /* bad argument (null, size, id out of range, ...) */
+#define RTM_ERR_UNSUPPORTED -2 /* valid in the reference but not on this path (perspective rasterize) */
+#define RTM_ERR_HIP -3         /* a HIP runtime call failed */
+#define RTM_ERR_NO_DEVICE -4   /* no usable gfx950 device */
+#define RTM_ERR_OOM -5         /* device allocation failed */
+
+/* ---- enums (values mirror the reference's enum order) ---- */
+#define RTM_CAMERA_ORTHOGONAL 0 /* EnumCameraType::ORTHOGONAL main.rs:1882 */
+#define RTM_CAMERA_PERSPECTIVE 1 /* EnumCameraType::PERSPECTIVE main.rs:1883 */
+#define RTM_FACE_FRONT 0 /* EnumFace::FRONT main.rs:226 */
+#define RTM_FACE_BACK 1  /* EnumFace::BACK  main.rs:227 */
+
+/* ---- render flags ---- */
+#define RTM_FLAG_NO_MARCH 0x1         /* skip processRaymarchingRays (BASELINE config 1; scenes whose
+                                         shadow pass is commented out, main.rs:1399-1403) */
+#define RTM_FLAG_NO_SHADOW_RASTER 0x2 /* skip the shadow viewport's sphere rasterize (main.rs:1400) */
+#define RTM_FLAG_FUSED_SHADOW 0x4     /* evaluate each shadow texel on demand inside the eye pass
+                                         instead of materialising the shadow map; same image bits */
+
+/* PrimitiveSphere (main.rs:343-349) + Shading (main.rs:336-340). 64 bytes. */
+typedef struct rtm_sphere {
+    int64_t id;      /* must be a valid index into the sphere array (the reference indexes
+                        scene.spherePrimitives[id], main.rs:158, 748) */
+    double pos[3];   /* Point */
+    double r;        /* radius */
+    double color[3]; /* colorR, colorG, colorB */
+} rtm_sphere;
+
+/* Bilinear{_0: Linear{a,b}, _1: Linear{a,b}} (main.rs:2134-2142): the implicit
+ * surface f(p) = p.z - bilinear(p.xy) marched by raymarchPatch (main.rs:2219). */
+typedef struct rtm_patch {
+    double a0, b0; /* _0 */
+    double a1, b1; /* _1 */
+} rtm_patch;
+
+/* Camera (main.rs:1887-1898).  resolutionX/Y come from the viewport size. */
+typedef struct rtm_camera {
+    int32_t type; /* RTM_CAMERA_* */
+    int32_t reserved;
+    double pos[3];  /* position */
+    double dir[3];  /* dirNormalized */
+    double up[3];   /* upNormalized */
+    double side[3]; /* sideNormalized */
+} rtm_camera;
+
+/* Scene (main.rs:404-410) restricted to the hot path: spheres + implicit patches.
+ * The reference marches one hard-coded patch (main.rs:2024-2031); n_patches
+ * patches are marched in order, each with a strict-min depth update (main.rs:559). */
+typedef struct rtm_scene {
+    const rtm_sphere* spheres;
+    const rtm_patch* patches;
+    int32_t n_spheres;
+    int32_t n_patches;
+} rtm_scene;
+
+/* Per-call statistics (filled by rtm_render_stats on the GPU). */
+typedef struct rtm_stats {
+    int64_t eye_hits[RTM_MAX_SPHERES]; /* eye pixels whose front surface is sphere i */
+    int64_t eye_hit_pixels;            /* pixels with any hit */
+    int64_t lit_pixels;                /* hit pixels that pass the shadow test */
+    int64_t eye_sphere_tests;          /* (pixel, sphere) pairs with d < 1 in the eye pass */
+    int64_t shadow_sphere_tests;       /* (texel, sphere) pairs with d < 1 in the shadow pass */
+    int64_t march_iterations;          /* loop iterations executed by raymarchPatch, all texels/patches */
+    int64_t march_hits;                /* texels*patches where the march returned Some(t) */
+    int64_t march_in_range;            /* texels*patches whose start is inside the [0,1]^2 domain */
+} rtm_stats;
+
+/* ---- library ---- */
+int32_t rtm_abi_version(void);
+const char* rtm_last_error(void);
+/* number of visible HIP devices (0 when none); never fails */
+int32_t rtm_device_count(void);
+
+/* ---- context (one per device; owns the stream, the shadow map and events) ---- */
+typedef struct rtm_ctx rtm_ctx;
+int rtm_ctx_create(int32_t device, rtm_ctx** out);
+void rtm_ctx_destroy(rtm_ctx* ctx);
+/* hipStream_t the context enqueues on (as void*) */
+void* rtm_ctx_stream(rtm_ctx* ctx);
+int rtm_ctx_synchronize(rtm_ctx* ctx);
+/* Durations in ms of the last render's two kernels, from HIP events recorded on
+ * the context stream around each launch (valid after rtm_ctx_synchronize). */
+int rtm_ctx_last_kernel_ms(rtm_ctx* ctx, float* shadow_pass_ms, float* eye_pass_ms);
+/* Keep HIP events for the last `capacity` renders (0 disables; default 1).  After
+ * rtm_ctx_synchronize, rtm_ctx_kernel_ms_history writes up to `max` per-render
+ * durations, oldest first, and the number written to *count. */
+int rtm_ctx_set_timing_capacity(rtm_ctx* ctx, int32_t capacity);
+int rtm_ctx_kernel_ms_history(rtm_ctx* ctx, float* shadow_pass_ms, float* eye_pass_ms, int32_t max,
+                              int32_t* count);
+
+/* ---- whole frame, host output (blocking) ----
+ * Equivalent of: shadow viewport (ORTHO, face BACK, zBuffer=+INF) rasterize +
+ * processRaymarchingRays; eye viewport (face FRONT) rasterize; renderColorImage
+ * (main.rs:1568-1628).  out_rgba: width*height*4 floats. Uses a per-thread
+ * default context on device 0. */
+int rtm_render(const rtm_scene* scene, const rtm_camera* eye, const rtm_camera* shadow,
+               int32_t width, int32_t height, int32_t march_steps, int32_t flags,
+               float* out_rgba);
+
+/* ---- whole frame, device output (asynchronous on ctx's stream) ----
+ * Renders eye rows [row_begin, row_end) into out_rgba_dev (device memory,
+ * (row_end-row_begin)*width*4 floats, row-major, row 0 = row_begin).  The
+ * shadow map is full size unless RTM_FLAG_FUSED_SHADOW. */
+int rtm_render_async(rtm_ctx* ctx, const rtm_scene* scene, const rtm_camera* eye,
+                     const rtm_camera* shadow, int32_t width, int32_t height,
+                     int32_t march_steps, int32_t flags, int32_t row_begin, int32_t row_end,
+                     float* out_rgba_dev);
+/* Device pointer of the context's shadow map (width*height f64) after a
+ * non-fused render (NULL before the first one). */
+const double* rtm_ctx_shadow_map(rtm_ctx* ctx);
+
+/* Counting variant of the frame (separate, untimed kernels): the per-pass
+ * work counts behind the roofline's algorithmic flop count. */
+int rtm_render_stats(rtm_ctx* ctx, const rtm_scene* scene, const rtm_camera* eye,
+                     const rtm_camera* shadow, int32_t width, int32_t height,
+                     int32_t march_steps, int32_t flags, rtm_stats* out);
+
+/* ---- reference-seam API (one call per reference function) ---- */
+typedef struct rtm_viewport rtm_viewport;
+/* Viewport{rasterized: vec![None; w*h], zBuffer: +INF, face, camera} (main.rs:426-439, 951-983) */
+int rtm_viewport_create(rtm_ctx* ctx, int32_t width, int32_t height, int32_t face,
+                        const rtm_camera* camera, rtm_viewport** out);
+void rtm_viewport_destroy(rtm_viewport* vp);
+/* Viewport::rasterize (main.rs:445): ORTHOGONAL cameras only (perspective
+ * projection is BASELINE "next" row f-3 -> RTM_ERR_UNSUPPORTED). */
+int rtm_viewport_rasterize(rtm_viewport* vp, const rtm_scene* scene);
+/* Viewport::processRaymarchingRays (main.rs:551) generalised: the reference's
+ * hard-coded patch {0.1,0.1,0.1,0.1} and 500 steps (main.rs:2024-2031) become
+ * arguments; patches are marched in order. */
+int rtm_viewport_process_raymarching_rays(rtm_viewport* vp, const rtm_patch* patches,
+                                          int32_t n_patches, int32_t steps);
+/* renderColorImage (main.rs:710): viewport and shadow viewport must share a
+ * context; the shadow camera must be ORTHOGONAL (Camera::project asserts it,
+ * main.rs:1949).  out_rgba: host, vp width*height*4 floats. */
+int rtm_render_color_image(const rtm_scene* scene, const rtm_viewport* vp,
+                           const rtm_viewport* shadow_vp, float* out_rgba);
+/* Copy the viewport's zBuffer (width*height f64) to host memory. */
+int rtm_viewport_read_zbuffer(const rtm_viewport* vp, double* out);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* RTM_H */

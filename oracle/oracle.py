@@ -1,0 +1,141 @@
+"""ctypes wrapper of the CPU ORACLE (oracle/librtm_oracle.so).
+
+TEST INFRASTRUCTURE ONLY — imported by tests/, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg, never by the product package.  See rtm_oracle.c.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import importlib
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "librtm_oracle.so")
+RTMO_FLAG_REF_BBOX = 0x100
+
+_abi = importlib.import_module("2018rustraytracer_amd.abi")
+_lib = None
+
+
+def build() -> str:
+    subprocess.run(["make", "-C", HERE, "-s"], check=True)
+    return LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = C.CDLL(LIB_PATH)
+        P = C.c_void_p
+        I = C.c_int32
+        L.rtmo_render.restype = C.c_int
+        L.rtmo_render.argtypes = [C.POINTER(_abi.rtm_scene), C.POINTER(_abi.rtm_camera),
+                                  C.POINTER(_abi.rtm_camera), I, I, I, I, I,
+                                  C.POINTER(C.c_float), C.POINTER(C.c_double),
+                                  C.POINTER(_abi.rtm_stats)]
+        L.rtmo_viewport_create.restype = C.c_int
+        L.rtmo_viewport_create.argtypes = [I, I, I, C.POINTER(_abi.rtm_camera), C.POINTER(P)]
+        L.rtmo_viewport_destroy.restype = None
+        L.rtmo_viewport_destroy.argtypes = [P]
+        L.rtmo_viewport_rasterize.restype = C.c_int
+        L.rtmo_viewport_rasterize.argtypes = [P, C.POINTER(_abi.rtm_scene), I]
+        L.rtmo_viewport_process_raymarching_rays.restype = C.c_int
+        L.rtmo_viewport_process_raymarching_rays.argtypes = [P, C.POINTER(_abi.rtm_patch), I, I]
+        L.rtmo_render_color_image.restype = C.c_int
+        L.rtmo_render_color_image.argtypes = [C.POINTER(_abi.rtm_scene), P, P, C.POINTER(C.c_float)]
+        L.rtmo_viewport_read_zbuffer.restype = C.c_int
+        L.rtmo_viewport_read_zbuffer.argtypes = [P, C.POINTER(C.c_double)]
+        L.rtmo_calc_ray_plane.restype = C.c_int
+        L.rtmo_calc_ray_plane.argtypes = [C.POINTER(C.c_double)] * 4 + [C.POINTER(C.c_double)]
+        L.rtmo_encode_rgb8.restype = None
+        L.rtmo_encode_rgb8.argtypes = [C.POINTER(C.c_float), C.c_int64, C.POINTER(C.c_int64)]
+        _lib = L
+    return _lib
+
+
+def _fp(a, ct):
+    return a.ctypes.data_as(C.POINTER(ct))
+
+
+def render(scene, eye, shadow, width, height, steps, flags=0, nthreads=1, want_shadow=False,
+           want_stats=False):
+    """Oracle frame.  scene: scenes.Scene; eye/shadow: scenes.Camera.
+    Returns dict(rgba=(H,W,4) f32, shadow=(H,W) f64 | None, stats=dict | None)."""
+    L = lib()
+    sc, keep = scene.to_c()
+    ec, sc_cam = eye.to_c(), shadow.to_c()
+    out = np.empty((height, width, 4), np.float32)
+    sh = np.empty((height, width), np.float64) if want_shadow else None
+    st = _abi.rtm_stats() if want_stats else None
+    rc = L.rtmo_render(C.byref(sc), C.byref(ec), C.byref(sc_cam), width, height, steps, flags,
+                       nthreads, _fp(out, C.c_float),
+                       _fp(sh, C.c_double) if sh is not None else None,
+                       C.byref(st) if st is not None else None)
+    if rc != 0:
+        raise RuntimeError(f"rtmo_render failed: {rc}")
+    return dict(rgba=out, shadow=sh, stats=st.as_dict() if st is not None else None)
+
+
+class Viewport:
+    """Staged oracle viewport (reference Viewport, main.rs:426-643)."""
+
+    def __init__(self, width, height, face, camera):
+        self.width, self.height = width, height
+        self._h = C.c_void_p()
+        c = camera.to_c()
+        rc = lib().rtmo_viewport_create(width, height, face, C.byref(c), C.byref(self._h))
+        if rc != 0:
+            raise RuntimeError(f"rtmo_viewport_create: {rc}")
+
+    def rasterize(self, scene, flags=0):
+        sc, keep = scene.to_c()
+        rc = lib().rtmo_viewport_rasterize(self._h, C.byref(sc), flags)
+        if rc != 0:
+            raise RuntimeError(f"rtmo_viewport_rasterize: {rc}")
+
+    def processRaymarchingRays(self, patches, steps):
+        arr = (_abi.rtm_patch * max(len(patches), 1))()
+        for i, p in enumerate(patches):
+            arr[i].a0, arr[i].b0, arr[i].a1, arr[i].b1 = p._0.a, p._0.b, p._1.a, p._1.b
+        rc = lib().rtmo_viewport_process_raymarching_rays(self._h, arr, len(patches), steps)
+        if rc != 0:
+            raise RuntimeError(f"rtmo_viewport_process_raymarching_rays: {rc}")
+
+    def zbuffer(self):
+        out = np.empty((self.height, self.width), np.float64)
+        lib().rtmo_viewport_read_zbuffer(self._h, _fp(out, C.c_double))
+        return out
+
+    def __del__(self):
+        if getattr(self, "_h", None) and _lib is not None:
+            _lib.rtmo_viewport_destroy(self._h)
+            self._h = None
+
+
+def render_color_image(scene, vp: Viewport, vps: Viewport):
+    sc, keep = scene.to_c()
+    out = np.empty((vp.height, vp.width, 4), np.float32)
+    rc = lib().rtmo_render_color_image(C.byref(sc), vp._h, vps._h, _fp(out, C.c_float))
+    if rc != 0:
+        raise RuntimeError(f"rtmo_render_color_image: {rc}")
+    return out
+
+
+def calc_ray_plane(origin, direction, plane_n, plane_center):
+    arrs = [(C.c_double * 3)(*v) for v in (origin, direction, plane_n, plane_center)]
+    t = C.c_double()
+    ok = lib().rtmo_calc_ray_plane(*arrs, C.byref(t))
+    return t.value if ok else None
+
+
+def encode_rgb8(rgba):
+    rgba = np.ascontiguousarray(rgba, np.float32)
+    n = rgba.size // 4
+    out = np.empty(n * 3, np.int64)
+    lib().rtmo_encode_rgb8(_fp(rgba, C.c_float), n, _fp(out, C.c_int64))
+    return out.reshape(rgba.shape[:-1] + (3,))

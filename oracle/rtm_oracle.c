@@ -1,0 +1,607 @@
+/*
+ * rtm_oracle.c — CPU ORACLE (test infrastructure only; never shipped, never on
+ * the product path).  Only tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg may load it, and only as the checker / CPU baseline.
+ *
+ * A plain-C f64 restatement of the per-pixel hot path of
+ * PtrMan/2018RustRayTracer src/main.rs, written function by function in the
+ * reference's structure and floating-point operation order (no hoisting, no
+ * FMA contraction: build with -ffp-contract=off -fno-fast-math).  Each
+ * function cites the reference lines it restates.
+ *
+ * Parity status: the reference cannot be built here (Rust toolchain absent;
+ * SURVEY.md §8c-1) and holds no golden vectors for this path (its only tests,
+ * main.rs:2415-2457, cover calcRayPlane / calcRayQuadPlane).  This oracle is
+ * therefore pinned by (a) the independent f64 cross-check values of SURVEY.md
+ * §8c-3 (hit counts, pixel values, sha256 of the 512x512 frames 0 and 100),
+ * (b) an independent pure-Python restatement (tests/golden/gen_golden.py) and
+ * (c) the reference's own calcRayPlane test (main.rs:2415-2425) for the
+ * ray-plane intersector.  See DESIGN.md §Parity.
+ *
+ * Generalisation: the reference's 512 constants become the
+ * viewport width/height; with RTMO_FLAG_REF_BBOX the sphere bounding box of
+ * main.rs:256-300 is applied exactly as written (a pure cull on square images).
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../include/rtm.h"
+
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+#define RTMO_FLAG_REF_BBOX 0x100 /* oracle-only: reference sphere bbox, main.rs:256-300 */
+
+/* ------------------------------------------------------------------ */
+/* L0 math — Vec3 / Vec2 (main.rs:58-115, 2083-2130)                   */
+/* ------------------------------------------------------------------ */
+typedef struct { double x, y, z; } Vec3;
+typedef struct { double x, y; } Vec2;
+
+static Vec3 v3(double x, double y, double z) { Vec3 r = {x, y, z}; return r; }
+/* Add / Sub (main.rs:85-99) */
+static Vec3 v3_add(Vec3 a, Vec3 b) { return v3(a.x + b.x, a.y + b.y, a.z + b.z); }
+static Vec3 v3_sub(Vec3 a, Vec3 b) { return v3(a.x - b.x, a.y - b.y, a.z - b.z); }
+/* Vec3::scale (main.rs:76-78) */
+static Vec3 v3_scale(Vec3 a, double s) { return v3(a.x * s, a.y * s, a.z * s); }
+/* dot (main.rs:101-103): (a.x*b.x + a.y*b.y) + a.z*b.z */
+static double dot(Vec3 a, Vec3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+/* Vec3::magnitude (main.rs:71-73) */
+static double v3_magnitude(Vec3 a) { return sqrt(dot(a, a)); }
+/* normalize (main.rs:105-108) */
+static Vec3 normalize(Vec3 v) { double m = v3_magnitude(v); return v3_scale(v, 1.0 / m); }
+
+static Vec2 v2(double x, double y) { Vec2 r = {x, y}; return r; }
+static Vec2 v2_sub(Vec2 a, Vec2 b) { return v2(a.x - b.x, a.y - b.y); }
+static Vec2 v2_scale(Vec2 a, double s) { return v2(a.x * s, a.y * s); }
+/* Vec2::magnitudeSquared / magnitude / normalized (main.rs:2098-2109) */
+static double v2_magnitude(Vec2 a) { return sqrt(a.x * a.x + a.y * a.y); }
+static Vec2 v2_normalized(Vec2 a) { double m = v2_magnitude(a); return v2_scale(a, 1.0 / m); }
+/* dot2d (main.rs:2128-2130) */
+static double dot2d(Vec2 a, Vec2 b) { return a.x * b.x + a.y * b.y; }
+
+/* Rust f64::signum: +1 for +0/+x/+inf, -1 for -0/-x/-inf, NaN for NaN */
+static double rust_signum(double v) { return isnan(v) ? v : copysign(1.0, v); }
+/* Rust f64::max: NaN-ignoring maximum */
+static double rust_max(double a, double b) { return fmax(a, b); }
+/* Rust `as i64` from f64: truncate toward zero, saturate, NaN -> 0 */
+static int64_t rust_as_i64(double v) {
+    if (isnan(v)) return 0;
+    if (v >= 9223372036854775807.0) return INT64_MAX;
+    if (v <= -9223372036854775808.0) return INT64_MIN;
+    return (int64_t)v;
+}
+/* Rust i64 `+` in a release build wraps */
+static int64_t wrap_add_i64(int64_t a, int64_t b) { return (int64_t)((uint64_t)a + (uint64_t)b); }
+/* f64::powi(32) = compiler-rt __powidf2: repeated squaring (exact op sequence) */
+static double powi(double a, int b) {
+    int recip = b < 0;
+    double r = 1.0;
+    for (;;) {
+        if (b & 1) r *= a;
+        b /= 2;
+        if (b == 0) break;
+        a *= a;
+    }
+    return recip ? 1.0 / r : r;
+}
+
+/* ------------------------------------------------------------------ */
+/* L1 camera (main.rs:1880-2014)                                       */
+/* ------------------------------------------------------------------ */
+typedef struct {
+    int32_t type;
+    Vec3 pos, dir, up, side;
+    int64_t resX, resY;
+} Camera;
+
+static Camera camera_from(const rtm_camera* c, int64_t resX, int64_t resY) {
+    Camera k;
+    k.type = c->type;
+    k.pos = v3(c->pos[0], c->pos[1], c->pos[2]);
+    k.dir = v3(c->dir[0], c->dir[1], c->dir[2]);
+    k.up = v3(c->up[0], c->up[1], c->up[2]);
+    k.side = v3(c->side[0], c->side[1], c->side[2]);
+    k.resX = resX;
+    k.resY = resY;
+    return k;
+}
+
+/* Camera::calcRayOriginAndDirection (main.rs:1902-1942) */
+static void calcRayOriginAndDirection(const Camera* c, int64_t pixelX, int64_t pixelY, Vec3* origin,
+                                      Vec3* dir) {
+    double sideScale01 = (double)pixelX / (double)c->resX;
+    double upScale01 = (double)pixelY / (double)c->resY;
+    double sideScalem11 = sideScale01 * 2.0 - 1.0;
+    double upScalem11 = upScale01 * 2.0 - 1.0;
+    if (c->type == RTM_CAMERA_ORTHOGONAL) {
+        Vec3 positionP = c->pos;
+        positionP = v3_add(positionP, v3_scale(c->side, sideScalem11));
+        positionP = v3_add(positionP, v3_scale(c->up, upScalem11));
+        *origin = positionP;
+        *dir = c->dir;
+    } else {
+        double scaleSide = 1.0, scaleUp = 1.0;
+        Vec3 rayDirection = c->dir;
+        rayDirection = v3_add(rayDirection, v3_scale(c->side, sideScalem11 * scaleSide));
+        rayDirection = v3_add(rayDirection, v3_scale(c->up, upScalem11 * scaleUp));
+        *origin = c->pos;
+        *dir = normalize(rayDirection);
+    }
+}
+
+/* Camera::project, orthogonal only (main.rs:1947-1958) */
+static Vec3 camera_project(const Camera* c, Vec3 position) {
+    Vec3 diff = v3(position.x - c->pos.x, position.y - c->pos.y, position.z - c->pos.z);
+    return v3(dot(diff, c->side), dot(diff, c->up), dot(diff, c->dir));
+}
+
+/* Camera::calcDepthOfProjectedPoint (main.rs:1962-1978); both branches are the same dot */
+static double calcDepthOfProjectedPoint(const Camera* c, Vec3 p) {
+    Vec3 positionDiff = v3_sub(p, c->pos);
+    return dot(c->dir, positionDiff);
+}
+
+/* Camera::retViewDirOfPixel (main.rs:1981-2013) */
+static Vec3 retViewDirOfPixel(const Camera* c, int64_t pixelX, int64_t pixelY) {
+    if (c->type == RTM_CAMERA_ORTHOGONAL) return v3_scale(c->dir, -1.0);
+    double sideScale01 = (double)pixelX / (double)c->resX;
+    double upScale01 = (double)pixelY / (double)c->resY;
+    double sideScalem11 = sideScale01 * 2.0 - 1.0;
+    double upScalem11 = upScale01 * 2.0 - 1.0;
+    Vec3 rayDirection = c->dir;
+    rayDirection = v3_add(rayDirection, v3_scale(c->side, sideScalem11 * 1.0));
+    rayDirection = v3_add(rayDirection, v3_scale(c->up, upScalem11 * 1.0));
+    Vec3 dirNormalized = normalize(rayDirection);
+    return v3_scale(dirNormalized, -1.0);
+}
+
+/* ------------------------------------------------------------------ */
+/* L2 sphere coverage (main.rs:122-331, 2844-2857)                     */
+/* ------------------------------------------------------------------ */
+typedef struct {
+    int64_t id;
+    double z;
+    Vec2 center;
+    double r;
+    Vec2 axisA, axisB;
+} ProjectedSphere; /* main.rs:199-208 */
+
+/* calcHeightOfSphereOnUnit (main.rs:123-133); returns 1 and *h if Some */
+static int calcHeightOfSphereOnUnit(double distUnit, double* h) {
+    if (distUnit < 1.0) {
+        *h = sqrt(1.0 - distUnit * distUnit);
+        return 1;
+    }
+    return 0;
+}
+
+/* calcZValueOfProjectedSphere (main.rs:236-246) */
+static double calcZValueOfProjectedSphere(double z, double absoluteProjectedRadius, int face) {
+    return face == RTM_FACE_FRONT ? z - absoluteProjectedRadius : z + absoluteProjectedRadius;
+}
+
+/* calcEllipseDistToCenter + calcDistToCenter (main.rs:2848-2857) */
+static double calcEllipseDistToCenter(Vec2 rel, Vec2 axisA, Vec2 axisB) {
+    double projectedA = dot2d(rel, v2_normalized(axisA)) / v2_magnitude(axisA);
+    double projectedB = dot2d(rel, v2_normalized(axisB)) / v2_magnitude(axisB);
+    return v2_magnitude(v2(projectedA, projectedB));
+}
+
+/* ProjectedSphere::calcOthoDistanceByAbsPosition (main.rs:214-217) */
+static double calcOthoDistanceByAbsPosition(const ProjectedSphere* s, Vec2 p) {
+    Vec2 rel = v2_sub(p, s->center);
+    return calcEllipseDistToCenter(rel, s->axisA, s->axisB);
+}
+
+/* G-buffer entry: Option<PixelSurfaceInfo::RasterizedSphere{relativeHeight,id,z}> (main.rs:136-150) */
+typedef struct {
+    int32_t some;
+    int64_t id;
+    double relativeHeight;
+    double z;
+} GEntry;
+
+typedef struct {
+    int64_t W, H;
+    int face;
+    Camera camera;
+    double* zBuffer; /* Map2d<f64> row-major y*W+x (main.rs:2351-2373) */
+    GEntry* rasterized;
+} Viewport;
+
+typedef struct {
+    int64_t eye_hits[RTM_MAX_SPHERES];
+    int64_t eye_hit_pixels, lit_pixels, eye_sphere_tests, shadow_sphere_tests;
+    int64_t march_iterations, march_hits, march_in_range;
+} Counts; /* layout == rtm_stats */
+
+/* rasterizeSphere (main.rs:249-331).  Pixel loop over rows [y0,y1).  The
+ * bbox (main.rs:256-300) is applied only with RTMO_FLAG_REF_BBOX. */
+static void rasterizeSphere(const ProjectedSphere* ps, double r, Viewport* vp, int flags, int64_t y0,
+                            int64_t y1, int64_t* tests) {
+    int64_t minX = 0, maxX = vp->W, minY = 0, maxY = vp->H;
+    if (flags & RTMO_FLAG_REF_BBOX) {
+        double maxAxisLength = v2_magnitude(ps->axisA);
+        maxAxisLength = rust_max(maxAxisLength, v2_magnitude(ps->axisB));
+        double resW = (double)vp->W, resH = (double)vp->H;
+        double aspectY = (double)vp->H / (double)vp->W;
+#define CONV(rel, res, asp) rust_as_i64((((rel) + 1.0) * 0.5) * (asp) * (res))
+        int64_t boundXMin = CONV(ps->center.x - maxAxisLength, resW, 1.0) + 1;
+        boundXMin -= 1;
+        int64_t boundXMax = CONV(ps->center.x + maxAxisLength, resW, 1.0) + 1;
+        boundXMax += 1;
+        if (boundXMin > minX) minX = boundXMin;
+        if (boundXMax < maxX) maxX = boundXMax;
+        int64_t boundYMin = CONV(ps->center.y - maxAxisLength, resH, aspectY) + 1;
+        boundYMin -= 1;
+        int64_t boundYMax = CONV(ps->center.y + maxAxisLength, resH, aspectY) + 1;
+        boundYMax += 1;
+#undef CONV
+        if (boundYMin > minY) minY = boundYMin;
+        if (boundYMax < maxY) maxY = boundYMax;
+    }
+    if (minY < y0) minY = y0;
+    if (maxY > y1) maxY = y1;
+    for (int64_t yi = minY; yi < maxY; yi++) {
+        for (int64_t xi = minX; xi < maxX; xi++) {
+            /* main.rs:306-307 with 512 -> W/H */
+            double x = ((double)xi / (double)vp->W) * 2.0 - 1.0;
+            double y = ((double)yi / (double)vp->H) * 2.0 - 1.0;
+            Vec2 p = v2(x, y);
+            /* projectSphereAtZBuffer (main.rs:176-195) */
+            double distanceToCenterUnit = calcOthoDistanceByAbsPosition(ps, p);
+            double relativeHeight;
+            if (!calcHeightOfSphereOnUnit(distanceToCenterUnit, &relativeHeight)) continue;
+            if (tests) (*tests)++;
+            double depth = calcZValueOfProjectedSphere(ps->z, relativeHeight * r, vp->face);
+            int64_t idx = yi * vp->W + xi;
+            if (depth < vp->zBuffer[idx]) {
+                vp->rasterized[idx].some = 1;
+                vp->rasterized[idx].id = ps->id;
+                vp->rasterized[idx].relativeHeight = relativeHeight;
+                vp->rasterized[idx].z = ps->z;
+                vp->zBuffer[idx] = depth;
+            }
+        }
+    }
+}
+
+/* Viewport::rasterize, ORTHOGONAL branch (main.rs:445-471, 540-542) over rows [y0,y1). */
+static int viewport_rasterize(Viewport* vp, const rtm_scene* scene, int flags, int64_t y0, int64_t y1,
+                              int64_t* tests) {
+    if (vp->camera.type != RTM_CAMERA_ORTHOGONAL) return RTM_ERR_UNSUPPORTED;
+    for (int32_t i = 0; i < scene->n_spheres; i++) {
+        const rtm_sphere* s = &scene->spheres[i];
+        Vec3 pos = v3(s->pos[0], s->pos[1], s->pos[2]);
+        double z = calcDepthOfProjectedPoint(&vp->camera, pos);
+        Vec3 projectedPosition = camera_project(&vp->camera, pos);
+        ProjectedSphere ps;
+        ps.id = s->id;
+        ps.z = z;
+        ps.center = v2(projectedPosition.x, projectedPosition.y);
+        ps.r = s->r;
+        ps.axisA = v2(s->r, 0.0);
+        ps.axisB = v2(0.0, s->r);
+        rasterizeSphere(&ps, ps.r, vp, flags, y0, y1, tests);
+    }
+    return RTM_OK;
+}
+
+/* ------------------------------------------------------------------ */
+/* L2 implicit-surface march (main.rs:2016-2051, 2066-2080, 2133-2284) */
+/* ------------------------------------------------------------------ */
+/* linear (main.rs:2066-2069) */
+static double linear(double t, double a, double b) {
+    double diff = b - a;
+    return a + diff * t;
+}
+/* bilinear (main.rs:2073-2080) */
+static double bilinear(Vec2 t, double d00, double d01, double d10, double d11) {
+    double d0 = linear(t.x, d00, d01);
+    double d1 = linear(t.x, d10, d11);
+    return linear(t.y, d0, d1);
+}
+/* calcDepthBilinear (main.rs:2146-2148) */
+static double calcDepthBilinear(Vec3 p, const rtm_patch* b) {
+    return bilinear(v2(p.x, p.y), b->a0, b->b0, b->a1, b->b1);
+}
+/* inRange01 (main.rs:2282-2284) */
+static int inRange01(double v) { return fabs(v - 0.5) <= 0.5; }
+
+/* raymarchPatch (main.rs:2219-2278).  The normal (calcNormalBilinear,
+ * main.rs:2151-2174) is computed by the reference but discarded by its only
+ * caller (main.rs:2047), so it is not restated. */
+static int raymarchPatch(Vec3 pStart, Vec3 dir, int64_t steps, const rtm_patch* patch, double* tOut,
+                         int64_t* iters) {
+    const int checkBoundsIteration = 1;
+    double magnitudeOfStepsize = 0.03;
+    Vec3 step = v3_scale(dir, magnitudeOfStepsize);
+    Vec3 p = pStart;
+    double t = 0.0;
+    double signEntry;
+    {
+        double depthOfSurface = calcDepthBilinear(p, patch);
+        signEntry = rust_signum(p.z - depthOfSurface);
+    }
+    for (int64_t s = 0; s < steps; s++) {
+        if (iters) (*iters)++;
+        if (checkBoundsIteration) {
+            if (!inRange01(p.x) || !inRange01(p.y)) {
+                p = v3_add(p, step);
+                t += magnitudeOfStepsize;
+                continue;
+            }
+        }
+        double depthOfSurface = calcDepthBilinear(p, patch);
+        double sign = rust_signum(p.z - depthOfSurface);
+        if (sign != signEntry) {
+            *tOut = t;
+            return 1;
+        }
+        p = v3_add(p, step);
+        t += magnitudeOfStepsize;
+    }
+    return 0;
+}
+
+/* raymarchPatchDomainM11 (main.rs:2179-2197) */
+static int raymarchPatchDomainM11(Vec3 pStart, Vec3 dir, int64_t steps, const rtm_patch* patch,
+                                  double* tOut, int64_t* iters) {
+    double x = (pStart.x + 1.0) * 0.5;
+    double y = (pStart.y + 1.0) * 0.5;
+    return raymarchPatch(v3(x, y, pStart.z), dir, steps, patch, tOut, iters);
+}
+
+/* Viewport::processRaymarchingRays + rayEntry_ShadowRay_testing (main.rs:551-565,
+ * 2022-2051), with the patch list and step count as arguments. */
+static void viewport_process_raymarching_rays(Viewport* vp, const rtm_patch* patches, int32_t n_patches,
+                                              int64_t steps, int64_t y0, int64_t y1, Counts* cnt) {
+    for (int64_t yi = y0; yi < y1; yi++) {
+        for (int64_t xi = 0; xi < vp->W; xi++) {
+            for (int32_t k = 0; k < n_patches; k++) {
+                Vec3 pStart, dirN;
+                calcRayOriginAndDirection(&vp->camera, xi, yi, &pStart, &dirN);
+                if (cnt) {
+                    double mx = (pStart.x + 1.0) * 0.5, my = (pStart.y + 1.0) * 0.5;
+                    if (inRange01(mx) && inRange01(my)) cnt->march_in_range++;
+                }
+                double rayDepth;
+                if (raymarchPatchDomainM11(pStart, dirN, steps, &patches[k], &rayDepth,
+                                           cnt ? &cnt->march_iterations : NULL)) {
+                    if (cnt) cnt->march_hits++;
+                    int64_t idx = yi * vp->W + xi;
+                    if (rayDepth < vp->zBuffer[idx]) vp->zBuffer[idx] = rayDepth;
+                }
+            }
+        }
+    }
+}
+
+/* ------------------------------------------------------------------ */
+/* L3 shading (main.rs:155-173, 709-902, 2872-2875)                    */
+/* ------------------------------------------------------------------ */
+/* reflect (main.rs:2872-2875) — sign-flipped as written */
+static Vec3 reflect(Vec3 d, Vec3 n) { return v3_sub(d, v3_scale(n, -2.0 * dot(d, n))); }
+
+/* renderColorImage (main.rs:710-902) over rows [y0,y1) */
+static void renderColorImage(const rtm_scene* scene, const Viewport* vp, const Viewport* vps, float* out,
+                             int64_t y0, int64_t y1, Counts* cnt) {
+    for (int64_t iy = y0; iy < y1; iy++) {
+        for (int64_t ix = 0; ix < vp->W; ix++) {
+            const GEntry* iPixel = &vp->rasterized[iy * vp->W + ix];
+            double r = 0.0, g = 0.2, b = 0.2;
+            if (iPixel->some) {
+                Vec3 viewDir = retViewDirOfPixel(&vp->camera, ix, iy);
+                const rtm_sphere* prim = &scene->spheres[iPixel->id];
+                /* calcDepth (main.rs:155-165) */
+                double rMulHeight = iPixel->relativeHeight * prim->r;
+                double depth = calcZValueOfProjectedSphere(iPixel->z, rMulHeight, RTM_FACE_FRONT);
+                Vec3 o, d;
+                calcRayOriginAndDirection(&vp->camera, ix, iy, &o, &d);
+                Vec3 worldPosition = v3_add(o, v3_scale(d, depth));
+                Vec3 diffOfPositionToCenter = v3_sub(worldPosition, v3(prim->pos[0], prim->pos[1], prim->pos[2]));
+                Vec3 normal = v3_scale(diffOfPositionToCenter, 1.0 / prim->r);
+
+                Vec3 incommingLightDir = v3(1.0, 0.0, 0.0);
+                Vec3 invertedIncommingLightDir = v3_scale(incommingLightDir, -1.0);
+                double diffuse = dot(normal, invertedIncommingLightDir);
+                diffuse = rust_max(diffuse, 0.0);
+                Vec3 reflectionDir = reflect(invertedIncommingLightDir, normal);
+                double specularMagnitude = powi(rust_max(dot(viewDir, reflectionDir), 0.0), 32);
+                double lightMagnitude = 1.0;
+
+                /* shadow mapping (main.rs:834-857) */
+                Vec3 projectedPosition = camera_project(&vps->camera, worldPosition);
+                int64_t halfW = vps->W / 2, halfH = vps->H / 2;
+                int64_t texX = wrap_add_i64(halfW, rust_as_i64(projectedPosition.x * (double)halfW));
+                int64_t texY = wrap_add_i64(halfH, rust_as_i64(projectedPosition.y * (double)halfH));
+                double depthFromShadowMap = INFINITY;
+                if (texY >= 0 && texY < vps->H && texX >= 0 && texX < vps->W)
+                    depthFromShadowMap = vps->zBuffer[texY * vps->W + texX];
+                double bias = 0.0;
+                int inLight = depthFromShadowMap > projectedPosition.z - bias;
+                if (!inLight) lightMagnitude = 0.25;
+
+                r = (diffuse + specularMagnitude) * lightMagnitude * prim->color[0];
+                g = (diffuse + specularMagnitude) * lightMagnitude * prim->color[1];
+                b = (diffuse + specularMagnitude) * lightMagnitude * prim->color[2];
+                if (cnt) {
+                    cnt->eye_hit_pixels++;
+                    if (iPixel->id >= 0 && iPixel->id < RTM_MAX_SPHERES) cnt->eye_hits[iPixel->id]++;
+                    if (inLight) cnt->lit_pixels++;
+                }
+            }
+            float* px = out + 4 * (iy * vp->W + ix);
+            px[0] = (float)r;
+            px[1] = (float)g;
+            px[2] = (float)b;
+            px[3] = 1.0f;
+        }
+    }
+}
+
+/* ------------------------------------------------------------------ */
+/* Exported oracle API (prefix rtmo_)                                   */
+/* ------------------------------------------------------------------ */
+static int validate_scene(const rtm_scene* scene) {
+    if (!scene || scene->n_spheres < 0 || scene->n_patches < 0) return RTM_ERR_INVALID;
+    if (scene->n_spheres > 0 && !scene->spheres) return RTM_ERR_INVALID;
+    if (scene->n_patches > 0 && !scene->patches) return RTM_ERR_INVALID;
+    for (int32_t i = 0; i < scene->n_spheres; i++)
+        if (scene->spheres[i].id < 0 || scene->spheres[i].id >= scene->n_spheres) return RTM_ERR_INVALID;
+    return RTM_OK;
+}
+
+static void viewport_init(Viewport* vp, int64_t W, int64_t H, int face, const rtm_camera* cam) {
+    vp->W = W;
+    vp->H = H;
+    vp->face = face;
+    vp->camera = camera_from(cam, W, H);
+    vp->zBuffer = (double*)malloc(sizeof(double) * (size_t)(W * H));
+    vp->rasterized = (GEntry*)calloc((size_t)(W * H), sizeof(GEntry));
+    for (int64_t i = 0; i < W * H; i++) vp->zBuffer[i] = INFINITY;
+}
+
+static void viewport_free(Viewport* vp) {
+    free(vp->zBuffer);
+    free(vp->rasterized);
+}
+
+int32_t rtmo_abi_version(void) { return RTM_ABI_VERSION; }
+
+/* Whole two-viewport frame (testscene_closelyOrbitingSphere body, main.rs:1533-1628).
+ * nthreads<=1: single thread, the reference's sequential loops; otherwise
+ * OpenMP over row bands (pixels are independent; per-pixel sphere order kept).
+ * out_shadow (nullable): the shadow viewport's zBuffer.  stats (nullable). */
+int rtmo_render(const rtm_scene* scene, const rtm_camera* eye, const rtm_camera* shadow, int32_t W,
+                int32_t H, int32_t steps, int32_t flags, int32_t nthreads, float* out_rgba,
+                double* out_shadow, rtm_stats* stats) {
+    int rc = validate_scene(scene);
+    if (rc) return rc;
+    if (!eye || !shadow || !out_rgba || W <= 0 || H <= 0 || steps < 0) return RTM_ERR_INVALID;
+    if (eye->type != RTM_CAMERA_ORTHOGONAL || shadow->type != RTM_CAMERA_ORTHOGONAL) return RTM_ERR_UNSUPPORTED;
+    Viewport vs, ve;
+    viewport_init(&vs, W, H, RTM_FACE_BACK, shadow);
+    viewport_init(&ve, W, H, RTM_FACE_FRONT, eye);
+    Counts total;
+    memset(&total, 0, sizeof total);
+    int nt = nthreads < 1 ? 1 : nthreads;
+    int64_t band = 8;
+    int64_t nb = (H + band - 1) / band;
+
+    /* pass 1: shadow viewport rasterize + march; pass 2: eye rasterize; pass 3: shade.
+     * Rows are independent within a pass, so bands may run in any order. */
+    for (int pass = 0; pass < 3; pass++) {
+#ifdef _OPENMP
+#pragma omp parallel for schedule(dynamic, 1) num_threads(nt)
+#endif
+        for (int64_t bi = 0; bi < nb; bi++) {
+            int64_t y0 = bi * band, y1 = y0 + band < H ? y0 + band : H;
+            Counts c;
+            memset(&c, 0, sizeof c);
+            if (pass == 0) {
+                if (!(flags & RTM_FLAG_NO_SHADOW_RASTER))
+                    viewport_rasterize(&vs, scene, flags, y0, y1, &c.shadow_sphere_tests);
+                if (!(flags & RTM_FLAG_NO_MARCH))
+                    viewport_process_raymarching_rays(&vs, scene->patches, scene->n_patches, steps, y0, y1, &c);
+            } else if (pass == 1) {
+                viewport_rasterize(&ve, scene, flags, y0, y1, &c.eye_sphere_tests);
+            } else {
+                renderColorImage(scene, &ve, &vs, out_rgba, y0, y1, &c);
+            }
+#ifdef _OPENMP
+#pragma omp critical
+#endif
+            {
+                int64_t* dst = (int64_t*)&total;
+                const int64_t* src = (const int64_t*)&c;
+                for (size_t k = 0; k < sizeof(Counts) / sizeof(int64_t); k++) dst[k] += src[k];
+            }
+        }
+    }
+    if (out_shadow) memcpy(out_shadow, vs.zBuffer, sizeof(double) * (size_t)W * (size_t)H);
+    if (stats) memcpy(stats, &total, sizeof total);
+    viewport_free(&vs);
+    viewport_free(&ve);
+    return RTM_OK;
+}
+
+/* ---- staged (reference-seam) oracle API, host buffers ---- */
+typedef struct rtmo_viewport {
+    Viewport vp;
+} rtmo_viewport;
+
+int rtmo_viewport_create(int32_t W, int32_t H, int32_t face, const rtm_camera* cam, rtmo_viewport** out) {
+    if (!cam || !out || W <= 0 || H <= 0 || (face != RTM_FACE_FRONT && face != RTM_FACE_BACK)) return RTM_ERR_INVALID;
+    rtmo_viewport* v = (rtmo_viewport*)calloc(1, sizeof *v);
+    viewport_init(&v->vp, W, H, face, cam);
+    *out = v;
+    return RTM_OK;
+}
+
+void rtmo_viewport_destroy(rtmo_viewport* v) {
+    if (!v) return;
+    viewport_free(&v->vp);
+    free(v);
+}
+
+int rtmo_viewport_rasterize(rtmo_viewport* v, const rtm_scene* scene, int32_t flags) {
+    int rc = validate_scene(scene);
+    if (rc) return rc;
+    return viewport_rasterize(&v->vp, scene, flags, 0, v->vp.H, NULL);
+}
+
+int rtmo_viewport_process_raymarching_rays(rtmo_viewport* v, const rtm_patch* patches, int32_t n, int32_t steps) {
+    if (n < 0 || (n > 0 && !patches) || steps < 0) return RTM_ERR_INVALID;
+    viewport_process_raymarching_rays(&v->vp, patches, n, steps, 0, v->vp.H, NULL);
+    return RTM_OK;
+}
+
+int rtmo_render_color_image(const rtm_scene* scene, const rtmo_viewport* v, const rtmo_viewport* vs, float* out) {
+    int rc = validate_scene(scene);
+    if (rc) return rc;
+    if (!v || !vs || !out) return RTM_ERR_INVALID;
+    if (vs->vp.camera.type != RTM_CAMERA_ORTHOGONAL) return RTM_ERR_UNSUPPORTED;
+    renderColorImage(scene, &v->vp, &vs->vp, out, 0, v->vp.H, NULL);
+    return RTM_OK;
+}
+
+int rtmo_viewport_read_zbuffer(const rtmo_viewport* v, double* out) {
+    if (!v || !out) return RTM_ERR_INVALID;
+    memcpy(out, v->vp.zBuffer, sizeof(double) * (size_t)(v->vp.W * v->vp.H));
+    return RTM_OK;
+}
+
+/* ---- row f-1 helpers, pinned by the reference's own unit test ---- */
+/* calcRayPlane (main.rs:2398-2408); returns 1 and *t on Some */
+int rtmo_calc_ray_plane(const double origin[3], const double dir[3], const double plane_n[3],
+                        const double plane_center[3], double* t) {
+    Vec3 n = v3(plane_n[0], plane_n[1], plane_n[2]);
+    Vec3 d = v3(dir[0], dir[1], dir[2]);
+    double denom = dot(n, d);
+    if (fabs(denom) > 0.0001) {
+        Vec3 c = v3(plane_center[0], plane_center[1], plane_center[2]);
+        Vec3 o = v3(origin[0], origin[1], origin[2]);
+        *t = dot(v3_sub(c, o), n) / denom;
+        return 1;
+    }
+    return 0;
+}
+
+/* writeColorImage pixel encode (main.rs:674-684): clamp, f32 powf(1/2.2), (v*255) as i64 */
+void rtmo_encode_rgb8(const float* rgba, int64_t n_pixels, int64_t* out_rgb) {
+    for (int64_t i = 0; i < n_pixels; i++) {
+        for (int c = 0; c < 3; c++) {
+            float v = rgba[4 * i + c];
+            v = fmaxf(v, 0.0f);
+            v = fminf(v, 1.0f);
+            float gamma = 2.2f;
+            v = powf(v, 1.0f / gamma);
+            out_rgb[3 * i + c] = rust_as_i64((double)(v * 255.0f));
+        }
+    }
+}

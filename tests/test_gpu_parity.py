@@ -1,0 +1,267 @@
+"""GPU parity: the HIP path (through the C ABI) against the CPU oracle.
+
+Bar: bit-exact RGBA f32 and f64 shadow maps (the north
+star's 1e-5 per-channel tolerance is implied by bit equality, which is what we
+assert).  Sizes cover every BASELINE config at full size plus ragged and edge
+cases.  All calls go through librtm.so; nothing here falls back to the CPU.
+"""
+import math
+import os
+
+import numpy as np
+import pytest
+
+from conftest import bits_equal, first_mismatch
+
+pytestmark = pytest.mark.gpu
+
+NT = min(16, os.cpu_count() or 1)
+
+
+def _oracle(oracle, scene, eye, shadow, w, h, k, flags=0, **kw):
+    return oracle.render(scene, eye, shadow, w, h, k, flags, nthreads=NT, **kw)
+
+
+def _check_frame(rtm, oracle, scene, eye, shadow, w, h, k, flags=0):
+    got = rtm.render_frame(scene, eye, shadow, w, h, k, flags)
+    want = _oracle(oracle, scene, eye, shadow, w, h, k, flags)["rgba"]
+    assert bits_equal(got, want), first_mismatch(got, want)
+    return got
+
+
+@pytest.mark.parametrize("frame", [0, 37, 100, 250])
+def test_reference_scene_512(rtm, oracle, scenes, frame):
+    """testscene_closelyOrbitingSphere at the reference's own 512x512, 500 steps."""
+    _check_frame(rtm, oracle, scenes.closely_orbiting_sphere(frame), scenes.eye_camera(),
+                 scenes.shadow_camera(), 512, 512, 500)
+
+
+def test_survey_kat_frame0_and_100(rtm, scenes):
+    """SURVEY.md §8c-3 cross-check values, straight from the GPU."""
+    import hashlib
+    for frame, sha in ((0, "cf557d736f83a4f6"), (100, "cb7008f728da5208")):
+        img = rtm.render_frame(scenes.closely_orbiting_sphere(frame), scenes.eye_camera(),
+                               scenes.shadow_camera(), 512, 512, 500)
+        rgb = np.ascontiguousarray(img[:, :, :3])
+        assert hashlib.sha256(rgb.tobytes()).hexdigest()[:16] == sha
+    img = rtm.render_frame(scenes.closely_orbiting_sphere(0), scenes.eye_camera(),
+                           scenes.shadow_camera(), 512, 512, 500)
+    assert img[256, 384, :3].tolist() == [9265101144064.0, 9265101144064.0, 463255038328832.0]
+    assert img[300, 384, :3].tolist() == [3506.7421875, 3506.7421875, 175337.109375]
+
+
+@pytest.mark.parametrize("cfg", [1, 2, 3])
+def test_baseline_configs_full_size(rtm, oracle, scenes, cfg):
+    c = scenes.CONFIGS[cfg]
+    _check_frame(rtm, oracle, c["scene"](), scenes.eye_camera(), scenes.shadow_camera(),
+                 c["width"], c["height"], c["steps"], c["flags"])
+
+
+@pytest.mark.parametrize("cfg", [4, 5])
+def test_baseline_configs_8k(rtm, oracle, scenes, cfg):
+    c = scenes.CONFIGS[cfg]
+    _check_frame(rtm, oracle, c["scene"](), scenes.eye_camera(), scenes.shadow_camera(),
+                 c["width"], c["height"], c["steps"], c["flags"])
+
+
+def test_overlapping_spheres(rtm, oracle, scenes):
+    """testscene_overlappingSpheres: shadow pass commented out in the reference."""
+    _check_frame(rtm, oracle, scenes.overlapping_spheres(), scenes.eye_camera(), scenes.shadow_camera(),
+                 512, 512, 0, scenes.OVERLAPPING_FLAGS)
+
+
+@pytest.mark.parametrize("wh", [(1, 1), (2, 3), (63, 65), (1000, 7), (7, 1000), (130, 66)])
+def test_ragged_sizes(rtm, oracle, scenes, wh):
+    w, h = wh
+    _check_frame(rtm, oracle, scenes.scene_a_bench(), scenes.eye_camera(), scenes.shadow_camera(), w, h, 64)
+
+
+@pytest.mark.parametrize("k", [0, 1, 5, 33, 500])
+def test_march_steps(rtm, oracle, scenes, k):
+    _check_frame(rtm, oracle, scenes.scene_a_bench(), scenes.eye_camera(), scenes.shadow_camera(), 256, 192, k)
+
+
+def test_shadow_map_bits(rtm, oracle, scenes, gpu_ctx):
+    """The shadow viewport's zBuffer (rasterize BACK + march) bit for bit."""
+    import torch
+    for scene, w, h, k in ((scenes.closely_orbiting_sphere(100), 512, 512, 500),
+                           (scenes.scene_a_bench(), 1920, 1080, 32),
+                           (scenes.scene_b(), 640, 360, 128)):
+        out = torch.empty((h, w, 4), dtype=torch.float32, device="cuda")
+        torch.cuda.synchronize()
+        gpu_ctx.render_async(scene, scenes.eye_camera(), scenes.shadow_camera(), w, h, k, 0, out.data_ptr())
+        gpu_ctx.synchronize()
+        ptr = gpu_ctx.shadow_map_ptr()
+        assert ptr
+        got = _read_device_f64(ptr, h * w).reshape(h, w)
+        want = _oracle(oracle, scene, scenes.eye_camera(), scenes.shadow_camera(), w, h, k,
+                       want_shadow=True)
+        assert bits_equal(got, want["shadow"]), first_mismatch(got, want["shadow"])
+        assert bits_equal(out.cpu().numpy(), want["rgba"])
+
+
+def _read_device_f64(ptr, n):
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so")
+    out = np.empty(n, np.float64)
+    rc = hip.hipMemcpy(out.ctypes.data_as(ctypes.c_void_p), ctypes.c_void_p(ptr), ctypes.c_size_t(8 * n), 2)
+    assert rc == 0
+    return out
+
+
+def test_fused_shadow_identical(rtm, oracle, scenes):
+    """RTM_FLAG_FUSED_SHADOW evaluates texels on demand: same image bits."""
+    for scene, w, h, k in ((scenes.closely_orbiting_sphere(100), 512, 512, 500),
+                           (scenes.scene_a_bench(), 1920, 1080, 32), (scenes.scene_b(), 800, 600, 128)):
+        a = rtm.render_frame(scene, scenes.eye_camera(), scenes.shadow_camera(), w, h, k, 0)
+        b = rtm.render_frame(scene, scenes.eye_camera(), scenes.shadow_camera(), w, h, k,
+                             rtm.abi.RTM_FLAG_FUSED_SHADOW)
+        assert bits_equal(a, b), first_mismatch(b, a)
+
+
+def test_row_bands_assemble(rtm, scenes, gpu_ctx):
+    """rtm_render_async over row bands == the full frame (the multi-GPU shard unit)."""
+    import torch
+    w, h, k = 1000, 601, 64
+    scene = scenes.scene_a_bench()
+    full = rtm.render_frame(scene, scenes.eye_camera(), scenes.shadow_camera(), w, h, k)
+    for flags in (0, rtm.abi.RTM_FLAG_FUSED_SHADOW):
+        parts = []
+        bounds = [0, 1, 150, 333, 600, 601]
+        for b0, b1 in zip(bounds[:-1], bounds[1:]):
+            out = torch.empty((b1 - b0, w, 4), dtype=torch.float32, device="cuda")
+            torch.cuda.synchronize()
+            gpu_ctx.render_async(scene, scenes.eye_camera(), scenes.shadow_camera(), w, h, k, flags,
+                                 out.data_ptr(), b0, b1)
+            gpu_ctx.synchronize()
+            parts.append(out.cpu().numpy())
+        assert bits_equal(np.concatenate(parts, 0), full)
+
+
+def test_staged_api_matches_oracle(rtm, oracle, scenes, gpu_ctx):
+    """Viewport.rasterize / processRaymarchingRays / renderColorImage, one call
+    per reference function, against the oracle's staged API."""
+    for frame, w, h in ((100, 512, 512), (37, 300, 200)):
+        scene = scenes.closely_orbiting_sphere(frame)
+        vp1 = rtm.Viewport(gpu_ctx, w, h, scenes.EnumFace.BACK, scenes.shadow_camera())
+        vp1.rasterize(scene)
+        vp1.processRaymarchingRays()
+        vp0 = rtm.Viewport(gpu_ctx, w, h, scenes.EnumFace.FRONT, scenes.eye_camera())
+        vp0.rasterize(scene)
+        img = rtm.renderColorImage(scene, vp0, vp1)
+        o1 = oracle.Viewport(w, h, scenes.EnumFace.BACK, scenes.shadow_camera())
+        o1.rasterize(scene)
+        o1.processRaymarchingRays([scenes.REFERENCE_PATCH], 500)
+        o0 = oracle.Viewport(w, h, scenes.EnumFace.FRONT, scenes.eye_camera())
+        o0.rasterize(scene)
+        want = oracle.render_color_image(scene, o0, o1)
+        assert bits_equal(vp1.zBuffer(), o1.zbuffer())
+        assert bits_equal(vp0.zBuffer(), o0.zbuffer())
+        assert bits_equal(img, want), first_mismatch(img, want)
+        # and the staged path equals the one-call frame path
+        frame_img = rtm.render_frame(scene, scenes.eye_camera(), scenes.shadow_camera(), w, h, 500)
+        assert bits_equal(img, frame_img)
+
+
+def test_staged_perspective_march(rtm, oracle, scenes, gpu_ctx):
+    """processRaymarchingRays with a PERSPECTIVE camera (normalised ray dirs,
+    main.rs:1922-1939): the general (non-axis-aligned) march loop."""
+    cam = scenes.Camera(scenes.PERSPECTIVE, (0.1, -0.2, -0.3), (0.0, 0.0, 1.0), (0.0, 1.0, 0.0),
+                        (1.0, 0.0, 0.0))
+    patches = [scenes.BENCH_PATCH, scenes.SCENE_B_PATCH2]
+    vp = rtm.Viewport(gpu_ctx, 200, 150, scenes.EnumFace.BACK, cam)
+    vp.processRaymarchingRays(patches, 200)
+    o = oracle.Viewport(200, 150, scenes.EnumFace.BACK, cam)
+    o.processRaymarchingRays(patches, 200)
+    got, want = vp.zBuffer(), o.zbuffer()
+    assert np.isfinite(want).sum() > 1000
+    assert bits_equal(got, want), first_mismatch(got, want)
+
+
+def test_stats_match_oracle(rtm, oracle, scenes, gpu_ctx):
+    for scene, w, h, k in ((scenes.closely_orbiting_sphere(100), 512, 512, 500),
+                           (scenes.scene_a_bench(), 1920, 1080, 32), (scenes.scene_b(), 640, 480, 128)):
+        got = gpu_ctx.stats(scene, scenes.eye_camera(), scenes.shadow_camera(), w, h, k)
+        want = _oracle(oracle, scene, scenes.eye_camera(), scenes.shadow_camera(), w, h, k,
+                       want_stats=True)["stats"]
+        assert got == want
+
+
+def _rotation(rng):
+    q = rng.normal(size=4)
+    q /= np.linalg.norm(q)
+    a, b, c, d = q
+    return np.array([[a*a+b*b-c*c-d*d, 2*(b*c-a*d), 2*(b*d+a*c)],
+                     [2*(b*c+a*d), a*a-b*b+c*c-d*d, 2*(c*d-a*b)],
+                     [2*(b*d-a*c), 2*(c*d+a*b), a*a-b*b-c*c+d*d]])
+
+
+def _random_scene(scenes, rng, ns, npch):
+    sph = []
+    for i in range(ns):
+        sph.append(scenes.PrimitiveSphere(
+            int(i), scenes.Shading(*[float(v) for v in rng.uniform(0, 1, 3)]),
+            tuple(float(v) for v in rng.uniform(-0.8, 0.8, 3)), float(rng.uniform(0.02, 0.4))))
+    # permute ids (the reference shades with spherePrimitives[id], main.rs:748)
+    perm = rng.permutation(ns)
+    for s, p in zip(sph, perm):
+        s.id = int(p)
+    pats = [scenes.Bilinear(scenes.Linear(*map(float, rng.uniform(-0.5, 1.5, 2))),
+                            scenes.Linear(*map(float, rng.uniform(-0.5, 1.5, 2)))) for _ in range(npch)]
+    return scenes.Scene(sph, pats)
+
+
+def _random_camera(scenes, rng, axis_aligned):
+    if axis_aligned:
+        return scenes.shadow_camera()
+    R = _rotation(rng)
+    pos = tuple(float(v) for v in rng.uniform(-0.5, 0.5, 3))
+    return scenes.Camera(scenes.ORTHOGONAL, pos, tuple(map(float, R[:, 2])), tuple(map(float, R[:, 1])),
+                         tuple(map(float, R[:, 0])))
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_random_scenes(rtm, oracle, scenes, seed):
+    """Seeded fuzz (splitmix-free numpy PCG64, seed 0x2018+i): random spheres,
+    patches, permuted ids and rotated orthographic cameras (general march loop)."""
+    rng = np.random.default_rng(0x2018 + seed)
+    ns = int(rng.integers(0, 17))
+    npch = int(rng.integers(0, 5))
+    scene = _random_scene(scenes, rng, ns, npch)
+    eye = _random_camera(scenes, rng, seed % 3 == 0)
+    shadow = _random_camera(scenes, rng, seed % 2 == 0)
+    w, h = int(rng.integers(1, 400)), int(rng.integers(1, 300))
+    k = int(rng.integers(0, 200))
+    _check_frame(rtm, oracle, scene, eye, shadow, w, h, k)
+
+
+def test_degenerate_spheres(rtm, oracle, scenes):
+    s = scenes.closely_orbiting_sphere(10)
+    s.spherePrimitives.append(scenes.PrimitiveSphere(3, scenes.Shading(1, 1, 1), (0.0, 0.1, 0.2), 0.0))
+    s.spherePrimitives.append(scenes.PrimitiveSphere(4, scenes.Shading(1, 1, 1), (0.0, 0.1, 0.2), -0.15))
+    s.spherePrimitives.append(scenes.PrimitiveSphere(5, scenes.Shading(1, 0, 1), (5.0, 5.0, 5.0), 0.3))
+    s.spherePrimitives.append(scenes.PrimitiveSphere(6, scenes.Shading(0, 1, 1), (0.0, 0.0, 0.0), 3.0))
+    _check_frame(rtm, oracle, s, scenes.eye_camera(), scenes.shadow_camera(), 200, 200, 100)
+    empty = scenes.Scene([], [])
+    _check_frame(rtm, oracle, empty, scenes.eye_camera(), scenes.shadow_camera(), 64, 64, 10)
+
+
+def test_error_codes(rtm, scenes):
+    abi = rtm.abi
+    persp = scenes.Camera(scenes.PERSPECTIVE, (0, 0, 0), (0, 0, 1), (0, 1, 0), (1, 0, 0))
+    with pytest.raises(abi.RtmError) as e:
+        rtm.render_frame(scenes.scene_a_bench(), persp, scenes.shadow_camera(), 64, 64, 10)
+    assert e.value.code == abi.RTM_ERR_UNSUPPORTED
+    with pytest.raises(abi.RtmError) as e:
+        rtm.render_frame(scenes.scene_a_bench(), scenes.eye_camera(), scenes.shadow_camera(), 0, 64, 10)
+    assert e.value.code == abi.RTM_ERR_INVALID
+    bad = scenes.scene_a_bench()
+    bad.spherePrimitives[0].id = 7
+    with pytest.raises(abi.RtmError) as e:
+        rtm.render_frame(bad, scenes.eye_camera(), scenes.shadow_camera(), 64, 64, 10)
+    assert e.value.code == abi.RTM_ERR_INVALID
+    many = scenes.scene_b()
+    many.spherePrimitives.append(scenes.PrimitiveSphere(16, scenes.Shading(1, 1, 1), (0, 0, 0), 0.1))
+    with pytest.raises(abi.RtmError) as e:
+        rtm.render_frame(many, scenes.eye_camera(), scenes.shadow_camera(), 64, 64, 10)
+    assert e.value.code == abi.RTM_ERR_INVALID
