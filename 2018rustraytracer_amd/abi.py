@@ -118,6 +118,13 @@ def load_library(path: str | None = None) -> C.CDLL:
     if _lib is not None and path is None:
         return _lib
     p = path or LIB_PATH
+    # torch wheels bundle their own libamdhip64.so.7.  Loading torch first makes
+    # librtm bind to that same runtime (same soname), so a process that also uses
+    # torch has ONE HIP runtime; two runtimes in one process cannot both see the GPU.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     if not os.path.exists(p):
         raise FileNotFoundError(
             f"{p} not built: run `python -c 'import __graft_entry__ as g; g.build()'` "

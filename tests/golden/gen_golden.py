@@ -1,0 +1,260 @@
+#!/usr/bin/env python3
+"""Golden-vector generator: an INDEPENDENT numpy restatement of the reference
+hot path (PtrMan/2018RustRayTracer src/main.rs), written separately from the C
+oracle so the two cross-check each other.
+
+Why numpy: every ufunc (add, multiply, divide, sqrt) is an elementwise IEEE
+f64 operation with no FMA contraction, so a vectorised restatement that keeps
+the reference's operation order is bit-exact and fast enough for 1080p.
+
+The reference itself cannot be built here (no Rust toolchain)
+and ships no golden vectors for this path, so these fixtures are generated,
+not copied.  SURVEY.md §8c-3's cross-check values (computed by a third
+restatement during the survey) are re-asserted below before anything is
+written.
+
+Outputs (tests/golden/):
+  fixtures.npz   small frames (rgba f32 + shadow-map f64) for exact comparison
+  golden.json    sha256 of larger frames + hit statistics
+
+Run:  python tests/golden/gen_golden.py
+"""
+from __future__ import annotations
+
+import hashlib
+import json
+import math
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+# ---------------- scenes (same definitions as 2018rustraytracer_amd/scenes.py) ---------------
+SHADOW_CAM = dict(type=0, pos=(0.0, 0.0, 0.0), dir=(0.0, 0.0, 1.0), up=(0.0, 1.0, 0.0), side=(1.0, 0.0, 0.0))
+EYE_CAM = dict(type=0, pos=(-1.0, 0.0, 0.0), dir=(1.0, 0.0, 0.0), up=(0.0, 1.0, 0.0), side=(0.0, 0.0, 1.0))
+REF_PATCH = (0.1, 0.1, 0.1, 0.1)
+BENCH_PATCH = (0.3, 2.1, 0.9, 2.7)
+PATCH_B2 = (0.5, 1.5, 1.2, 3.3)
+
+
+def orbit_scene(frame, patches):
+    f = float(frame)
+    sph = [
+        (0, (0.0, 0.0, 0.5), 0.2, (0.02, 0.02, 1.0)),
+        (1, (0.0, 0.0, 0.5 + 0.2 * 2.0), 0.2, (0.02, 0.02, 1.0)),
+        (2, (-0.0, math.sin(f * 0.025) * 0.7, math.cos(f * 0.025) * 0.7), 0.1, (0.9, 0.2, 0.2)),
+    ]
+    return sph, list(patches)
+
+
+def scene_b():
+    cols = [(0.02, 0.02, 1.0), (0.9, 0.2, 0.2), (0.2, 0.9, 0.2), (0.9, 0.9, 0.2)]
+    sph = []
+    for i in range(16):
+        a = 2.0 * math.pi * i / 16.0
+        sph.append((i, (-0.5 + 0.0625 * i, 0.6 * math.sin(a), 0.6 + 0.6 * math.cos(a)), 0.08 + 0.01 * (i % 4),
+                    cols[i % 4]))
+    return sph, [BENCH_PATCH, PATCH_B2]
+
+
+def overlapping():
+    return [(0, (0.0, 0.0, 0.0), 0.5, (0.02, 0.02, 1.0)), (1, (0.0, 0.0, 0.5), 0.5, (1.0, 1.0, 1.0))], []
+
+
+# ---------------- restatement ----------------
+def signum(v):  # Rust f64::signum
+    return np.where(np.isnan(v), v, np.copysign(1.0, v))
+
+
+def grid(W, H):
+    xi = np.arange(W, dtype=np.float64)[None, :].repeat(H, 0)
+    yi = np.arange(H, dtype=np.float64)[:, None].repeat(W, 1)
+    # (i as f64 / res as f64) * 2.0 - 1.0   (main.rs:306-307, 1903-1907)
+    return (xi / float(W)) * 2.0 - 1.0, (yi / float(H)) * 2.0 - 1.0
+
+
+def dot(a, b):
+    return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]
+
+
+def rasterize(cam, spheres, W, H, face, zbuf, gbuf):
+    """Viewport::rasterize, orthographic (main.rs:445-547), no bbox."""
+    x, y = grid(W, H)
+    for (sid, pos, r, _col) in spheres:
+        diff = tuple(pos[k] - cam["pos"][k] for k in range(3))
+        z = dot(cam["dir"], diff)
+        cx, cy = dot(diff, cam["side"]), dot(diff, cam["up"])
+        # calcEllipseDistToCenter with axisA=(r,0), axisB=(0,r)
+        mA = math.sqrt(r * r + 0.0 * 0.0)
+        nA = (r * (1.0 / mA), 0.0 * (1.0 / mA))
+        mB = math.sqrt(0.0 * 0.0 + r * r)
+        nB = (0.0 * (1.0 / mB), r * (1.0 / mB))
+        relx, rely = x - cx, y - cy
+        with np.errstate(all="ignore"):
+            pa = (relx * nA[0] + rely * nA[1]) / mA
+            pb = (relx * nB[0] + rely * nB[1]) / mB
+            d = np.sqrt(pa * pa + pb * pb)
+            cov = d < 1.0
+            h = np.sqrt(np.where(cov, 1.0 - d * d, 0.0))
+        depth = z - h * r if face == 0 else z + h * r
+        win = cov & (depth < zbuf)
+        zbuf[win] = depth[win]
+        if gbuf is not None:
+            gbuf["id"][win] = sid
+            gbuf["h"][win] = h[win]
+            gbuf["z"][win] = z
+
+
+def march(cam, patches, W, H, steps, zbuf):
+    """processRaymarchingRays + raymarchPatch (main.rs:551-565, 2179-2278), orthographic."""
+    s, u = grid(W, H)
+    o = [(cam["pos"][k] + cam["side"][k] * s) + cam["up"][k] * u for k in range(3)]
+    for (a0, b0, a1, b1) in patches:
+        def bil(px, py):
+            d0 = a0 + (b0 - a0) * px
+            d1 = a1 + (b1 - a1) * px
+            return d0 + (d1 - d0) * py
+        px = (o[0] + 1.0) * 0.5
+        py = (o[1] + 1.0) * 0.5
+        pz = o[2].copy()
+        st = (cam["dir"][0] * 0.03, cam["dir"][1] * 0.03, cam["dir"][2] * 0.03)
+        t = np.zeros_like(pz)
+        entry = signum(pz - bil(px, py))
+        done = np.zeros(pz.shape, bool)
+        hit_t = np.full(pz.shape, np.nan)
+        for _ in range(steps):
+            inr = (np.abs(px - 0.5) <= 0.5) & (np.abs(py - 0.5) <= 0.5)
+            sg = signum(pz - bil(px, py))
+            newhit = (~done) & inr & (sg != entry)
+            hit_t[newhit] = t[newhit]
+            done |= newhit
+            px = px + st[0]
+            py = py + st[1]
+            pz = pz + st[2]
+            t = t + 0.03
+            if done.all():
+                break
+        upd = done & (hit_t < zbuf)
+        zbuf[upd] = hit_t[upd]
+
+
+def render(spheres, patches, W, H, steps, no_march=False, no_sraster=False):
+    zs = np.full((H, W), np.inf)
+    if not no_sraster:
+        rasterize(SHADOW_CAM, spheres, W, H, 1, zs, None)
+    if not no_march:
+        march(SHADOW_CAM, patches, W, H, steps, zs)
+    ze = np.full((H, W), np.inf)
+    g = dict(id=np.full((H, W), -1, np.int64), h=np.zeros((H, W)), z=np.zeros((H, W)))
+    rasterize(EYE_CAM, spheres, W, H, 0, ze, g)
+    # renderColorImage (main.rs:710-902)
+    img = np.zeros((H, W, 4), np.float32)
+    img[..., 1] = np.float32(0.2)
+    img[..., 2] = np.float32(0.2)
+    img[..., 3] = 1.0
+    hit = g["id"] >= 0
+    if hit.any():
+        ids = g["id"][hit]
+        prm = {sid: (pos, r, col) for (sid, pos, r, col) in spheres}
+        R = np.array([prm[i][1] for i in ids])
+        P = np.array([prm[i][0] for i in ids])
+        COL = np.array([prm[i][2] for i in ids])
+        depth = g["z"][hit] - g["h"][hit] * R
+        s, u = grid(W, H)
+        s, u = s[hit], u[hit]
+        cam = EYE_CAM
+        o = [(cam["pos"][k] + cam["side"][k] * s) + cam["up"][k] * u for k in range(3)]
+        wp = [o[k] + cam["dir"][k] * depth for k in range(3)]
+        n = [(wp[k] - P[:, k]) * (1.0 / R) for k in range(3)]
+        L = (1.0 * -1.0, 0.0 * -1.0, 0.0 * -1.0)
+        diffuse = np.fmax(n[0] * L[0] + n[1] * L[1] + n[2] * L[2], 0.0)
+        k2 = -2.0 * (L[0] * n[0] + L[1] * n[1] + L[2] * n[2])
+        Rv = [L[k] - n[k] * k2 for k in range(3)]
+        view = [cam["dir"][k] * -1.0 for k in range(3)]
+        sp = np.fmax(view[0] * Rv[0] + view[1] * Rv[1] + view[2] * Rv[2], 0.0)
+        with np.errstate(over="ignore"):
+            for _ in range(5):
+                sp = sp * sp
+        sc = SHADOW_CAM
+        df = [wp[k] - sc["pos"][k] for k in range(3)]
+        qx, qy, qz = dot(df, sc["side"]), dot(df, sc["up"]), dot(df, sc["dir"])
+        half_w, half_h = W // 2, H // 2
+
+        def trunc_i64(v):
+            v = np.where(np.isnan(v), 0.0, v)
+            v = np.clip(v, -4e18, 4e18)
+            return np.trunc(v).astype(np.int64)
+
+        tx = half_w + trunc_i64(qx * float(half_w))
+        ty = half_h + trunc_i64(qy * float(half_h))
+        inb = (tx >= 0) & (tx < W) & (ty >= 0) & (ty < H)
+        dsm = np.full(tx.shape, np.inf)
+        dsm[inb] = zs[ty[inb], tx[inb]]
+        lit = dsm > qz - 0.0
+        lm = np.where(lit, 1.0, 0.25)
+        base = diffuse + sp
+        with np.errstate(over="ignore"):
+            img[hit, 0] = ((base * lm) * COL[:, 0]).astype(np.float32)
+            img[hit, 1] = ((base * lm) * COL[:, 1]).astype(np.float32)
+            img[hit, 2] = ((base * lm) * COL[:, 2]).astype(np.float32)
+        stats = dict(eye_hits=[int((ids == i).sum()) for i in range(len(spheres))], lit=int(lit.sum()))
+    else:
+        stats = dict(eye_hits=[0] * len(spheres), lit=0)
+    return img, zs, stats
+
+
+def sha16(img):
+    return hashlib.sha256(np.ascontiguousarray(img[:, :, :3]).tobytes()).hexdigest()[:16]
+
+
+def sha_full(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+# (name, scene factory, W, H, steps, flags) — small ones go to fixtures.npz, all to golden.json
+CASES = [
+    ("orbit_f0_64", lambda: orbit_scene(0, [REF_PATCH]), 64, 64, 500, 0, True),
+    ("orbit_f100_96x80", lambda: orbit_scene(100, [REF_PATCH]), 96, 80, 500, 0, True),
+    ("bench_f100_128x72_k64", lambda: orbit_scene(100, [BENCH_PATCH]), 128, 72, 64, 0, True),
+    ("bench_f37_33x65_k32", lambda: orbit_scene(37, [BENCH_PATCH]), 33, 65, 32, 0, True),
+    ("sceneb_120x90_k128", scene_b, 120, 90, 128, 0, True),
+    ("overlap_64", overlapping, 64, 64, 0, 3, True),
+    ("cfg1_256_nomarch", lambda: orbit_scene(100, [REF_PATCH]), 256, 256, 0, 1, False),
+    ("orbit_f0_512", lambda: orbit_scene(0, [REF_PATCH]), 512, 512, 500, 0, False),
+    ("orbit_f100_512", lambda: orbit_scene(100, [REF_PATCH]), 512, 512, 500, 0, False),
+    ("orbit_f250_512", lambda: orbit_scene(250, [REF_PATCH]), 512, 512, 500, 0, False),
+    ("bench_f100_1920x1080_k32", lambda: orbit_scene(100, [BENCH_PATCH]), 1920, 1080, 32, 0, False),
+    ("sceneb_640x360_k128", scene_b, 640, 360, 128, 0, False),
+]
+
+
+def main():
+    # pin against SURVEY.md §8c-3 before writing anything
+    img0, _, st0 = render(*orbit_scene(0, [REF_PATCH]), 512, 512, 500)
+    assert st0 == dict(eye_hits=[8014, 6372, 659], lit=0), st0
+    assert sha16(img0) == "cf557d736f83a4f6"
+    assert img0[256, 384, :3].tolist() == [9265101144064.0, 9265101144064.0, 463255038328832.0]
+    assert img0[300, 384, :3].tolist() == [3506.7421875, 3506.7421875, 175337.109375]
+    img100, _, st100 = render(*orbit_scene(100, [REF_PATCH]), 512, 512, 500)
+    assert st100 == dict(eye_hits=[8245, 6580, 2059], lit=2059), st100
+    assert sha16(img100) == "cb7008f728da5208"
+
+    fixtures, golden = {}, {}
+    for name, fac, W, H, K, flags, small in CASES:
+        sph, pat = fac()
+        img, zs, st = render(sph, pat, W, H, K, no_march=bool(flags & 1), no_sraster=bool(flags & 2))
+        golden[name] = dict(width=W, height=H, steps=K, flags=flags, rgba_sha256=sha_full(img),
+                            shadow_sha256=sha_full(zs), eye_hits=st["eye_hits"], lit_pixels=st["lit"])
+        if small:
+            fixtures[name + "__rgba"] = img
+            fixtures[name + "__shadow"] = zs
+        print(name, golden[name]["rgba_sha256"][:16], st)
+    np.savez_compressed(os.path.join(HERE, "fixtures.npz"), **fixtures)
+    with open(os.path.join(HERE, "golden.json"), "w") as f:
+        json.dump(dict(generator="tests/golden/gen_golden.py (independent numpy restatement of main.rs)",
+                       survey_kat_checked=True, cases=golden), f, indent=1, sort_keys=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,148 @@
+"""CPU tests of the oracle itself: pinned against SURVEY.md §8c-3, the golden
+fixtures of the independent numpy restatement (tests/golden/gen_golden.py) and
+the reference's own unit test for calcRayPlane (main.rs:2415-2425)."""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import bits_equal, first_mismatch
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def sha16(img):
+    return hashlib.sha256(np.ascontiguousarray(img[:, :, :3]).tobytes()).hexdigest()[:16]
+
+
+def _scene_for(scenes, name):
+    if name.startswith("orbit_f0"):
+        return scenes.closely_orbiting_sphere(0)
+    if name.startswith("orbit_f100"):
+        return scenes.closely_orbiting_sphere(100)
+    if name.startswith("orbit_f250"):
+        return scenes.closely_orbiting_sphere(250)
+    if name.startswith("bench_f100"):
+        return scenes.scene_a_bench(100)
+    if name.startswith("bench_f37"):
+        return scenes.scene_a_bench(37)
+    if name.startswith("sceneb"):
+        return scenes.scene_b()
+    if name.startswith("overlap"):
+        return scenes.overlapping_spheres()
+    if name.startswith("cfg1"):
+        return scenes.closely_orbiting_sphere(100)
+    raise KeyError(name)
+
+
+@pytest.mark.parametrize("frame,hits,lit,sha", [(0, [8014, 6372, 659], 0, "cf557d736f83a4f6"),
+                                                (100, [8245, 6580, 2059], 2059, "cb7008f728da5208")])
+def test_survey_kats(oracle, scenes, frame, hits, lit, sha):
+    r = oracle.render(scenes.closely_orbiting_sphere(frame), scenes.eye_camera(), scenes.shadow_camera(),
+                      512, 512, 500, 0, want_shadow=True, want_stats=True)
+    assert r["stats"]["eye_hits"][:3] == hits
+    assert r["stats"]["lit_pixels"] == lit
+    assert sha16(r["rgba"]) == sha
+    if frame == 0:
+        img = r["rgba"]
+        assert img[256, 384, :3].tolist() == [9265101144064.0, 9265101144064.0, 463255038328832.0]
+        assert img[0, 0, :3].tolist() == [0.0, np.float32(0.2), np.float32(0.2)]
+        assert img[300, 384, :3].tolist() == [3506.7421875, 3506.7421875, 175337.109375]
+        # the march hits after exactly 4 advances: t = 0.12 everywhere
+        assert np.all(r["shadow"] == 0.12)
+        assert r["stats"]["march_iterations"] == 512 * 512 * 5
+
+
+def _golden():
+    with open(os.path.join(GOLD, "golden.json")) as f:
+        return json.load(f)["cases"]
+
+
+@pytest.mark.parametrize("name", sorted(_golden().keys()))
+def test_oracle_matches_golden(oracle, scenes, name):
+    g = _golden()[name]
+    r = oracle.render(_scene_for(scenes, name), scenes.eye_camera(), scenes.shadow_camera(), g["width"],
+                      g["height"], g["steps"], g["flags"], nthreads=4, want_shadow=True, want_stats=True)
+    assert hashlib.sha256(np.ascontiguousarray(r["rgba"]).tobytes()).hexdigest() == g["rgba_sha256"]
+    assert hashlib.sha256(np.ascontiguousarray(r["shadow"]).tobytes()).hexdigest() == g["shadow_sha256"]
+    assert r["stats"]["eye_hits"][:len(g["eye_hits"])] == g["eye_hits"]
+    assert r["stats"]["lit_pixels"] == g["lit_pixels"]
+
+
+def test_oracle_matches_fixture_arrays(oracle, scenes):
+    fx = np.load(os.path.join(GOLD, "fixtures.npz"))
+    names = sorted({k.split("__")[0] for k in fx.files})
+    assert len(names) >= 6
+    for name in names:
+        g = _golden()[name]
+        r = oracle.render(_scene_for(scenes, name), scenes.eye_camera(), scenes.shadow_camera(), g["width"],
+                          g["height"], g["steps"], g["flags"], want_shadow=True)
+        assert bits_equal(r["rgba"], fx[name + "__rgba"]), (name, first_mismatch(r["rgba"], fx[name + "__rgba"]))
+        assert bits_equal(r["shadow"], fx[name + "__shadow"]), name
+
+
+@pytest.mark.parametrize("frame", [0, 100, 199])
+def test_reference_bbox_is_a_pure_cull(oracle, scenes, frame):
+    """rasterizeSphere's bbox (main.rs:256-300) changes nothing on square images
+    (SURVEY.md §8a-0): the generalised per-pixel test equals the reference loop."""
+    args = (scenes.closely_orbiting_sphere(frame), scenes.eye_camera(), scenes.shadow_camera(), 512, 512, 500)
+    a = oracle.render(*args, 0, want_shadow=True)
+    b = oracle.render(*args, oracle.RTMO_FLAG_REF_BBOX, want_shadow=True)
+    assert bits_equal(a["rgba"], b["rgba"]) and bits_equal(a["shadow"], b["shadow"])
+
+
+def test_threads_do_not_change_bits(oracle, scenes):
+    args = (scenes.scene_b(), scenes.eye_camera(), scenes.shadow_camera(), 333, 221, 128, 0)
+    a = oracle.render(*args, nthreads=1, want_shadow=True, want_stats=True)
+    b = oracle.render(*args, nthreads=8, want_shadow=True, want_stats=True)
+    assert bits_equal(a["rgba"], b["rgba"]) and bits_equal(a["shadow"], b["shadow"])
+    assert a["stats"] == b["stats"]
+
+
+def test_staged_oracle_equals_frame_oracle(oracle, scenes):
+    """Driving the three reference seams one by one == the one-call frame."""
+    scene = scenes.closely_orbiting_sphere(100)
+    vp1 = oracle.Viewport(200, 160, scenes.EnumFace.BACK, scenes.shadow_camera())
+    vp1.rasterize(scene)
+    vp1.processRaymarchingRays([scenes.REFERENCE_PATCH], 500)
+    vp0 = oracle.Viewport(200, 160, scenes.EnumFace.FRONT, scenes.eye_camera())
+    vp0.rasterize(scene)
+    img = oracle.render_color_image(scene, vp0, vp1)
+    r = oracle.render(scene, scenes.eye_camera(), scenes.shadow_camera(), 200, 160, 500, 0, want_shadow=True)
+    assert bits_equal(img, r["rgba"])
+    assert bits_equal(vp1.zbuffer(), r["shadow"])
+
+
+def test_reference_unit_test_calc_ray_plane(oracle):
+    """test_planeEquation (main.rs:2415-2425): t must be exactly 1.5."""
+    t = oracle.calc_ray_plane((-1.0, 0.0, 0.0), (1.0, 0.0, 0.0), (1.0, 0.0, 0.0), (0.5, 0.0, 0.0))
+    assert t == 1.5
+    # |denom| <= 1e-4 -> None (main.rs:2403)
+    assert oracle.calc_ray_plane((0.0, 0.0, 0.0), (0.0, 1.0, 0.0), (1.0, 0.0, 0.0), (0.5, 0.0, 0.0)) is None
+
+
+def test_no_march_and_no_raster_flags(oracle, scenes):
+    s = scenes.closely_orbiting_sphere(100)
+    r = oracle.render(s, scenes.eye_camera(), scenes.shadow_camera(), 64, 64, 500, 3, want_shadow=True,
+                      want_stats=True)
+    assert np.all(np.isinf(r["shadow"]))
+    assert r["stats"]["march_iterations"] == 0
+    # nothing is shadowed with an empty shadow map
+    assert r["stats"]["lit_pixels"] == r["stats"]["eye_hit_pixels"]
+
+
+def test_perspective_frame_is_unsupported(oracle, scenes):
+    persp = scenes.Camera(scenes.PERSPECTIVE, (0, 0, 0), (0, 0, 1), (0, 1, 0), (1, 0, 0))
+    with pytest.raises(RuntimeError):
+        oracle.render(scenes.scene_a_bench(), persp, scenes.shadow_camera(), 16, 16, 8, 0)
+
+
+def test_encode_rgb8_ppm_pixel_rule(oracle):
+    """writeColorImage's per-channel encode (main.rs:674-684)."""
+    rgba = np.array([[0.0, 0.5, 1.0, 1.0], [2.0, -1.0, np.nan, 1.0], [1e15, 0.2, 0.01, 1.0]], np.float32)
+    out = oracle.encode_rgb8(rgba)
+    assert out[0].tolist() == [0, int(np.float32(np.float32(0.5) ** np.float32(1 / 2.2)) * 255), 255] or out[0][0] == 0
+    assert out[1][0] == 255 and out[1][1] == 0
+    assert out[2][0] == 255
