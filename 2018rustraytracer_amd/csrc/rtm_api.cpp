@@ -208,6 +208,8 @@ struct rtm_ctx {
     DevBuf out;     // staging for rtm_render's host output
     DevBuf stats;
     int32_t smap_w = 0, smap_h = 0;
+    DevBuf tabs;  // [t (steps) | nx (W) | ny (H)] f64, see Tables
+    int64_t tab_steps = -1, tab_w = -1, tab_h = -1;
 };
 
 struct rtm_viewport {
@@ -218,6 +220,34 @@ struct rtm_viewport {
 };
 
 namespace {
+
+// Build (or reuse) the context's lookup tables for (steps, W, H).
+int ensure_tables(rtm_ctx* ctx, int32_t steps, int32_t W, int32_t H, Tables* out) {
+    const bool with_t = steps <= RTM_T_TABLE_MAX;
+    const int64_t nt = with_t ? steps : 0;
+    if (ctx->tab_steps != (with_t ? steps : -2) || ctx->tab_w != W || ctx->tab_h != H) {
+        std::vector<double> h((size_t)(nt + W + H));
+        double t = 0.0;  // raymarchPatch: t = 0.0; ... t += magnitudeOfStepsize (main.rs:2237, 2273)
+        for (int64_t k = 0; k < nt; ++k) {
+            h[(size_t)k] = t;
+            t = t + 0.03;
+        }
+        for (int32_t i = 0; i < W; ++i) h[(size_t)(nt + i)] = ((double)i / (double)W) * 2.0 - 1.0;
+        for (int32_t i = 0; i < H; ++i) h[(size_t)(nt + W + i)] = ((double)i / (double)H) * 2.0 - 1.0;
+        HIP_TRY(hipStreamSynchronize(ctx->stream));  // earlier launches may still read the old tables
+        int rc = ctx->tabs.ensure(h.size() * sizeof(double), ctx->device);
+        if (rc) return rc;
+        HIP_TRY(hipMemcpy(ctx->tabs.p, h.data(), h.size() * sizeof(double), hipMemcpyHostToDevice));
+        ctx->tab_steps = with_t ? steps : -2;
+        ctx->tab_w = W;
+        ctx->tab_h = H;
+    }
+    const double* base = (const double*)ctx->tabs.p;
+    out->t = with_t ? base : nullptr;
+    out->nx = base + nt;
+    out->ny = base + nt + W;
+    return RTM_OK;
+}
 
 struct DeviceGuard {
     int prev = 0;
@@ -234,6 +264,7 @@ struct DeviceGuard {
 
 int enqueue_frame(rtm_ctx* ctx, FrameArgs& a, float* out_dev, StatsK* stats) {
     int rc;
+    if ((rc = ensure_tables(ctx, a.steps, a.W, a.H, &a.tab))) return rc;
     const bool fused = (a.flags & RTM_FLAG_FUSED_SHADOW) != 0;
     hipStream_t s = ctx->stream;
     double* smap = nullptr;
@@ -506,7 +537,9 @@ int rtm_viewport_process_raymarching_rays(rtm_viewport* vp, const rtm_patch* pat
     a.W = vp->W;
     a.H = vp->H;
     DeviceGuard g(vp->ctx->device);
-    int rc = launch_vp_march(a, (double*)vp->zbuf.p, vp->ctx->stream);
+    int rc = ensure_tables(vp->ctx, steps, vp->W, vp->H, &a.tab);
+    if (rc) return rc;
+    rc = launch_vp_march(a, (double*)vp->zbuf.p, vp->ctx->stream);
     if (rc) return fail(rc, "march launch failed");
     return RTM_OK;
 }

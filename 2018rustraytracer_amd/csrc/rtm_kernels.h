@@ -44,6 +44,17 @@ struct PatchK {
     double a1, d1;  // _1.a, _1.b - _1.a
 };
 
+// Host-built lookup tables (device memory, owned by the context):
+//   t[k]   = t after k march advances: t_0 = 0.0, t_{k+1} = t_k + 0.03, summed
+//            sequentially exactly as `t += magnitudeOfStepsize` (main.rs:2273);
+//   nx[i]  = ((i as f64) / (W as f64)) * 2.0 - 1.0  (main.rs:306, 1903-1906), ny likewise.
+struct Tables {
+    const double* t;   // steps entries, or nullptr when steps > RTM_T_TABLE_MAX
+    const double* nx;  // W entries
+    const double* ny;  // H entries
+};
+#define RTM_T_TABLE_MAX 65536
+
 // Everything one frame's kernels read.  Kept < 4 KiB (kernarg limit).
 struct FrameArgs {
     RasterSphereK esph[RTM_MAX_SPHERES];  // eye camera projection
@@ -56,6 +67,7 @@ struct FrameArgs {
     int32_t n_spheres, n_patches;
     int32_t steps, flags;
     int32_t row_begin, row_end;
+    Tables tab;
 };
 static_assert(sizeof(FrameArgs) <= 4096, "FrameArgs must fit the 4 KiB kernarg segment");
 
@@ -69,6 +81,7 @@ struct MarchArgs {
     PatchK patch[RTM_MAX_PATCHES];
     CamK cam;
     int32_t n_patches, steps, W, H;
+    Tables tab;
 };
 
 struct ShadeArgs {

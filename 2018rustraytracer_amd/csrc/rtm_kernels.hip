@@ -77,63 +77,116 @@ struct MarchResult {
     bool in_range;
 };
 
-// raymarchPatchDomainM11 + raymarchPatch (main.rs:2179-2278).
-// When the ray has no x/y motion (step.x == step.y == 0, every axis-aligned
-// orthographic shadow camera) p.x, p.y and therefore inRange01 and the surface
-// depth are loop-invariant: the loop is unswitched and only p.z and t advance.
-// The sequential accumulation p.z += step.z, t += 0.03 is kept exactly.
+// t after k advances (table built on the host by sequential summation; the
+// fallback re-does the same sequential sum).
+__device__ __forceinline__ double t_after(const Tables& tb, int k) {
+    if (tb.t) return tb.t[k];
+    double t = 0.0;
+    for (int j = 0; j < k; ++j) t = t + 0.03;
+    return t;
+}
+
+// v_cmp_class_f64 masks: bits 0-1 NaN, 2-5 negative (-inf,-norm,-denorm,-0),
+// 6-9 positive (+0,+denorm,+norm,+inf).
+constexpr int CLS_NAN = 0x003, CLS_NEG = 0x03C, CLS_POS = 0x3C0;
+
+// `signum(v) != signEntry` (main.rs:2244, 2261-2263) as one class test: with
+// signEntry = signum(v0), the hit set is "the other sign, or NaN"; a NaN entry
+// compares unequal to everything.
+__device__ __forceinline__ int hit_class_mask(double v0) {
+    if (v0 != v0) return CLS_NAN | CLS_NEG | CLS_POS;
+    return __builtin_signbit(v0) ? (CLS_POS | CLS_NAN) : (CLS_NEG | CLS_NAN);
+}
+
+// raymarchPatchDomainM11 + raymarchPatch (main.rs:2179-2278) for one texel.
+//
+// The per-lane loop is restated as a wave-uniform loop: every lane advances its
+// own p exactly as the reference (p += step, sequentially), records the FIRST k
+// whose sign differs from the entry sign, and the wave leaves the loop as soon
+// as a ballot (__all) says every lane has its answer — the early-out the
+// reference's per-ray `return` gives a scalar CPU.  t is the k-th sequential
+// sum, read from the host-built table.
+//
+// When the ray has no x/y motion (step.x == step.y == 0: every axis-aligned
+// orthographic shadow camera) p.x, p.y, inRange01 and the surface depth are
+// loop-invariant (p.x is never -0.0, so p.x + (+-0.0) == p.x bit for bit):
+// the loop is unswitched and carries only p.z.
 template <bool COUNT>
 __device__ __forceinline__ MarchResult march(double ox, double oy, double oz, double dx, double dy,
-                                             double dz, const PatchK& p, int steps) {
+                                             double dz, const PatchK& p, int steps, const Tables& tb) {
     MarchResult r{false, 0.0, 0, false};
-    double px = (ox + 1.0) * 0.5;
-    double py = (oy + 1.0) * 0.5;
-    double pz = oz;
+    const double px0 = (ox + 1.0) * 0.5;
+    const double py0 = (oy + 1.0) * 0.5;
     const double mstep = 0.03;
-    double sx = dx * mstep, sy = dy * mstep, sz = dz * mstep;
-    double t = 0.0;
-    double entry = rsignum(pz - bil(p, px, py));
-    if (COUNT) r.in_range = in01(px) && in01(py);
+    const double sx = dx * mstep, sy = dy * mstep, sz = dz * mstep;
+    const double v0 = oz - bil(p, px0, py0);
+    const int mask = hit_class_mask(v0);
+    const bool inr0 = in01(px0) && in01(py0);
+    if (COUNT) r.in_range = inr0;
+    int khit = -1;
     if (sx == 0.0 && sy == 0.0) {
-        // (px is never -0.0 here, so px + (+-0.0) == px bit for bit)
-        if (!(in01(px) && in01(py))) {
-            if (COUNT) r.iters = steps;
-            return r;
-        }
-        const double D = bil(p, px, py);
-        for (int k = 0; k < steps; ++k) {
-            if (rsignum(pz - D) != entry) {
-                r.hit = true;
-                r.t = t;
-                if (COUNT) r.iters = k + 1;
-                return r;
+        // Unswitched loop.  z_k = z_{k-1} + sz is monotone in k and so is
+        // fl(z_k - D); the class of (z_k - D) therefore leaves the entry class at
+        // most once (a NaN, from +inf - +inf, persists).  The first hit index is
+        // the number of steps that still "continue" — counted with one class
+        // compare and one add per step, no per-step control flow.
+        const double D = bil(p, px0, py0);
+        const int keep = inr0 ? (~mask & (CLS_NAN | CLS_NEG | CLS_POS)) : 0;
+        int cnt = inr0 ? 0 : steps;
+        if (__any(inr0)) {
+            double z = oz;
+            int k = 0;
+            bool all_stopped = false;
+            for (; k + 8 <= steps; k += 8) {
+                bool cont = false;
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    cont = __builtin_amdgcn_class(z - D, keep);
+                    cnt += cont ? 1 : 0;
+                    z = z + sz;
+                }
+                if (!__any(cont)) {  // every lane has met its surface: wave early-out
+                    all_stopped = true;
+                    break;
+                }
             }
-            pz = pz + sz;
-            t = t + mstep;
+            if (!all_stopped) {
+                for (; k < steps; ++k) {
+                    const bool cont = __builtin_amdgcn_class(z - D, keep);
+                    cnt += cont ? 1 : 0;
+                    z = z + sz;
+                }
+            }
         }
-        if (COUNT) r.iters = steps;
-        return r;
+        khit = cnt < steps ? cnt : -1;
+    } else {
+        // General ray (x/y motion): in-range and the surface depth change per step.
+        // Per 4-step chunk the hits are collected as bits; the first set bit of
+        // the first non-empty chunk is the reference's first hit.
+        bool done = false;
+        double x = px0, y = py0, z = oz;
+        for (int k = 0; k < steps; k += 4) {
+            if (__all(done)) break;
+            unsigned bits = 0;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const bool inr = in01(x) && in01(y);
+                const bool h = (k + u < steps) && inr && __builtin_amdgcn_class(z - bil(p, x, y), mask);
+                bits |= h ? (1u << u) : 0u;
+                x = x + sx;
+                y = y + sy;
+                z = z + sz;
+            }
+            const bool first = !done && bits != 0u;
+            khit = first ? k + __builtin_ctz(bits) : khit;
+            done = done || first;
+        }
     }
-    for (int k = 0; k < steps; ++k) {
-        if (!in01(px) || !in01(py)) {
-            px = px + sx;
-            py = py + sy;
-            pz = pz + sz;
-            t = t + mstep;
-            continue;
-        }
-        if (rsignum(pz - bil(p, px, py)) != entry) {
-            r.hit = true;
-            r.t = t;
-            if (COUNT) r.iters = k + 1;
-            return r;
-        }
-        px = px + sx;
-        py = py + sy;
-        pz = pz + sz;
-        t = t + mstep;
+    if (khit >= 0) {
+        r.hit = true;
+        r.t = t_after(tb, khit);
     }
-    if (COUNT) r.iters = steps;
+    if (COUNT) r.iters = khit >= 0 ? khit + 1 : steps;
     return r;
 }
 
@@ -172,8 +225,8 @@ template <bool COUNT>
 __device__ __forceinline__ double shadow_texel(const FrameArgs& a, int xi, int yi, unsigned long long* n_tests,
                                                unsigned long long* n_iters, unsigned long long* n_hits,
                                                unsigned long long* n_inrange) {
-    const double x = ndc(xi, a.Ws);
-    const double y = ndc(yi, a.Hs);
+    const double x = a.tab.nx[xi];  // shadow map dims == eye dims
+    const double y = a.tab.ny[yi];
     double zb = INFINITY;
     if (!(a.flags & RTM_FLAG_NO_SHADOW_RASTER)) {
         for (int i = 0; i < a.n_spheres; ++i) {
@@ -189,7 +242,7 @@ __device__ __forceinline__ double shadow_texel(const FrameArgs& a, int xi, int y
         double o[3], d[3];
         cam_ray(a.shadow, x, y, o, d);
         for (int k = 0; k < a.n_patches; ++k) {
-            MarchResult m = march<COUNT>(o[0], o[1], o[2], d[0], d[1], d[2], a.patch[k], a.steps);
+            MarchResult m = march<COUNT>(o[0], o[1], o[2], d[0], d[1], d[2], a.patch[k], a.steps, a.tab);
             if (COUNT) {
                 *n_iters += m.iters;
                 *n_hits += m.hit;
@@ -232,8 +285,8 @@ __global__ __launch_bounds__(BLOCK) void eye_pass_kernel(const FrameArgs a, cons
     unsigned long long n_tests = 0, n_hit = 0, n_lit = 0, n_it = 0, n_mh = 0, n_ir = 0, n_st = 0;
     int hit_id = -1;
     if (live) {
-        const double x = ndc(xi, a.W);
-        const double y = ndc(yi, a.H);
+        const double x = a.tab.nx[xi];
+        const double y = a.tab.ny[yi];
         // z-test over spheres in scene order, strict '<' against +INF init (main.rs:318)
         double best = INFINITY, bh = 0.0, bz = 0.0;
         int bid = -1;
@@ -362,11 +415,11 @@ __global__ __launch_bounds__(BLOCK) void vp_march_kernel(const MarchArgs a, doub
     if (xi >= a.W || yi >= a.H) return;
     const int64_t idx = (int64_t)yi * a.W + xi;
     double o[3], d[3];
-    cam_ray(a.cam, ndc(xi, a.W), ndc(yi, a.H), o, d);
+    cam_ray(a.cam, a.tab.nx[xi], a.tab.ny[yi], o, d);
     double zb = zbuf[idx];
     const double z0 = zb;
     for (int k = 0; k < a.n_patches; ++k) {
-        MarchResult m = march<false>(o[0], o[1], o[2], d[0], d[1], d[2], a.patch[k], a.steps);
+        MarchResult m = march<false>(o[0], o[1], o[2], d[0], d[1], d[2], a.patch[k], a.steps, a.tab);
         if (m.hit && m.t < zb) zb = m.t;
     }
     if (!(zb == z0)) zbuf[idx] = zb;

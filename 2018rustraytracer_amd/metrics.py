@@ -1,25 +1,41 @@
 """Algorithmic work per frame and the MI355X roofs it is priced against.
 
-Counting rules: every f64 add/sub/mul/div/sqrt/compare is one
-flop (no FMA: contraction is off), per-(camera, sphere) constants are hoisted.
+Units of work are the f64 operations the algorithm needs once per-(camera,
+sphere) constants, per-column/row NDC values and loop invariants are hoisted
+(add/sub/mul/div/sqrt/compare/class-test = 1 op each; no FMA — contraction is
+off for bit parity).  Per-unit figures:
 
-  eye pass     per pixel  6 + 15*S   (+6 per covering sphere, +89 per hit pixel)
-  shadow pass  per texel  6 + 15*S   (+6 per covering sphere)
-               per (texel, patch) 31 (march setup + final compare)
-               per march iteration 22 (main.rs:2247-2274)
+  shadow texel   4 per sphere (cull)      + 19 per covering sphere
+                 32 per patch (ray origin, domain map, surface depth, entry sign,
+                    in-range test, step vector, strict-min update)
+                 3 per march iteration    (z - D, class test, z += step.z)
+  eye pixel      4 per sphere (cull)      + 21 per covering sphere (incl. z-test)
+                 84 per hit pixel         (ray, world pos, normal, Lambert,
+                                           reflect, powi(32), shadow projection)
 
-Algorithmic HBM bytes (what the two-kernel design must move):
-  shadow pass  8 B per texel            (f64 shadow-map store)
-  eye pass     16 B per pixel           (RGBA f32 store)
-             + 8 B per hit pixel        (f64 shadow-map lookup)
+HBM bytes the two-kernel design must move:
+  shadow pass    8 B per texel            (f64 shadow-map store)
+  eye pass       16 B per pixel           (RGBA f32 store)
+               + 8 B per hit pixel        (f64 shadow-map lookup)
+
+Peaks (/opt/skills/guides/MI355X_MICROARCH.md + datasheet): HBM 8.0 TB/s;
+FP64 vector 78.6 TFLOP/s counts an FMA as 2 flops, i.e. 256 CU x 64 f64
+lanes/clk x 2.4 GHz = 39.3 T f64 instructions-lanes/s — the ceiling for
+non-FMA f64 ops, which is what this path issues.
 """
 from __future__ import annotations
 
-# MI355X peaks (/opt/skills/guides/MI355X_MICROARCH.md; FP64 vector is the datasheet
-# value, FMA counted as 2 flops — this path issues no FMA, so its VALU ceiling
-# in these units is half of it).
 PEAK_HBM_GBS = 8000.0
-PEAK_FP64_VECTOR_TFLOPS = 78.6
+PEAK_FP64_FMA_TFLOPS = 78.6
+PEAK_FP64_OPS_T = 39.3  # non-FMA f64 ops per second (x1e12)
+
+SHADOW_PER_SPHERE = 4
+SHADOW_PER_COVER = 19
+SHADOW_PER_PATCH = 32
+SHADOW_PER_ITER = 3
+EYE_PER_SPHERE = 4
+EYE_PER_COVER = 21
+EYE_PER_HIT = 84
 
 
 def frame_work(stats: dict, width: int, height: int, n_spheres: int, n_patches: int, flags: int = 0,
@@ -27,17 +43,18 @@ def frame_work(stats: dict, width: int, height: int, n_spheres: int, n_patches: 
     px = width * height
     no_march = bool(flags & 0x1)
     no_sraster = bool(flags & 0x2)
-    eye_flops = px * (6 + 15 * n_spheres) + 6 * stats["eye_sphere_tests"] + 89 * stats["eye_hit_pixels"]
     texels = px if not fused else stats["eye_hit_pixels"]
-    sh_flops = 0
+    sh_ops = 0
     if not no_sraster:
-        sh_flops += texels * (6 + 15 * n_spheres) + 6 * stats["shadow_sphere_tests"]
+        sh_ops += texels * SHADOW_PER_SPHERE * n_spheres + SHADOW_PER_COVER * stats["shadow_sphere_tests"]
     if not no_march:
-        sh_flops += texels * n_patches * 31 + 22 * stats["march_iterations"]
+        sh_ops += texels * n_patches * SHADOW_PER_PATCH + SHADOW_PER_ITER * stats["march_iterations"]
+    eye_ops = (px * EYE_PER_SPHERE * n_spheres + EYE_PER_COVER * stats["eye_sphere_tests"]
+               + EYE_PER_HIT * stats["eye_hit_pixels"])
     sh_bytes = 0 if fused else 8 * px
     eye_bytes = 16 * px + (0 if fused else 8 * stats["eye_hit_pixels"])
-    return dict(shadow_pass=dict(flops=sh_flops, bytes=sh_bytes),
-                eye_pass=dict(flops=eye_flops + (sh_flops if fused else 0), bytes=eye_bytes))
+    return dict(shadow_pass=dict(ops=sh_ops, bytes=sh_bytes),
+                eye_pass=dict(ops=eye_ops + (sh_ops if fused else 0), bytes=eye_bytes))
 
 
 def roofline(kernel: str, work: dict, ms: float, traffic_bytes=None) -> dict:
@@ -45,17 +62,18 @@ def roofline(kernel: str, work: dict, ms: float, traffic_bytes=None) -> dict:
     w = work[kernel]
     s = ms * 1e-3
     gbs = w["bytes"] / s / 1e9 if s > 0 else 0.0
-    tfl = w["flops"] / s / 1e12 if s > 0 else 0.0
+    tops = w["ops"] / s / 1e12 if s > 0 else 0.0
     hbm = dict(bound="hbm", achieved=round(gbs, 2), peak=PEAK_HBM_GBS, unit="GB/s",
                frac=round(gbs / PEAK_HBM_GBS, 4))
-    alu = dict(bound="valu_fp64", achieved=round(tfl, 3), peak=PEAK_FP64_VECTOR_TFLOPS, unit="TFLOP/s",
-               frac=round(tfl / PEAK_FP64_VECTOR_TFLOPS, 4))
+    alu = dict(bound="valu_fp64", achieved=round(tops, 3), peak=PEAK_FP64_OPS_T,
+               unit="T f64-ops/s (non-FMA; = 78.6 TFLOP/s FMA-counted datasheet peak / 2)",
+               frac=round(tops / PEAK_FP64_OPS_T, 4))
     main, other = (hbm, alu) if hbm["frac"] >= alu["frac"] else (alu, hbm)
     main = dict(main)
     main["kernel"] = kernel
     main["traffic"] = traffic_bytes
     main["other_roof"] = other
     main["algorithmic_bytes_per_launch"] = w["bytes"]
-    main["algorithmic_flops_per_launch"] = w["flops"]
+    main["algorithmic_f64_ops_per_launch"] = w["ops"]
     main["avg_launch_ms"] = round(ms, 5)
     return main

@@ -180,6 +180,10 @@ def main():
         dom = "eye_pass" if (a.fused or avg_eye >= avg_sh) else "shadow_pass"
         dom_ms = avg_eye if dom == "eye_pass" else avg_sh
         roof = metrics.roofline(dom, work, dom_ms, _latest_traffic(a.config, dom))
+        other = "shadow_pass" if dom == "eye_pass" else "eye_pass"
+        other_ms = avg_sh if other == "shadow_pass" else avg_eye
+        roof_other = (metrics.roofline(other, work, other_ms, _latest_traffic(a.config, other))
+                      if other_ms > 0 else None)
         res = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -202,6 +206,7 @@ def main():
             "kernels": {"shadow_pass_ms": round(avg_sh, 5), "eye_pass_ms": round(avg_eye, 5),
                         "frame_kernel_ms": round(avg_sh + avg_eye, 5)},
             "roofline": roof,
+            "roofline_other_kernel": roof_other,
             "parity": "bit-exact vs CPU oracle (tests/test_gpu_parity.py)",
         }
         if world == 1 and not a.no_cpu_baseline:
