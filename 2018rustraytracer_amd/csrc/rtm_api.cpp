@@ -210,6 +210,8 @@ struct rtm_ctx {
     int32_t smap_w = 0, smap_h = 0;
     DevBuf tabs;  // [t (steps) | nx (W) | ny (H)] f64, see Tables
     int64_t tab_steps = -1, tab_w = -1, tab_h = -1;
+    uint64_t tab_zkey = 0;
+    bool tab_hasz = false;
 };
 
 struct rtm_viewport {
@@ -221,12 +223,47 @@ struct rtm_viewport {
 
 namespace {
 
-// Build (or reuse) the context's lookup tables for (steps, W, H).
-int ensure_tables(rtm_ctx* ctx, int32_t steps, int32_t W, int32_t H, Tables* out) {
+// Shared march depth sequence: an ORTHOGONAL camera with no x/y ray motion and
+// side.z == up.z == 0 starts every texel at the same z (origin z =
+// (pos.z + side.z*s) + up.z*u == pos.z bit for bit, or +0.0 when pos.z == +0.0;
+// a -0.0 pos.z would make the sign of zero depend on s, u: not shared).
+bool shared_z0(const rtm_camera* c, double* z0, double* sz) {
+    if (!c || c->type != RTM_CAMERA_ORTHOGONAL) return false;
+    if (!(c->dir[0] * 0.03 == 0.0 && c->dir[1] * 0.03 == 0.0)) return false;
+    if (!(c->side[2] == 0.0 && c->up[2] == 0.0)) return false;
+    if (c->pos[2] == 0.0 && std::signbit(c->pos[2])) return false;
+    *z0 = c->pos[2] == 0.0 ? 0.0 : c->pos[2];
+    *sz = c->dir[2] * 0.03;  // dir.scale(magnitudeOfStepsize) (main.rs:2233)
+    return std::isfinite(*z0) && std::isfinite(*sz);
+}
+
+uint64_t bits_of(double v) {
+    uint64_t b;
+    std::memcpy(&b, &v, sizeof b);
+    return b;
+}
+
+// Build (or reuse) the context's lookup tables for (steps, W, H, march camera).
+int ensure_tables(rtm_ctx* ctx, int32_t steps, int32_t W, int32_t H, const rtm_camera* march_cam, Tables* out) {
     const bool with_t = steps <= RTM_T_TABLE_MAX;
     const int64_t nt = with_t ? steps : 0;
-    if (ctx->tab_steps != (with_t ? steps : -2) || ctx->tab_w != W || ctx->tab_h != H) {
-        std::vector<double> h((size_t)(nt + W + H));
+    double z0 = 0.0, sz = 0.0;
+    bool with_z = with_t && shared_z0(march_cam, &z0, &sz);
+    std::vector<double> zt;
+    if (with_z) {
+        zt.resize((size_t)nt);
+        double z = z0;  // p.z after k advances: p = &p + &step (main.rs:2272)
+        for (int64_t k = 0; k < nt; ++k) {
+            zt[(size_t)k] = z;
+            z = z + sz;
+            if (!std::isfinite(zt[(size_t)k])) with_z = false;
+        }
+    }
+    const int64_t nz = with_z ? nt : 0;
+    const uint64_t zkey = with_z ? (bits_of(z0) * 1000003u) ^ bits_of(sz) : 0x5eed;
+    if (ctx->tab_steps != (with_t ? steps : -2) || ctx->tab_w != W || ctx->tab_h != H || ctx->tab_zkey != zkey ||
+        ctx->tab_hasz != with_z) {
+        std::vector<double> h((size_t)(nt + W + H + nz));
         double t = 0.0;  // raymarchPatch: t = 0.0; ... t += magnitudeOfStepsize (main.rs:2237, 2273)
         for (int64_t k = 0; k < nt; ++k) {
             h[(size_t)k] = t;
@@ -234,6 +271,7 @@ int ensure_tables(rtm_ctx* ctx, int32_t steps, int32_t W, int32_t H, Tables* out
         }
         for (int32_t i = 0; i < W; ++i) h[(size_t)(nt + i)] = ((double)i / (double)W) * 2.0 - 1.0;
         for (int32_t i = 0; i < H; ++i) h[(size_t)(nt + W + i)] = ((double)i / (double)H) * 2.0 - 1.0;
+        for (int64_t k = 0; k < nz; ++k) h[(size_t)(nt + W + H + k)] = zt[(size_t)k];
         HIP_TRY(hipStreamSynchronize(ctx->stream));  // earlier launches may still read the old tables
         int rc = ctx->tabs.ensure(h.size() * sizeof(double), ctx->device);
         if (rc) return rc;
@@ -241,11 +279,14 @@ int ensure_tables(rtm_ctx* ctx, int32_t steps, int32_t W, int32_t H, Tables* out
         ctx->tab_steps = with_t ? steps : -2;
         ctx->tab_w = W;
         ctx->tab_h = H;
+        ctx->tab_zkey = zkey;
+        ctx->tab_hasz = with_z;
     }
     const double* base = (const double*)ctx->tabs.p;
     out->t = with_t ? base : nullptr;
     out->nx = base + nt;
     out->ny = base + nt + W;
+    out->z = with_z ? base + nt + W + H : nullptr;
     return RTM_OK;
 }
 
@@ -264,7 +305,15 @@ struct DeviceGuard {
 
 int enqueue_frame(rtm_ctx* ctx, FrameArgs& a, float* out_dev, StatsK* stats) {
     int rc;
-    if ((rc = ensure_tables(ctx, a.steps, a.W, a.H, &a.tab))) return rc;
+    rtm_camera sc{};
+    sc.type = a.shadow.type;
+    for (int i = 0; i < 3; ++i) {
+        sc.pos[i] = a.shadow.pos[i];
+        sc.dir[i] = a.shadow.dir[i];
+        sc.up[i] = a.shadow.up[i];
+        sc.side[i] = a.shadow.side[i];
+    }
+    if ((rc = ensure_tables(ctx, a.steps, a.W, a.H, &sc, &a.tab))) return rc;
     const bool fused = (a.flags & RTM_FLAG_FUSED_SHADOW) != 0;
     hipStream_t s = ctx->stream;
     double* smap = nullptr;
@@ -537,7 +586,7 @@ int rtm_viewport_process_raymarching_rays(rtm_viewport* vp, const rtm_patch* pat
     a.W = vp->W;
     a.H = vp->H;
     DeviceGuard g(vp->ctx->device);
-    int rc = ensure_tables(vp->ctx, steps, vp->W, vp->H, &a.tab);
+    int rc = ensure_tables(vp->ctx, steps, vp->W, vp->H, &vp->cam, &a.tab);
     if (rc) return rc;
     rc = launch_vp_march(a, (double*)vp->zbuf.p, vp->ctx->stream);
     if (rc) return fail(rc, "march launch failed");

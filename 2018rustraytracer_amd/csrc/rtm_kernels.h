@@ -48,10 +48,13 @@ struct PatchK {
 //   t[k]   = t after k march advances: t_0 = 0.0, t_{k+1} = t_k + 0.03, summed
 //            sequentially exactly as `t += magnitudeOfStepsize` (main.rs:2273);
 //   nx[i]  = ((i as f64) / (W as f64)) * 2.0 - 1.0  (main.rs:306, 1903-1906), ny likewise.
+//   z[k]   = p.z after k advances when every texel of the shadow camera starts at
+//            the same z (host-proved, see ensure_tables): z_0 = z0, z_{k+1} = z_k + step.z.
 struct Tables {
     const double* t;   // steps entries, or nullptr when steps > RTM_T_TABLE_MAX
     const double* nx;  // W entries
     const double* ny;  // H entries
+    const double* z;   // steps entries, or nullptr (no shared z sequence)
 };
 #define RTM_T_TABLE_MAX 65536
 

@@ -128,12 +128,41 @@ __device__ __forceinline__ MarchResult march(double ox, double oy, double oz, do
         // Unswitched loop.  z_k = z_{k-1} + sz is monotone in k and so is
         // fl(z_k - D); the class of (z_k - D) therefore leaves the entry class at
         // most once (a NaN, from +inf - +inf, persists).  The first hit index is
-        // the number of steps that still "continue" — counted with one class
-        // compare and one add per step, no per-step control flow.
+        // the number of steps that still "continue" — counted with one compare
+        // and one add per step, no per-step control flow.
         const double D = bil(p, px0, py0);
-        const int keep = inr0 ? (~mask & (CLS_NAN | CLS_NEG | CLS_POS)) : 0;
         int cnt = inr0 ? 0 : steps;
-        if (__any(inr0)) {
+        // Shared z sequence (host table): for finite, nonzero D and finite z,
+        // class(z - D) is POS iff z >= D and NEG iff z < D (z - D is +0 when
+        // z == D), so a plain compare against the table decides each step.
+        const bool fast_ok = tb.z != nullptr && (!inr0 || (fabs(D) < INFINITY && D != 0.0));
+        if (__any(inr0) && __all(fast_ok)) {
+            const __attribute__((address_space(4))) double* zt =
+                (const __attribute__((address_space(4))) double*)tb.z;
+            const bool epos = !(oz < D);  // entry class POS <=> z0 >= D
+            int lt = 0;                   // #steps with z_k < D
+            int k = 0;
+            bool all_stopped = false;
+            for (; k + 8 <= steps; k += 8) {
+                bool last_lt = false;
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    last_lt = zt[k + u] < D;
+                    lt += last_lt ? 1 : 0;
+                }
+                const bool cont = inr0 && (epos ? !last_lt : last_lt);
+                if (!__any(cont)) {
+                    k += 8;
+                    all_stopped = true;
+                    break;
+                }
+            }
+            if (!all_stopped)
+                for (; k < steps; ++k) lt += (zt[k] < D) ? 1 : 0;
+            const int ran = k;
+            if (inr0) cnt = epos ? ran - lt : lt;
+        } else if (__any(inr0)) {
+            const int keep = inr0 ? (~mask & (CLS_NAN | CLS_NEG | CLS_POS)) : 0;
             double z = oz;
             int k = 0;
             bool all_stopped = false;

@@ -86,10 +86,13 @@ def main():
 
     rtm = importlib.import_module("2018rustraytracer_amd")
     sc = importlib.import_module("2018rustraytracer_amd.scenes")
+    shard = importlib.import_module("2018rustraytracer_amd.shard")
     metrics = importlib.import_module("2018rustraytracer_amd.metrics")
     cfg = sc.CONFIGS[a.config]
     W, H, K = cfg["width"], cfg["height"], cfg["steps"]
-    flags = cfg["flags"] | (rtm.abi.RTM_FLAG_FUSED_SHADOW if a.fused else 0)
+    # tile-gather: each band evaluates only the shadow texels it reads (no cross-rank shadow map)
+    fused = a.fused or a.mode == "tile-gather"
+    flags = cfg["flags"] | (rtm.abi.RTM_FLAG_FUSED_SHADOW if fused else 0)
     eye, shadow = sc.eye_camera(), sc.shadow_camera()
     ctx = rtm.Context(local)
     ctx.set_timing_capacity(a.steps)
@@ -109,14 +112,11 @@ def main():
         out = torch.empty((H, W, 4), dtype=torch.float32, device=f"cuda:{local}")
         rows = (0, H)
     else:
-        band = (H + world - 1) // world
-        r0, r1 = min(H, rank * band), min(H, (rank + 1) * band)
-        rows = (r0, r1)
+        band = shard.band_rows(H, world)
+        rows = shard.row_band(H, world, rank)
         scenes = [scene_for(i) for i in range(total)]
         c_scenes = [s.to_c() for s in scenes]
         bufs = [torch.zeros((band, W, 4), dtype=torch.float32, device=f"cuda:{local}") for _ in range(2)]
-        gathered = ([torch.empty((band, W, 4), dtype=torch.float32, device=f"cuda:{local}")
-                     for _ in range(world)] if rank == 0 else None)
         ext = torch.cuda.ExternalStream(ctx.stream, device=torch.device("cuda", local))
 
     lib = rtm.load_library()
@@ -140,7 +140,7 @@ def main():
                                           flags, rows[0], rows[1], C.c_void_p(bufs[b].data_ptr()))
                 rtm.abi.check(lib, rc, "rtm_render_async")
             if world > 1:
-                pending[b] = dist.gather(bufs[b], gathered, dst=0, async_op=True)
+                pending[b], _ = shard.gather_bands(bufs[b], rank, world, H, dist, async_op=True)
 
     def barrier():
         if world > 1:
@@ -176,8 +176,12 @@ def main():
         s0 = scenes[a.warmup]
         band_h = rows[1] - rows[0]
         st = ctx.stats(s0, eye, shadow, W, H, K, flags)
-        work = metrics.frame_work(st, W, H, len(s0.spherePrimitives), len(s0.patches), flags, fused=a.fused)
-        dom = "eye_pass" if (a.fused or avg_eye >= avg_sh) else "shadow_pass"
+        work = metrics.frame_work(st, W, H, len(s0.spherePrimitives), len(s0.patches), flags, fused=fused)
+        if band_h != H:  # rank 0 renders one band: scale the frame's work to it (approximate)
+            for kk in work.values():
+                kk["ops"] = int(kk["ops"] * band_h / H)
+                kk["bytes"] = int(kk["bytes"] * band_h / H)
+        dom = "eye_pass" if (fused or avg_eye >= avg_sh) else "shadow_pass"
         dom_ms = avg_eye if dom == "eye_pass" else avg_sh
         roof = metrics.roofline(dom, work, dom_ms, _latest_traffic(a.config, dom))
         other = "shadow_pass" if dom == "eye_pass" else "eye_pass"
@@ -199,7 +203,7 @@ def main():
             "data": "synthetic: Scene A-bench (SURVEY.md §8d-2) animation frames 100+i, f64 scene built on host"
                     if a.config in (2, 3, 4) else "synthetic: SURVEY.md §8d-2 scene",
             "config": {"workload": cfg["desc"], "config_id": a.config, "width": W, "height": H,
-                       "march_steps": K, "mode": a.mode, "shadow": "fused" if a.fused else "two-pass",
+                       "march_steps": K, "mode": a.mode, "shadow": "fused" if fused else "two-pass",
                        "parallelism": (f"frame-parallel x{world}" if a.mode == "frames"
                                        else f"row-bands x{world} + rccl gather"),
                        "rows_rank0": band_h},

@@ -1,0 +1,65 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 --pmc passes into per-kernel averages per dispatch.
+
+HBM bytes follow /opt/skills/guides/MI355X_MICROARCH.md §HBM: FETCH_SIZE and
+WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE reports 1/2 of the bytes of wide
+coalesced streaming reads (x2 applied, flagged), WRITE_SIZE is exact for
+16-B-per-lane streaming stores.  The counters include Infinity-Cache hits."""
+import argparse
+import csv
+import glob
+import json
+import os
+import re
+from collections import defaultdict
+
+
+def short(name):
+    m = re.search(r"(shadow_pass_kernel|eye_pass_kernel|vp_\w+_kernel|fill_kernel)(<[^>]*>)?", name)
+    return (m.group(1) + (m.group(2) or "")) if m else name[:60]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("dir")
+    ap.add_argument("--config", type=int, default=3)
+    ap.add_argument("--tag", default="")
+    a = ap.parse_args()
+    vals = defaultdict(lambda: defaultdict(list))  # kernel -> counter -> per-dispatch values
+    durs = defaultdict(list)
+    for f in glob.glob(os.path.join(a.dir, "**", "*counter_collection.csv"), recursive=True):
+        per = defaultdict(lambda: defaultdict(float))
+        for row in csv.DictReader(open(f)):
+            k = short(row.get("Kernel_Name", ""))
+            did = row.get("Dispatch_Id") or row.get("Correlation_Id")
+            per[(k, did)][row["Counter_Name"]] += float(row["Counter_Value"])
+        for (k, did), cs in per.items():
+            for c, v in cs.items():
+                vals[k][c].append(v)
+    for f in glob.glob(os.path.join(a.dir, "**", "*kernel_trace.csv"), recursive=True):
+        for row in csv.DictReader(open(f)):
+            durs[short(row["Kernel_Name"])].append(int(row["End_Timestamp"]) - int(row["Start_Timestamp"]))
+    out = {"config": a.config, "tag": a.tag, "source": "rocprofv3 --pmc, one pass per counter group",
+           "kernels": {}}
+    for k, cs in vals.items():
+        d = {c: sum(v) / len(v) for c, v in cs.items()}
+        d["dispatches"] = max(len(v) for v in cs.values())
+        if durs.get(k):
+            d["avg_duration_ns_profiled"] = sum(durs[k]) / len(durs[k])
+        if "FETCH_SIZE" in d or "WRITE_SIZE" in d:
+            fetch = d.get("FETCH_SIZE", 0.0) * 1024 * 2  # gfx950: FETCH_SIZE reads 1/2 of wide streaming reads
+            write = d.get("WRITE_SIZE", 0.0) * 1024
+            d["hbm_bytes_per_launch"] = int(fetch + write)
+            d["hbm_bytes_note"] = "(FETCH_SIZE*2 + WRITE_SIZE) KiB->B; includes Infinity-Cache hits"
+        if "SQ_INSTS_VALU" in d and "SQ_WAVES" in d and d["SQ_WAVES"]:
+            d["valu_insts_per_wave"] = d["SQ_INSTS_VALU"] / d["SQ_WAVES"]
+            d["salu_insts_per_wave"] = d.get("SQ_INSTS_SALU", 0) / d["SQ_WAVES"]
+        name = ("shadow_pass" if k.startswith("shadow_pass_kernel<false") else
+                "eye_pass" if k.startswith("eye_pass_kernel<false, false") else
+                "eye_pass_fused" if k.startswith("eye_pass_kernel<true, false") else k)
+        out["kernels"][name] = d
+    print(json.dumps(out, indent=1, sort_keys=True))
+
+
+if __name__ == "__main__":
+    main()
