@@ -83,6 +83,7 @@ ABI_SYMBOLS = [
     ("rtm_ctx_synchronize", C.c_int, [_P]),
     ("rtm_ctx_last_kernel_ms", C.c_int, [_P, C.POINTER(C.c_float), C.POINTER(C.c_float)]),
     ("rtm_ctx_set_timing_capacity", C.c_int, [_P, _I32]),
+    ("rtm_ctx_set_timing_stride", C.c_int, [_P, _I32]),
     ("rtm_ctx_kernel_ms_history", C.c_int, [_P, C.POINTER(C.c_float), C.POINTER(C.c_float), _I32,
                                             C.POINTER(_I32)]),
     ("rtm_render", C.c_int, [C.POINTER(rtm_scene), C.POINTER(rtm_camera), C.POINTER(rtm_camera),

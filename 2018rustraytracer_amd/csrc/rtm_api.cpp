@@ -71,24 +71,63 @@ struct DevBuf {
 // ---- host-side precompute, reference op order ----
 inline double dot3(const double a[3], const double b[3]) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
 
+// ((i as f64) / (n as f64)) * 2.0 - 1.0 (main.rs:306-307, 1903-1906)
+inline double ndc(int32_t i, int32_t n) { return ((double)i / (double)n) * 2.0 - 1.0; }
+
+// {i in [0,n) : |ndc(i) - c| <= R} is an interval because ndc(i) - c is
+// monotone in i; found by binary search on exactly the values the kernel sees.
+void pixel_range(double c, double R, int32_t n, int32_t* lo, int32_t* hi) {
+    *lo = 1;
+    *hi = 0;
+    if (!(R >= 0.0) || !std::isfinite(c)) return;
+    int32_t a = 0, b = n;  // first i with ndc(i) - c >= -R
+    while (a < b) {
+        int32_t m = a + (b - a) / 2;
+        if (ndc(m, n) - c >= -R) b = m;
+        else a = m + 1;
+    }
+    int32_t first = a;
+    a = 0;
+    b = n;  // first i with ndc(i) - c > R
+    while (a < b) {
+        int32_t m = a + (b - a) / 2;
+        if (ndc(m, n) - c > R) b = m;
+        else a = m + 1;
+    }
+    int32_t last = a - 1;
+    if (first <= last) {
+        *lo = first;
+        *hi = last;
+    }
+}
+
 // Viewport::rasterize ORTHOGONAL projection of one sphere (main.rs:449-470) and the
-// axis normalisation of calcEllipseDistToCenter (main.rs:2849-2850).
-RasterSphereK project_sphere(const rtm_camera& c, const rtm_sphere& s) {
+// axis normalisation of calcEllipseDistToCenter (main.rs:2849-2850), for a W x H viewport.
+RasterSphereK project_sphere(const rtm_camera& c, const rtm_sphere& s, int32_t W, int32_t H) {
     RasterSphereK k{};
     double diff[3] = {s.pos[0] - c.pos[0], s.pos[1] - c.pos[1], s.pos[2] - c.pos[2]};
-    k.z = dot3(c.dir, diff);  // calcDepthOfProjectedPoint: dot(dir, p - pos)
+    k.z = dot3(c.dir, diff);    // calcDepthOfProjectedPoint: dot(dir, p - pos)
     k.cx = dot3(diff, c.side);  // Camera::project: dot(diff, side)
     k.cy = dot3(diff, c.up);
     k.r = s.r;
     const double m = std::sqrt(s.r * s.r + 0.0 * 0.0);  // Vec2::magnitude of (r, 0)
     const double inv = 1.0 / m;                          // Vec2::normalized: scale(1.0/m)
     k.n = s.r * inv;
-    k.z0 = 0.0 * inv;
     k.m = m;
-    // Cull radius: a covered pixel has |rel.x|, |rel.y| < m*(1+4 ulp); 1e-9 relative margin.
-    k.R = std::fabs(m) * (1.0 + 1e-9) + 1e-300;
-    if (!(k.R == k.R)) k.R = INFINITY;  // NaN m: let the exact test decide (it yields NaN -> no hit)
-    k.id = s.id;
+    k.id = (int32_t)s.id;
+    // A covered pixel has d < 1, hence |rel.x|, |rel.y| < m*(1 + 8 ulp); R adds a
+    // 1e-9 relative margin.  Non-finite / zero m can never cover a pixel.
+    k.ix0 = k.iy0 = 1;
+    k.ix1 = k.iy1 = 0;
+    if (std::isfinite(m) && m > 0.0 && std::isfinite(k.n)) {
+        const double R = m * (1.0 + 1e-9);
+        pixel_range(k.cx, R, W, &k.ix0, &k.ix1);
+        pixel_range(k.cy, R, H, &k.iy0, &k.iy1);
+        if (k.ix0 > k.ix1 || k.iy0 > k.iy1) {
+            k.ix0 = k.iy0 = 1;
+            k.ix1 = k.iy1 = 0;
+        }
+    }
     return k;
 }
 
@@ -171,8 +210,8 @@ int build_frame(FrameArgs& a, const rtm_scene* scene, const rtm_camera* eye, con
         return fail(RTM_ERR_UNSUPPORTED, "frame path needs ORTHOGONAL eye and shadow cameras");
     std::memset(&a, 0, sizeof a);
     for (int i = 0; i < scene->n_spheres; ++i) {
-        a.esph[i] = project_sphere(*eye, scene->spheres[i]);
-        a.ssph[i] = project_sphere(*shadow, scene->spheres[i]);
+        a.esph[i] = project_sphere(*eye, scene->spheres[i], W, H);
+        a.ssph[i] = project_sphere(*shadow, scene->spheres[i], W, H);
         a.shade[i] = shade_sphere(scene->spheres[i]);
     }
     for (int i = 0; i < scene->n_patches; ++i) a.patch[i] = patch_k(scene->patches[i]);
@@ -203,15 +242,18 @@ struct rtm_ctx {
     hipStream_t stream = nullptr;
     std::vector<TimingSlot> ring;  // per-render kernel events (capacity = ring.size())
     int64_t renders = 0;           // renders recorded into the ring
+    int64_t calls = 0;             // renders enqueued (for the stride)
+    int32_t stride = 1;
     bool have_shadow_pass = false;
     DevBuf smap;    // shadow map, W*H f64
     DevBuf out;     // staging for rtm_render's host output
     DevBuf stats;
     int32_t smap_w = 0, smap_h = 0;
     DevBuf tabs;  // [t (steps) | nx (W) | ny (H)] f64, see Tables
-    int64_t tab_steps = -1, tab_w = -1, tab_h = -1;
-    uint64_t tab_zkey = 0;
-    bool tab_hasz = false;
+    uint64_t tab_key = 0;
+    int64_t tab_nt = 0, tab_nz = 0, tab_nd = 0;
+    int32_t tab_w = 0, tab_h = 0, tab_np = 0;
+    bool tab_hast = false, tab_sep = false;
 };
 
 struct rtm_viewport {
@@ -243,50 +285,126 @@ uint64_t bits_of(double v) {
     return b;
 }
 
-// Build (or reuse) the context's lookup tables for (steps, W, H, march camera).
-int ensure_tables(rtm_ctx* ctx, int32_t steps, int32_t W, int32_t H, const rtm_camera* march_cam, Tables* out) {
+uint64_t fnv(uint64_t h, const void* p, size_t n) {
+    const unsigned char* b = (const unsigned char*)p;
+    for (size_t i = 0; i < n; ++i) h = (h ^ b[i]) * 1099511628211ull;
+    return h;
+}
+
+// Separable axis-aligned march camera: the domain-mapped ray start
+// ((o.x+1)*0.5, (o.y+1)*0.5) (main.rs:2187-2188) depends only on the column (x) and
+// only on the row (y), bit for bit.  o.x = (pos.x + side.x*s) + up.x*u: with
+// up.x == 0 the second term is +-0, which leaves a non-(-0) first term unchanged;
+// o.y = (pos.y + side.y*s) + up.y*u: with side.y == 0 and pos.y != -0 the first
+// term is the same for every column.
+bool separable(const rtm_camera* c, int32_t W, std::vector<double>& colx, double* cy) {
+    if (!(c->up[0] == 0.0 && c->side[1] == 0.0)) return false;
+    if (c->pos[1] == 0.0 && std::signbit(c->pos[1])) return false;
+    colx.resize((size_t)W);
+    for (int32_t i = 0; i < W; ++i) {
+        colx[(size_t)i] = c->pos[0] + c->side[0] * ndc(i, W);
+        if (colx[(size_t)i] == 0.0 && std::signbit(colx[(size_t)i])) return false;
+    }
+    *cy = c->pos[1] == 0.0 ? 0.0 : c->pos[1];
+    return true;
+}
+
+inline bool in01(double v) { return std::fabs(v - 0.5) <= 0.5; }
+
+// Build (or reuse) the context's lookup tables for (steps, W, H, march camera, patches).
+int ensure_tables(rtm_ctx* ctx, int32_t steps, int32_t W, int32_t H, const rtm_camera* march_cam,
+                  const PatchK* patches, int32_t n_patches, Tables* out) {
     const bool with_t = steps <= RTM_T_TABLE_MAX;
     const int64_t nt = with_t ? steps : 0;
-    double z0 = 0.0, sz = 0.0;
-    bool with_z = with_t && shared_z0(march_cam, &z0, &sz);
-    std::vector<double> zt;
-    if (with_z) {
-        zt.resize((size_t)nt);
-        double z = z0;  // p.z after k advances: p = &p + &step (main.rs:2272)
-        for (int64_t k = 0; k < nt; ++k) {
-            zt[(size_t)k] = z;
-            z = z + sz;
-            if (!std::isfinite(zt[(size_t)k])) with_z = false;
+    uint64_t key = 1469598103934665603ull;
+    key = fnv(key, &steps, sizeof steps);
+    key = fnv(key, &W, sizeof W);
+    key = fnv(key, &H, sizeof H);
+    if (march_cam) key = fnv(key, march_cam, sizeof *march_cam);
+    key = fnv(key, &n_patches, sizeof n_patches);
+    if (n_patches > 0) key = fnv(key, patches, sizeof(PatchK) * (size_t)n_patches);
+    if (!(ctx->tabs.p && ctx->tab_key == key)) {
+        double z0 = 0.0, sz = 0.0;
+        bool with_z = with_t && shared_z0(march_cam, &z0, &sz);
+        std::vector<double> zt;
+        if (with_z) {
+            // 8 entries of padding past `steps`: the kernels prefetch one 8-step chunk ahead
+            zt.resize((size_t)nt + 8);
+            double z = z0;  // p.z after k advances: p = &p + &step (main.rs:2272)
+            for (int64_t k = 0; k < nt + 8; ++k) {
+                zt[(size_t)k] = z;
+                z = z + sz;
+                if (k < nt && !std::isfinite(zt[(size_t)k])) with_z = false;
+            }
+            if (nt == 0) with_z = false;
         }
-    }
-    const int64_t nz = with_z ? nt : 0;
-    const uint64_t zkey = with_z ? (bits_of(z0) * 1000003u) ^ bits_of(sz) : 0x5eed;
-    if (ctx->tab_steps != (with_t ? steps : -2) || ctx->tab_w != W || ctx->tab_h != H || ctx->tab_zkey != zkey ||
-        ctx->tab_hasz != with_z) {
-        std::vector<double> h((size_t)(nt + W + H + nz));
+        std::vector<double> colx;
+        double cy = 0.0;
+        const bool with_sep = with_z && n_patches > 0 && separable(march_cam, W, colx, &cy);
+        const int64_t nz = with_z ? nt + 8 : 0;
+        const int64_t nsep = with_sep ? (int64_t)H + 2 * (int64_t)n_patches * W : 0;
+        const int64_t nd = nt + W + H + nz + nsep;
+        const int64_t nok = with_sep ? (int64_t)W + H : 0;
+        std::vector<double> h((size_t)nd + (size_t)(nok + 1) / 2);
         double t = 0.0;  // raymarchPatch: t = 0.0; ... t += magnitudeOfStepsize (main.rs:2237, 2273)
         for (int64_t k = 0; k < nt; ++k) {
             h[(size_t)k] = t;
             t = t + 0.03;
         }
-        for (int32_t i = 0; i < W; ++i) h[(size_t)(nt + i)] = ((double)i / (double)W) * 2.0 - 1.0;
-        for (int32_t i = 0; i < H; ++i) h[(size_t)(nt + W + i)] = ((double)i / (double)H) * 2.0 - 1.0;
+        for (int32_t i = 0; i < W; ++i) h[(size_t)(nt + i)] = ndc(i, W);
+        for (int32_t i = 0; i < H; ++i) h[(size_t)(nt + W + i)] = ndc(i, H);
         for (int64_t k = 0; k < nz; ++k) h[(size_t)(nt + W + H + k)] = zt[(size_t)k];
+        if (with_sep) {
+            double* py = &h[(size_t)(nt + W + H + nz)];
+            double* d0 = py + H;
+            double* dd = d0 + (int64_t)n_patches * W;
+            int32_t* ok = (int32_t*)&h[(size_t)nd];
+            for (int32_t j = 0; j < H; ++j) {
+                const double oy = cy + march_cam->up[1] * ndc(j, H);
+                py[j] = (oy + 1.0) * 0.5;  // raymarchPatchDomainM11 (main.rs:2188)
+                ok[W + j] = in01(py[j]);
+            }
+            for (int32_t i = 0; i < W; ++i) {
+                const double px = (colx[(size_t)i] + 1.0) * 0.5;  // main.rs:2187
+                ok[i] = in01(px);
+                for (int32_t k = 0; k < n_patches; ++k) {
+                    const PatchK& p = patches[k];
+                    const double a = p.a0 + p.d0 * px;  // linear(t.x, d00, d01): d00 + (d01-d00)*x
+                    const double b = p.a1 + p.d1 * px;  // linear(t.x, d10, d11)
+                    d0[(int64_t)k * W + i] = a;
+                    dd[(int64_t)k * W + i] = b - a;  // linear(t.y, d0, d1): diff = d1 - d0
+                }
+            }
+        }
         HIP_TRY(hipStreamSynchronize(ctx->stream));  // earlier launches may still read the old tables
         int rc = ctx->tabs.ensure(h.size() * sizeof(double), ctx->device);
         if (rc) return rc;
         HIP_TRY(hipMemcpy(ctx->tabs.p, h.data(), h.size() * sizeof(double), hipMemcpyHostToDevice));
-        ctx->tab_steps = with_t ? steps : -2;
+        ctx->tab_key = key;
+        ctx->tab_nt = nt;
+        ctx->tab_hast = with_t;
+        ctx->tab_nz = nz;
+        ctx->tab_sep = with_sep;
+        ctx->tab_nd = nd;
         ctx->tab_w = W;
         ctx->tab_h = H;
-        ctx->tab_zkey = zkey;
-        ctx->tab_hasz = with_z;
+        ctx->tab_np = n_patches;
     }
     const double* base = (const double*)ctx->tabs.p;
-    out->t = with_t ? base : nullptr;
-    out->nx = base + nt;
-    out->ny = base + nt + W;
-    out->z = with_z ? base + nt + W + H : nullptr;
+    const int64_t nt2 = ctx->tab_nt, nz2 = ctx->tab_nz;
+    out->t = ctx->tab_hast ? base : nullptr;
+    out->nx = base + nt2;
+    out->ny = base + nt2 + W;
+    out->z = nz2 ? base + nt2 + W + H : nullptr;
+    if (ctx->tab_sep) {
+        out->py = base + nt2 + W + H + nz2;
+        out->d0 = out->py + H;
+        out->dd = out->d0 + (int64_t)ctx->tab_np * W;
+        out->ok = (const int32_t*)(base + ctx->tab_nd);
+    } else {
+        out->py = out->d0 = out->dd = nullptr;
+        out->ok = nullptr;
+    }
     return RTM_OK;
 }
 
@@ -313,11 +431,12 @@ int enqueue_frame(rtm_ctx* ctx, FrameArgs& a, float* out_dev, StatsK* stats) {
         sc.up[i] = a.shadow.up[i];
         sc.side[i] = a.shadow.side[i];
     }
-    if ((rc = ensure_tables(ctx, a.steps, a.W, a.H, &sc, &a.tab))) return rc;
+    if ((rc = ensure_tables(ctx, a.steps, a.W, a.H, &sc, a.patch, a.n_patches, &a.tab))) return rc;
     const bool fused = (a.flags & RTM_FLAG_FUSED_SHADOW) != 0;
     hipStream_t s = ctx->stream;
     double* smap = nullptr;
-    TimingSlot* slot = ctx->ring.empty() ? nullptr : &ctx->ring[(size_t)(ctx->renders % (int64_t)ctx->ring.size())];
+    const bool timed = !ctx->ring.empty() && (ctx->calls++ % ctx->stride) == 0;
+    TimingSlot* slot = timed ? &ctx->ring[(size_t)(ctx->renders % (int64_t)ctx->ring.size())] : nullptr;
     if (!fused) {
         if ((rc = ctx->smap.ensure(sizeof(double) * (size_t)a.Ws * (size_t)a.Hs, ctx->device))) return rc;
         smap = (double*)ctx->smap.p;
@@ -429,6 +548,13 @@ int rtm_ctx_set_timing_capacity(rtm_ctx* ctx, int32_t capacity) {
     ctx->renders = 0;
     for (auto& sl : ctx->ring)
         for (auto& e : sl.ev) HIP_TRY(hipEventCreate(&e));
+    return RTM_OK;
+}
+
+int rtm_ctx_set_timing_stride(rtm_ctx* ctx, int32_t stride) {
+    if (!ctx || stride < 1) return fail(RTM_ERR_INVALID, "ctx NULL or stride %d < 1", stride);
+    ctx->stride = stride;
+    ctx->calls = 0;
     return RTM_OK;
 }
 
@@ -559,7 +685,7 @@ int rtm_viewport_rasterize(rtm_viewport* vp, const rtm_scene* scene) {
     if ((rc = validate_scene(scene)) || (rc = check_ortho_raster(vp->cam))) return rc;
     RasterArgs a;
     std::memset(&a, 0, sizeof a);
-    for (int i = 0; i < scene->n_spheres; ++i) a.sph[i] = project_sphere(vp->cam, scene->spheres[i]);
+    for (int i = 0; i < scene->n_spheres; ++i) a.sph[i] = project_sphere(vp->cam, scene->spheres[i], vp->W, vp->H);
     a.n_spheres = scene->n_spheres;
     a.face = vp->face;
     a.W = vp->W;
@@ -586,7 +712,8 @@ int rtm_viewport_process_raymarching_rays(rtm_viewport* vp, const rtm_patch* pat
     a.W = vp->W;
     a.H = vp->H;
     DeviceGuard g(vp->ctx->device);
-    int rc = ensure_tables(vp->ctx, steps, vp->W, vp->H, &vp->cam, &a.tab);
+    // (the staged march uses the per-ray path; no separable tables)
+    int rc = ensure_tables(vp->ctx, steps, vp->W, vp->H, &vp->cam, nullptr, 0, &a.tab);
     if (rc) return rc;
     rc = launch_vp_march(a, (double*)vp->zbuf.p, vp->ctx->stream);
     if (rc) return fail(rc, "march launch failed");

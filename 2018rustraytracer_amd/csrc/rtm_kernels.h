@@ -12,17 +12,24 @@
 namespace rtm {
 
 // One sphere as seen by one ORTHOGONAL camera (Viewport::rasterize, main.rs:449-470).
-// For axisA=(r,0), axisB=(0,r): axisA.normalized()=(n,z0), axisB.normalized()=(z0,n),
-// |axisA|=|axisB|=m (main.rs:2849-2850, 2098-2109).
+// axisA=(r,0), axisB=(0,r): axisA.normalized()=(n, 0*(1/m)), axisB.normalized()=(0*(1/m), n),
+// |axisA|=|axisB|=m (main.rs:2849-2850, 2098-2109).  The 0*(1/m) terms only ever add
+// a signed zero (or turn an already-missing pixel into NaN), which cannot change
+// d = sqrt(pa^2 + pb^2) < 1, so pa = (rel.x*n)/m and pb = (rel.y*n)/m.
 struct RasterSphereK {
     double cx, cy;  // Camera::project(pos).xy (main.rs:455, 464)
     double z;       // calcDepthOfProjectedPoint(pos) (main.rs:450)
     double r;       // the r rasterizeSphere multiplies relativeHeight by (main.rs:541, 316)
-    double n, z0;   // r*(1/m), 0*(1/m)
+    double n;       // r*(1/m)
     double m;       // sqrt(r*r + 0*0)
-    double R;       // cull radius: |rel.x|>R or |rel.y|>R implies d>=1 (pure cull)
-    int64_t id;     // PrimitiveSphere.id -> G-buffer (main.rs:189)
+    int32_t id;     // PrimitiveSphere.id -> G-buffer (main.rs:189)
+    // Pixel-index ranges outside which no pixel can be covered (the reference's
+    // screen-space bbox, main.rs:256-300, made exact): column xi can be covered
+    // only if ix0 <= xi <= ix1, row yi only if iy0 <= yi <= iy1.  Empty: ix0 > ix1.
+    int32_t ix0, ix1, iy0, iy1;
+    int32_t pad;
 };
+static_assert(sizeof(RasterSphereK) == 72, "RasterSphereK layout");
 
 // Per-sphere shading constants, indexed by id (renderColorImage, main.rs:748-759).
 struct ShadeSphereK {
@@ -44,17 +51,28 @@ struct PatchK {
     double a1, d1;  // _1.a, _1.b - _1.a
 };
 
-// Host-built lookup tables (device memory, owned by the context):
-//   t[k]   = t after k march advances: t_0 = 0.0, t_{k+1} = t_k + 0.03, summed
-//            sequentially exactly as `t += magnitudeOfStepsize` (main.rs:2273);
-//   nx[i]  = ((i as f64) / (W as f64)) * 2.0 - 1.0  (main.rs:306, 1903-1906), ny likewise.
-//   z[k]   = p.z after k advances when every texel of the shadow camera starts at
-//            the same z (host-proved, see ensure_tables): z_0 = z0, z_{k+1} = z_k + step.z.
+// Host-built lookup tables (device memory, owned by the context), all computed
+// with the reference's operations in its order:
+//   t[k]   = t after k march advances: t_0 = 0.0, t_{k+1} = t_k + 0.03 (main.rs:2237, 2273)
+//   nx[i]  = ((i as f64) / (W as f64)) * 2.0 - 1.0  (main.rs:306, 1903-1906), ny likewise
+//   z[k]   = p.z after k advances when every shadow texel starts at the same z
+//            (z_0 = z0, z_{k+1} = z_k + step.z, main.rs:2272)
+// Separable shadow camera (host-proved: p.x of the domain-mapped ray start depends
+// only on the column and p.y only on the row, bit for bit):
+//   py[j]          = p.y of row j                        (main.rs:2188)
+//   d0[k*W + i]    = _0.a + (_0.b - _0.a) * p.x(i)       (linear, main.rs:2074)
+//   dd[k*W + i]    = (_1.a + (_1.b - _1.a) * p.x(i)) - d0 (main.rs:2075, 2077 diff)
+//   ok[i] / ok[W+j] = inRange01(p.x(i)) / inRange01(p.y(j)) (main.rs:2249)
+//   so the surface depth is D = d0 + dd * py (main.rs:2077, one mul + one add).
 struct Tables {
     const double* t;   // steps entries, or nullptr when steps > RTM_T_TABLE_MAX
     const double* nx;  // W entries
     const double* ny;  // H entries
     const double* z;   // steps entries, or nullptr (no shared z sequence)
+    const double* py;  // H entries, or nullptr (not separable)
+    const double* d0;  // n_patches*W
+    const double* dd;  // n_patches*W
+    const int32_t* ok; // W + H
 };
 #define RTM_T_TABLE_MAX 65536
 

@@ -3,16 +3,19 @@
 //
 // Numerics: IEEE f64 in the reference's operation order, FMA contraction off
 // (file pragma + -ffp-contract=off), correctly-rounded f64 div/sqrt (the
-// AMDGPU default lowering).  Results are bit-identical to the CPU oracle.
+// AMDGPU default lowering).  Every result is bit-identical to the reference
+// semantics (tests/test_gpu_parity.py).
 //
 // Work mapping: one work-item per pixel; a 256-thread workgroup is a 64x4
 // pixel tile, so each wave owns 64 consecutive pixels of one row: the RGBA f32
 // store is one contiguous 1 KiB global_store_dwordx4 per wave and the f64
-// shadow-map store 512 B.  Scene constants are kernel arguments (uniform,
-// scalar-cache/SGPR operands).  No MFMA: this is scalar per-pixel math.
+// shadow-map store 512 B.  Scene constants are kernel arguments (uniform:
+// scalar cache -> SGPR operands); sphere culls are per-wave scalar compares.
+// No MFMA: this is scalar per-pixel math, VALU-issue bound (profiles/).
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "rtm_kernels.h"
 
@@ -26,11 +29,10 @@ constexpr int TILE_X = 64;  // one wave per tile row
 constexpr int TILE_Y = 4;   // four waves per workgroup
 constexpr int BLOCK = TILE_X * TILE_Y;
 
+using cdouble = const __attribute__((address_space(4))) double;  // scalar-loaded table
+
 // main.rs:306-307 / 1903-1907: ((i as f64) / (res as f64)) * 2.0 - 1.0
 __device__ __forceinline__ double ndc(int i, int res) { return ((double)i / (double)res) * 2.0 - 1.0; }
-
-// Rust f64::signum (used by raymarchPatch, main.rs:2244, 2261)
-__device__ __forceinline__ double rsignum(double v) { return v != v ? v : copysign(1.0, v); }
 
 // inRange01 (main.rs:2282-2284)
 __device__ __forceinline__ bool in01(double v) { return fabs(v - 0.5) <= 0.5; }
@@ -54,15 +56,20 @@ __device__ __forceinline__ int64_t tex_index(int64_t half, double v) {
     return half + t;
 }
 
+// Can any pixel of columns [xb, xe] in row y be covered by sphere s?  (exact
+// pixel-index bbox, host-computed; wave-uniform when xb, xe, y are)
+__device__ __forceinline__ bool may_cover(const RasterSphereK& s, int xb, int xe, int y) {
+    return y >= s.iy0 && y <= s.iy1 && xe >= s.ix0 && xb <= s.ix1;
+}
+
 // Sphere coverage of one pixel (projectSphereAtZBuffer, main.rs:176-195):
-// calcOthoDistanceByAbsPosition + calcHeightOfSphereOnUnit.
+// calcOthoDistanceByAbsPosition -> calcEllipseDistToCenter -> calcHeightOfSphereOnUnit.
 __device__ __forceinline__ bool cover(const RasterSphereK& s, double x, double y, double& h) {
-    double relx = x - s.cx;
-    double rely = y - s.cy;
-    if (!(fabs(relx) <= s.R && fabs(rely) <= s.R)) return false;  // pure cull (reference bbox, main.rs:256-300)
-    double pa = (relx * s.n + rely * s.z0) / s.m;
-    double pb = (relx * s.z0 + rely * s.n) / s.m;
-    double d = sqrt(pa * pa + pb * pb);
+    const double relx = x - s.cx;
+    const double rely = y - s.cy;
+    const double pa = (relx * s.n) / s.m;
+    const double pb = (rely * s.n) / s.m;
+    const double d = sqrt(pa * pa + pb * pb);
     if (d < 1.0) {
         h = sqrt(1.0 - d * d);
         return true;
@@ -74,7 +81,6 @@ struct MarchResult {
     bool hit;
     double t;
     int iters;  // loop iterations executed (stats only)
-    bool in_range;
 };
 
 // t after k advances (table built on the host by sequential summation; the
@@ -88,128 +94,129 @@ __device__ __forceinline__ double t_after(const Tables& tb, int k) {
 
 // v_cmp_class_f64 masks: bits 0-1 NaN, 2-5 negative (-inf,-norm,-denorm,-0),
 // 6-9 positive (+0,+denorm,+norm,+inf).
-constexpr int CLS_NAN = 0x003, CLS_NEG = 0x03C, CLS_POS = 0x3C0;
+constexpr int CLS_NAN = 0x003, CLS_NEG = 0x03C, CLS_POS = 0x3C0, CLS_ALL = 0x3FF;
 
 // `signum(v) != signEntry` (main.rs:2244, 2261-2263) as one class test: with
 // signEntry = signum(v0), the hit set is "the other sign, or NaN"; a NaN entry
 // compares unequal to everything.
 __device__ __forceinline__ int hit_class_mask(double v0) {
-    if (v0 != v0) return CLS_NAN | CLS_NEG | CLS_POS;
+    if (v0 != v0) return CLS_ALL;
     return __builtin_signbit(v0) ? (CLS_POS | CLS_NAN) : (CLS_NEG | CLS_NAN);
 }
 
-// raymarchPatchDomainM11 + raymarchPatch (main.rs:2179-2278) for one texel.
+// raymarchPatch's loop for a ray with no x/y motion (step.x == step.y == 0,
+// main.rs:2247-2274): p.x, p.y, inRange01 and the surface depth D are loop
+// invariants (p.x is never -0.0 here, so p.x + (+-0.0) == p.x bit for bit), so
+// the loop carries only p.z.
 //
-// The per-lane loop is restated as a wave-uniform loop: every lane advances its
-// own p exactly as the reference (p += step, sequentially), records the FIRST k
-// whose sign differs from the entry sign, and the wave leaves the loop as soon
-// as a ballot (__all) says every lane has its answer — the early-out the
-// reference's per-ray `return` gives a scalar CPU.  t is the k-th sequential
-// sum, read from the host-built table.
+// z_k = z_{k-1} + sz is monotone in k and so is fl(z_k - D); the class of
+// (z_k - D) therefore leaves the entry class at most once (a NaN, from
+// +inf - +inf, persists).  The first hit index is the number of steps that
+// still "continue": counted with one compare and one add per step, no per-step
+// control flow; every 8 steps the wave leaves the loop as soon as a ballot
+// (__any) says no lane still continues — the per-ray `return` of the reference.
 //
-// When the ray has no x/y motion (step.x == step.y == 0: every axis-aligned
-// orthographic shadow camera) p.x, p.y, inRange01 and the surface depth are
-// loop-invariant (p.x is never -0.0, so p.x + (+-0.0) == p.x bit for bit):
-// the loop is unswitched and carries only p.z.
+// With a shared z sequence (host table: every texel starts at the same z) and
+// finite nonzero D, class(z - D) is POS iff z >= D (z - D is +0 when z == D)
+// and NEG iff z < D, so each step is one compare against a scalar-loaded table
+// entry.  Otherwise each step is fl(z - D) + a class test, exactly as written.
+template <bool COUNT>
+__device__ __forceinline__ MarchResult march_axis(double D, bool inr0, double oz, double sz, int steps,
+                                                  const Tables& tb) {
+    MarchResult r{false, 0.0, 0};
+    int cnt = inr0 ? 0 : steps;
+    const bool fast_ok = tb.z != nullptr && (!inr0 || (fabs(D) < INFINITY && D != 0.0));
+    if (__any(inr0) && __all(fast_ok)) {
+        cdouble* zt = (cdouble*)tb.z;
+        const bool epos = !(oz < D);  // entry class POS <=> z0 >= D
+        int lt = 0;                   // #steps with z_k < D
+        int k = 0;
+        bool all_stopped = false;
+        for (; k + 8 <= steps; k += 8) {
+            bool last_lt = false;
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                last_lt = zt[k + u] < D;
+                lt += last_lt ? 1 : 0;
+            }
+            const bool cont = inr0 && (epos ? !last_lt : last_lt);
+            if (!__any(cont)) {
+                k += 8;
+                all_stopped = true;
+                break;
+            }
+        }
+        if (!all_stopped)
+            for (; k < steps; ++k) lt += (zt[k] < D) ? 1 : 0;
+        if (inr0) cnt = epos ? k - lt : lt;
+    } else if (__any(inr0)) {
+        const int keep = inr0 ? (~hit_class_mask(oz - D) & CLS_ALL) : 0;
+        double z = oz;
+        int k = 0;
+        bool all_stopped = false;
+        for (; k + 8 <= steps; k += 8) {
+            bool cont = false;
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                cont = __builtin_amdgcn_class(z - D, keep);
+                cnt += cont ? 1 : 0;
+                z = z + sz;
+            }
+            if (!__any(cont)) {
+                all_stopped = true;
+                break;
+            }
+        }
+        if (!all_stopped) {
+            for (; k < steps; ++k) {
+                const bool cont = __builtin_amdgcn_class(z - D, keep);
+                cnt += cont ? 1 : 0;
+                z = z + sz;
+            }
+        }
+    }
+    if (cnt < steps) {
+        r.hit = true;
+        r.t = t_after(tb, cnt);
+    }
+    if (COUNT) r.iters = cnt < steps ? cnt + 1 : steps;
+    return r;
+}
+
+// raymarchPatchDomainM11 + raymarchPatch (main.rs:2179-2278) for one ray from
+// origin o along d (any camera).
 template <bool COUNT>
 __device__ __forceinline__ MarchResult march(double ox, double oy, double oz, double dx, double dy,
                                              double dz, const PatchK& p, int steps, const Tables& tb) {
-    MarchResult r{false, 0.0, 0, false};
     const double px0 = (ox + 1.0) * 0.5;
     const double py0 = (oy + 1.0) * 0.5;
     const double mstep = 0.03;
     const double sx = dx * mstep, sy = dy * mstep, sz = dz * mstep;
-    const double v0 = oz - bil(p, px0, py0);
-    const int mask = hit_class_mask(v0);
     const bool inr0 = in01(px0) && in01(py0);
-    if (COUNT) r.in_range = inr0;
+    if (sx == 0.0 && sy == 0.0) return march_axis<COUNT>(bil(p, px0, py0), inr0, oz, sz, steps, tb);
+    // General ray (x/y motion): in-range and the surface depth change per step.
+    // Per 4-step chunk the hits are collected as bits; the first set bit of the
+    // first non-empty chunk is the reference's first hit.
+    MarchResult r{false, 0.0, 0};
+    const int mask = hit_class_mask(oz - bil(p, px0, py0));
     int khit = -1;
-    if (sx == 0.0 && sy == 0.0) {
-        // Unswitched loop.  z_k = z_{k-1} + sz is monotone in k and so is
-        // fl(z_k - D); the class of (z_k - D) therefore leaves the entry class at
-        // most once (a NaN, from +inf - +inf, persists).  The first hit index is
-        // the number of steps that still "continue" — counted with one compare
-        // and one add per step, no per-step control flow.
-        const double D = bil(p, px0, py0);
-        int cnt = inr0 ? 0 : steps;
-        // Shared z sequence (host table): for finite, nonzero D and finite z,
-        // class(z - D) is POS iff z >= D and NEG iff z < D (z - D is +0 when
-        // z == D), so a plain compare against the table decides each step.
-        const bool fast_ok = tb.z != nullptr && (!inr0 || (fabs(D) < INFINITY && D != 0.0));
-        if (__any(inr0) && __all(fast_ok)) {
-            const __attribute__((address_space(4))) double* zt =
-                (const __attribute__((address_space(4))) double*)tb.z;
-            const bool epos = !(oz < D);  // entry class POS <=> z0 >= D
-            int lt = 0;                   // #steps with z_k < D
-            int k = 0;
-            bool all_stopped = false;
-            for (; k + 8 <= steps; k += 8) {
-                bool last_lt = false;
+    bool done = false;
+    double x = px0, y = py0, z = oz;
+    for (int k = 0; k < steps; k += 4) {
+        if (__all(done)) break;
+        unsigned bits = 0;
 #pragma unroll
-                for (int u = 0; u < 8; ++u) {
-                    last_lt = zt[k + u] < D;
-                    lt += last_lt ? 1 : 0;
-                }
-                const bool cont = inr0 && (epos ? !last_lt : last_lt);
-                if (!__any(cont)) {
-                    k += 8;
-                    all_stopped = true;
-                    break;
-                }
-            }
-            if (!all_stopped)
-                for (; k < steps; ++k) lt += (zt[k] < D) ? 1 : 0;
-            const int ran = k;
-            if (inr0) cnt = epos ? ran - lt : lt;
-        } else if (__any(inr0)) {
-            const int keep = inr0 ? (~mask & (CLS_NAN | CLS_NEG | CLS_POS)) : 0;
-            double z = oz;
-            int k = 0;
-            bool all_stopped = false;
-            for (; k + 8 <= steps; k += 8) {
-                bool cont = false;
-#pragma unroll
-                for (int u = 0; u < 8; ++u) {
-                    cont = __builtin_amdgcn_class(z - D, keep);
-                    cnt += cont ? 1 : 0;
-                    z = z + sz;
-                }
-                if (!__any(cont)) {  // every lane has met its surface: wave early-out
-                    all_stopped = true;
-                    break;
-                }
-            }
-            if (!all_stopped) {
-                for (; k < steps; ++k) {
-                    const bool cont = __builtin_amdgcn_class(z - D, keep);
-                    cnt += cont ? 1 : 0;
-                    z = z + sz;
-                }
-            }
+        for (int u = 0; u < 4; ++u) {
+            const bool inr = in01(x) && in01(y);
+            const bool h = (k + u < steps) && inr && __builtin_amdgcn_class(z - bil(p, x, y), mask);
+            bits |= h ? (1u << u) : 0u;
+            x = x + sx;
+            y = y + sy;
+            z = z + sz;
         }
-        khit = cnt < steps ? cnt : -1;
-    } else {
-        // General ray (x/y motion): in-range and the surface depth change per step.
-        // Per 4-step chunk the hits are collected as bits; the first set bit of
-        // the first non-empty chunk is the reference's first hit.
-        bool done = false;
-        double x = px0, y = py0, z = oz;
-        for (int k = 0; k < steps; k += 4) {
-            if (__all(done)) break;
-            unsigned bits = 0;
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const bool inr = in01(x) && in01(y);
-                const bool h = (k + u < steps) && inr && __builtin_amdgcn_class(z - bil(p, x, y), mask);
-                bits |= h ? (1u << u) : 0u;
-                x = x + sx;
-                y = y + sy;
-                z = z + sz;
-            }
-            const bool first = !done && bits != 0u;
-            khit = first ? k + __builtin_ctz(bits) : khit;
-            done = done || first;
-        }
+        const bool first = !done && bits != 0u;
+        khit = first ? k + __builtin_ctz(bits) : khit;
+        done = done || first;
     }
     if (khit >= 0) {
         r.hit = true;
@@ -248,36 +255,60 @@ __device__ __forceinline__ void stat_add(unsigned long long* ctr, unsigned long 
     if ((threadIdx.x & 63) == 0 && v) atomicAdd(ctr, v);
 }
 
+struct ShadowCounts {
+    unsigned long long tests = 0, iters = 0, hits = 0, inrange = 0;
+};
+
 // One shadow-map texel: shadow viewport rasterize (face BACK, main.rs:1569) then
 // processRaymarchingRays (main.rs:1571) with a strict-min update (main.rs:559).
+// [xb, xe] x yw is the pixel set the caller's wave covers (for the cull).
 template <bool COUNT>
-__device__ __forceinline__ double shadow_texel(const FrameArgs& a, int xi, int yi, unsigned long long* n_tests,
-                                               unsigned long long* n_iters, unsigned long long* n_hits,
-                                               unsigned long long* n_inrange) {
-    const double x = a.tab.nx[xi];  // shadow map dims == eye dims
-    const double y = a.tab.ny[yi];
+__device__ __forceinline__ double shadow_texel(const FrameArgs& a, int xi, int yi, int xb, int xe, int yw,
+                                               ShadowCounts& c) {
     double zb = INFINITY;
     if (!(a.flags & RTM_FLAG_NO_SHADOW_RASTER)) {
+        const double x = a.tab.nx[xi];  // shadow map dims == eye dims
+        const double y = a.tab.ny[yi];
         for (int i = 0; i < a.n_spheres; ++i) {
+            if (!may_cover(a.ssph[i], xb, xe, yw)) continue;
             double h;
             if (cover(a.ssph[i], x, y, h)) {
-                if (COUNT) ++*n_tests;
-                double depth = a.ssph[i].z + h * a.ssph[i].r;  // EnumFace::BACK (main.rs:243)
+                if (COUNT) ++c.tests;
+                const double depth = a.ssph[i].z + h * a.ssph[i].r;  // EnumFace::BACK (main.rs:243)
                 if (depth < zb) zb = depth;
             }
         }
     }
-    if (!(a.flags & RTM_FLAG_NO_MARCH)) {
-        double o[3], d[3];
-        cam_ray(a.shadow, x, y, o, d);
-        for (int k = 0; k < a.n_patches; ++k) {
-            MarchResult m = march<COUNT>(o[0], o[1], o[2], d[0], d[1], d[2], a.patch[k], a.steps, a.tab);
-            if (COUNT) {
-                *n_iters += m.iters;
-                *n_hits += m.hit;
-                *n_inrange += m.in_range;
+    if (!(a.flags & RTM_FLAG_NO_MARCH) && a.n_patches > 0) {
+        if (a.tab.d0) {
+            // separable axis-aligned shadow camera: the texel's domain-mapped start
+            // and surface depth come from per-column / per-row tables
+            const double py = a.tab.py[yi];
+            const bool inr0 = a.tab.ok[xi] && a.tab.ok[a.Ws + yi];
+            const double oz = a.tab.z[0];
+            const double sz = a.shadow.dir[2] * 0.03;
+            for (int k = 0; k < a.n_patches; ++k) {
+                const double D = a.tab.d0[k * a.Ws + xi] + a.tab.dd[k * a.Ws + xi] * py;
+                MarchResult m = march_axis<COUNT>(D, inr0, oz, sz, a.steps, a.tab);
+                if (COUNT) {
+                    c.iters += m.iters;
+                    c.hits += m.hit;
+                    c.inrange += inr0;
+                }
+                if (m.hit && m.t < zb) zb = m.t;
             }
-            if (m.hit && m.t < zb) zb = m.t;
+        } else {
+            double o[3], d[3];
+            cam_ray(a.shadow, a.tab.nx[xi], a.tab.ny[yi], o, d);
+            for (int k = 0; k < a.n_patches; ++k) {
+                MarchResult m = march<COUNT>(o[0], o[1], o[2], d[0], d[1], d[2], a.patch[k], a.steps, a.tab);
+                if (COUNT) {
+                    c.iters += m.iters;
+                    c.hits += m.hit;
+                    c.inrange += in01((o[0] + 1.0) * 0.5) && in01((o[1] + 1.0) * 0.5);
+                }
+                if (m.hit && m.t < zb) zb = m.t;
+            }
         }
     }
     return zb;
@@ -286,19 +317,153 @@ __device__ __forceinline__ double shadow_texel(const FrameArgs& a, int xi, int y
 template <bool COUNT>
 __global__ __launch_bounds__(BLOCK) void shadow_pass_kernel(const FrameArgs a, double* __restrict__ smap,
                                                             StatsK* __restrict__ st) {
-    const int xi = blockIdx.x * TILE_X + (threadIdx.x & (TILE_X - 1));
-    const int yi = blockIdx.y * TILE_Y + (threadIdx.x >> 6);
-    const bool live = xi < a.Ws && yi < a.Hs;
-    unsigned long long nt = 0, ni = 0, nh = 0, nr = 0;
-    if (live) {
-        double zb = shadow_texel<COUNT>(a, xi, yi, &nt, &ni, &nh, &nr);
+    const int xb = blockIdx.x * TILE_X;
+    const int xi = xb + (threadIdx.x & (TILE_X - 1));
+    const int yi = __builtin_amdgcn_readfirstlane(blockIdx.y * TILE_Y + (threadIdx.x >> 6));  // wave-uniform row
+    ShadowCounts c;
+    if (xi < a.Ws && yi < a.Hs) {
+        const double zb = shadow_texel<COUNT>(a, xi, yi, xb, xb + TILE_X - 1, yi, c);
         smap[(int64_t)yi * a.Ws + xi] = zb;
     }
     if (COUNT) {
-        stat_add(&st->shadow_sphere_tests, nt);
-        stat_add(&st->march_iterations, ni);
-        stat_add(&st->march_hits, nh);
-        stat_add(&st->march_in_range, nr);
+        stat_add(&st->shadow_sphere_tests, c.tests);
+        stat_add(&st->march_iterations, c.iters);
+        stat_add(&st->march_hits, c.hits);
+        stat_add(&st->march_in_range, c.inrange);
+    }
+}
+
+// Shadow pass for the separable axis-aligned shadow camera with a shared z
+// sequence (the BASELINE scenes): NR rows per wave give every lane NR
+// independent march chains (ILP against the VALU and scalar-load latencies the
+// one-texel kernel stalls on), the 8-step table chunks are prefetched one
+// chunk ahead, and each step is the sign bit of fl(z_k - D) (D finite and
+// nonzero on this path, so that bit is exactly [z_k < D], see march_axis).
+// Lanes whose D is not finite/nonzero send their wave to the exact per-texel
+// path, so results never depend on the fast path being taken.
+template <int NR>
+__global__ __launch_bounds__(BLOCK) void shadow_sep_kernel(const FrameArgs a, double* __restrict__ smap, int diag) {
+    const int lane = threadIdx.x & (TILE_X - 1);
+    const int xb = blockIdx.x * TILE_X;
+    const int xi = xb + lane;
+    const int y0 = __builtin_amdgcn_readfirstlane(blockIdx.y * (TILE_Y * NR) + (threadIdx.x >> 6) * NR);
+    const bool colv = xi < a.Ws;
+    const int xs = colv ? xi : a.Ws - 1;  // clamped column for table reads
+    double zb[NR];
+    bool rowv[NR];
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+        zb[r] = INFINITY;
+        rowv[r] = y0 + r < a.Hs;
+    }
+    // shadow viewport rasterize, face BACK (main.rs:1569, 243)
+    if (!(a.flags & RTM_FLAG_NO_SHADOW_RASTER) && !(diag & 1)) {
+        const double x = a.tab.nx[xs];
+        for (int i = 0; i < a.n_spheres; ++i) {
+#pragma unroll
+            for (int r = 0; r < NR; ++r) {
+                if (!rowv[r] || !may_cover(a.ssph[i], xb, xb + TILE_X - 1, y0 + r)) continue;
+                double h;
+                if (cover(a.ssph[i], x, a.tab.ny[y0 + r], h)) {
+                    const double depth = a.ssph[i].z + h * a.ssph[i].r;
+                    if (depth < zb[r]) zb[r] = depth;
+                }
+            }
+        }
+    }
+    if (!(a.flags & RTM_FLAG_NO_MARCH) && !(diag & 2)) {
+        const double oz = a.tab.z[0];
+        const double sz = a.shadow.dir[2] * 0.03;
+        const int steps = a.steps;
+        const bool colok = a.tab.ok[xs] != 0;
+        for (int k = 0; k < a.n_patches; ++k) {
+            double D[NR];
+            bool inr[NR], fast = true;
+            const double d0 = a.tab.d0[k * a.Ws + xs];
+            const double dd = a.tab.dd[k * a.Ws + xs];
+#pragma unroll
+            for (int r = 0; r < NR; ++r) {
+                const int yr = rowv[r] ? y0 + r : y0;
+                D[r] = d0 + dd * a.tab.py[yr];
+                inr[r] = colv && rowv[r] && colok && a.tab.ok[a.Ws + yr] != 0;
+                fast = fast && (!inr[r] || (fabs(D[r]) < INFINITY && D[r] != 0.0));
+            }
+            int cnt[NR];
+            if (__all(fast)) {
+                cdouble* zt = (cdouble*)a.tab.z;  // padded by 8 entries past `steps`
+                bool epos[NR];
+                unsigned eposb[NR], inrb[NR];
+                int lt[NR];
+                bool any_inr = false;
+#pragma unroll
+                for (int r = 0; r < NR; ++r) {
+                    epos[r] = !(oz < D[r]);
+                    eposb[r] = epos[r] ? 1u : 0u;
+                    inrb[r] = inr[r] ? 1u : 0u;
+                    lt[r] = 0;
+                    any_inr = any_inr || inr[r];
+                }
+                int kk = 0;
+                if (__any(any_inr)) {
+                    double zc[8];
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) zc[u] = zt[u];
+                    bool stopped = false;
+                    for (; kk + 8 <= steps; kk += 8) {
+                        double zn[8];
+#pragma unroll
+                        for (int u = 0; u < 8; ++u) zn[u] = zt[kk + 8 + u];
+                        unsigned cont = 0u;  // lane still marching in some row: inr & (last ^ epos)
+#pragma unroll
+                        for (int r = 0; r < NR; ++r) {
+                            unsigned last = 0u;
+#pragma unroll
+                            for (int u = 0; u < 8; ++u) {
+                                last = (unsigned)__double2hiint(zc[u] - D[r]) >> 31;
+                                lt[r] += (int)last;
+                            }
+                            cont |= inrb[r] & (last ^ eposb[r]);
+                        }
+                        if (!__any(cont != 0u)) {
+                            kk += 8;
+                            stopped = true;
+                            break;
+                        }
+#pragma unroll
+                        for (int u = 0; u < 8; ++u) zc[u] = zn[u];
+                    }
+                    if (!stopped) {
+                        for (; kk < steps; ++kk) {
+                            const double z = zt[kk];
+#pragma unroll
+                            for (int r = 0; r < NR; ++r) lt[r] += (int)((unsigned)__double2hiint(z - D[r]) >> 31);
+                        }
+                    }
+                }
+#pragma unroll
+                for (int r = 0; r < NR; ++r) cnt[r] = inr[r] ? (epos[r] ? kk - lt[r] : lt[r]) : steps;
+            } else {
+                // exact per-texel path (march_axis applies the result itself)
+#pragma unroll
+                for (int r = 0; r < NR; ++r) {
+                    MarchResult m = march_axis<false>(D[r], inr[r], oz, sz, steps, a.tab);
+                    if (m.hit && m.t < zb[r]) zb[r] = m.t;
+                    cnt[r] = steps;
+                }
+            }
+#pragma unroll
+            for (int r = 0; r < NR; ++r) {
+                if (cnt[r] < steps) {
+                    const double t = t_after(a.tab, cnt[r]);
+                    if (t < zb[r]) zb[r] = t;
+                }
+            }
+        }
+    }
+    if (colv) {
+#pragma unroll
+        for (int r = 0; r < NR; ++r)
+            if (rowv[r]) smap[(int64_t)(y0 + r) * a.Ws + xi] = zb[r];
     }
 }
 
@@ -307,11 +472,13 @@ __global__ __launch_bounds__(BLOCK) void shadow_pass_kernel(const FrameArgs a, d
 template <bool FUSED, bool COUNT>
 __global__ __launch_bounds__(BLOCK) void eye_pass_kernel(const FrameArgs a, const double* __restrict__ smap,
                                                          float4* __restrict__ out, StatsK* __restrict__ st) {
-    const int xi = blockIdx.x * TILE_X + (threadIdx.x & (TILE_X - 1));
-    const int yl = blockIdx.y * TILE_Y + (threadIdx.x >> 6);
+    const int xb = blockIdx.x * TILE_X;
+    const int xi = xb + (threadIdx.x & (TILE_X - 1));
+    const int yl = __builtin_amdgcn_readfirstlane(blockIdx.y * TILE_Y + (threadIdx.x >> 6));
     const int yi = a.row_begin + yl;
     const bool live = xi < a.W && yi < a.row_end;
-    unsigned long long n_tests = 0, n_hit = 0, n_lit = 0, n_it = 0, n_mh = 0, n_ir = 0, n_st = 0;
+    unsigned long long n_tests = 0, n_hit = 0, n_lit = 0;
+    ShadowCounts sc;
     int hit_id = -1;
     if (live) {
         const double x = a.tab.nx[xi];
@@ -320,15 +487,16 @@ __global__ __launch_bounds__(BLOCK) void eye_pass_kernel(const FrameArgs a, cons
         double best = INFINITY, bh = 0.0, bz = 0.0;
         int bid = -1;
         for (int i = 0; i < a.n_spheres; ++i) {
+            if (!may_cover(a.esph[i], xb, xb + TILE_X - 1, yi)) continue;
             double h;
             if (cover(a.esph[i], x, y, h)) {
                 if (COUNT) ++n_tests;
-                double depth = a.esph[i].z - h * a.esph[i].r;  // EnumFace::FRONT (main.rs:239)
+                const double depth = a.esph[i].z - h * a.esph[i].r;  // EnumFace::FRONT (main.rs:239)
                 if (depth < best) {
                     best = depth;
                     bh = h;
                     bz = a.esph[i].z;
-                    bid = (int)a.esph[i].id;
+                    bid = a.esph[i].id;
                 }
             }
         }
@@ -344,7 +512,7 @@ __global__ __launch_bounds__(BLOCK) void eye_pass_kernel(const FrameArgs a, cons
             const double nx = (wx - s.px) * s.inv_r, ny = (wy - s.py) * s.inv_r, nz = (wz - s.pz) * s.inv_r;
             // light (1,0,0).scale(-1.0) (main.rs:810-813)
             const double Lx = 1.0 * -1.0, Ly = 0.0 * -1.0, Lz = 0.0 * -1.0;
-            double diffuse = fmax(nx * Lx + ny * Ly + nz * Lz, 0.0);
+            const double diffuse = fmax(nx * Lx + ny * Ly + nz * Lz, 0.0);
             // reflect(L, n) = L - n*(-2 dot(L,n))  (main.rs:2872-2875, sign as written)
             const double k2 = -2.0 * (Lx * nx + Ly * ny + Lz * nz);
             const double Rx = Lx - nx * k2, Ry = Ly - ny * k2, Rz = Lz - nz * k2;
@@ -367,7 +535,7 @@ __global__ __launch_bounds__(BLOCK) void eye_pass_kernel(const FrameArgs a, cons
             double dsm = INFINITY;
             if (ty >= 0 && ty < a.Hs && tx >= 0 && tx < a.Ws) {
                 if (FUSED)
-                    dsm = shadow_texel<COUNT>(a, (int)tx, (int)ty, &n_st, &n_it, &n_mh, &n_ir);
+                    dsm = shadow_texel<COUNT>(a, (int)tx, (int)ty, (int)tx, (int)tx, (int)ty, sc);
                 else
                     dsm = smap[ty * a.Ws + tx];
             }
@@ -391,10 +559,10 @@ __global__ __launch_bounds__(BLOCK) void eye_pass_kernel(const FrameArgs a, cons
         stat_add(&st->lit_pixels, n_lit);
         for (int i = 0; i < a.n_spheres; ++i) stat_add(&st->eye_hits[i], hit_id == i);
         if (FUSED) {
-            stat_add(&st->shadow_sphere_tests, n_st);
-            stat_add(&st->march_iterations, n_it);
-            stat_add(&st->march_hits, n_mh);
-            stat_add(&st->march_in_range, n_ir);
+            stat_add(&st->shadow_sphere_tests, sc.tests);
+            stat_add(&st->march_iterations, sc.iters);
+            stat_add(&st->march_hits, sc.hits);
+            stat_add(&st->march_in_range, sc.inrange);
         }
     }
 }
@@ -406,8 +574,9 @@ __global__ __launch_bounds__(BLOCK) void eye_pass_kernel(const FrameArgs a, cons
 __global__ __launch_bounds__(BLOCK) void vp_rasterize_kernel(const RasterArgs a, double* __restrict__ zbuf,
                                                              double* __restrict__ gh, double* __restrict__ gz,
                                                              int32_t* __restrict__ gid) {
-    const int xi = blockIdx.x * TILE_X + (threadIdx.x & (TILE_X - 1));
-    const int yi = blockIdx.y * TILE_Y + (threadIdx.x >> 6);
+    const int xb = blockIdx.x * TILE_X;
+    const int xi = xb + (threadIdx.x & (TILE_X - 1));
+    const int yi = __builtin_amdgcn_readfirstlane(blockIdx.y * TILE_Y + (threadIdx.x >> 6));
     if (xi >= a.W || yi >= a.H) return;
     const int64_t idx = (int64_t)yi * a.W + xi;
     const double x = ndc(xi, a.W), y = ndc(yi, a.H);
@@ -416,16 +585,17 @@ __global__ __launch_bounds__(BLOCK) void vp_rasterize_kernel(const RasterArgs a,
     double wh = 0.0, wz = 0.0;
     int32_t wid = 0;
     for (int i = 0; i < a.n_spheres; ++i) {
+        if (!may_cover(a.sph[i], xb, xb + TILE_X - 1, yi)) continue;
         double h;
         if (cover(a.sph[i], x, y, h)) {
-            double hr = h * a.sph[i].r;
-            double depth = a.face == RTM_FACE_FRONT ? a.sph[i].z - hr : a.sph[i].z + hr;
+            const double hr = h * a.sph[i].r;
+            const double depth = a.face == RTM_FACE_FRONT ? a.sph[i].z - hr : a.sph[i].z + hr;
             if (depth < zb) {
                 zb = depth;
                 wrote = true;
                 wh = h;
                 wz = a.sph[i].z;
-                wid = (int32_t)a.sph[i].id;
+                wid = a.sph[i].id;
             }
         }
     }
@@ -480,7 +650,7 @@ __global__ __launch_bounds__(BLOCK) void vp_shade_kernel(const ShadeArgs a, cons
         const double wx = o[0] + d[0] * depth, wy = o[1] + d[1] * depth, wz = o[2] + d[2] * depth;
         const double nx = (wx - s.px) * s.inv_r, ny = (wy - s.py) * s.inv_r, nz = (wz - s.pz) * s.inv_r;
         const double Lx = 1.0 * -1.0, Ly = 0.0 * -1.0, Lz = 0.0 * -1.0;
-        double diffuse = fmax(nx * Lx + ny * Ly + nz * Lz, 0.0);
+        const double diffuse = fmax(nx * Lx + ny * Ly + nz * Lz, 0.0);
         const double k2 = -2.0 * (Lx * nx + Ly * ny + Lz * nz);
         const double Rx = Lx - nx * k2, Ry = Ly - ny * k2, Rz = Lz - nz * k2;
         double sp = fmax(view[0] * Rx + view[1] * Ry + view[2] * Rz, 0.0);
@@ -514,14 +684,52 @@ __global__ void fill_kernel(double* __restrict__ p, int64_t n, double v, int32_t
     }
 }
 
+}  // namespace
+
+namespace {
+
 inline dim3 grid_for(int w, int h) { return dim3((unsigned)((w + TILE_X - 1) / TILE_X), (unsigned)((h + TILE_Y - 1) / TILE_Y)); }
 
 inline int launched() { return hipGetLastError() == hipSuccess ? 0 : RTM_ERR_HIP; }
 
 }  // namespace
 
+// Rows per wave of the separable shadow kernel (0 = generic kernel).  Default
+// chosen by measurement (profiles/); RTM_SEP_ROWS overrides it for A/B runs.
+// Timing diagnostics only (RTM_DIAG_SHADOW: 1 = skip rasterize, 2 = skip march,
+// 3 = store only); results are wrong under it and no test sets it.
+static int diag_mode() {
+    static int v = [] {
+        const char* e = getenv("RTM_DIAG_SHADOW");
+        return e ? atoi(e) : 0;
+    }();
+    return v;
+}
+
+static int sep_rows() {
+    static int v = [] {
+        const char* e = getenv("RTM_SEP_ROWS");
+        int r = e ? atoi(e) : 4;
+        return (r == 0 || r == 1 || r == 2 || r == 4) ? r : 4;
+    }();
+    return v;
+}
+
+template <int NR>
+static void launch_sep(const FrameArgs& a, double* smap, hipStream_t s) {
+    dim3 g((unsigned)((a.Ws + TILE_X - 1) / TILE_X), (unsigned)((a.Hs + TILE_Y * NR - 1) / (TILE_Y * NR)));
+    hipLaunchKernelGGL(shadow_sep_kernel<NR>, g, dim3(BLOCK), 0, s, a, smap, diag_mode());
+}
+
 int launch_shadow_pass(const FrameArgs& a, double* smap, void* stream, StatsK* stats) {
     hipStream_t s = (hipStream_t)stream;
+    const int nr = sep_rows();
+    if (!stats && nr > 0 && a.tab.d0 && a.tab.z && a.tab.t) {
+        if (nr == 1) launch_sep<1>(a, smap, s);
+        else if (nr == 2) launch_sep<2>(a, smap, s);
+        else launch_sep<4>(a, smap, s);
+        return launched();
+    }
     if (stats)
         hipLaunchKernelGGL(shadow_pass_kernel<true>, grid_for(a.Ws, a.Hs), dim3(BLOCK), 0, s, a, smap, stats);
     else

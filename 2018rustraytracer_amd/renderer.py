@@ -59,6 +59,10 @@ class Context:
         lib = _lib()
         abi.check(lib, lib.rtm_ctx_set_timing_capacity(self._h, n), "rtm_ctx_set_timing_capacity")
 
+    def set_timing_stride(self, n: int):
+        lib = _lib()
+        abi.check(lib, lib.rtm_ctx_set_timing_stride(self._h, n), "rtm_ctx_set_timing_stride")
+
     def kernel_ms_history(self, n: int):
         """Per-render (shadow_pass_ms, eye_pass_ms) from HIP events, oldest first."""
         sm = (C.c_float * max(n, 1))()

@@ -135,6 +135,10 @@ int rtm_ctx_last_kernel_ms(rtm_ctx* ctx, float* shadow_pass_ms, float* eye_pass_
  * rtm_ctx_synchronize, rtm_ctx_kernel_ms_history writes up to `max` per-render
  * durations, oldest first, and the number written to *count. */
 int rtm_ctx_set_timing_capacity(rtm_ctx* ctx, int32_t capacity);
+/* Record events only for every `stride`-th render (default 1).  Each event is a
+ * barrier packet on the stream (~3-4 us per frame for four), so throughput runs
+ * sample kernel durations instead of timing every frame. */
+int rtm_ctx_set_timing_stride(rtm_ctx* ctx, int32_t stride);
 int rtm_ctx_kernel_ms_history(rtm_ctx* ctx, float* shadow_pass_ms, float* eye_pass_ms, int32_t max,
                               int32_t* count);
 
