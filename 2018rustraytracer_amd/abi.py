@@ -90,6 +90,8 @@ ABI_SYMBOLS = [
                              _I32, _I32, _I32, _I32, C.POINTER(C.c_float)]),
     ("rtm_render_async", C.c_int, [_P, C.POINTER(rtm_scene), C.POINTER(rtm_camera),
                                    C.POINTER(rtm_camera), _I32, _I32, _I32, _I32, _I32, _I32, _P]),
+    ("rtm_render_frames_async", C.c_int, [_P, _I32, C.POINTER(rtm_scene), C.POINTER(rtm_camera),
+                                          C.POINTER(rtm_camera), _I32, _I32, _I32, _I32, C.POINTER(_P)]),
     ("rtm_ctx_shadow_map", _P, [_P]),
     ("rtm_render_stats", C.c_int, [_P, C.POINTER(rtm_scene), C.POINTER(rtm_camera),
                                    C.POINTER(rtm_camera), _I32, _I32, _I32, _I32,

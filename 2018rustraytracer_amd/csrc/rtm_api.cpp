@@ -209,31 +209,38 @@ int build_frame(FrameArgs& a, const rtm_scene* scene, const rtm_camera* eye, con
     if (eye->type != RTM_CAMERA_ORTHOGONAL || shadow->type != RTM_CAMERA_ORTHOGONAL)
         return fail(RTM_ERR_UNSUPPORTED, "frame path needs ORTHOGONAL eye and shadow cameras");
     std::memset(&a, 0, sizeof a);
+    ShadowPart& sh = a.sh;
+    EyePart& ey = a.ey;
     for (int i = 0; i < scene->n_spheres; ++i) {
-        a.esph[i] = project_sphere(*eye, scene->spheres[i], W, H);
-        a.ssph[i] = project_sphere(*shadow, scene->spheres[i], W, H);
-        a.shade[i] = shade_sphere(scene->spheres[i]);
+        ey.sph[i] = project_sphere(*eye, scene->spheres[i], W, H);
+        sh.sph[i] = project_sphere(*shadow, scene->spheres[i], W, H);
+        ey.shade[i] = shade_sphere(scene->spheres[i]);
     }
-    for (int i = 0; i < scene->n_patches; ++i) a.patch[i] = patch_k(scene->patches[i]);
-    a.eye = cam_k(*eye);
-    a.shadow = cam_k(*shadow);
-    a.W = W;
-    a.H = H;
-    a.Ws = W;
-    a.Hs = H;
-    a.n_spheres = scene->n_spheres;
-    a.n_patches = scene->n_patches;
-    a.steps = steps;
-    a.flags = flags;
-    a.row_begin = 0;
-    a.row_end = H;
+    for (int i = 0; i < scene->n_patches; ++i) sh.patch[i] = patch_k(scene->patches[i]);
+    sh.cam = cam_k(*shadow);
+    sh.W = W;  // the shadow map has the eye image's size
+    sh.H = H;
+    sh.n_spheres = scene->n_spheres;
+    sh.n_patches = scene->n_patches;
+    sh.steps = steps;
+    sh.flags = flags;
+    ey.eye = cam_k(*eye);
+    ey.shadow = sh.cam;
+    ey.W = W;
+    ey.H = H;
+    ey.Ws = W;
+    ey.Hs = H;
+    ey.n_spheres = scene->n_spheres;
+    ey.flags = flags;
+    ey.row_begin = 0;
+    ey.row_end = H;
     return RTM_OK;
 }
 
 }  // namespace
 
 struct TimingSlot {
-    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};  // shadow start/stop, eye start/stop
+    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};  // shadow start/stop, eye (or pipe) start/stop
     bool shadow = false;
 };
 
@@ -246,6 +253,8 @@ struct rtm_ctx {
     int32_t stride = 1;
     bool have_shadow_pass = false;
     DevBuf smap;    // shadow map, W*H f64
+    DevBuf smap2;   // second shadow map for the pipelined frame sequence
+    const double* last_smap = nullptr;
     DevBuf out;     // staging for rtm_render's host output
     DevBuf stats;
     int32_t smap_w = 0, smap_h = 0;
@@ -421,31 +430,49 @@ struct DeviceGuard {
     }
 };
 
+rtm_camera to_camera(const CamK& k) {
+    rtm_camera c{};
+    c.type = k.type;
+    for (int i = 0; i < 3; ++i) {
+        c.pos[i] = k.pos[i];
+        c.dir[i] = k.dir[i];
+        c.up[i] = k.up[i];
+        c.side[i] = k.side[i];
+    }
+    return c;
+}
+
+int frame_tables(rtm_ctx* ctx, FrameArgs& a) {
+    rtm_camera sc = to_camera(a.sh.cam);
+    int rc = ensure_tables(ctx, a.sh.steps, a.sh.W, a.sh.H, &sc, a.sh.patch, a.sh.n_patches, &a.sh.tab);
+    if (rc) return rc;
+    a.ey.nx = a.sh.tab.nx;  // eye and shadow viewports share dims
+    a.ey.ny = a.sh.tab.ny;
+    return RTM_OK;
+}
+
+TimingSlot* next_slot(rtm_ctx* ctx) {
+    const bool timed = !ctx->ring.empty() && (ctx->calls++ % ctx->stride) == 0;
+    return timed ? &ctx->ring[(size_t)(ctx->renders % (int64_t)ctx->ring.size())] : nullptr;
+}
+
 int enqueue_frame(rtm_ctx* ctx, FrameArgs& a, float* out_dev, StatsK* stats) {
     int rc;
-    rtm_camera sc{};
-    sc.type = a.shadow.type;
-    for (int i = 0; i < 3; ++i) {
-        sc.pos[i] = a.shadow.pos[i];
-        sc.dir[i] = a.shadow.dir[i];
-        sc.up[i] = a.shadow.up[i];
-        sc.side[i] = a.shadow.side[i];
-    }
-    if ((rc = ensure_tables(ctx, a.steps, a.W, a.H, &sc, a.patch, a.n_patches, &a.tab))) return rc;
-    const bool fused = (a.flags & RTM_FLAG_FUSED_SHADOW) != 0;
+    if ((rc = frame_tables(ctx, a))) return rc;
+    const bool fused = (a.ey.flags & RTM_FLAG_FUSED_SHADOW) != 0;
     hipStream_t s = ctx->stream;
     double* smap = nullptr;
-    const bool timed = !ctx->ring.empty() && (ctx->calls++ % ctx->stride) == 0;
-    TimingSlot* slot = timed ? &ctx->ring[(size_t)(ctx->renders % (int64_t)ctx->ring.size())] : nullptr;
+    TimingSlot* slot = next_slot(ctx);
     if (!fused) {
-        if ((rc = ctx->smap.ensure(sizeof(double) * (size_t)a.Ws * (size_t)a.Hs, ctx->device))) return rc;
+        if ((rc = ctx->smap.ensure(sizeof(double) * (size_t)a.sh.W * (size_t)a.sh.H, ctx->device))) return rc;
         smap = (double*)ctx->smap.p;
-        ctx->smap_w = a.Ws;
-        ctx->smap_h = a.Hs;
+        ctx->smap_w = a.sh.W;
+        ctx->smap_h = a.sh.H;
         if (slot) HIP_TRY(hipEventRecord(slot->ev[0], s));
         if ((rc = launch_shadow_pass(a, smap, s, stats))) return fail(rc, "shadow pass launch failed");
         if (slot) HIP_TRY(hipEventRecord(slot->ev[1], s));
         ctx->have_shadow_pass = true;
+        ctx->last_smap = smap;
     } else {
         ctx->have_shadow_pass = false;
     }
@@ -598,15 +625,96 @@ int rtm_render_async(rtm_ctx* ctx, const rtm_scene* scene, const rtm_camera* eye
     if (rc) return rc;
     if (row_begin < 0 || row_end > height || row_begin >= row_end)
         return fail(RTM_ERR_INVALID, "row range [%d,%d) outside [0,%d)", row_begin, row_end, height);
-    a.row_begin = row_begin;
-    a.row_end = row_end;
+    a.ey.row_begin = row_begin;
+    a.ey.row_end = row_end;
     DeviceGuard g(ctx->device);
     return enqueue_frame(ctx, a, out_rgba_dev, nullptr);
 }
 
 const double* rtm_ctx_shadow_map(rtm_ctx* ctx) {
     if (!ctx || !ctx->have_shadow_pass) return nullptr;
-    return (const double*)ctx->smap.p;
+    return ctx->last_smap;
+}
+
+int rtm_render_frames_async(rtm_ctx* ctx, int32_t n_frames, const rtm_scene* scenes, const rtm_camera* eye,
+                            const rtm_camera* shadow, int32_t width, int32_t height, int32_t march_steps,
+                            int32_t flags, float* const* out_rgba_dev) {
+    if (!ctx || !scenes || !out_rgba_dev || n_frames < 1) return fail(RTM_ERR_INVALID, "bad arguments");
+    for (int32_t i = 0; i < n_frames; ++i)
+        if (!out_rgba_dev[i]) return fail(RTM_ERR_INVALID, "out_rgba_dev[%d] is NULL", i);
+    std::vector<FrameArgs> f((size_t)n_frames);
+    for (int32_t i = 0; i < n_frames; ++i) {
+        int rc = build_frame(f[(size_t)i], &scenes[i], eye, shadow, width, height, march_steps, flags);
+        if (rc) return rc;
+    }
+    DeviceGuard g(ctx->device);
+    // The pipeline shares one table set: every frame must have the same patches
+    // (the cameras are shared by construction).  Otherwise render frame by frame.
+    bool same = (flags & RTM_FLAG_FUSED_SHADOW) == 0 && n_frames > 1;
+    for (int32_t i = 1; same && i < n_frames; ++i)
+        same = f[(size_t)i].sh.n_patches == f[0].sh.n_patches &&
+               std::memcmp(f[(size_t)i].sh.patch, f[0].sh.patch, sizeof(PatchK) * (size_t)f[0].sh.n_patches) == 0;
+    if (!same) {
+        for (int32_t i = 0; i < n_frames; ++i) {
+            int rc = enqueue_frame(ctx, f[(size_t)i], out_rgba_dev[i], nullptr);
+            if (rc) return rc;
+        }
+        return RTM_OK;
+    }
+    int rc = frame_tables(ctx, f[0]);
+    if (rc) return rc;
+    for (int32_t i = 1; i < n_frames; ++i) {
+        f[(size_t)i].sh.tab = f[0].sh.tab;
+        f[(size_t)i].ey.nx = f[0].ey.nx;
+        f[(size_t)i].ey.ny = f[0].ey.ny;
+    }
+    const size_t smap_bytes = sizeof(double) * (size_t)width * (size_t)height;
+    if ((rc = ctx->smap.ensure(smap_bytes, ctx->device)) || (rc = ctx->smap2.ensure(smap_bytes, ctx->device)))
+        return rc;
+    double* sm[2] = {(double*)ctx->smap.p, (double*)ctx->smap2.p};
+    hipStream_t s = ctx->stream;
+    // prologue: shadow pass of frame 0
+    TimingSlot* slot = next_slot(ctx);
+    if (slot) HIP_TRY(hipEventRecord(slot->ev[0], s));
+    if ((rc = launch_shadow_pass(f[0], sm[0], s, nullptr))) return fail(rc, "shadow pass launch failed");
+    if (slot) {
+        HIP_TRY(hipEventRecord(slot->ev[1], s));
+        HIP_TRY(hipEventRecord(slot->ev[2], s));
+        HIP_TRY(hipEventRecord(slot->ev[3], s));
+        slot->shadow = true;
+        ctx->renders++;
+    }
+    // steady state: shadow pass of frame i + eye pass of frame i-1, one launch
+    for (int32_t i = 1; i < n_frames; ++i) {
+        FrameArgs a;
+        a.sh = f[(size_t)i].sh;
+        a.ey = f[(size_t)(i - 1)].ey;
+        slot = next_slot(ctx);
+        if (slot) HIP_TRY(hipEventRecord(slot->ev[2], s));
+        if ((rc = launch_frame_pipe(a, sm[i & 1], sm[(i - 1) & 1], out_rgba_dev[i - 1], s)))
+            return fail(rc, "pipelined frame launch failed");
+        if (slot) {
+            HIP_TRY(hipEventRecord(slot->ev[3], s));
+            slot->shadow = false;
+            ctx->renders++;
+        }
+    }
+    // epilogue: eye pass of the last frame
+    slot = next_slot(ctx);
+    if (slot) HIP_TRY(hipEventRecord(slot->ev[2], s));
+    const int32_t last = n_frames - 1;
+    if ((rc = launch_eye_pass(f[(size_t)last], sm[last & 1], out_rgba_dev[last], s, nullptr)))
+        return fail(rc, "eye pass launch failed");
+    if (slot) {
+        HIP_TRY(hipEventRecord(slot->ev[3], s));
+        slot->shadow = false;
+        ctx->renders++;
+    }
+    ctx->have_shadow_pass = true;
+    ctx->last_smap = sm[last & 1];
+    ctx->smap_w = width;
+    ctx->smap_h = height;
+    return RTM_OK;
 }
 
 int rtm_render(const rtm_scene* scene, const rtm_camera* eye, const rtm_camera* shadow, int32_t width,

@@ -76,19 +76,36 @@ struct Tables {
 };
 #define RTM_T_TABLE_MAX 65536
 
-// Everything one frame's kernels read.  Kept < 4 KiB (kernarg limit).
-struct FrameArgs {
-    RasterSphereK esph[RTM_MAX_SPHERES];  // eye camera projection
-    RasterSphereK ssph[RTM_MAX_SPHERES];  // shadow camera projection
-    ShadeSphereK shade[RTM_MAX_SPHERES];
+// What the shadow pass of one frame reads (shadow viewport rasterize + march).
+struct ShadowPart {
+    RasterSphereK sph[RTM_MAX_SPHERES];  // shadow camera projection
     PatchK patch[RTM_MAX_PATCHES];
-    CamK eye, shadow;
-    int32_t W, H;            // eye image
-    int32_t Ws, Hs;          // shadow map (== W, H)
+    CamK cam;                            // shadow camera
+    Tables tab;                          // shadow-map dims
+    int32_t W, H;                        // shadow map (== eye image dims)
     int32_t n_spheres, n_patches;
     int32_t steps, flags;
+};
+
+// What the eye pass of one frame reads (eye viewport rasterize + renderColorImage).
+struct EyePart {
+    RasterSphereK sph[RTM_MAX_SPHERES];  // eye camera projection
+    ShadeSphereK shade[RTM_MAX_SPHERES];
+    CamK eye, shadow;                    // shadow: Camera::project for the lookup (main.rs:836)
+    const double* nx;                    // eye NDC tables (Tables::nx / ny)
+    const double* ny;
+    int32_t W, H;                        // eye image
+    int32_t Ws, Hs;                      // shadow map
+    int32_t n_spheres, flags;
     int32_t row_begin, row_end;
-    Tables tab;
+};
+
+// One launch's arguments: the shadow pass of frame i and the eye pass of frame
+// i (plain launches, RTM_FLAG_FUSED_SHADOW) or of frame i-1 (the software-
+// pipelined frame kernel).  Kept < 4 KiB (kernarg limit).
+struct FrameArgs {
+    ShadowPart sh;
+    EyePart ey;
 };
 static_assert(sizeof(FrameArgs) <= 4096, "FrameArgs must fit the 4 KiB kernarg segment");
 
@@ -123,6 +140,11 @@ static_assert(sizeof(StatsK) == sizeof(rtm_stats), "StatsK layout");
 // Launchers (rtm_kernels.hip).  All asynchronous on `stream`.
 int launch_shadow_pass(const FrameArgs& a, double* smap, void* stream, StatsK* stats);
 int launch_eye_pass(const FrameArgs& a, const double* smap, float* out, void* stream, StatsK* stats);
+// Software-pipelined frame step: the shadow pass of a.sh into smap_w and the eye
+// pass of a.ey (the previous frame) from smap_r into out, in ONE launch whose
+// workgroups interleave the two roles (VALU-bound and HBM-store-bound tiles
+// share the CUs).  smap_w != smap_r.
+int launch_frame_pipe(const FrameArgs& a, double* smap_w, const double* smap_r, float* out, void* stream);
 int launch_vp_rasterize(const RasterArgs& a, double* zbuf, double* gh, double* gz, int32_t* gid,
                         void* stream);
 int launch_vp_march(const MarchArgs& a, double* zbuf, void* stream);

@@ -259,22 +259,23 @@ struct ShadowCounts {
     unsigned long long tests = 0, iters = 0, hits = 0, inrange = 0;
 };
 
-// One shadow-map texel: shadow viewport rasterize (face BACK, main.rs:1569) then
-// processRaymarchingRays (main.rs:1571) with a strict-min update (main.rs:559).
-// [xb, xe] x yw is the pixel set the caller's wave covers (for the cull).
+// One shadow-map texel (any shadow camera): shadow viewport rasterize (face BACK,
+// main.rs:1569) then processRaymarchingRays (main.rs:1571) with a strict-min
+// update (main.rs:559).  [xb, xe] x yw is the pixel set the caller's wave
+// covers (for the per-wave cull).
 template <bool COUNT>
-__device__ __forceinline__ double shadow_texel(const FrameArgs& a, int xi, int yi, int xb, int xe, int yw,
+__device__ __forceinline__ double shadow_texel(const ShadowPart& a, int xi, int yi, int xb, int xe, int yw,
                                                ShadowCounts& c) {
     double zb = INFINITY;
     if (!(a.flags & RTM_FLAG_NO_SHADOW_RASTER)) {
-        const double x = a.tab.nx[xi];  // shadow map dims == eye dims
+        const double x = a.tab.nx[xi];
         const double y = a.tab.ny[yi];
         for (int i = 0; i < a.n_spheres; ++i) {
-            if (!may_cover(a.ssph[i], xb, xe, yw)) continue;
+            if (!may_cover(a.sph[i], xb, xe, yw)) continue;
             double h;
-            if (cover(a.ssph[i], x, y, h)) {
+            if (cover(a.sph[i], x, y, h)) {
                 if (COUNT) ++c.tests;
-                const double depth = a.ssph[i].z + h * a.ssph[i].r;  // EnumFace::BACK (main.rs:243)
+                const double depth = a.sph[i].z + h * a.sph[i].r;  // EnumFace::BACK (main.rs:243)
                 if (depth < zb) zb = depth;
             }
         }
@@ -284,11 +285,11 @@ __device__ __forceinline__ double shadow_texel(const FrameArgs& a, int xi, int y
             // separable axis-aligned shadow camera: the texel's domain-mapped start
             // and surface depth come from per-column / per-row tables
             const double py = a.tab.py[yi];
-            const bool inr0 = a.tab.ok[xi] && a.tab.ok[a.Ws + yi];
+            const bool inr0 = a.tab.ok[xi] && a.tab.ok[a.W + yi];
             const double oz = a.tab.z[0];
-            const double sz = a.shadow.dir[2] * 0.03;
+            const double sz = a.cam.dir[2] * 0.03;
             for (int k = 0; k < a.n_patches; ++k) {
-                const double D = a.tab.d0[k * a.Ws + xi] + a.tab.dd[k * a.Ws + xi] * py;
+                const double D = a.tab.d0[k * a.W + xi] + a.tab.dd[k * a.W + xi] * py;
                 MarchResult m = march_axis<COUNT>(D, inr0, oz, sz, a.steps, a.tab);
                 if (COUNT) {
                     c.iters += m.iters;
@@ -299,7 +300,7 @@ __device__ __forceinline__ double shadow_texel(const FrameArgs& a, int xi, int y
             }
         } else {
             double o[3], d[3];
-            cam_ray(a.shadow, a.tab.nx[xi], a.tab.ny[yi], o, d);
+            cam_ray(a.cam, a.tab.nx[xi], a.tab.ny[yi], o, d);
             for (int k = 0; k < a.n_patches; ++k) {
                 MarchResult m = march<COUNT>(o[0], o[1], o[2], d[0], d[1], d[2], a.patch[k], a.steps, a.tab);
                 if (COUNT) {
@@ -314,16 +315,17 @@ __device__ __forceinline__ double shadow_texel(const FrameArgs& a, int xi, int y
     return zb;
 }
 
+// Generic shadow tile: 64 x TILE_Y texels, one wave per row.
 template <bool COUNT>
-__global__ __launch_bounds__(BLOCK) void shadow_pass_kernel(const FrameArgs a, double* __restrict__ smap,
-                                                            StatsK* __restrict__ st) {
-    const int xb = blockIdx.x * TILE_X;
+__device__ __forceinline__ void shadow_tile_generic(const ShadowPart& a, double* __restrict__ smap, int bx, int by,
+                                                    StatsK* __restrict__ st) {
+    const int xb = bx * TILE_X;
     const int xi = xb + (threadIdx.x & (TILE_X - 1));
-    const int yi = __builtin_amdgcn_readfirstlane(blockIdx.y * TILE_Y + (threadIdx.x >> 6));  // wave-uniform row
+    const int yi = __builtin_amdgcn_readfirstlane(by * TILE_Y + (threadIdx.x >> 6));  // wave-uniform row
     ShadowCounts c;
-    if (xi < a.Ws && yi < a.Hs) {
+    if (xi < a.W && yi < a.H) {
         const double zb = shadow_texel<COUNT>(a, xi, yi, xb, xb + TILE_X - 1, yi, c);
-        smap[(int64_t)yi * a.Ws + xi] = zb;
+        smap[(int64_t)yi * a.W + xi] = zb;
     }
     if (COUNT) {
         stat_add(&st->shadow_sphere_tests, c.tests);
@@ -333,28 +335,28 @@ __global__ __launch_bounds__(BLOCK) void shadow_pass_kernel(const FrameArgs a, d
     }
 }
 
-// Shadow pass for the separable axis-aligned shadow camera with a shared z
-// sequence (the BASELINE scenes): NR rows per wave give every lane NR
-// independent march chains (ILP against the VALU and scalar-load latencies the
-// one-texel kernel stalls on), the 8-step table chunks are prefetched one
-// chunk ahead, and each step is the sign bit of fl(z_k - D) (D finite and
-// nonzero on this path, so that bit is exactly [z_k < D], see march_axis).
-// Lanes whose D is not finite/nonzero send their wave to the exact per-texel
-// path, so results never depend on the fast path being taken.
+// Shadow tile for the separable axis-aligned shadow camera with a shared z
+// sequence (the BASELINE scenes): 64 x (TILE_Y*NR) texels, NR rows per wave, so
+// every lane runs NR independent march chains (ILP against VALU and load
+// latency), the 8-step table chunks are prefetched one chunk ahead, and each
+// step is the sign bit of fl(z_k - D) (D finite and nonzero on this path, so
+// that bit is exactly [z_k < D], see march_axis).  If any lane's D is not
+// finite/nonzero the wave takes the exact per-texel loop instead.
 template <int NR>
-__global__ __launch_bounds__(BLOCK) void shadow_sep_kernel(const FrameArgs a, double* __restrict__ smap, int diag) {
+__device__ __forceinline__ void shadow_tile_sep(const ShadowPart& a, double* __restrict__ smap, int bx, int by,
+                                                int diag) {
     const int lane = threadIdx.x & (TILE_X - 1);
-    const int xb = blockIdx.x * TILE_X;
+    const int xb = bx * TILE_X;
     const int xi = xb + lane;
-    const int y0 = __builtin_amdgcn_readfirstlane(blockIdx.y * (TILE_Y * NR) + (threadIdx.x >> 6) * NR);
-    const bool colv = xi < a.Ws;
-    const int xs = colv ? xi : a.Ws - 1;  // clamped column for table reads
+    const int y0 = __builtin_amdgcn_readfirstlane(by * (TILE_Y * NR) + (threadIdx.x >> 6) * NR);
+    const bool colv = xi < a.W;
+    const int xs = colv ? xi : a.W - 1;  // clamped column for table reads
     double zb[NR];
     bool rowv[NR];
 #pragma unroll
     for (int r = 0; r < NR; ++r) {
         zb[r] = INFINITY;
-        rowv[r] = y0 + r < a.Hs;
+        rowv[r] = y0 + r < a.H;
     }
     // shadow viewport rasterize, face BACK (main.rs:1569, 243)
     if (!(a.flags & RTM_FLAG_NO_SHADOW_RASTER) && !(diag & 1)) {
@@ -362,10 +364,10 @@ __global__ __launch_bounds__(BLOCK) void shadow_sep_kernel(const FrameArgs a, do
         for (int i = 0; i < a.n_spheres; ++i) {
 #pragma unroll
             for (int r = 0; r < NR; ++r) {
-                if (!rowv[r] || !may_cover(a.ssph[i], xb, xb + TILE_X - 1, y0 + r)) continue;
+                if (!rowv[r] || !may_cover(a.sph[i], xb, xb + TILE_X - 1, y0 + r)) continue;
                 double h;
-                if (cover(a.ssph[i], x, a.tab.ny[y0 + r], h)) {
-                    const double depth = a.ssph[i].z + h * a.ssph[i].r;
+                if (cover(a.sph[i], x, a.tab.ny[y0 + r], h)) {
+                    const double depth = a.sph[i].z + h * a.sph[i].r;
                     if (depth < zb[r]) zb[r] = depth;
                 }
             }
@@ -373,31 +375,31 @@ __global__ __launch_bounds__(BLOCK) void shadow_sep_kernel(const FrameArgs a, do
     }
     if (!(a.flags & RTM_FLAG_NO_MARCH) && !(diag & 2)) {
         const double oz = a.tab.z[0];
-        const double sz = a.shadow.dir[2] * 0.03;
+        const double sz = a.cam.dir[2] * 0.03;
         const int steps = a.steps;
         const bool colok = a.tab.ok[xs] != 0;
         for (int k = 0; k < a.n_patches; ++k) {
             double D[NR];
             bool inr[NR], fast = true;
-            const double d0 = a.tab.d0[k * a.Ws + xs];
-            const double dd = a.tab.dd[k * a.Ws + xs];
+            const double d0 = a.tab.d0[k * a.W + xs];
+            const double dd = a.tab.dd[k * a.W + xs];
 #pragma unroll
             for (int r = 0; r < NR; ++r) {
                 const int yr = rowv[r] ? y0 + r : y0;
                 D[r] = d0 + dd * a.tab.py[yr];
-                inr[r] = colv && rowv[r] && colok && a.tab.ok[a.Ws + yr] != 0;
+                inr[r] = colv && rowv[r] && colok && a.tab.ok[a.W + yr] != 0;
                 fast = fast && (!inr[r] || (fabs(D[r]) < INFINITY && D[r] != 0.0));
             }
             int cnt[NR];
             if (__all(fast)) {
                 cdouble* zt = (cdouble*)a.tab.z;  // padded by 8 entries past `steps`
-                bool epos[NR];
                 unsigned eposb[NR], inrb[NR];
+                bool epos[NR];
                 int lt[NR];
                 bool any_inr = false;
 #pragma unroll
                 for (int r = 0; r < NR; ++r) {
-                    epos[r] = !(oz < D[r]);
+                    epos[r] = !(oz < D[r]);  // entry class POS <=> z0 >= D
                     eposb[r] = epos[r] ? 1u : 0u;
                     inrb[r] = inr[r] ? 1u : 0u;
                     lt[r] = 0;
@@ -424,7 +426,7 @@ __global__ __launch_bounds__(BLOCK) void shadow_sep_kernel(const FrameArgs a, do
                             }
                             cont |= inrb[r] & (last ^ eposb[r]);
                         }
-                        if (!__any(cont != 0u)) {
+                        if (!__any(cont != 0u)) {  // every lane met its surface: wave early-out
                             kk += 8;
                             stopped = true;
                             break;
@@ -443,7 +445,7 @@ __global__ __launch_bounds__(BLOCK) void shadow_sep_kernel(const FrameArgs a, do
 #pragma unroll
                 for (int r = 0; r < NR; ++r) cnt[r] = inr[r] ? (epos[r] ? kk - lt[r] : lt[r]) : steps;
             } else {
-                // exact per-texel path (march_axis applies the result itself)
+                // exact per-texel path (march_axis returns t itself)
 #pragma unroll
                 for (int r = 0; r < NR; ++r) {
                     MarchResult m = march_axis<false>(D[r], inr[r], oz, sz, steps, a.tab);
@@ -463,40 +465,41 @@ __global__ __launch_bounds__(BLOCK) void shadow_sep_kernel(const FrameArgs a, do
     if (colv) {
 #pragma unroll
         for (int r = 0; r < NR; ++r)
-            if (rowv[r]) smap[(int64_t)(y0 + r) * a.Ws + xi] = zb[r];
+            if (rowv[r]) smap[(int64_t)(y0 + r) * a.W + xi] = zb[r];
     }
 }
 
-// Eye pixel: eye viewport rasterize (face FRONT, main.rs:1616) + renderColorImage
-// (main.rs:714-898).  FUSED evaluates the looked-up shadow texel on demand.
+// Eye tile: 64 x TILE_Y pixels: eye viewport rasterize (face FRONT, main.rs:1616)
+// + renderColorImage (main.rs:714-898).  FUSED evaluates the looked-up shadow
+// texel on demand from `sh` (same frame) instead of reading `smap`.
 template <bool FUSED, bool COUNT>
-__global__ __launch_bounds__(BLOCK) void eye_pass_kernel(const FrameArgs a, const double* __restrict__ smap,
-                                                         float4* __restrict__ out, StatsK* __restrict__ st) {
-    const int xb = blockIdx.x * TILE_X;
+__device__ __forceinline__ void eye_tile(const EyePart& a, const ShadowPart& sh, const double* __restrict__ smap,
+                                         float4* __restrict__ out, int bx, int by, StatsK* __restrict__ st) {
+    const int xb = bx * TILE_X;
     const int xi = xb + (threadIdx.x & (TILE_X - 1));
-    const int yl = __builtin_amdgcn_readfirstlane(blockIdx.y * TILE_Y + (threadIdx.x >> 6));
+    const int yl = __builtin_amdgcn_readfirstlane(by * TILE_Y + (threadIdx.x >> 6));
     const int yi = a.row_begin + yl;
     const bool live = xi < a.W && yi < a.row_end;
     unsigned long long n_tests = 0, n_hit = 0, n_lit = 0;
     ShadowCounts sc;
     int hit_id = -1;
     if (live) {
-        const double x = a.tab.nx[xi];
-        const double y = a.tab.ny[yi];
+        const double x = a.nx[xi];
+        const double y = a.ny[yi];
         // z-test over spheres in scene order, strict '<' against +INF init (main.rs:318)
         double best = INFINITY, bh = 0.0, bz = 0.0;
         int bid = -1;
         for (int i = 0; i < a.n_spheres; ++i) {
-            if (!may_cover(a.esph[i], xb, xb + TILE_X - 1, yi)) continue;
+            if (!may_cover(a.sph[i], xb, xb + TILE_X - 1, yi)) continue;
             double h;
-            if (cover(a.esph[i], x, y, h)) {
+            if (cover(a.sph[i], x, y, h)) {
                 if (COUNT) ++n_tests;
-                const double depth = a.esph[i].z - h * a.esph[i].r;  // EnumFace::FRONT (main.rs:239)
+                const double depth = a.sph[i].z - h * a.sph[i].r;  // EnumFace::FRONT (main.rs:239)
                 if (depth < best) {
                     best = depth;
                     bh = h;
-                    bz = a.esph[i].z;
-                    bid = a.esph[i].id;
+                    bz = a.sph[i].z;
+                    bid = a.sph[i].id;
                 }
             }
         }
@@ -535,7 +538,7 @@ __global__ __launch_bounds__(BLOCK) void eye_pass_kernel(const FrameArgs a, cons
             double dsm = INFINITY;
             if (ty >= 0 && ty < a.Hs && tx >= 0 && tx < a.Ws) {
                 if (FUSED)
-                    dsm = shadow_texel<COUNT>(a, (int)tx, (int)ty, (int)tx, (int)tx, (int)ty, sc);
+                    dsm = shadow_texel<COUNT>(sh, (int)tx, (int)ty, (int)tx, (int)tx, (int)ty, sc);
                 else
                     dsm = smap[ty * a.Ws + tx];
             }
@@ -564,6 +567,48 @@ __global__ __launch_bounds__(BLOCK) void eye_pass_kernel(const FrameArgs a, cons
             stat_add(&st->march_hits, sc.hits);
             stat_add(&st->march_in_range, sc.inrange);
         }
+    }
+}
+
+template <bool COUNT>
+__global__ __launch_bounds__(BLOCK) void shadow_pass_kernel(const FrameArgs a, double* __restrict__ smap,
+                                                            StatsK* __restrict__ st) {
+    shadow_tile_generic<COUNT>(a.sh, smap, blockIdx.x, blockIdx.y, st);
+}
+
+template <int NR>
+__global__ __launch_bounds__(BLOCK) void shadow_sep_kernel(const FrameArgs a, double* __restrict__ smap, int diag) {
+    shadow_tile_sep<NR>(a.sh, smap, blockIdx.x, blockIdx.y, diag);
+}
+
+template <bool FUSED, bool COUNT>
+__global__ __launch_bounds__(BLOCK) void eye_pass_kernel(const FrameArgs a, const double* __restrict__ smap,
+                                                         float4* __restrict__ out, StatsK* __restrict__ st) {
+    eye_tile<FUSED, COUNT>(a.ey, a.sh, smap, out, blockIdx.x, blockIdx.y, st);
+}
+
+// Software-pipelined frame step (launch_frame_pipe): a 1-D grid of
+// n_sh shadow tiles (frame i) and n_eye eye tiles (frame i-1) merged in
+// proportion (Bresenham), so both roles are resident on every CU through the
+// whole launch.  SEP: shadow tiles use shadow_tile_sep<NR>, else the generic one.
+template <bool SEP, int NR>
+__global__ __launch_bounds__(BLOCK) void frame_pipe_kernel(const FrameArgs a, double* __restrict__ smap_w,
+                                                           const double* __restrict__ smap_r,
+                                                           float4* __restrict__ out, int sh_gx, int n_sh,
+                                                           int eye_gx, int n_eye) {
+    const int64_t b = blockIdx.x;
+    const int64_t total = (int64_t)n_sh + n_eye;
+    const int64_t s_before = (b * n_sh) / total;         // shadow tiles among blocks [0, b)
+    const int64_t s_after = ((b + 1) * n_sh) / total;    // ... among [0, b]
+    if (s_after > s_before) {
+        const int t = (int)s_before;
+        if (SEP)
+            shadow_tile_sep<NR>(a.sh, smap_w, t % sh_gx, t / sh_gx, 0);
+        else
+            shadow_tile_generic<false>(a.sh, smap_w, t % sh_gx, t / sh_gx, nullptr);
+    } else {
+        const int t = (int)(b - s_before);
+        eye_tile<false, false>(a.ey, a.sh, smap_r, out, t % eye_gx, t / eye_gx, nullptr);
     }
 }
 
@@ -706,6 +751,8 @@ static int diag_mode() {
     return v;
 }
 
+// Rows per wave of the separable shadow tile (0 = generic tile).  Default chosen
+// by measurement (profiles/); RTM_SEP_ROWS overrides it for A/B runs.
 static int sep_rows() {
     static int v = [] {
         const char* e = getenv("RTM_SEP_ROWS");
@@ -715,33 +762,35 @@ static int sep_rows() {
     return v;
 }
 
+static bool use_sep(const ShadowPart& s) { return sep_rows() > 0 && s.tab.d0 && s.tab.z && s.tab.t; }
+
 template <int NR>
 static void launch_sep(const FrameArgs& a, double* smap, hipStream_t s) {
-    dim3 g((unsigned)((a.Ws + TILE_X - 1) / TILE_X), (unsigned)((a.Hs + TILE_Y * NR - 1) / (TILE_Y * NR)));
+    dim3 g((unsigned)((a.sh.W + TILE_X - 1) / TILE_X), (unsigned)((a.sh.H + TILE_Y * NR - 1) / (TILE_Y * NR)));
     hipLaunchKernelGGL(shadow_sep_kernel<NR>, g, dim3(BLOCK), 0, s, a, smap, diag_mode());
 }
 
 int launch_shadow_pass(const FrameArgs& a, double* smap, void* stream, StatsK* stats) {
     hipStream_t s = (hipStream_t)stream;
-    const int nr = sep_rows();
-    if (!stats && nr > 0 && a.tab.d0 && a.tab.z && a.tab.t) {
+    if (!stats && use_sep(a.sh)) {
+        const int nr = sep_rows();
         if (nr == 1) launch_sep<1>(a, smap, s);
         else if (nr == 2) launch_sep<2>(a, smap, s);
         else launch_sep<4>(a, smap, s);
         return launched();
     }
     if (stats)
-        hipLaunchKernelGGL(shadow_pass_kernel<true>, grid_for(a.Ws, a.Hs), dim3(BLOCK), 0, s, a, smap, stats);
+        hipLaunchKernelGGL(shadow_pass_kernel<true>, grid_for(a.sh.W, a.sh.H), dim3(BLOCK), 0, s, a, smap, stats);
     else
-        hipLaunchKernelGGL(shadow_pass_kernel<false>, grid_for(a.Ws, a.Hs), dim3(BLOCK), 0, s, a, smap, stats);
+        hipLaunchKernelGGL(shadow_pass_kernel<false>, grid_for(a.sh.W, a.sh.H), dim3(BLOCK), 0, s, a, smap, stats);
     return launched();
 }
 
 int launch_eye_pass(const FrameArgs& a, const double* smap, float* out, void* stream, StatsK* stats) {
     hipStream_t s = (hipStream_t)stream;
-    dim3 g = grid_for(a.W, a.row_end - a.row_begin);
+    dim3 g = grid_for(a.ey.W, a.ey.row_end - a.ey.row_begin);
     float4* o = reinterpret_cast<float4*>(out);
-    const bool fused = (a.flags & RTM_FLAG_FUSED_SHADOW) != 0;
+    const bool fused = (a.ey.flags & RTM_FLAG_FUSED_SHADOW) != 0;
     if (fused && stats)
         hipLaunchKernelGGL((eye_pass_kernel<true, true>), g, dim3(BLOCK), 0, s, a, smap, o, stats);
     else if (fused)
@@ -750,6 +799,31 @@ int launch_eye_pass(const FrameArgs& a, const double* smap, float* out, void* st
         hipLaunchKernelGGL((eye_pass_kernel<false, true>), g, dim3(BLOCK), 0, s, a, smap, o, stats);
     else
         hipLaunchKernelGGL((eye_pass_kernel<false, false>), g, dim3(BLOCK), 0, s, a, smap, o, stats);
+    return launched();
+}
+
+template <bool SEP, int NR>
+static void launch_pipe(const FrameArgs& a, double* smap_w, const double* smap_r, float4* out, hipStream_t s) {
+    const int sh_gx = (a.sh.W + TILE_X - 1) / TILE_X;
+    const int sh_gy = (a.sh.H + TILE_Y * NR - 1) / (TILE_Y * NR);
+    const int eye_gx = (a.ey.W + TILE_X - 1) / TILE_X;
+    const int eye_gy = (a.ey.row_end - a.ey.row_begin + TILE_Y - 1) / TILE_Y;
+    const int n_sh = sh_gx * sh_gy, n_eye = eye_gx * eye_gy;
+    hipLaunchKernelGGL((frame_pipe_kernel<SEP, NR>), dim3((unsigned)(n_sh + n_eye)), dim3(BLOCK), 0, s, a, smap_w,
+                       smap_r, out, sh_gx, n_sh, eye_gx, n_eye);
+}
+
+int launch_frame_pipe(const FrameArgs& a, double* smap_w, const double* smap_r, float* out, void* stream) {
+    hipStream_t s = (hipStream_t)stream;
+    float4* o = reinterpret_cast<float4*>(out);
+    if (use_sep(a.sh)) {
+        const int nr = sep_rows();
+        if (nr == 1) launch_pipe<true, 1>(a, smap_w, smap_r, o, s);
+        else if (nr == 2) launch_pipe<true, 2>(a, smap_w, smap_r, o, s);
+        else launch_pipe<true, 4>(a, smap_w, smap_r, o, s);
+    } else {
+        launch_pipe<false, 1>(a, smap_w, smap_r, o, s);
+    }
     return launched();
 }
 

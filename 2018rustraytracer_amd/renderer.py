@@ -84,6 +84,28 @@ class Context:
                                             steps, flags, row_begin, row_end, C.c_void_p(out_ptr)),
                   "rtm_render_async")
 
+    def prepare_frames(self, scenes):
+        """ctypes array of rtm_scene for render_frames_async (+ keepalive)."""
+        arr = (abi.rtm_scene * len(scenes))()
+        keep = []
+        for i, s in enumerate(scenes):
+            c, k = s.to_c()
+            arr[i] = c
+            keep.append(k)
+        return arr, keep
+
+    def render_frames_async(self, scenes, eye: Camera, shadow: Camera, width: int, height: int, steps: int,
+                            flags: int, out_ptrs, prepared=None):
+        """Enqueue len(scenes) frames (software-pipelined when the patches agree);
+        frame i goes to device pointer out_ptrs[i]."""
+        arr, keep = prepared if prepared is not None else self.prepare_frames(scenes)  # scenes unused if prepared
+        n = len(arr)
+        outs = (C.c_void_p * n)(*[C.c_void_p(p) for p in out_ptrs])
+        e, s = eye.to_c(), shadow.to_c()
+        lib = _lib()
+        abi.check(lib, lib.rtm_render_frames_async(self._h, n, arr, C.byref(e), C.byref(s), width, height, steps,
+                                                   flags, outs), "rtm_render_frames_async")
+
     def shadow_map_ptr(self) -> int:
         return _lib().rtm_ctx_shadow_map(self._h) or 0
 

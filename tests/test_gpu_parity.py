@@ -265,3 +265,64 @@ def test_error_codes(rtm, scenes):
     with pytest.raises(abi.RtmError) as e:
         rtm.render_frame(many, scenes.eye_camera(), scenes.shadow_camera(), 64, 64, 10)
     assert e.value.code == abi.RTM_ERR_INVALID
+
+
+def _frames_vs_single(rtm, scenes, gpu_ctx, frames, eye, shadow, w, h, k, flags=0):
+    import torch
+    outs = [torch.empty((h, w, 4), dtype=torch.float32, device="cuda") for _ in frames]
+    torch.cuda.synchronize()
+    gpu_ctx.render_frames_async(frames, eye, shadow, w, h, k, flags, [o.data_ptr() for o in outs])
+    gpu_ctx.synchronize()
+    for s, o in zip(frames, outs):
+        want = rtm.render_frame(s, eye, shadow, w, h, k, flags)
+        got = o.cpu().numpy()
+        assert bits_equal(got, want), first_mismatch(got, want)
+
+
+@pytest.mark.parametrize("n", [1, 2, 5])
+def test_pipelined_frames_match_single_frames(rtm, scenes, gpu_ctx, n):
+    """rtm_render_frames_async (shadow pass of frame i + eye pass of frame i-1 in
+    one launch, double-buffered shadow maps) == frame-by-frame rtm_render."""
+    frames = [scenes.scene_a_bench(100 + 7 * i) for i in range(n)]
+    _frames_vs_single(rtm, scenes, gpu_ctx, frames, scenes.eye_camera(), scenes.shadow_camera(), 1920, 1080, 32)
+
+
+def test_pipelined_frames_reference_scene_and_oracle(rtm, oracle, scenes, gpu_ctx):
+    import torch
+    frames = [scenes.closely_orbiting_sphere(f) for f in (0, 1, 2, 100)]
+    outs = [torch.empty((512, 512, 4), dtype=torch.float32, device="cuda") for _ in frames]
+    torch.cuda.synchronize()
+    gpu_ctx.render_frames_async(frames, scenes.eye_camera(), scenes.shadow_camera(), 512, 512, 500, 0,
+                                [o.data_ptr() for o in outs])
+    gpu_ctx.synchronize()
+    for s, o in zip(frames, outs):
+        want = oracle.render(s, scenes.eye_camera(), scenes.shadow_camera(), 512, 512, 500, 0)["rgba"]
+        assert bits_equal(o.cpu().numpy(), want)
+
+
+def test_pipelined_frames_generic_shadow_tiles(rtm, scenes, gpu_ctx):
+    """Rotated shadow camera: the pipelined launch uses the generic shadow tile."""
+    rng = np.random.default_rng(7)
+    shadow = _random_camera(scenes, rng, False)
+    frames = [_random_scene(scenes, np.random.default_rng(11), 6, 2) for _ in range(3)]
+    _frames_vs_single(rtm, scenes, gpu_ctx, frames, scenes.eye_camera(), shadow, 333, 217, 80)
+
+
+def test_pipelined_frames_differing_patches_fallback(rtm, scenes, gpu_ctx):
+    frames = [scenes.scene_a_bench(100), scenes.scene_b(), scenes.closely_orbiting_sphere(3)]
+    _frames_vs_single(rtm, scenes, gpu_ctx, frames, scenes.eye_camera(), scenes.shadow_camera(), 640, 360, 64)
+
+
+def test_pipelined_frames_scene_b_8k(rtm, oracle, scenes, gpu_ctx):
+    """BASELINE config 5 geometry through the pipelined path, against the oracle."""
+    import torch
+    w, h, k = 7680, 4320, 128
+    frames = [scenes.scene_b(), scenes.scene_b()]
+    outs = [torch.empty((h, w, 4), dtype=torch.float32, device="cuda") for _ in frames]
+    torch.cuda.synchronize()
+    gpu_ctx.render_frames_async(frames, scenes.eye_camera(), scenes.shadow_camera(), w, h, k, 0,
+                                [o.data_ptr() for o in outs])
+    gpu_ctx.synchronize()
+    want = oracle.render(frames[0], scenes.eye_camera(), scenes.shadow_camera(), w, h, k, 0, nthreads=NT)["rgba"]
+    for o in outs:
+        assert bits_equal(o.cpu().numpy(), want)
