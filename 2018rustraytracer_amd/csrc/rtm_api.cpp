@@ -9,6 +9,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <string>
@@ -648,9 +649,17 @@ int rtm_render_frames_async(rtm_ctx* ctx, int32_t n_frames, const rtm_scene* sce
         if (rc) return rc;
     }
     DeviceGuard g(ctx->device);
+    // The pipelined launch (shadow pass of frame i + eye pass of frame i-1) is
+    // opt-in: measured on MI355X it is slower than two back-to-back kernels per
+    // frame (config 3: 99.5 vs 79.1 us/frame, profiles/r01_ab_pipe.txt) — the
+    // latency-bound march slows down beside the eye pass's store stream.
+    static const bool pipeline_on = [] {
+        const char* e = getenv("RTM_PIPELINE");
+        return e && atoi(e) != 0;
+    }();
     // The pipeline shares one table set: every frame must have the same patches
     // (the cameras are shared by construction).  Otherwise render frame by frame.
-    bool same = (flags & RTM_FLAG_FUSED_SHADOW) == 0 && n_frames > 1;
+    bool same = pipeline_on && (flags & RTM_FLAG_FUSED_SHADOW) == 0 && n_frames > 1;
     for (int32_t i = 1; same && i < n_frames; ++i)
         same = f[(size_t)i].sh.n_patches == f[0].sh.n_patches &&
                std::memcmp(f[(size_t)i].sh.patch, f[0].sh.patch, sizeof(PatchK) * (size_t)f[0].sh.n_patches) == 0;

@@ -28,8 +28,28 @@ namespace {
 constexpr int TILE_X = 64;  // one wave per tile row
 constexpr int TILE_Y = 4;   // four waves per workgroup
 constexpr int BLOCK = TILE_X * TILE_Y;
+#ifndef SEP_MIN_WAVES
+#define SEP_MIN_WAVES 1
+#endif
 
 using cdouble = const __attribute__((address_space(4))) double;  // scalar-loaded table
+using cint = const __attribute__((address_space(4))) int32_t;
+
+// Output stores: plain, or non-temporal (streamed past the caches) when `nt`.
+__device__ __forceinline__ void store_px(float4* p, float4 v, bool nt) {
+    if (nt) {
+        __builtin_nontemporal_store(v.x, &p->x);
+        __builtin_nontemporal_store(v.y, &p->y);
+        __builtin_nontemporal_store(v.z, &p->z);
+        __builtin_nontemporal_store(v.w, &p->w);
+    } else {
+        *p = v;
+    }
+}
+__device__ __forceinline__ void store_d(double* p, double v, bool nt) {
+    if (nt) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
 
 // main.rs:306-307 / 1903-1907: ((i as f64) / (res as f64)) * 2.0 - 1.0
 __device__ __forceinline__ double ndc(int i, int res) { return ((double)i / (double)res) * 2.0 - 1.0; }
@@ -335,6 +355,25 @@ __device__ __forceinline__ void shadow_tile_generic(const ShadowPart& a, double*
     }
 }
 
+// One 8-step chunk of the shared-z march for NR rows: lt[r] += #(z_k < D[r]);
+// returns true when no lane is still marching in any row (wave early-out).
+template <int NR>
+__device__ __forceinline__ bool chunk8(const double (&z)[8], const double (&D)[NR], int (&lt)[NR],
+                                       const unsigned (&inrb)[NR], const unsigned (&eposb)[NR]) {
+    unsigned cont = 0u;  // lane still marching in some row: inr & (last ^ epos)
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+        unsigned last = 0u;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            last = (unsigned)__double2hiint(z[u] - D[r]) >> 31;
+            lt[r] += (int)last;
+        }
+        cont |= inrb[r] & (last ^ eposb[r]);
+    }
+    return !__any(cont != 0u);
+}
+
 // Shadow tile for the separable axis-aligned shadow camera with a shared z
 // sequence (the BASELINE scenes): 64 x (TILE_Y*NR) texels, NR rows per wave, so
 // every lane runs NR independent march chains (ILP against VALU and load
@@ -344,7 +383,7 @@ __device__ __forceinline__ void shadow_tile_generic(const ShadowPart& a, double*
 // finite/nonzero the wave takes the exact per-texel loop instead.
 template <int NR>
 __device__ __forceinline__ void shadow_tile_sep(const ShadowPart& a, double* __restrict__ smap, int bx, int by,
-                                                int diag) {
+                                                int diag, bool nt) {
     const int lane = threadIdx.x & (TILE_X - 1);
     const int xb = bx * TILE_X;
     const int xi = xb + lane;
@@ -362,13 +401,17 @@ __device__ __forceinline__ void shadow_tile_sep(const ShadowPart& a, double* __r
     if (!(a.flags & RTM_FLAG_NO_SHADOW_RASTER) && !(diag & 1)) {
         const double x = a.tab.nx[xs];
         for (int i = 0; i < a.n_spheres; ++i) {
-#pragma unroll
-            for (int r = 0; r < NR; ++r) {
-                if (!rowv[r] || !may_cover(a.sph[i], xb, xb + TILE_X - 1, y0 + r)) continue;
+            const RasterSphereK& sp = a.sph[i];
+            if (y0 + NR - 1 < sp.iy0 || y0 > sp.iy1 || xb + TILE_X - 1 < sp.ix0 || xb > sp.ix1) continue;
+#pragma unroll 1
+            for (int r = 0; r < NR; ++r) {  // rows are wave-uniform: scalar loop, one copy of cover()
+                if (y0 + r >= a.H || !may_cover(a.sph[i], xb, xb + TILE_X - 1, y0 + r)) continue;
                 double h;
                 if (cover(a.sph[i], x, a.tab.ny[y0 + r], h)) {
                     const double depth = a.sph[i].z + h * a.sph[i].r;
-                    if (depth < zb[r]) zb[r] = depth;
+#pragma unroll
+                    for (int q = 0; q < NR; ++q)
+                        if (q == r && depth < zb[q]) zb[q] = depth;
                 }
             }
         }
@@ -385,9 +428,9 @@ __device__ __forceinline__ void shadow_tile_sep(const ShadowPart& a, double* __r
             const double dd = a.tab.dd[k * a.W + xs];
 #pragma unroll
             for (int r = 0; r < NR; ++r) {
-                const int yr = rowv[r] ? y0 + r : y0;
-                D[r] = d0 + dd * a.tab.py[yr];
-                inr[r] = colv && rowv[r] && colok && a.tab.ok[a.W + yr] != 0;
+                const int yr = rowv[r] ? y0 + r : y0;  // wave-uniform: scalar loads
+                D[r] = d0 + dd * ((cdouble*)a.tab.py)[yr];
+                inr[r] = colv && rowv[r] && colok && ((cint*)a.tab.ok)[a.W + yr] != 0;
                 fast = fast && (!inr[r] || (fabs(D[r]) < INFINITY && D[r] != 0.0));
             }
             int cnt[NR];
@@ -407,32 +450,34 @@ __device__ __forceinline__ void shadow_tile_sep(const ShadowPart& a, double* __r
                 }
                 int kk = 0;
                 if (__any(any_inr)) {
-                    double zc[8];
+                    // 8-step chunks, two per iteration with ping-pong table buffers (A, B):
+                    // the next chunk's 8 values are in flight while the current 8 are compared
+                    double zA[8], zB[8];
 #pragma unroll
-                    for (int u = 0; u < 8; ++u) zc[u] = zt[u];
+                    for (int u = 0; u < 8; ++u) zA[u] = zt[u];
                     bool stopped = false;
-                    for (; kk + 8 <= steps; kk += 8) {
-                        double zn[8];
+                    while (kk + 8 <= steps) {
 #pragma unroll
-                        for (int u = 0; u < 8; ++u) zn[u] = zt[kk + 8 + u];
-                        unsigned cont = 0u;  // lane still marching in some row: inr & (last ^ epos)
-#pragma unroll
-                        for (int r = 0; r < NR; ++r) {
-                            unsigned last = 0u;
-#pragma unroll
-                            for (int u = 0; u < 8; ++u) {
-                                last = (unsigned)__double2hiint(zc[u] - D[r]) >> 31;
-                                lt[r] += (int)last;
-                            }
-                            cont |= inrb[r] & (last ^ eposb[r]);
-                        }
-                        if (!__any(cont != 0u)) {  // every lane met its surface: wave early-out
+                        for (int u = 0; u < 8; ++u) zB[u] = zt[kk + 8 + u];
+                        if (chunk8<NR>(zA, D, lt, inrb, eposb)) {
                             kk += 8;
                             stopped = true;
                             break;
                         }
+                        kk += 8;
+                        if (kk + 8 > steps) {
 #pragma unroll
-                        for (int u = 0; u < 8; ++u) zc[u] = zn[u];
+                            for (int u = 0; u < 8; ++u) zA[u] = zB[u];
+                            break;
+                        }
+#pragma unroll
+                        for (int u = 0; u < 8; ++u) zA[u] = zt[kk + 8 + u];
+                        if (chunk8<NR>(zB, D, lt, inrb, eposb)) {
+                            kk += 8;
+                            stopped = true;
+                            break;
+                        }
+                        kk += 8;
                     }
                     if (!stopped) {
                         for (; kk < steps; ++kk) {
@@ -445,19 +490,32 @@ __device__ __forceinline__ void shadow_tile_sep(const ShadowPart& a, double* __r
 #pragma unroll
                 for (int r = 0; r < NR; ++r) cnt[r] = inr[r] ? (epos[r] ? kk - lt[r] : lt[r]) : steps;
             } else {
-                // exact per-texel path (march_axis returns t itself)
+                // exact per-texel path (march_axis returns t itself);
+                // one (not unrolled) copy of the exact loop: keeps the fast path's registers low
+#pragma unroll 1
+                for (int r = 0; r < NR; ++r) {
+                    double Dr = D[0];
+                    bool ir = inr[0];
+#pragma unroll
+                    for (int q = 1; q < NR; ++q) {
+                        Dr = r == q ? D[q] : Dr;
+                        ir = r == q ? inr[q] : ir;
+                    }
+                    MarchResult m = march_axis<false>(Dr, ir, oz, sz, steps, a.tab);
+#pragma unroll
+                    for (int q = 0; q < NR; ++q)
+                        if (q == r && m.hit && m.t < zb[q]) zb[q] = m.t;
+                }
+#pragma unroll
+                for (int r = 0; r < NR; ++r) cnt[r] = steps;
+            }
+            if (steps > 0) {
+                // t of the first hit step (branch-free: clamped table index + select)
 #pragma unroll
                 for (int r = 0; r < NR; ++r) {
-                    MarchResult m = march_axis<false>(D[r], inr[r], oz, sz, steps, a.tab);
-                    if (m.hit && m.t < zb[r]) zb[r] = m.t;
-                    cnt[r] = steps;
-                }
-            }
-#pragma unroll
-            for (int r = 0; r < NR; ++r) {
-                if (cnt[r] < steps) {
-                    const double t = t_after(a.tab, cnt[r]);
-                    if (t < zb[r]) zb[r] = t;
+                    const bool hit = cnt[r] < steps;
+                    const double t = a.tab.t[hit ? cnt[r] : 0];
+                    zb[r] = (hit && t < zb[r]) ? t : zb[r];
                 }
             }
         }
@@ -465,7 +523,7 @@ __device__ __forceinline__ void shadow_tile_sep(const ShadowPart& a, double* __r
     if (colv) {
 #pragma unroll
         for (int r = 0; r < NR; ++r)
-            if (rowv[r]) smap[(int64_t)(y0 + r) * a.W + xi] = zb[r];
+            if (rowv[r]) store_d(&smap[(int64_t)(y0 + r) * a.W + xi], zb[r], nt);
     }
 }
 
@@ -474,7 +532,8 @@ __device__ __forceinline__ void shadow_tile_sep(const ShadowPart& a, double* __r
 // texel on demand from `sh` (same frame) instead of reading `smap`.
 template <bool FUSED, bool COUNT>
 __device__ __forceinline__ void eye_tile(const EyePart& a, const ShadowPart& sh, const double* __restrict__ smap,
-                                         float4* __restrict__ out, int bx, int by, StatsK* __restrict__ st) {
+                                         float4* __restrict__ out, int bx, int by, StatsK* __restrict__ st,
+                                         bool nt = false, int diag_eye = 0) {
     const int xb = bx * TILE_X;
     const int xi = xb + (threadIdx.x & (TILE_X - 1));
     const int yl = __builtin_amdgcn_readfirstlane(by * TILE_Y + (threadIdx.x >> 6));
@@ -483,7 +542,9 @@ __device__ __forceinline__ void eye_tile(const EyePart& a, const ShadowPart& sh,
     unsigned long long n_tests = 0, n_hit = 0, n_lit = 0;
     ShadowCounts sc;
     int hit_id = -1;
-    if (live) {
+    if (live && (diag_eye & 1)) {  // timing diagnostic: store-only (wrong output)
+        store_px(&out[(int64_t)yl * a.W + xi], make_float4(0.0f, 0.2f, 0.2f, 1.0f), nt);
+    } else if (live) {
         const double x = a.nx[xi];
         const double y = a.ny[yi];
         // z-test over spheres in scene order, strict '<' against +INF init (main.rs:318)
@@ -554,7 +615,7 @@ __device__ __forceinline__ void eye_tile(const EyePart& a, const ShadowPart& sh,
                 hit_id = bid;
             }
         }
-        out[(int64_t)yl * a.W + xi] = c;
+        store_px(&out[(int64_t)yl * a.W + xi], c, nt);
     }
     if (COUNT) {
         stat_add(&st->eye_sphere_tests, n_tests);
@@ -577,14 +638,16 @@ __global__ __launch_bounds__(BLOCK) void shadow_pass_kernel(const FrameArgs a, d
 }
 
 template <int NR>
-__global__ __launch_bounds__(BLOCK) void shadow_sep_kernel(const FrameArgs a, double* __restrict__ smap, int diag) {
-    shadow_tile_sep<NR>(a.sh, smap, blockIdx.x, blockIdx.y, diag);
+__global__ __launch_bounds__(BLOCK, SEP_MIN_WAVES) void shadow_sep_kernel(const FrameArgs a, double* __restrict__ smap, int diag,
+                                                           int nt) {
+    shadow_tile_sep<NR>(a.sh, smap, blockIdx.x, blockIdx.y, diag, nt != 0);
 }
 
 template <bool FUSED, bool COUNT>
 __global__ __launch_bounds__(BLOCK) void eye_pass_kernel(const FrameArgs a, const double* __restrict__ smap,
-                                                         float4* __restrict__ out, StatsK* __restrict__ st) {
-    eye_tile<FUSED, COUNT>(a.ey, a.sh, smap, out, blockIdx.x, blockIdx.y, st);
+                                                         float4* __restrict__ out, StatsK* __restrict__ st, int nt,
+                                                         int diag) {
+    eye_tile<FUSED, COUNT>(a.ey, a.sh, smap, out, blockIdx.x, blockIdx.y, st, nt != 0, diag);
 }
 
 // Software-pipelined frame step (launch_frame_pipe): a 1-D grid of
@@ -603,7 +666,7 @@ __global__ __launch_bounds__(BLOCK) void frame_pipe_kernel(const FrameArgs a, do
     if (s_after > s_before) {
         const int t = (int)s_before;
         if (SEP)
-            shadow_tile_sep<NR>(a.sh, smap_w, t % sh_gx, t / sh_gx, 0);
+            shadow_tile_sep<NR>(a.sh, smap_w, t % sh_gx, t / sh_gx, 0, false);
         else
             shadow_tile_generic<false>(a.sh, smap_w, t % sh_gx, t / sh_gx, nullptr);
     } else {
@@ -742,10 +805,18 @@ inline int launched() { return hipGetLastError() == hipSuccess ? 0 : RTM_ERR_HIP
 // Rows per wave of the separable shadow kernel (0 = generic kernel).  Default
 // chosen by measurement (profiles/); RTM_SEP_ROWS overrides it for A/B runs.
 // Timing diagnostics only (RTM_DIAG_SHADOW: 1 = skip rasterize, 2 = skip march,
-// 3 = store only); results are wrong under it and no test sets it.
+// 3 = store only; RTM_DIAG_EYE=1: store-only eye pass); results are wrong under
+// them and no test sets them.
 static int diag_mode() {
     static int v = [] {
         const char* e = getenv("RTM_DIAG_SHADOW");
+        return e ? atoi(e) : 0;
+    }();
+    return v;
+}
+static int diag_eye() {
+    static int v = [] {
+        const char* e = getenv("RTM_DIAG_EYE");
         return e ? atoi(e) : 0;
     }();
     return v;
@@ -762,12 +833,21 @@ static int sep_rows() {
     return v;
 }
 
+// Non-temporal output stores (RTM_NT_STORE=1 for A/B; default measured in profiles/).
+static int nt_store() {
+    static int v = [] {
+        const char* e = getenv("RTM_NT_STORE");
+        return e ? atoi(e) : 0;
+    }();
+    return v;
+}
+
 static bool use_sep(const ShadowPart& s) { return sep_rows() > 0 && s.tab.d0 && s.tab.z && s.tab.t; }
 
 template <int NR>
 static void launch_sep(const FrameArgs& a, double* smap, hipStream_t s) {
     dim3 g((unsigned)((a.sh.W + TILE_X - 1) / TILE_X), (unsigned)((a.sh.H + TILE_Y * NR - 1) / (TILE_Y * NR)));
-    hipLaunchKernelGGL(shadow_sep_kernel<NR>, g, dim3(BLOCK), 0, s, a, smap, diag_mode());
+    hipLaunchKernelGGL(shadow_sep_kernel<NR>, g, dim3(BLOCK), 0, s, a, smap, diag_mode(), nt_store());
 }
 
 int launch_shadow_pass(const FrameArgs& a, double* smap, void* stream, StatsK* stats) {
@@ -791,14 +871,15 @@ int launch_eye_pass(const FrameArgs& a, const double* smap, float* out, void* st
     dim3 g = grid_for(a.ey.W, a.ey.row_end - a.ey.row_begin);
     float4* o = reinterpret_cast<float4*>(out);
     const bool fused = (a.ey.flags & RTM_FLAG_FUSED_SHADOW) != 0;
+    const int nt = nt_store();
     if (fused && stats)
-        hipLaunchKernelGGL((eye_pass_kernel<true, true>), g, dim3(BLOCK), 0, s, a, smap, o, stats);
+        hipLaunchKernelGGL((eye_pass_kernel<true, true>), g, dim3(BLOCK), 0, s, a, smap, o, stats, nt, diag_eye());
     else if (fused)
-        hipLaunchKernelGGL((eye_pass_kernel<true, false>), g, dim3(BLOCK), 0, s, a, smap, o, stats);
+        hipLaunchKernelGGL((eye_pass_kernel<true, false>), g, dim3(BLOCK), 0, s, a, smap, o, stats, nt, diag_eye());
     else if (stats)
-        hipLaunchKernelGGL((eye_pass_kernel<false, true>), g, dim3(BLOCK), 0, s, a, smap, o, stats);
+        hipLaunchKernelGGL((eye_pass_kernel<false, true>), g, dim3(BLOCK), 0, s, a, smap, o, stats, nt, diag_eye());
     else
-        hipLaunchKernelGGL((eye_pass_kernel<false, false>), g, dim3(BLOCK), 0, s, a, smap, o, stats);
+        hipLaunchKernelGGL((eye_pass_kernel<false, false>), g, dim3(BLOCK), 0, s, a, smap, o, stats, nt, diag_eye());
     return launched();
 }
 

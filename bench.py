@@ -37,8 +37,8 @@ def parse():
     ap.add_argument("--config", type=int, default=3)
     ap.add_argument("--mode", choices=["frames", "tile-gather"], default="frames")
     ap.add_argument("--fused", action="store_true", help="evaluate shadow texels on demand (same image)")
-    ap.add_argument("--no-pipeline", action="store_true",
-                    help="frames mode: one rtm_render_async per frame instead of the software-pipelined sequence")
+    ap.add_argument("--per-frame-calls", action="store_true",
+                    help="frames mode: one rtm_render_async call per frame instead of one rtm_render_frames_async")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=1)
     return ap.parse_args()
@@ -152,15 +152,16 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
 
-    pipelined = a.mode == "frames" and not a.no_pipeline and not fused
-    if pipelined:
-        # the whole timed region is ONE software-pipelined frame sequence:
-        # launch j = shadow pass of frame j + eye pass of frame j-1 (rtm_render_frames_async)
+    sequence = a.mode == "frames" and not a.per_frame_calls and not fused
+    pipelined = sequence and os.environ.get("RTM_PIPELINE", "0") not in ("", "0")
+    if sequence:
+        # the whole timed region is ONE rtm_render_frames_async call over the animation
+        # frames (two kernels per frame; with RTM_PIPELINE=1 the software-pipelined launch)
         warm = ctx.prepare_frames(scenes[:a.warmup])
         timed = ctx.prepare_frames(scenes[a.warmup:])
         outp = [out.data_ptr()] * max(a.warmup, a.steps)
 
-    if pipelined:
+    if sequence:
         if a.warmup:
             ctx.render_frames_async([0] * a.warmup, eye, shadow, W, H, K, flags, outp[:a.warmup], warm)
     else:
@@ -169,7 +170,7 @@ def main():
     barrier()
     ctx.set_timing_stride(timing_stride)  # restarts the stride count: launch 0 of the timed region is timed
     t0 = time.perf_counter()
-    if pipelined:
+    if sequence:
         ctx.render_frames_async([0] * a.steps, eye, shadow, W, H, K, flags, outp[:a.steps], timed)
     else:
         for i in range(a.warmup, total):

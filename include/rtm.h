@@ -161,11 +161,12 @@ int rtm_render_async(rtm_ctx* ctx, const rtm_scene* scene, const rtm_camera* eye
                      float* out_rgba_dev);
 /* A sequence of frames (e.g. the animation of testscene_closelyOrbitingSphere,
  * main.rs:1469), asynchronous on ctx's stream: frame i is scenes[i] rendered
- * into out_rgba_dev[i] (full frames; pointers may repeat).  When every frame
- * has the same patches the frames are software-pipelined: the shadow pass of
- * frame i and the eye pass of frame i-1 run in ONE launch (double-buffered
- * shadow maps), overlapping the VALU-bound march with the HBM-bound
- * framebuffer stores.  Each frame's output is bit-identical to rtm_render. */
+ * into out_rgba_dev[i] (full frames; pointers may repeat), two kernels per
+ * frame.  With RTM_PIPELINE=1 in the environment and equal patches in every
+ * frame the sequence is software-pipelined instead: the shadow pass of frame i
+ * and the eye pass of frame i-1 run in ONE launch (double-buffered shadow
+ * maps) — correct, but measured slower on MI355X.  Each frame's
+ * output is bit-identical to rtm_render. */
 int rtm_render_frames_async(rtm_ctx* ctx, int32_t n_frames, const rtm_scene* scenes,
                             const rtm_camera* eye, const rtm_camera* shadow, int32_t width,
                             int32_t height, int32_t march_steps, int32_t flags,

@@ -29,7 +29,12 @@ scenes = [sc.scene_a_bench(100 + i) if %(cfg)d in (2, 3, 4) else cfg["scene"]() 
 cs = [s.to_c() for s in scenes]
 e, s_ = sc.eye_camera().to_c(), sc.shadow_camera().to_c()
 out = torch.empty((H, W, 4), dtype=torch.float32, device="cuda")
+prep = ctx.prepare_frames(scenes)
 def run(n):
+    if %(pipe)d:
+        ctx.render_frames_async(None, sc.eye_camera(), sc.shadow_camera(), W, H, K, flags, [out.data_ptr()] * n,
+                                (prep[0], prep[1]) if n == len(scenes) else ctx.prepare_frames(scenes[:n]))
+        return
     for i in range(n):
         rc = lib.rtm_render_async(ctx.handle, C.byref(cs[i][0]), C.byref(e), C.byref(s_), W, H, K, flags, 0, H,
                                   C.c_void_p(out.data_ptr()))
@@ -38,7 +43,7 @@ run(10); torch.cuda.synchronize()
 t0 = time.perf_counter(); run(%(n)d); torch.cuda.synchronize(); dt = time.perf_counter() - t0
 res = {"ms_per_frame": dt / %(n)d * 1e3}
 if %(events)d:
-    sh, ey = ctx.kernel_ms_history(%(n)d)
+    sh, ey = ctx.kernel_ms_history(%(n)d + 1)
     res["shadow_ms"] = sum(sh) / len(sh); res["eye_ms"] = sum(ey) / len(ey)
 print(json.dumps(res))
 '''
@@ -54,7 +59,7 @@ def main():
             env = dict(os.environ)
             env.update(v.get("env", {}))
             code = CHILD % dict(root=ROOT, cfg=cfg, flags=v.get("flags", 0), events=v.get("events", 200), n=200,
-                               steps=v.get("steps", -1))
+                               steps=v.get("steps", -1), pipe=1 if v.get("pipe") else 0)
             p = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
             if p.returncode != 0:
                 print(name, "FAILED", p.stderr[-2000:])
