@@ -28,28 +28,10 @@ namespace {
 constexpr int TILE_X = 64;  // one wave per tile row
 constexpr int TILE_Y = 4;   // four waves per workgroup
 constexpr int BLOCK = TILE_X * TILE_Y;
-#ifndef SEP_MIN_WAVES
-#define SEP_MIN_WAVES 1
-#endif
 
 using cdouble = const __attribute__((address_space(4))) double;  // scalar-loaded table
 using cint = const __attribute__((address_space(4))) int32_t;
 
-// Output stores: plain, or non-temporal (streamed past the caches) when `nt`.
-__device__ __forceinline__ void store_px(float4* p, float4 v, bool nt) {
-    if (nt) {
-        __builtin_nontemporal_store(v.x, &p->x);
-        __builtin_nontemporal_store(v.y, &p->y);
-        __builtin_nontemporal_store(v.z, &p->z);
-        __builtin_nontemporal_store(v.w, &p->w);
-    } else {
-        *p = v;
-    }
-}
-__device__ __forceinline__ void store_d(double* p, double v, bool nt) {
-    if (nt) __builtin_nontemporal_store(v, p);
-    else *p = v;
-}
 
 // main.rs:306-307 / 1903-1907: ((i as f64) / (res as f64)) * 2.0 - 1.0
 __device__ __forceinline__ double ndc(int i, int res) { return ((double)i / (double)res) * 2.0 - 1.0; }
@@ -357,7 +339,7 @@ __device__ __forceinline__ void shadow_tile_generic(const ShadowPart& a, double*
 
 // One 8-step chunk of the shared-z march for NR rows: lt[r] += #(z_k < D[r]);
 // returns true when no lane is still marching in any row (wave early-out).
-template <int NR>
+template <int NR, bool CMP>
 __device__ __forceinline__ bool chunk8(const double (&z)[8], const double (&D)[NR], int (&lt)[NR],
                                        const unsigned (&inrb)[NR], const unsigned (&eposb)[NR]) {
     unsigned cont = 0u;  // lane still marching in some row: inr & (last ^ epos)
@@ -366,7 +348,8 @@ __device__ __forceinline__ bool chunk8(const double (&z)[8], const double (&D)[N
         unsigned last = 0u;
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
-            last = (unsigned)__double2hiint(z[u] - D[r]) >> 31;
+            // [z_k < D]: a compare, or the sign bit of fl(z_k - D) (equal for finite nonzero D)
+            last = CMP ? (z[u] < D[r] ? 1u : 0u) : (unsigned)__double2hiint(z[u] - D[r]) >> 31;
             lt[r] += (int)last;
         }
         cont |= inrb[r] & (last ^ eposb[r]);
@@ -381,9 +364,9 @@ __device__ __forceinline__ bool chunk8(const double (&z)[8], const double (&D)[N
 // step is the sign bit of fl(z_k - D) (D finite and nonzero on this path, so
 // that bit is exactly [z_k < D], see march_axis).  If any lane's D is not
 // finite/nonzero the wave takes the exact per-texel loop instead.
-template <int NR>
+template <int NR, bool CMP = false>
 __device__ __forceinline__ void shadow_tile_sep(const ShadowPart& a, double* __restrict__ smap, int bx, int by,
-                                                int diag, bool nt) {
+                                                int diag) {
     const int lane = threadIdx.x & (TILE_X - 1);
     const int xb = bx * TILE_X;
     const int xi = xb + lane;
@@ -459,7 +442,7 @@ __device__ __forceinline__ void shadow_tile_sep(const ShadowPart& a, double* __r
                     while (kk + 8 <= steps) {
 #pragma unroll
                         for (int u = 0; u < 8; ++u) zB[u] = zt[kk + 8 + u];
-                        if (chunk8<NR>(zA, D, lt, inrb, eposb)) {
+                        if (chunk8<NR, CMP>(zA, D, lt, inrb, eposb)) {
                             kk += 8;
                             stopped = true;
                             break;
@@ -472,7 +455,7 @@ __device__ __forceinline__ void shadow_tile_sep(const ShadowPart& a, double* __r
                         }
 #pragma unroll
                         for (int u = 0; u < 8; ++u) zA[u] = zt[kk + 8 + u];
-                        if (chunk8<NR>(zB, D, lt, inrb, eposb)) {
+                        if (chunk8<NR, CMP>(zB, D, lt, inrb, eposb)) {
                             kk += 8;
                             stopped = true;
                             break;
@@ -483,7 +466,7 @@ __device__ __forceinline__ void shadow_tile_sep(const ShadowPart& a, double* __r
                         for (; kk < steps; ++kk) {
                             const double z = zt[kk];
 #pragma unroll
-                            for (int r = 0; r < NR; ++r) lt[r] += (int)((unsigned)__double2hiint(z - D[r]) >> 31);
+                            for (int r = 0; r < NR; ++r) lt[r] += (z < D[r]) ? 1 : 0;
                         }
                     }
                 }
@@ -523,7 +506,7 @@ __device__ __forceinline__ void shadow_tile_sep(const ShadowPart& a, double* __r
     if (colv) {
 #pragma unroll
         for (int r = 0; r < NR; ++r)
-            if (rowv[r]) store_d(&smap[(int64_t)(y0 + r) * a.W + xi], zb[r], nt);
+            if (rowv[r]) smap[(int64_t)(y0 + r) * a.W + xi] = zb[r];
     }
 }
 
@@ -532,8 +515,7 @@ __device__ __forceinline__ void shadow_tile_sep(const ShadowPart& a, double* __r
 // texel on demand from `sh` (same frame) instead of reading `smap`.
 template <bool FUSED, bool COUNT>
 __device__ __forceinline__ void eye_tile(const EyePart& a, const ShadowPart& sh, const double* __restrict__ smap,
-                                         float4* __restrict__ out, int bx, int by, StatsK* __restrict__ st,
-                                         bool nt = false, int diag_eye = 0) {
+                                         float4* __restrict__ out, int bx, int by, StatsK* __restrict__ st) {
     const int xb = bx * TILE_X;
     const int xi = xb + (threadIdx.x & (TILE_X - 1));
     const int yl = __builtin_amdgcn_readfirstlane(by * TILE_Y + (threadIdx.x >> 6));
@@ -542,9 +524,7 @@ __device__ __forceinline__ void eye_tile(const EyePart& a, const ShadowPart& sh,
     unsigned long long n_tests = 0, n_hit = 0, n_lit = 0;
     ShadowCounts sc;
     int hit_id = -1;
-    if (live && (diag_eye & 1)) {  // timing diagnostic: store-only (wrong output)
-        store_px(&out[(int64_t)yl * a.W + xi], make_float4(0.0f, 0.2f, 0.2f, 1.0f), nt);
-    } else if (live) {
+    if (live) {
         const double x = a.nx[xi];
         const double y = a.ny[yi];
         // z-test over spheres in scene order, strict '<' against +INF init (main.rs:318)
@@ -615,7 +595,7 @@ __device__ __forceinline__ void eye_tile(const EyePart& a, const ShadowPart& sh,
                 hit_id = bid;
             }
         }
-        store_px(&out[(int64_t)yl * a.W + xi], c, nt);
+        out[(int64_t)yl * a.W + xi] = c;
     }
     if (COUNT) {
         stat_add(&st->eye_sphere_tests, n_tests);
@@ -637,17 +617,23 @@ __global__ __launch_bounds__(BLOCK) void shadow_pass_kernel(const FrameArgs a, d
     shadow_tile_generic<COUNT>(a.sh, smap, blockIdx.x, blockIdx.y, st);
 }
 
-template <int NR>
-__global__ __launch_bounds__(BLOCK, SEP_MIN_WAVES) void shadow_sep_kernel(const FrameArgs a, double* __restrict__ smap, int diag,
-                                                           int nt) {
-    shadow_tile_sep<NR>(a.sh, smap, blockIdx.x, blockIdx.y, diag, nt != 0);
+template <int NR, bool CMP>
+__global__ __launch_bounds__(BLOCK) void shadow_sep_kernel(const FrameArgs a, double* __restrict__ smap, int diag) {
+    shadow_tile_sep<NR, CMP>(a.sh, smap, blockIdx.x, blockIdx.y, diag);
 }
 
 template <bool FUSED, bool COUNT>
 __global__ __launch_bounds__(BLOCK) void eye_pass_kernel(const FrameArgs a, const double* __restrict__ smap,
-                                                         float4* __restrict__ out, StatsK* __restrict__ st, int nt,
-                                                         int diag) {
-    eye_tile<FUSED, COUNT>(a.ey, a.sh, smap, out, blockIdx.x, blockIdx.y, st, nt != 0, diag);
+                                                         float4* __restrict__ out, StatsK* __restrict__ st) {
+    eye_tile<FUSED, COUNT>(a.ey, a.sh, smap, out, blockIdx.x, blockIdx.y, st);
+}
+
+// Timing diagnostic only (RTM_DIAG_EYE=1): the eye pass's stores without its work.
+__global__ __launch_bounds__(BLOCK) void eye_store_only_kernel(const FrameArgs a, float4* __restrict__ out) {
+    const int xi = blockIdx.x * TILE_X + (threadIdx.x & (TILE_X - 1));
+    const int yl = blockIdx.y * TILE_Y + (threadIdx.x >> 6);
+    if (xi < a.ey.W && a.ey.row_begin + yl < a.ey.row_end)
+        out[(int64_t)yl * a.ey.W + xi] = make_float4(0.0f, 0.2f, 0.2f, 1.0f);
 }
 
 // Software-pipelined frame step (launch_frame_pipe): a 1-D grid of
@@ -666,7 +652,7 @@ __global__ __launch_bounds__(BLOCK) void frame_pipe_kernel(const FrameArgs a, do
     if (s_after > s_before) {
         const int t = (int)s_before;
         if (SEP)
-            shadow_tile_sep<NR>(a.sh, smap_w, t % sh_gx, t / sh_gx, 0, false);
+            shadow_tile_sep<NR>(a.sh, smap_w, t % sh_gx, t / sh_gx, 0);
         else
             shadow_tile_generic<false>(a.sh, smap_w, t % sh_gx, t / sh_gx, nullptr);
     } else {
@@ -833,21 +819,26 @@ static int sep_rows() {
     return v;
 }
 
-// Non-temporal output stores (RTM_NT_STORE=1 for A/B; default measured in profiles/).
-static int nt_store() {
+static bool use_sep(const ShadowPart& s) { return sep_rows() > 0 && s.tab.d0 && s.tab.z && s.tab.t; }
+
+// Per-step test of the shared-z march: a compare (default; 47.1 vs 52.9 us for
+// the sign bit of fl(z - D) at config 3, profiles/r01_ab_cmp.txt) or the sign
+// bit (RTM_SEP_CMP=0) — identical results.
+static int sep_cmp() {
     static int v = [] {
-        const char* e = getenv("RTM_NT_STORE");
-        return e ? atoi(e) : 0;
+        const char* e = getenv("RTM_SEP_CMP");
+        return e ? atoi(e) : 1;
     }();
     return v;
 }
 
-static bool use_sep(const ShadowPart& s) { return sep_rows() > 0 && s.tab.d0 && s.tab.z && s.tab.t; }
-
 template <int NR>
 static void launch_sep(const FrameArgs& a, double* smap, hipStream_t s) {
     dim3 g((unsigned)((a.sh.W + TILE_X - 1) / TILE_X), (unsigned)((a.sh.H + TILE_Y * NR - 1) / (TILE_Y * NR)));
-    hipLaunchKernelGGL(shadow_sep_kernel<NR>, g, dim3(BLOCK), 0, s, a, smap, diag_mode(), nt_store());
+    if (sep_cmp())
+        hipLaunchKernelGGL((shadow_sep_kernel<NR, true>), g, dim3(BLOCK), 0, s, a, smap, diag_mode());
+    else
+        hipLaunchKernelGGL((shadow_sep_kernel<NR, false>), g, dim3(BLOCK), 0, s, a, smap, diag_mode());
 }
 
 int launch_shadow_pass(const FrameArgs& a, double* smap, void* stream, StatsK* stats) {
@@ -871,15 +862,18 @@ int launch_eye_pass(const FrameArgs& a, const double* smap, float* out, void* st
     dim3 g = grid_for(a.ey.W, a.ey.row_end - a.ey.row_begin);
     float4* o = reinterpret_cast<float4*>(out);
     const bool fused = (a.ey.flags & RTM_FLAG_FUSED_SHADOW) != 0;
-    const int nt = nt_store();
+    if (diag_eye()) {
+        hipLaunchKernelGGL(eye_store_only_kernel, g, dim3(BLOCK), 0, s, a, o);
+        return launched();
+    }
     if (fused && stats)
-        hipLaunchKernelGGL((eye_pass_kernel<true, true>), g, dim3(BLOCK), 0, s, a, smap, o, stats, nt, diag_eye());
+        hipLaunchKernelGGL((eye_pass_kernel<true, true>), g, dim3(BLOCK), 0, s, a, smap, o, stats);
     else if (fused)
-        hipLaunchKernelGGL((eye_pass_kernel<true, false>), g, dim3(BLOCK), 0, s, a, smap, o, stats, nt, diag_eye());
+        hipLaunchKernelGGL((eye_pass_kernel<true, false>), g, dim3(BLOCK), 0, s, a, smap, o, stats);
     else if (stats)
-        hipLaunchKernelGGL((eye_pass_kernel<false, true>), g, dim3(BLOCK), 0, s, a, smap, o, stats, nt, diag_eye());
+        hipLaunchKernelGGL((eye_pass_kernel<false, true>), g, dim3(BLOCK), 0, s, a, smap, o, stats);
     else
-        hipLaunchKernelGGL((eye_pass_kernel<false, false>), g, dim3(BLOCK), 0, s, a, smap, o, stats, nt, diag_eye());
+        hipLaunchKernelGGL((eye_pass_kernel<false, false>), g, dim3(BLOCK), 0, s, a, smap, o, stats);
     return launched();
 }
 
