@@ -814,7 +814,7 @@ static int sep_rows() {
     static int v = [] {
         const char* e = getenv("RTM_SEP_ROWS");
         int r = e ? atoi(e) : 4;
-        return (r == 0 || r == 1 || r == 2 || r == 4) ? r : 4;
+        return (r == 0 || r == 1 || r == 2 || r == 4 || r == 8) ? r : 4;
     }();
     return v;
 }
@@ -847,6 +847,7 @@ int launch_shadow_pass(const FrameArgs& a, double* smap, void* stream, StatsK* s
         const int nr = sep_rows();
         if (nr == 1) launch_sep<1>(a, smap, s);
         else if (nr == 2) launch_sep<2>(a, smap, s);
+        else if (nr == 8) launch_sep<8>(a, smap, s);
         else launch_sep<4>(a, smap, s);
         return launched();
     }
@@ -895,6 +896,7 @@ int launch_frame_pipe(const FrameArgs& a, double* smap_w, const double* smap_r, 
         const int nr = sep_rows();
         if (nr == 1) launch_pipe<true, 1>(a, smap_w, smap_r, o, s);
         else if (nr == 2) launch_pipe<true, 2>(a, smap_w, smap_r, o, s);
+        else if (nr == 8) launch_pipe<true, 8>(a, smap_w, smap_r, o, s);
         else launch_pipe<true, 4>(a, smap_w, smap_r, o, s);
     } else {
         launch_pipe<false, 1>(a, smap_w, smap_r, o, s);

@@ -9,6 +9,11 @@ off for bit parity).  Per-unit figures:
                  32 per patch (ray origin, domain map, surface depth, entry sign,
                     in-range test, step vector, strict-min update)
                  3 per march iteration    (z - D, class test, z += step.z)
+    separable axis-aligned shadow camera with a shared z sequence (every
+    BASELINE scene): the per-wave cull is scalar, D = d0[x] + dd[x]*py[y],
+    z_k is one host table for all texels, so per texel:
+                 19 per covering sphere, 4 per patch (D: mul+add, entry compare,
+                 min), 1 per march iteration (the compare z_k < D)
   eye pixel      4 per sphere (cull)      + 21 per covering sphere (incl. z-test)
                  84 per hit pixel         (ray, world pos, normal, Lambert,
                                            reflect, powi(32), shadow projection)
@@ -33,22 +38,36 @@ SHADOW_PER_SPHERE = 4
 SHADOW_PER_COVER = 19
 SHADOW_PER_PATCH = 32
 SHADOW_PER_ITER = 3
+SEP_PER_PATCH = 4
+SEP_PER_ITER = 1
 EYE_PER_SPHERE = 4
 EYE_PER_COVER = 21
 EYE_PER_HIT = 84
 
 
+def shared_z_separable(shadow_cam) -> bool:
+    """The host-side rule (rtm_api.cpp shared_z0 + separable) for the shadow camera."""
+    import math
+    d, u, s, p = shadow_cam.dirNormalized, shadow_cam.upNormalized, shadow_cam.sideNormalized, shadow_cam.position
+    return (shadow_cam.type_ == 0 and d[0] * 0.03 == 0.0 and d[1] * 0.03 == 0.0 and s[2] == 0.0 and u[2] == 0.0
+            and not (p[2] == 0.0 and math.copysign(1.0, p[2]) < 0) and u[0] == 0.0 and s[1] == 0.0
+            and not (p[1] == 0.0 and math.copysign(1.0, p[1]) < 0))
+
+
 def frame_work(stats: dict, width: int, height: int, n_spheres: int, n_patches: int, flags: int = 0,
-               fused: bool = False) -> dict:
+               fused: bool = False, sep: bool = False) -> dict:
     px = width * height
     no_march = bool(flags & 0x1)
     no_sraster = bool(flags & 0x2)
     texels = px if not fused else stats["eye_hit_pixels"]
     sh_ops = 0
     if not no_sraster:
-        sh_ops += texels * SHADOW_PER_SPHERE * n_spheres + SHADOW_PER_COVER * stats["shadow_sphere_tests"]
+        sh_ops += (0 if sep else texels * SHADOW_PER_SPHERE * n_spheres) + SHADOW_PER_COVER * stats["shadow_sphere_tests"]
     if not no_march:
-        sh_ops += texels * n_patches * SHADOW_PER_PATCH + SHADOW_PER_ITER * stats["march_iterations"]
+        if sep and not fused:
+            sh_ops += texels * n_patches * SEP_PER_PATCH + SEP_PER_ITER * stats["march_iterations"]
+        else:
+            sh_ops += texels * n_patches * SHADOW_PER_PATCH + SHADOW_PER_ITER * stats["march_iterations"]
     eye_ops = (px * EYE_PER_SPHERE * n_spheres + EYE_PER_COVER * stats["eye_sphere_tests"]
                + EYE_PER_HIT * stats["eye_hit_pixels"])
     sh_bytes = 0 if fused else 8 * px

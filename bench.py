@@ -207,7 +207,8 @@ def main():
         s0 = scenes[a.warmup]
         band_h = rows[1] - rows[0]
         st = ctx.stats(s0, eye, shadow, W, H, K, flags)
-        work = metrics.frame_work(st, W, H, len(s0.spherePrimitives), len(s0.patches), flags, fused=fused)
+        work = metrics.frame_work(st, W, H, len(s0.spherePrimitives), len(s0.patches), flags, fused=fused,
+                                  sep=metrics.shared_z_separable(shadow))
         if band_h != H:  # rank 0 renders one band: scale the frame's work to it (approximate)
             for kk in work.values():
                 kk["ops"] = int(kk["ops"] * band_h / H)
