@@ -11,4 +11,5 @@ from . import abi, scenes  # noqa: F401
 from .abi import RtmError, load_library  # noqa: F401
 from .scenes import (Bilinear, Camera, EnumFace, Linear, PrimitiveSphere, Scene, Shading,  # noqa: F401
                      eye_camera, shadow_camera)
-from .renderer import Context, Viewport, device_count, renderColorImage, render_frame  # noqa: F401
+from .renderer import (Context, Viewport, device_count, encode_thresholds, renderColorImage,  # noqa: F401
+                       render_frame, writeColorImage)

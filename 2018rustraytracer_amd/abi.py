@@ -96,6 +96,10 @@ ABI_SYMBOLS = [
     ("rtm_render_stats", C.c_int, [_P, C.POINTER(rtm_scene), C.POINTER(rtm_camera),
                                    C.POINTER(rtm_camera), _I32, _I32, _I32, _I32,
                                    C.POINTER(rtm_stats)]),
+    ("rtm_encode_rgb8_async", C.c_int, [_P, _P, C.c_int64, _P]),
+    ("rtm_ppm_max_bytes", C.c_int64, [_I32, _I32]),
+    ("rtm_write_ppm", C.c_int, [_P, _P, _I32, _I32, C.c_char_p, C.c_int64, C.POINTER(C.c_int64)]),
+    ("rtm_encode_thresholds", C.c_int, [C.POINTER(C.c_float)]),
     ("rtm_viewport_create", C.c_int, [_P, _I32, _I32, _I32, C.POINTER(rtm_camera), C.POINTER(_P)]),
     ("rtm_viewport_destroy", None, [_P]),
     ("rtm_viewport_rasterize", C.c_int, [_P, C.POINTER(rtm_scene)]),

@@ -6,6 +6,7 @@
 // context, and return status codes instead of panicking (main.rs:700, 1949).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -15,6 +16,7 @@
 #include <string>
 #include <vector>
 
+#include "rtm_encode.h"
 #include "rtm_kernels.h"
 
 #pragma clang fp contract(off)
@@ -238,6 +240,55 @@ int build_frame(FrameArgs& a, const rtm_scene* scene, const rtm_camera* eye, con
     return RTM_OK;
 }
 
+// writeColorImage's per-channel byte (main.rs:674-684), f32 arithmetic with the
+// platform powf — the same libm call the Rust binary makes.
+inline int64_t enc_byte(float v) {
+    const float gamma = 2.2f;
+    const float p = powf(v, 1.0f / gamma);
+    return (int64_t)(p * 255.0f);
+}
+
+inline float f32_from_bits(uint32_t b) {
+    float f;
+    std::memcpy(&f, &b, sizeof f);
+    return f;
+}
+
+// T[k] = smallest f32 in [0,1] with enc_byte >= k, by binary search over the
+// ordered bit patterns of [+0, 1.0]; bucket[i] = number of thresholds <= the
+// first value of bucket i (its byte), see rtm_encode.h.
+const EncodeTable& encode_table() {
+    static const EncodeTable tab = [] {
+        EncodeTable t{};
+        uint32_t tb[256];
+        t.t[0] = 0.0f;
+        tb[0] = 0u;
+        for (int k = 1; k < 256; ++k) {
+            uint32_t lo = 0u, hi = 0x3F800000u + 1u;  // [lo, hi)
+            while (lo < hi) {
+                const uint32_t mid = lo + (hi - lo) / 2u;
+                if (enc_byte(f32_from_bits(mid)) >= k) hi = mid;
+                else lo = mid + 1u;
+            }
+            tb[k] = lo;
+            t.t[k] = lo <= 0x3F800000u ? f32_from_bits(lo) : INFINITY;
+        }
+        int k = 0;
+        t.max_crossings = 0;
+        for (int i = 0; i < ENC_BUCKETS; ++i) {
+            const uint32_t first = (uint32_t)i << ENC_BUCKET_SHIFT;
+            const uint32_t last = std::min(first + ((1u << ENC_BUCKET_SHIFT) - 1u), 0x3F800000u);
+            while (k < 255 && tb[k + 1] <= first) ++k;
+            t.bucket[i] = (uint8_t)k;
+            int c = 0;
+            while (k + c < 255 && tb[k + c + 1] <= last) ++c;
+            t.max_crossings = std::max(t.max_crossings, c);
+        }
+        return t;
+    }();
+    return tab;
+}
+
 }  // namespace
 
 struct TimingSlot {
@@ -260,6 +311,9 @@ struct rtm_ctx {
     DevBuf stats;
     int32_t smap_w = 0, smap_h = 0;
     DevBuf tabs;  // [t (steps) | nx (W) | ny (H)] f64, see Tables
+    DevBuf enc_rgb, enc_rows, enc_text;  // writeColorImage scratch
+    DevBuf enc_tab;                      // EncodeTable on the device (t | bucket)
+    bool enc_tab_ready = false;
     uint64_t tab_key = 0;
     int64_t tab_nt = 0, tab_nz = 0, tab_nd = 0;
     int32_t tab_w = 0, tab_h = 0, tab_np = 0;
@@ -756,6 +810,87 @@ int rtm_render_stats(rtm_ctx* ctx, const rtm_scene* scene, const rtm_camera* eye
     HIP_TRY(hipMemsetAsync(ctx->stats.p, 0, sizeof(StatsK), ctx->stream));
     if ((rc = enqueue_frame(ctx, a, (float*)ctx->out.p, (StatsK*)ctx->stats.p))) return rc;
     HIP_TRY(hipMemcpyAsync(out, ctx->stats.p, sizeof(StatsK), hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    return RTM_OK;
+}
+
+// ---- writeColorImage (row f-2) ----
+
+int rtm_encode_thresholds(float out[256]) {
+    if (!out) return fail(RTM_ERR_INVALID, "out is NULL");
+    std::memcpy(out, encode_table().t, sizeof(float) * 256);
+    return RTM_OK;
+}
+
+namespace {
+// The encode tables on ctx's device (uploaded once per context, stream-ordered).
+int enc_tab_dev(rtm_ctx* ctx, const void** out) {
+    if (!ctx->enc_tab_ready) {
+        const EncodeTable& t = encode_table();
+        if (t.max_crossings > 1) return fail(RTM_ERR_UNSUPPORTED, "platform powf: bucket spans %d thresholds",
+                                             t.max_crossings);
+        int rc = ctx->enc_tab.ensure(ENC_DEV_BYTES, ctx->device);
+        if (rc) return rc;
+        HIP_TRY(hipMemcpyAsync(ctx->enc_tab.p, t.t, 1024, hipMemcpyHostToDevice, ctx->stream));
+        HIP_TRY(hipMemcpyAsync((char*)ctx->enc_tab.p + 1024, t.bucket, ENC_BUCKETS, hipMemcpyHostToDevice,
+                               ctx->stream));
+        ctx->enc_tab_ready = true;
+    }
+    *out = ctx->enc_tab.p;
+    return RTM_OK;
+}
+}  // namespace
+
+int rtm_encode_rgb8_async(rtm_ctx* ctx, const float* rgba_dev, int64_t n_pixels, uint8_t* rgb_dev) {
+    if (!ctx || !rgba_dev || !rgb_dev || n_pixels < 0) return fail(RTM_ERR_INVALID, "bad arguments");
+    if ((uintptr_t)rgba_dev & 15) return fail(RTM_ERR_INVALID, "rgba_dev must be 16-byte aligned");
+    DeviceGuard g(ctx->device);
+    const void* tab = nullptr;
+    int rc = enc_tab_dev(ctx, &tab);
+    if (rc) return rc;
+    rc = launch_encode_rgb8(rgba_dev, n_pixels, rgb_dev, tab, ctx->stream);
+    return rc ? fail(rc, "encode launch failed") : RTM_OK;
+}
+
+int64_t rtm_ppm_max_bytes(int32_t width, int32_t height) {
+    if (width <= 0 || height <= 0) return 0;
+    // header "P3\n" + "W H\n" + "255\n"; per pixel at most "255 255 255  " (13); '\n' per row
+    return 3 + 24 + 4 + (int64_t)width * height * 13 + height;
+}
+
+int rtm_write_ppm(rtm_ctx* ctx, const float* rgba_dev, int32_t width, int32_t height, char* out, int64_t capacity,
+                  int64_t* length) {
+    if (!ctx || !rgba_dev || !length) return fail(RTM_ERR_INVALID, "bad arguments");
+    if ((uintptr_t)rgba_dev & 15) return fail(RTM_ERR_INVALID, "rgba_dev must be 16-byte aligned");
+    int rc;
+    if ((rc = validate_dims(width, height))) return rc;
+    char header[64];
+    const int hl = snprintf(header, sizeof header, "P3\n%d %d\n255\n", width, height);  // main.rs:666-668
+    const int64_t n = (int64_t)width * height;
+    DeviceGuard g(ctx->device);
+    if ((rc = ctx->enc_rgb.ensure((size_t)n * 3, ctx->device)) ||
+        (rc = ctx->enc_rows.ensure(sizeof(int64_t) * (2 * (size_t)height + 1), ctx->device)) ||
+        (rc = ctx->enc_text.ensure((size_t)rtm_ppm_max_bytes(width, height), ctx->device)))
+        return rc;
+    uint8_t* rgb = (uint8_t*)ctx->enc_rgb.p;
+    int64_t* rowlen = (int64_t*)ctx->enc_rows.p;
+    int64_t* rowoff = rowlen + height;
+    int64_t* total = rowoff + height;
+    char* text = (char*)ctx->enc_text.p;
+    const void* tab = nullptr;
+    if ((rc = enc_tab_dev(ctx, &tab))) return rc;
+    if ((rc = launch_encode_rgb8(rgba_dev, n, rgb, tab, ctx->stream)))
+        return fail(rc, "encode launch failed");
+    if ((rc = launch_ppm_text(rgb, width, height, hl, rowlen, rowoff, total, text, ctx->stream)))
+        return fail(rc, "ppm launch failed");
+    int64_t tot = 0;
+    HIP_TRY(hipMemcpyAsync(&tot, total, sizeof tot, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    *length = tot;
+    if (!out || tot > capacity) return fail(RTM_ERR_INVALID, "ppm needs %lld bytes, capacity %lld", (long long)tot,
+                                            (long long)capacity);
+    std::memcpy(out, header, (size_t)hl);
+    HIP_TRY(hipMemcpyAsync(out + hl, text + hl, (size_t)(tot - hl), hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(hipStreamSynchronize(ctx->stream));
     return RTM_OK;
 }

@@ -5,6 +5,7 @@ Reference surface (src/main.rs) -> this module:
     Viewport::rasterize(&Scene)                   main.rs:445      -> Viewport.rasterize
     Viewport::processRaymarchingRays()            main.rs:551      -> Viewport.processRaymarchingRays
     renderColorImage(&Scene,&Viewport,&Viewport)  main.rs:710      -> renderColorImage
+    writeColorImage(&Map2d<Color32>, &path)       main.rs:660      -> writeColorImage / Context.write_ppm
     the whole two-viewport frame of a scene script (main.rs:1533-1628) -> render_frame / Context.render_async
 
 Errors surface as abi.RtmError (the reference panics).  There is no CPU
@@ -119,6 +120,23 @@ class Context:
                                             steps, flags, C.byref(st)), "rtm_render_stats")
         return st.as_dict()
 
+    def encode_rgb8_async(self, rgba_dev: int, n_pixels: int, rgb_dev: int):
+        """writeColorImage's per-pixel encode (main.rs:674-684) of a device RGBA f32
+        buffer into device RGB8 (3 bytes per pixel), on this context's stream."""
+        lib = _lib()
+        abi.check(lib, lib.rtm_encode_rgb8_async(self._h, C.c_void_p(rgba_dev), n_pixels, C.c_void_p(rgb_dev)),
+                  "rtm_encode_rgb8_async")
+
+    def write_ppm(self, rgba_dev: int, width: int, height: int) -> bytes:
+        """writeColorImage's P3 text (main.rs:660-688) of a device RGBA f32 image."""
+        lib = _lib()
+        cap = int(lib.rtm_ppm_max_bytes(width, height))
+        buf = C.create_string_buffer(max(cap, 1))
+        n = C.c_int64()
+        abi.check(lib, lib.rtm_write_ppm(self._h, C.c_void_p(rgba_dev), width, height, buf, cap, C.byref(n)),
+                  "rtm_write_ppm")
+        return buf.raw[:n.value]
+
     def close(self):
         if self._h:
             _lib().rtm_ctx_destroy(self._h)
@@ -141,6 +159,22 @@ def render_frame(scene: Scene, eye: Camera, shadow: Camera, width: int, height: 
     abi.check(lib, lib.rtm_render(C.byref(sc), C.byref(e), C.byref(s), width, height, steps, flags,
                                   out.ctypes.data_as(C.POINTER(C.c_float))), "rtm_render")
     return out
+
+
+def encode_thresholds() -> np.ndarray:
+    """T[k] = least f32 v in [0,1] whose writeColorImage byte is >= k (T[0] = 0)."""
+    t = (C.c_float * 256)()
+    lib = _lib()
+    abi.check(lib, lib.rtm_encode_thresholds(t), "rtm_encode_thresholds")
+    return np.array(t[:], np.float32)
+
+
+def writeColorImage(ctx: Context, rgba_dev: int, width: int, height: int, path: str):
+    """main.rs:660 — encode on the GPU, write the P3 file (the reference panics on
+    an I/O error; this raises)."""
+    data = ctx.write_ppm(rgba_dev, width, height)
+    with open(path, "wb") as f:
+        f.write(data)
 
 
 class Viewport:

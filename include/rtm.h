@@ -181,6 +181,23 @@ int rtm_render_stats(rtm_ctx* ctx, const rtm_scene* scene, const rtm_camera* eye
                      const rtm_camera* shadow, int32_t width, int32_t height,
                      int32_t march_steps, int32_t flags, rtm_stats* out);
 
+/* ---- output encoding: writeColorImage (main.rs:660-704), BASELINE row f-2 ----
+ * Per channel: c.max(0.0).min(1.0), f32::powf(v, 1.0/2.2), (v * 255.0) as i64,
+ * evaluated exactly via 255 thresholds computed with the platform powf. */
+/* RGBA f32 (device, n_pixels*4, 16-byte aligned) -> packed RGB8 (device,
+ * n_pixels*3, any alignment), async on ctx's stream. */
+int rtm_encode_rgb8_async(rtm_ctx* ctx, const float* rgba_dev, int64_t n_pixels, uint8_t* rgb_dev);
+/* Upper bound of the PPM text size for a width x height image (header included). */
+int64_t rtm_ppm_max_bytes(int32_t width, int32_t height);
+/* The whole P3 file text ("P3\n{W} {H}\n255\n" + "{r} {g} {b}  " per pixel + "\n"
+ * per row) of a device RGBA f32 frame, generated on the GPU, into host memory
+ * `out` (no terminating NUL).  rgba_dev 16-byte aligned.  Blocking.  *length receives the text size; if it
+ * exceeds `capacity` nothing is written and RTM_ERR_INVALID is returned. */
+int rtm_write_ppm(rtm_ctx* ctx, const float* rgba_dev, int32_t width, int32_t height, char* out,
+                  int64_t capacity, int64_t* length);
+/* The 256 encode thresholds in use (T[k] = smallest v with byte(v) >= k). */
+int rtm_encode_thresholds(float out[256]);
+
 /* ---- reference-seam API (one call per reference function) ---- */
 typedef struct rtm_viewport rtm_viewport;
 /* Viewport{rasterized: vec![None; w*h], zBuffer: +INF, face, camera} (main.rs:426-439, 951-983) */

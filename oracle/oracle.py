@@ -52,6 +52,10 @@ def lib():
         L.rtmo_viewport_read_zbuffer.argtypes = [P, C.POINTER(C.c_double)]
         L.rtmo_calc_ray_plane.restype = C.c_int
         L.rtmo_calc_ray_plane.argtypes = [C.POINTER(C.c_double)] * 4 + [C.POINTER(C.c_double)]
+        L.rtmo_encode_scan.restype = C.c_int64
+        L.rtmo_encode_scan.argtypes = [C.POINTER(C.c_float), C.c_int32]
+        L.rtmo_write_ppm.restype = C.c_int64
+        L.rtmo_write_ppm.argtypes = [C.POINTER(C.c_float), C.c_int32, C.c_int32, C.c_char_p, C.c_int64]
         L.rtmo_encode_rgb8.restype = None
         L.rtmo_encode_rgb8.argtypes = [C.POINTER(C.c_float), C.c_int64, C.POINTER(C.c_int64)]
         _lib = L
@@ -139,3 +143,21 @@ def encode_rgb8(rgba):
     out = np.empty(n * 3, np.int64)
     lib().rtmo_encode_rgb8(_fp(rgba, C.c_float), n, _fp(out, C.c_int64))
     return out.reshape(rgba.shape[:-1] + (3,))
+
+
+def encode_scan(nthreads=8):
+    """Exhaustive scan of every f32 in [0,1]: (violations, thresholds[256])."""
+    t = (C.c_float * 256)()
+    v = lib().rtmo_encode_scan(t, nthreads)
+    return int(v), np.array(t[:], np.float32)
+
+
+def write_ppm(rgba):
+    """writeColorImage's P3 text (bytes) for an (H, W, 4) f32 image."""
+    rgba = np.ascontiguousarray(rgba, np.float32)
+    h, w = rgba.shape[:2]
+    cap = 64 + w * h * 13 + h
+    buf = C.create_string_buffer(cap)
+    n = lib().rtmo_write_ppm(_fp(rgba, C.c_float), w, h, buf, cap)
+    assert n >= 0
+    return buf.raw[:n]

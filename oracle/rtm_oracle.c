@@ -24,6 +24,7 @@
  */
 #include <math.h>
 #include <stdint.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -65,8 +66,12 @@ static double dot2d(Vec2 a, Vec2 b) { return a.x * b.x + a.y * b.y; }
 
 /* Rust f64::signum: +1 for +0/+x/+inf, -1 for -0/-x/-inf, NaN for NaN */
 static double rust_signum(double v) { return isnan(v) ? v : copysign(1.0, v); }
-/* Rust f64::max: NaN-ignoring maximum */
-static double rust_max(double a, double b) { return fmax(a, b); }
+/* Rust f64::max: a NaN operand (quiet or signaling) yields the other one.
+ * (glibc fmax returns NaN for a signaling NaN, per IEEE 754-2008 maxNum.) */
+static double rust_max(double a, double b) { return isnan(a) ? b : (isnan(b) ? a : fmax(a, b)); }
+/* Rust f32::max / f32::min, same NaN rule */
+static float rust_maxf(float a, float b) { return isnan(a) ? b : (isnan(b) ? a : fmaxf(a, b)); }
+static float rust_minf(float a, float b) { return isnan(a) ? b : (isnan(b) ? a : fminf(a, b)); }
 /* Rust `as i64` from f64: truncate toward zero, saturate, NaN -> 0 */
 static int64_t rust_as_i64(double v) {
     if (isnan(v)) return 0;
@@ -592,16 +597,90 @@ int rtmo_calc_ray_plane(const double origin[3], const double dir[3], const doubl
     return 0;
 }
 
+
+/* writeColorImage per-channel byte (main.rs:674-684), f32 arithmetic, libm powf */
+static int64_t enc_byte(float c) {
+    float v = rust_minf(rust_maxf(c, 0.0f), 1.0f); /* c.max(0.0).min(1.0): any NaN -> 0.0 */
+    float gamma = 2.2f;
+    v = powf(v, 1.0f / gamma);
+    return rust_as_i64((double)(v * 255.0f));
+}
+
+/* Exhaustive scan of every f32 in [+0, 1.0]: is the byte map monotone, and its
+ * thresholds T[k] = first v with byte >= k.  Returns the number of monotonicity
+ * violations (0 expected). */
+int64_t rtmo_encode_scan(float thresholds[256], int32_t nthreads) {
+    const uint32_t top = 0x3F800000u; /* bits of 1.0f */
+    enum { NCH = 64 };
+    static uint32_t first[NCH][256];
+    static int64_t lo_b[NCH], hi_b[NCH], viol[NCH];
+    const uint32_t per = (top + NCH) / NCH;
+#ifdef _OPENMP
+#pragma omp parallel for schedule(dynamic, 1) num_threads(nthreads < 1 ? 1 : nthreads)
+#endif
+    for (int ch = 0; ch < NCH; ch++) {
+        uint32_t b0 = (uint32_t)ch * per, b1 = b0 + per - 1;
+        if (b1 > top) b1 = top;
+        for (int k = 0; k < 256; k++) first[ch][k] = 0xFFFFFFFFu;
+        viol[ch] = 0;
+        int64_t prev = -1;
+        for (uint32_t b = b0;; b++) {
+            float v;
+            memcpy(&v, &b, sizeof v);
+            int64_t k = enc_byte(v);
+            if (k < prev) viol[ch]++;
+            if (b == b0) lo_b[ch] = k;
+            if (k != prev)
+                for (int64_t j = prev + 1; j <= k && j < 256; j++)
+                    if (j >= 0 && first[ch][j] == 0xFFFFFFFFu) first[ch][j] = b;
+            prev = k;
+            if (b == b1) break;
+        }
+        hi_b[ch] = prev;
+    }
+    int64_t total = 0;
+    for (int ch = 0; ch < NCH; ch++) {
+        total += viol[ch];
+        if (ch > 0 && lo_b[ch] < hi_b[ch - 1]) total++;
+    }
+    for (int k = 0; k < 256; k++) {
+        uint32_t best = 0xFFFFFFFFu;
+        for (int ch = 0; ch < NCH; ch++)
+            if (first[ch][k] < best) best = first[ch][k];
+        float t = INFINITY;
+        if (best != 0xFFFFFFFFu) memcpy(&t, &best, sizeof t);
+        thresholds[k] = k == 0 ? 0.0f : t;
+    }
+    return total;
+}
+
+/* writeColorImage (main.rs:660-704) text: "P3\n{W} {H}\n255\n", then per pixel
+ * format!("{} {} {}  ", r, g, b), '\n' after each row.  Returns the length, or
+ * -1 if it does not fit `cap`. */
+int64_t rtmo_write_ppm(const float* rgba, int32_t W, int32_t H, char* out, int64_t cap) {
+    int64_t n = 0;
+    char buf[64];
+    int l = snprintf(buf, sizeof buf, "P3\n%d %d\n255\n", W, H);
+    if (n + l > cap) return -1;
+    memcpy(out + n, buf, (size_t)l);
+    n += l;
+    for (int64_t iy = 0; iy < H; iy++) {
+        for (int64_t ix = 0; ix < W; ix++) {
+            const float* c = rgba + 4 * (iy * W + ix);
+            l = snprintf(buf, sizeof buf, "%lld %lld %lld  ", (long long)enc_byte(c[0]), (long long)enc_byte(c[1]),
+                         (long long)enc_byte(c[2]));
+            if (n + l > cap) return -1;
+            memcpy(out + n, buf, (size_t)l);
+            n += l;
+        }
+        if (n + 1 > cap) return -1;
+        out[n++] = '\n';
+    }
+    return n;
+}
+
 /* writeColorImage pixel encode (main.rs:674-684): clamp, f32 powf(1/2.2), (v*255) as i64 */
 void rtmo_encode_rgb8(const float* rgba, int64_t n_pixels, int64_t* out_rgb) {
-    for (int64_t i = 0; i < n_pixels; i++) {
-        for (int c = 0; c < 3; c++) {
-            float v = rgba[4 * i + c];
-            v = fmaxf(v, 0.0f);
-            v = fminf(v, 1.0f);
-            float gamma = 2.2f;
-            v = powf(v, 1.0f / gamma);
-            out_rgb[3 * i + c] = rust_as_i64((double)(v * 255.0f));
-        }
-    }
+    for (int64_t i = 0; i < n_pixels; i++)
+        for (int c = 0; c < 3; c++) out_rgb[3 * i + c] = enc_byte(rgba[4 * i + c]);
 }
