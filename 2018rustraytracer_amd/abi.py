@@ -11,9 +11,11 @@ import os
 _PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_PKG_DIR, "librtm.so")
 
-RTM_ABI_VERSION = 1
+RTM_ABI_VERSION = 2
 RTM_MAX_SPHERES = 16
 RTM_MAX_PATCHES = 4
+RTM_MAX_CIRCLE_PLANES = 16
+RTM_MAX_CAPPED_CYLINDERS = 16
 RTM_MAX_DIM = 32768
 
 RTM_OK = 0
@@ -47,16 +49,30 @@ class rtm_camera(C.Structure):
                 ("dir", C.c_double * 3), ("up", C.c_double * 3), ("side", C.c_double * 3)]
 
 
+class rtm_circle_plane(C.Structure):
+    _fields_ = [("id", C.c_int64), ("pos", C.c_double * 3), ("n", C.c_double * 3), ("radius", C.c_double),
+                ("color", C.c_double * 3)]
+
+
+class rtm_capped_cylinder(C.Structure):
+    _fields_ = [("id", C.c_int64), ("pa", C.c_double * 3), ("pb", C.c_double * 3), ("ra", C.c_double),
+                ("rb", C.c_double), ("color", C.c_double * 3)]
+
+
 class rtm_scene(C.Structure):
     _fields_ = [("spheres", C.POINTER(rtm_sphere)), ("patches", C.POINTER(rtm_patch)),
-                ("n_spheres", C.c_int32), ("n_patches", C.c_int32)]
+                ("n_spheres", C.c_int32), ("n_patches", C.c_int32),
+                ("circle_planes", C.POINTER(rtm_circle_plane)),
+                ("capped_cylinders", C.POINTER(rtm_capped_cylinder)),
+                ("n_circle_planes", C.c_int32), ("n_capped_cylinders", C.c_int32)]
 
 
 class rtm_stats(C.Structure):
     _fields_ = [("eye_hits", C.c_int64 * RTM_MAX_SPHERES), ("eye_hit_pixels", C.c_int64),
                 ("lit_pixels", C.c_int64), ("eye_sphere_tests", C.c_int64),
                 ("shadow_sphere_tests", C.c_int64), ("march_iterations", C.c_int64),
-                ("march_hits", C.c_int64), ("march_in_range", C.c_int64)]
+                ("march_hits", C.c_int64), ("march_in_range", C.c_int64),
+                ("eye_circle_plane_pixels", C.c_int64), ("eye_capped_cylinder_pixels", C.c_int64)]
 
     def as_dict(self) -> dict:
         d = {name: getattr(self, name) for name, _ in self._fields_ if name != "eye_hits"}
@@ -67,8 +83,10 @@ class rtm_stats(C.Structure):
 assert C.sizeof(rtm_sphere) == 64
 assert C.sizeof(rtm_patch) == 32
 assert C.sizeof(rtm_camera) == 104
-assert C.sizeof(rtm_scene) == 24
-assert C.sizeof(rtm_stats) == 8 * (RTM_MAX_SPHERES + 7)
+assert C.sizeof(rtm_circle_plane) == 88
+assert C.sizeof(rtm_capped_cylinder) == 96
+assert C.sizeof(rtm_scene) == 48
+assert C.sizeof(rtm_stats) == 8 * (RTM_MAX_SPHERES + 9)
 
 # (name, restype, argtypes) for every symbol include/rtm.h declares.
 _P = C.c_void_p
@@ -103,6 +121,7 @@ ABI_SYMBOLS = [
     ("rtm_viewport_create", C.c_int, [_P, _I32, _I32, _I32, C.POINTER(rtm_camera), C.POINTER(_P)]),
     ("rtm_viewport_destroy", None, [_P]),
     ("rtm_viewport_rasterize", C.c_int, [_P, C.POINTER(rtm_scene)]),
+    ("rtm_viewport_process_raytracing_rays", C.c_int, [_P, C.POINTER(rtm_scene)]),
     ("rtm_viewport_process_raymarching_rays", C.c_int, [_P, C.POINTER(rtm_patch), _I32, _I32]),
     ("rtm_render_color_image", C.c_int, [C.POINTER(rtm_scene), _P, _P, C.POINTER(C.c_float)]),
     ("rtm_viewport_read_zbuffer", C.c_int, [_P, C.POINTER(C.c_double)]),

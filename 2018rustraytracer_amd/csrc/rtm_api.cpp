@@ -182,7 +182,67 @@ int validate_scene(const rtm_scene* scene) {
         if (id < 0 || id >= scene->n_spheres)
             return fail(RTM_ERR_INVALID, "sphere %d has id %lld outside [0,%d)", i, (long long)id, scene->n_spheres);
     }
+    const int np = scene->n_circle_planes, nc = scene->n_capped_cylinders;
+    if (np < 0 || np > RTM_MAX_CIRCLE_PLANES)
+        return fail(RTM_ERR_INVALID, "n_circle_planes=%d outside [0,%d]", np, RTM_MAX_CIRCLE_PLANES);
+    if (nc < 0 || nc > RTM_MAX_CAPPED_CYLINDERS)
+        return fail(RTM_ERR_INVALID, "n_capped_cylinders=%d outside [0,%d]", nc, RTM_MAX_CAPPED_CYLINDERS);
+    if (np > 0 && !scene->circle_planes) return fail(RTM_ERR_INVALID, "circle_planes is NULL");
+    if (nc > 0 && !scene->capped_cylinders) return fail(RTM_ERR_INVALID, "capped_cylinders is NULL");
+    // renderColorImage indexes circlePlanePrimitives[id] / cappedCylinderPrimitives[id] (main.rs:773, 791)
+    for (int i = 0; i < np; ++i)
+        if (scene->circle_planes[i].id < 0 || scene->circle_planes[i].id >= np)
+            return fail(RTM_ERR_INVALID, "circle plane %d has id %lld outside [0,%d)", i,
+                        (long long)scene->circle_planes[i].id, np);
+    for (int i = 0; i < nc; ++i)
+        if (scene->capped_cylinders[i].id < 0 || scene->capped_cylinders[i].id >= nc)
+            return fail(RTM_ERR_INVALID, "capped cylinder %d has id %lld outside [0,%d)", i,
+                        (long long)scene->capped_cylinders[i].id, nc);
     return RTM_OK;
+}
+
+// Ray-traced primitives of a (validated) scene, with iCappedCone's
+// ray-independent terms in the reference's operation order (main.rs:2906-2934).
+// Returns true when the scene has any.
+bool build_rt(const rtm_scene* scene, RtK& k) {
+    std::memset(&k, 0, sizeof k);
+    k.n_pl = scene->n_circle_planes;
+    k.n_cy = scene->n_capped_cylinders;
+    for (int i = 0; i < k.n_pl; ++i) {
+        const rtm_circle_plane& q = scene->circle_planes[i];
+        PlaneK& p = k.pl[i];
+        p.cx = q.pos[0];
+        p.cy = q.pos[1];
+        p.cz = q.pos[2];
+        p.nx = q.n[0];
+        p.ny = q.n[1];
+        p.nz = q.n[2];
+        p.radius = q.radius;
+        p.cr = q.color[0];
+        p.cg = q.color[1];
+        p.cb = q.color[2];
+        p.id = (int32_t)q.id;
+    }
+    for (int i = 0; i < k.n_cy; ++i) {
+        const rtm_capped_cylinder& q = scene->capped_cylinders[i];
+        CylK& c = k.cy[i];
+        for (int j = 0; j < 3; ++j) {
+            c.pa[j] = q.pa[j];
+            c.pb[j] = q.pb[j];
+            c.ba[j] = q.pb[j] - q.pa[j];
+        }
+        c.ra = q.ra;
+        c.rb = q.rb;
+        c.baba = c.ba[0] * c.ba[0] + c.ba[1] * c.ba[1] + c.ba[2] * c.ba[2];
+        c.rr = q.rb - q.ra;
+        c.hy = c.baba + c.rr * c.rr;
+        c.isq = 1.0 / std::sqrt(c.baba);
+        c.cr = q.color[0];
+        c.cg = q.color[1];
+        c.cb = q.color[2];
+        c.id = (int32_t)q.id;
+    }
+    return k.n_pl + k.n_cy > 0;
 }
 
 int validate_camera(const rtm_camera* c, const char* what) {
@@ -207,10 +267,14 @@ int build_frame(FrameArgs& a, const rtm_scene* scene, const rtm_camera* eye, con
     if (steps < 0) return fail(RTM_ERR_INVALID, "march_steps=%d < 0", steps);
     if (flags & ~(RTM_FLAG_NO_MARCH | RTM_FLAG_NO_SHADOW_RASTER | RTM_FLAG_FUSED_SHADOW))
         return fail(RTM_ERR_INVALID, "unknown flags 0x%x", flags);
-    // The frame path rasterizes both viewports: orthographic only (perspective
-    // projectSphere is BASELINE "next" row f-3); Camera::project asserts ORTHO (main.rs:1949).
-    if (eye->type != RTM_CAMERA_ORTHOGONAL || shadow->type != RTM_CAMERA_ORTHOGONAL)
-        return fail(RTM_ERR_UNSUPPORTED, "frame path needs ORTHOGONAL eye and shadow cameras");
+    // Camera::project asserts ORTHO (main.rs:1949) for the shadow lookup; the eye
+    // viewport rasterizes spheres orthographically only (perspective projectSphere
+    // is BASELINE "next" row f-3).  Without spheres the eye rasterize is a no-op
+    // and a PERSPECTIVE eye is exact (testscene_raytracingPlane0, main.rs:1016).
+    if (shadow->type != RTM_CAMERA_ORTHOGONAL)
+        return fail(RTM_ERR_UNSUPPORTED, "frame path needs an ORTHOGONAL shadow camera");
+    if (eye->type != RTM_CAMERA_ORTHOGONAL && scene->n_spheres > 0)
+        return fail(RTM_ERR_UNSUPPORTED, "spheres under a PERSPECTIVE eye camera need projectSphere (row f-3)");
     std::memset(&a, 0, sizeof a);
     ShadowPart& sh = a.sh;
     EyePart& ey = a.ey;
@@ -313,6 +377,8 @@ struct rtm_ctx {
     DevBuf tabs;  // [t (steps) | nx (W) | ny (H)] f64, see Tables
     DevBuf enc_rgb, enc_rows, enc_text;  // writeColorImage scratch
     DevBuf enc_tab;                      // EncodeTable on the device (t | bucket)
+    DevBuf rtk;                          // RtK of the frame being enqueued (row f-1)
+    std::vector<rtm_viewport*> viewports;  // live viewports (orphaned when the context goes first)
     bool enc_tab_ready = false;
     uint64_t tab_key = 0;
     int64_t tab_nt = 0, tab_nz = 0, tab_nd = 0;
@@ -325,6 +391,9 @@ struct rtm_viewport {
     int32_t W = 0, H = 0, face = 0;
     rtm_camera cam{};
     DevBuf zbuf, gh, gz, gid;
+    DevBuf gn;  // capped-cylinder hit normals (3 f64 per pixel), allocated by the first trace
+    int32_t traced_pl = 0, traced_cy = 0;  // max primitive counts traced into the G-buffer
+    int32_t raster_sp = 0;                 // ... and rasterized
 };
 
 namespace {
@@ -511,9 +580,21 @@ TimingSlot* next_slot(rtm_ctx* ctx) {
     return timed ? &ctx->ring[(size_t)(ctx->renders % (int64_t)ctx->ring.size())] : nullptr;
 }
 
-int enqueue_frame(rtm_ctx* ctx, FrameArgs& a, float* out_dev, StatsK* stats) {
+// The frame's ray-traced primitives into ctx->rtk (stream-ordered; the previous
+// frame's kernels have consumed the old contents by the time the upload runs).
+int upload_rt(rtm_ctx* ctx, const RtK& rt, const RtK** dev) {
+    int rc = ctx->rtk.ensure(sizeof(RtK), ctx->device);
+    if (rc) return rc;
+    if ((rc = launch_rt_upload(rt, (RtK*)ctx->rtk.p, ctx->stream))) return fail(rc, "rt upload launch failed");
+    *dev = (const RtK*)ctx->rtk.p;
+    return RTM_OK;
+}
+
+int enqueue_frame(rtm_ctx* ctx, FrameArgs& a, const RtK* rt_host, float* out_dev, StatsK* stats) {
     int rc;
     if ((rc = frame_tables(ctx, a))) return rc;
+    const RtK* rt = nullptr;
+    if (rt_host && (rc = upload_rt(ctx, *rt_host, &rt))) return rc;
     const bool fused = (a.ey.flags & RTM_FLAG_FUSED_SHADOW) != 0;
     hipStream_t s = ctx->stream;
     double* smap = nullptr;
@@ -532,7 +613,7 @@ int enqueue_frame(rtm_ctx* ctx, FrameArgs& a, float* out_dev, StatsK* stats) {
         ctx->have_shadow_pass = false;
     }
     if (slot) HIP_TRY(hipEventRecord(slot->ev[2], s));
-    if ((rc = launch_eye_pass(a, smap, out_dev, s, stats))) return fail(rc, "eye pass launch failed");
+    if ((rc = launch_eye_pass(a, smap, out_dev, s, stats, rt))) return fail(rc, "eye pass launch failed");
     if (slot) {
         HIP_TRY(hipEventRecord(slot->ev[3], s));
         slot->shadow = !fused;
@@ -553,8 +634,8 @@ rtm_ctx* default_ctx(int* rc) {
     return c.get();
 }
 
-int check_ortho_raster(const rtm_camera& c) {
-    if (c.type != RTM_CAMERA_ORTHOGONAL)
+int check_ortho_raster(const rtm_camera& c, const rtm_scene* scene) {
+    if (c.type != RTM_CAMERA_ORTHOGONAL && scene->n_spheres > 0)
         return fail(RTM_ERR_UNSUPPORTED, "rasterize: perspective projectSphere (main.rs:473-530) is not on this path");
     return RTM_OK;
 }
@@ -599,6 +680,7 @@ int rtm_ctx_create(int32_t device, rtm_ctx** out) {
 
 void rtm_ctx_destroy(rtm_ctx* ctx) {
     if (!ctx) return;
+    for (rtm_viewport* vp : ctx->viewports) vp->ctx = nullptr;  // calls on them now fail; destroy still frees
     {
         DeviceGuard g(ctx->device);
         if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
@@ -682,8 +764,10 @@ int rtm_render_async(rtm_ctx* ctx, const rtm_scene* scene, const rtm_camera* eye
         return fail(RTM_ERR_INVALID, "row range [%d,%d) outside [0,%d)", row_begin, row_end, height);
     a.ey.row_begin = row_begin;
     a.ey.row_end = row_end;
+    RtK rt;
+    const bool has_rt = build_rt(scene, rt);
     DeviceGuard g(ctx->device);
-    return enqueue_frame(ctx, a, out_rgba_dev, nullptr);
+    return enqueue_frame(ctx, a, has_rt ? &rt : nullptr, out_rgba_dev, nullptr);
 }
 
 const double* rtm_ctx_shadow_map(rtm_ctx* ctx) {
@@ -698,9 +782,12 @@ int rtm_render_frames_async(rtm_ctx* ctx, int32_t n_frames, const rtm_scene* sce
     for (int32_t i = 0; i < n_frames; ++i)
         if (!out_rgba_dev[i]) return fail(RTM_ERR_INVALID, "out_rgba_dev[%d] is NULL", i);
     std::vector<FrameArgs> f((size_t)n_frames);
+    std::vector<RtK> rt((size_t)n_frames);
+    bool any_rt = false;
     for (int32_t i = 0; i < n_frames; ++i) {
         int rc = build_frame(f[(size_t)i], &scenes[i], eye, shadow, width, height, march_steps, flags);
         if (rc) return rc;
+        any_rt |= build_rt(&scenes[i], rt[(size_t)i]);
     }
     DeviceGuard g(ctx->device);
     // The pipelined launch (shadow pass of frame i + eye pass of frame i-1) is
@@ -713,13 +800,15 @@ int rtm_render_frames_async(rtm_ctx* ctx, int32_t n_frames, const rtm_scene* sce
     }();
     // The pipeline shares one table set: every frame must have the same patches
     // (the cameras are shared by construction).  Otherwise render frame by frame.
-    bool same = pipeline_on && (flags & RTM_FLAG_FUSED_SHADOW) == 0 && n_frames > 1;
+    // (frames with ray-traced primitives always take the two-kernel path)
+    bool same = pipeline_on && !any_rt && (flags & RTM_FLAG_FUSED_SHADOW) == 0 && n_frames > 1;
     for (int32_t i = 1; same && i < n_frames; ++i)
         same = f[(size_t)i].sh.n_patches == f[0].sh.n_patches &&
                std::memcmp(f[(size_t)i].sh.patch, f[0].sh.patch, sizeof(PatchK) * (size_t)f[0].sh.n_patches) == 0;
     if (!same) {
         for (int32_t i = 0; i < n_frames; ++i) {
-            int rc = enqueue_frame(ctx, f[(size_t)i], out_rgba_dev[i], nullptr);
+            const RtK* r = rt[(size_t)i].n_pl + rt[(size_t)i].n_cy > 0 ? &rt[(size_t)i] : nullptr;
+            int rc = enqueue_frame(ctx, f[(size_t)i], r, out_rgba_dev[i], nullptr);
             if (rc) return rc;
         }
         return RTM_OK;
@@ -788,10 +877,12 @@ int rtm_render(const rtm_scene* scene, const rtm_camera* eye, const rtm_camera* 
     if (rc) return rc;
     rtm_ctx* ctx = default_ctx(&rc);
     if (!ctx) return rc;
+    RtK rt;
+    const bool has_rt = build_rt(scene, rt);
     DeviceGuard g(ctx->device);
     const size_t bytes = sizeof(float) * 4 * (size_t)width * (size_t)height;
     if ((rc = ctx->out.ensure(bytes, ctx->device))) return rc;
-    if ((rc = enqueue_frame(ctx, a, (float*)ctx->out.p, nullptr))) return rc;
+    if ((rc = enqueue_frame(ctx, a, has_rt ? &rt : nullptr, (float*)ctx->out.p, nullptr))) return rc;
     HIP_TRY(hipMemcpyAsync(out_rgba, ctx->out.p, bytes, hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(hipStreamSynchronize(ctx->stream));
     return RTM_OK;
@@ -803,12 +894,14 @@ int rtm_render_stats(rtm_ctx* ctx, const rtm_scene* scene, const rtm_camera* eye
     FrameArgs a;
     int rc = build_frame(a, scene, eye, shadow, width, height, march_steps, flags);
     if (rc) return rc;
+    RtK rt;
+    const bool has_rt = build_rt(scene, rt);
     DeviceGuard g(ctx->device);
     const size_t bytes = sizeof(float) * 4 * (size_t)width * (size_t)height;
     if ((rc = ctx->out.ensure(bytes, ctx->device))) return rc;
     if ((rc = ctx->stats.ensure(sizeof(StatsK), ctx->device))) return rc;
     HIP_TRY(hipMemsetAsync(ctx->stats.p, 0, sizeof(StatsK), ctx->stream));
-    if ((rc = enqueue_frame(ctx, a, (float*)ctx->out.p, (StatsK*)ctx->stats.p))) return rc;
+    if ((rc = enqueue_frame(ctx, a, has_rt ? &rt : nullptr, (float*)ctx->out.p, (StatsK*)ctx->stats.p))) return rc;
     HIP_TRY(hipMemcpyAsync(out, ctx->stats.p, sizeof(StatsK), hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(hipStreamSynchronize(ctx->stream));
     return RTM_OK;
@@ -918,23 +1011,27 @@ int rtm_viewport_create(rtm_ctx* ctx, int32_t width, int32_t height, int32_t fac
     // zBuffer: Map2d::new(.., INFINITY); rasterized: vec![None; ..] (main.rs:1534-1536)
     if ((rc = launch_fill((double*)v->zbuf.p, (int64_t)n, INFINITY, (int32_t*)v->gid.p, -1, ctx->stream)))
         return fail(rc, "viewport init launch failed");
+    ctx->viewports.push_back(v.get());
     *out = v.release();
     return RTM_OK;
 }
 
 void rtm_viewport_destroy(rtm_viewport* vp) {
     if (!vp) return;
-    {
+    if (vp->ctx) {  // (an orphaned viewport's context already drained its stream)
         DeviceGuard g(vp->ctx->device);
         (void)hipStreamSynchronize(vp->ctx->stream);
+        auto& v = vp->ctx->viewports;
+        v.erase(std::remove(v.begin(), v.end(), vp), v.end());
     }
     delete vp;
 }
 
 int rtm_viewport_rasterize(rtm_viewport* vp, const rtm_scene* scene) {
-    if (!vp) return fail(RTM_ERR_INVALID, "viewport is NULL");
+    if (!vp || !vp->ctx) return fail(RTM_ERR_INVALID, "viewport is NULL or its context was destroyed");
     int rc;
-    if ((rc = validate_scene(scene)) || (rc = check_ortho_raster(vp->cam))) return rc;
+    if ((rc = validate_scene(scene)) || (rc = check_ortho_raster(vp->cam, scene))) return rc;
+    if (scene->n_spheres == 0) return RTM_OK;  // main.rs:447: nothing to project
     RasterArgs a;
     std::memset(&a, 0, sizeof a);
     for (int i = 0; i < scene->n_spheres; ++i) a.sph[i] = project_sphere(vp->cam, scene->spheres[i], vp->W, vp->H);
@@ -946,12 +1043,36 @@ int rtm_viewport_rasterize(rtm_viewport* vp, const rtm_scene* scene) {
     if ((rc = launch_vp_rasterize(a, (double*)vp->zbuf.p, (double*)vp->gh.p, (double*)vp->gz.p, (int32_t*)vp->gid.p,
                                   vp->ctx->stream)))
         return fail(rc, "rasterize launch failed");
+    vp->raster_sp = std::max(vp->raster_sp, scene->n_spheres);
+    return RTM_OK;
+}
+
+int rtm_viewport_process_raytracing_rays(rtm_viewport* vp, const rtm_scene* scene) {
+    if (!vp || !vp->ctx) return fail(RTM_ERR_INVALID, "viewport is NULL or its context was destroyed");
+    int rc;
+    if ((rc = validate_scene(scene))) return rc;
+    RtK k;
+    if (!build_rt(scene, k)) return RTM_OK;  // no circle planes, no cylinders: nothing to trace
+    rtm_ctx* ctx = vp->ctx;
+    DeviceGuard g(ctx->device);
+    if ((rc = vp->gn.ensure(sizeof(double) * 3 * (size_t)vp->W * (size_t)vp->H, ctx->device))) return rc;
+    TraceArgs a;
+    std::memset(&a, 0, sizeof a);
+    a.cam = cam_k(vp->cam);
+    a.W = vp->W;
+    a.H = vp->H;
+    if ((rc = upload_rt(ctx, k, &a.rt))) return rc;
+    if ((rc = launch_vp_trace(a, (double*)vp->zbuf.p, (double*)vp->gh.p, (int32_t*)vp->gid.p, (double*)vp->gn.p,
+                              ctx->stream)))
+        return fail(rc, "trace launch failed");
+    vp->traced_pl = std::max(vp->traced_pl, k.n_pl);
+    vp->traced_cy = std::max(vp->traced_cy, k.n_cy);
     return RTM_OK;
 }
 
 int rtm_viewport_process_raymarching_rays(rtm_viewport* vp, const rtm_patch* patches, int32_t n_patches,
                                           int32_t steps) {
-    if (!vp) return fail(RTM_ERR_INVALID, "viewport is NULL");
+    if (!vp || !vp->ctx) return fail(RTM_ERR_INVALID, "viewport is NULL or its context was destroyed");
     if (n_patches < 0 || n_patches > RTM_MAX_PATCHES) return fail(RTM_ERR_INVALID, "n_patches=%d", n_patches);
     if (n_patches > 0 && !patches) return fail(RTM_ERR_INVALID, "patches is NULL");
     if (steps < 0) return fail(RTM_ERR_INVALID, "steps=%d", steps);
@@ -975,11 +1096,19 @@ int rtm_viewport_process_raymarching_rays(rtm_viewport* vp, const rtm_patch* pat
 int rtm_render_color_image(const rtm_scene* scene, const rtm_viewport* vp, const rtm_viewport* shadow_vp,
                            float* out_rgba) {
     if (!vp || !shadow_vp || !out_rgba) return fail(RTM_ERR_INVALID, "viewport/out is NULL");
+    if (!vp->ctx || !shadow_vp->ctx) return fail(RTM_ERR_INVALID, "a viewport's context was destroyed");
     if (vp->ctx != shadow_vp->ctx) return fail(RTM_ERR_INVALID, "viewports belong to different contexts");
     int rc;
     if ((rc = validate_scene(scene))) return rc;
     if (shadow_vp->cam.type != RTM_CAMERA_ORTHOGONAL)
         return fail(RTM_ERR_UNSUPPORTED, "Camera::project is orthographic only (main.rs:1949)");
+    // the G-buffer may hold ids of every primitive traced into it: the reference
+    // indexes the scene's arrays with them and panics when out of range (main.rs:773, 791)
+    if (vp->traced_pl > scene->n_circle_planes || vp->traced_cy > scene->n_capped_cylinders ||
+        vp->raster_sp > scene->n_spheres)
+        return fail(RTM_ERR_INVALID, "scene has fewer spheres/circle planes/cylinders (%d/%d/%d) than the viewport "
+                    "holds (%d/%d/%d)", scene->n_spheres, scene->n_circle_planes, scene->n_capped_cylinders,
+                    vp->raster_sp, vp->traced_pl, vp->traced_cy);
     ShadeArgs a;
     std::memset(&a, 0, sizeof a);
     for (int i = 0; i < scene->n_spheres; ++i) a.shade[i] = shade_sphere(scene->spheres[i]);
@@ -994,6 +1123,11 @@ int rtm_render_color_image(const rtm_scene* scene, const rtm_viewport* vp, const
     DeviceGuard g(ctx->device);
     const size_t bytes = sizeof(float) * 4 * (size_t)vp->W * (size_t)vp->H;
     if ((rc = ctx->out.ensure(bytes, ctx->device))) return rc;
+    RtK k;
+    if (build_rt(scene, k)) {  // shading lookups circlePlanePrimitives[id] / cappedCylinderPrimitives[id]
+        if ((rc = upload_rt(ctx, k, &a.rt))) return rc;
+        a.gn = (const double*)vp->gn.p;
+    }
     if ((rc = launch_vp_shade(a, (const double*)shadow_vp->zbuf.p, (const double*)vp->gh.p, (const double*)vp->gz.p,
                               (const int32_t*)vp->gid.p, (float*)ctx->out.p, ctx->stream)))
         return fail(rc, "shade launch failed");
@@ -1003,7 +1137,7 @@ int rtm_render_color_image(const rtm_scene* scene, const rtm_viewport* vp, const
 }
 
 int rtm_viewport_read_zbuffer(const rtm_viewport* vp, double* out) {
-    if (!vp || !out) return fail(RTM_ERR_INVALID, "viewport/out is NULL");
+    if (!vp || !out || !vp->ctx) return fail(RTM_ERR_INVALID, "viewport/out is NULL or its context was destroyed");
     DeviceGuard g(vp->ctx->device);
     HIP_TRY(hipMemcpyAsync(out, vp->zbuf.p, sizeof(double) * (size_t)vp->W * (size_t)vp->H, hipMemcpyDeviceToHost,
                            vp->ctx->stream));

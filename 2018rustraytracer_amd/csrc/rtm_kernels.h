@@ -109,6 +109,37 @@ struct FrameArgs {
 };
 static_assert(sizeof(FrameArgs) <= 4096, "FrameArgs must fit the 4 KiB kernarg segment");
 
+// Ray-traced primitives of one frame (row f-1: processRaytracingRays,
+// main.rs:569-642), with the ray-independent parts of calcRayPlane /
+// iCappedCone evaluated once on the host in the reference's operation order.
+// Lives in device memory (too large to share the 4 KiB kernarg segment with
+// FrameArgs); written per frame by a stream-ordered upload kernel.
+struct PlaneK {            // PrimitiveCirclePlane (main.rs:370-380)
+    double cx, cy, cz;     // pos (Plane.center)
+    double nx, ny, nz;     // n
+    double radius;
+    double cr, cg, cb;     // shading
+    int32_t id, pad;
+};
+struct CylK {              // PrimitiveCappedCylinder (main.rs:382-391)
+    double pa[3], pb[3];
+    double ba[3];          // pb - pa                   (main.rs:2906)
+    double ra, rb;
+    double baba;           // dot(ba, ba)               (main.rs:2910)
+    double rr;             // rb - ra                   (main.rs:2933)
+    double hy;             // baba + rr*rr              (main.rs:2934)
+    double isq;            // inversesqrt(baba) = 1.0/sqrt(baba) (main.rs:2919, 2963)
+    double cr, cg, cb;
+    int32_t id, pad;
+};
+struct RtK {
+    PlaneK pl[RTM_MAX_CIRCLE_PLANES];
+    CylK cy[RTM_MAX_CAPPED_CYLINDERS];
+    int32_t n_pl, n_cy;
+};
+static_assert(sizeof(PlaneK) == 88 && sizeof(CylK) == 152, "RtK layout");
+static_assert(sizeof(RtK) + sizeof(void*) <= 4096, "RtK must fit the upload kernel's kernarg segment");
+
 // Reference-seam kernels (one per reference function).
 struct RasterArgs {
     RasterSphereK sph[RTM_MAX_SPHERES];
@@ -127,19 +158,37 @@ struct ShadeArgs {
     CamK eye, shadow;
     int32_t W, H, Ws, Hs;
     int32_t n_spheres, pad;
+    const RtK* rt;      // plane / cylinder shading constants (device; nullptr: none)
+    const double* gn;   // cylinder hit normals, 3 per pixel (nullptr: none)
 };
+
+struct TraceArgs {      // processRaytracingRays of one viewport
+    CamK cam;
+    int32_t W, H;
+    const RtK* rt;
+};
+
+// Staged G-buffer id encoding: sphere id | GID_PLANE | GID_CYLINDER (kind in bits 16+).
+constexpr int32_t GID_PLANE = 1 << 16;
+constexpr int32_t GID_CYLINDER = 2 << 16;
 
 // Device counters for rtm_render_stats (layout == rtm_stats).
 struct StatsK {
     unsigned long long eye_hits[RTM_MAX_SPHERES];
     unsigned long long eye_hit_pixels, lit_pixels, eye_sphere_tests, shadow_sphere_tests;
     unsigned long long march_iterations, march_hits, march_in_range;
+    unsigned long long eye_circle_plane_pixels, eye_capped_cylinder_pixels;
 };
 static_assert(sizeof(StatsK) == sizeof(rtm_stats), "StatsK layout");
 
 // Launchers (rtm_kernels.hip).  All asynchronous on `stream`.
 int launch_shadow_pass(const FrameArgs& a, double* smap, void* stream, StatsK* stats);
-int launch_eye_pass(const FrameArgs& a, const double* smap, float* out, void* stream, StatsK* stats);
+// rt != nullptr: the frame has ray-traced primitives (device RtK, see launch_rt_upload).
+int launch_eye_pass(const FrameArgs& a, const double* smap, float* out, void* stream, StatsK* stats,
+                    const RtK* rt = nullptr);
+// Stream-ordered copy of a host RtK into device memory (a kernel, so the host
+// copy is consumed at launch: no pinned staging, no host synchronisation).
+int launch_rt_upload(const RtK& k, RtK* dst, void* stream);
 // Software-pipelined frame step: the shadow pass of a.sh into smap_w and the eye
 // pass of a.ey (the previous frame) from smap_r into out, in ONE launch whose
 // workgroups interleave the two roles (VALU-bound and HBM-store-bound tiles
@@ -150,6 +199,7 @@ int launch_vp_rasterize(const RasterArgs& a, double* zbuf, double* gh, double* g
 int launch_vp_march(const MarchArgs& a, double* zbuf, void* stream);
 int launch_vp_shade(const ShadeArgs& a, const double* szbuf, const double* gh, const double* gz,
                     const int32_t* gid, float* out, void* stream);
+int launch_vp_trace(const TraceArgs& a, double* zbuf, double* gh, int32_t* gid, double* gn, void* stream);
 int launch_fill(double* p, int64_t n, double v, int32_t* ip, int32_t iv, void* stream);
 
 }  // namespace rtm

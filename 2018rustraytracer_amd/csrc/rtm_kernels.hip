@@ -247,6 +247,119 @@ __device__ __forceinline__ void cam_ray(const CamK& c, double s, double u, doubl
     }
 }
 
+// ---- ray-traced primitives (row f-1) ----
+
+// One circle plane against one ray, as processRaytracingRays tests it
+// (main.rs:575-604): calcRayPlane (main.rs:2398-2408), t >= 0, t <= the pixel's
+// current depth zb, then |o + d*t - pos| <= radius.  NaN t passes both depth
+// tests exactly as in the reference.
+__device__ __forceinline__ bool plane_hit(const PlaneK& p, const double o[3], const double d[3], double zb,
+                                          double& t) {
+    const double denom = p.nx * d[0] + p.ny * d[1] + p.nz * d[2];  // dot(plane.n, rayDir)
+    if (!(fabs(denom) > 0.0001)) return false;
+    t = ((p.cx - o[0]) * p.nx + (p.cy - o[1]) * p.ny + (p.cz - o[2]) * p.nz) / denom;
+    if (t < 0.0) return false;  // behind the camera
+    if (t > zb) return false;   // behind a known intersection
+    const double qx = (o[0] + d[0] * t) - p.cx;
+    const double qy = (o[1] + d[1] * t) - p.cy;
+    const double qz = (o[2] + d[2] * t) - p.cz;
+    return !(sqrt(qx * qx + qy * qy + qz * qz) > p.radius);
+}
+
+// iCappedCone (main.rs:2889-2959) in the reference's operation order; the
+// ray-independent terms (ba, baba, rr, hy, inversesqrt(baba)) come from the
+// host.  Returns t (-1 on a miss) and the hit normal in n.
+__device__ __forceinline__ double icapped(const CylK& c, const double ro[3], const double rd[3], double n[3]) {
+    double oa[3], ob[3];
+    for (int k = 0; k < 3; ++k) {
+        oa[k] = ro[k] - c.pa[k];
+        ob[k] = ro[k] - c.pb[k];
+    }
+    const double rdba = rd[0] * c.ba[0] + rd[1] * c.ba[1] + rd[2] * c.ba[2];
+    const double oaba = oa[0] * c.ba[0] + oa[1] * c.ba[1] + oa[2] * c.ba[2];
+    const double obba = ob[0] * c.ba[0] + ob[1] * c.ba[1] + ob[2] * c.ba[2];
+    // caps
+    if (oaba < 0.0) {
+        double w[3];
+        for (int k = 0; k < 3; ++k) w[k] = oa[k] * rdba - rd[k] * oaba;
+        if (w[0] * w[0] + w[1] * w[1] + w[2] * w[2] < c.ra * c.ra * rdba * rdba) {
+            const double sc = -c.isq;
+            for (int k = 0; k < 3; ++k) n[k] = c.ba[k] * sc;
+            return -oaba / rdba;
+        }
+    } else if (obba > 0.0) {
+        const double t = -obba / rdba;
+        double w[3];
+        for (int k = 0; k < 3; ++k) w[k] = ob[k] + rd[k] * t;
+        if (w[0] * w[0] + w[1] * w[1] + w[2] * w[2] < c.rb * c.rb) {
+            for (int k = 0; k < 3; ++k) n[k] = c.ba[k] * c.isq;
+            return t;
+        }
+    }
+    // body
+    double oc[3];
+    for (int k = 0; k < 3; ++k) oc[k] = oa[k] * c.rb - ob[k] * c.ra;
+    const double ocba = oc[0] * c.ba[0] + oc[1] * c.ba[1] + oc[2] * c.ba[2];
+    const double ocrd = oc[0] * rd[0] + oc[1] * rd[1] + oc[2] * rd[2];
+    const double ococ = oc[0] * oc[0] + oc[1] * oc[1] + oc[2] * oc[2];
+    const double bb = c.baba * c.baba;
+    const double k2 = bb - c.hy * rdba * rdba;
+    const double k1 = bb * ocrd - c.hy * rdba * ocba;
+    const double k0 = bb * ococ - c.hy * ocba * ocba;
+    const double h = k1 * k1 - k2 * k0;
+    if (h < 0.0) return -1.0;
+    const double sg = c.rr >= 0.0 ? 1.0 : -1.0;  // sign (main.rs:2967-2974)
+    const double t = (-k1 - sg * sqrt(h)) / (k2 * c.rr);
+    const double y = oaba + rdba * t;
+    if (y > 0.0 && y < c.baba) {
+        const double rra = c.rr * c.ra, hyy = c.hy * y;
+        double v[3];
+        for (int k = 0; k < 3; ++k) v[k] = ((oa[k] + rd[k] * t) * c.baba - c.ba[k] * rra) * c.baba - c.ba[k] * hyy;
+        const double m = sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);  // normalize (main.rs:105-108)
+        const double inv = 1.0 / m;
+        for (int k = 0; k < 3; ++k) n[k] = v[k] * inv;
+        return t;
+    }
+    return -1.0;
+}
+
+// The ray-traced part of one eye pixel: planes, then cylinders, in scene order
+// (main.rs:573-638).  zb is the depth after the sphere rasterize; kind/rid/t/n
+// are updated in place when a primitive takes the pixel.
+struct RtHit {
+    int kind;  // 0 none, 1 sphere, 2 circle plane, 3 capped cylinder
+    int id;
+    double t;
+    double n[3];
+};
+
+__device__ __forceinline__ void trace_pixel(const RtK* __restrict__ rt, const double o[3], const double d[3],
+                                            double zb, RtHit& hit) {
+    const int npl = rt->n_pl, ncy = rt->n_cy;
+    for (int i = 0; i < npl; ++i) {
+        double t;
+        if (plane_hit(rt->pl[i], o, d, zb, t)) {
+            hit.kind = 2;
+            hit.id = rt->pl[i].id;
+            hit.t = t;
+            zb = t;
+        }
+    }
+    for (int i = 0; i < ncy; ++i) {
+        double n[3];
+        const double t = icapped(rt->cy[i], o, d, n);
+        if (t < 0.0) continue;  // behind the camera (and misses)
+        if (t > zb) continue;   // behind a known intersection
+        hit.kind = 3;
+        hit.id = rt->cy[i].id;
+        hit.t = t;
+        hit.n[0] = n[0];
+        hit.n[1] = n[1];
+        hit.n[2] = n[2];
+        zb = t;
+    }
+}
+
 // ---- statistics (rtm_render_stats only; never in the timed kernels) ----
 __device__ __forceinline__ unsigned long long wave_sum(unsigned long long v) {
     for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
@@ -511,11 +624,13 @@ __device__ __forceinline__ void shadow_tile_sep(const ShadowPart& a, double* __r
 }
 
 // Eye tile: 64 x TILE_Y pixels: eye viewport rasterize (face FRONT, main.rs:1616)
-// + renderColorImage (main.rs:714-898).  FUSED evaluates the looked-up shadow
-// texel on demand from `sh` (same frame) instead of reading `smap`.
-template <bool FUSED, bool COUNT>
+// [+ processRaytracingRays when RT, main.rs:1035] + renderColorImage
+// (main.rs:714-898).  FUSED evaluates the looked-up shadow texel on demand from
+// `sh` (same frame) instead of reading `smap`.
+template <bool FUSED, bool COUNT, bool RT>
 __device__ __forceinline__ void eye_tile(const EyePart& a, const ShadowPart& sh, const double* __restrict__ smap,
-                                         float4* __restrict__ out, int bx, int by, StatsK* __restrict__ st) {
+                                         float4* __restrict__ out, int bx, int by, StatsK* __restrict__ st,
+                                         const RtK* __restrict__ rt) {
     const int xb = bx * TILE_X;
     const int xi = xb + (threadIdx.x & (TILE_X - 1));
     const int yl = __builtin_amdgcn_readfirstlane(by * TILE_Y + (threadIdx.x >> 6));
@@ -523,7 +638,7 @@ __device__ __forceinline__ void eye_tile(const EyePart& a, const ShadowPart& sh,
     const bool live = xi < a.W && yi < a.row_end;
     unsigned long long n_tests = 0, n_hit = 0, n_lit = 0;
     ShadowCounts sc;
-    int hit_id = -1;
+    int hit_kind = 0, hit_id = -1;
     if (live) {
         const double x = a.nx[xi];
         const double y = a.ny[yi];
@@ -544,24 +659,70 @@ __device__ __forceinline__ void eye_tile(const EyePart& a, const ShadowPart& sh,
                 }
             }
         }
-        float4 c = make_float4(0.0f, 0.2f, 0.2f, 1.0f);  // (0.0, 0.2, 0.2) as f32 (main.rs:718-720)
-        if (bid >= 0) {
-            const ShadeSphereK& s = a.shade[bid];
-            // calcDepth (main.rs:160-162)
-            const double depth = bz - bh * s.r;
-            double o[3], d[3];
+        RtHit hit;
+        hit.kind = bid >= 0 ? 1 : 0;
+        hit.id = bid;
+        double o[3], d[3];
+        if (RT) {
             cam_ray(a.eye, x, y, o, d);
-            // world position and normal (main.rs:744-752)
-            const double wx = o[0] + d[0] * depth, wy = o[1] + d[1] * depth, wz = o[2] + d[2] * depth;
-            const double nx = (wx - s.px) * s.inv_r, ny = (wy - s.py) * s.inv_r, nz = (wz - s.pz) * s.inv_r;
+            trace_pixel(rt, o, d, best, hit);
+        }
+        float4 c = make_float4(0.0f, 0.2f, 0.2f, 1.0f);  // (0.0, 0.2, 0.2) as f32 (main.rs:718-720)
+        if (hit.kind) {
+            if (!RT) cam_ray(a.eye, x, y, o, d);
+            // world position and normal per surface kind (main.rs:729-796)
+            double wx, wy, wz, nx, ny, nz, cr, cg, cb;
+            if (!RT || hit.kind == 1) {
+                const ShadeSphereK& s = a.shade[bid];
+                const double depth = bz - bh * s.r;  // calcDepth (main.rs:160-162)
+                wx = o[0] + d[0] * depth;
+                wy = o[1] + d[1] * depth;
+                wz = o[2] + d[2] * depth;
+                nx = (wx - s.px) * s.inv_r;
+                ny = (wy - s.py) * s.inv_r;
+                nz = (wz - s.pz) * s.inv_r;
+                cr = s.cr;
+                cg = s.cg;
+                cb = s.cb;
+            } else {
+                wx = o[0] + d[0] * hit.t;  // calcDepth = rayT (main.rs:166-171)
+                wy = o[1] + d[1] * hit.t;
+                wz = o[2] + d[2] * hit.t;
+                if (hit.kind == 2) {
+                    const PlaneK& p = rt->pl[hit.id];
+                    nx = p.nx;
+                    ny = p.ny;
+                    nz = p.nz;
+                    cr = p.cr;
+                    cg = p.cg;
+                    cb = p.cb;
+                } else {
+                    const CylK& q = rt->cy[hit.id];
+                    nx = hit.n[0];
+                    ny = hit.n[1];
+                    nz = hit.n[2];
+                    cr = q.cr;
+                    cg = q.cg;
+                    cb = q.cb;
+                }
+            }
             // light (1,0,0).scale(-1.0) (main.rs:810-813)
             const double Lx = 1.0 * -1.0, Ly = 0.0 * -1.0, Lz = 0.0 * -1.0;
             const double diffuse = fmax(nx * Lx + ny * Ly + nz * Lz, 0.0);
             // reflect(L, n) = L - n*(-2 dot(L,n))  (main.rs:2872-2875, sign as written)
             const double k2 = -2.0 * (Lx * nx + Ly * ny + Lz * nz);
             const double Rx = Lx - nx * k2, Ry = Ly - ny * k2, Rz = Lz - nz * k2;
-            // retViewDirOfPixel, ORTHOGONAL (main.rs:1984)
-            const double vx = a.eye.dir[0] * -1.0, vy = a.eye.dir[1] * -1.0, vz = a.eye.dir[2] * -1.0;
+            // retViewDirOfPixel (main.rs:1981-2013): -dir (ORTHOGONAL) or -normalize(ray) (PERSPECTIVE)
+            double vx, vy, vz;
+            if (!RT || a.eye.type == RTM_CAMERA_ORTHOGONAL) {
+                vx = a.eye.dir[0] * -1.0;
+                vy = a.eye.dir[1] * -1.0;
+                vz = a.eye.dir[2] * -1.0;
+            } else {
+                vx = d[0] * -1.0;
+                vy = d[1] * -1.0;
+                vz = d[2] * -1.0;
+            }
             double sp = fmax(vx * Rx + vy * Ry + vz * Rz, 0.0);
             sp = sp * sp;  // powi(32): five squarings (compiler-rt __powidf2)
             sp = sp * sp;
@@ -586,13 +747,14 @@ __device__ __forceinline__ void eye_tile(const EyePart& a, const ShadowPart& sh,
             const bool lit = dsm > qz - 0.0;
             const double lm = lit ? 1.0 : 0.25;
             const double base = diffuse + sp;
-            c.x = (float)((base * lm) * s.cr);
-            c.y = (float)((base * lm) * s.cg);
-            c.z = (float)((base * lm) * s.cb);
+            c.x = (float)((base * lm) * cr);
+            c.y = (float)((base * lm) * cg);
+            c.z = (float)((base * lm) * cb);
             if (COUNT) {
                 n_hit = 1;
                 n_lit = lit;
-                hit_id = bid;
+                hit_kind = hit.kind;
+                hit_id = hit.id;
             }
         }
         out[(int64_t)yl * a.W + xi] = c;
@@ -601,7 +763,11 @@ __device__ __forceinline__ void eye_tile(const EyePart& a, const ShadowPart& sh,
         stat_add(&st->eye_sphere_tests, n_tests);
         stat_add(&st->eye_hit_pixels, n_hit);
         stat_add(&st->lit_pixels, n_lit);
-        for (int i = 0; i < a.n_spheres; ++i) stat_add(&st->eye_hits[i], hit_id == i);
+        for (int i = 0; i < a.n_spheres; ++i) stat_add(&st->eye_hits[i], hit_kind == 1 && hit_id == i);
+        if (RT) {
+            stat_add(&st->eye_circle_plane_pixels, hit_kind == 2);
+            stat_add(&st->eye_capped_cylinder_pixels, hit_kind == 3);
+        }
         if (FUSED) {
             stat_add(&st->shadow_sphere_tests, sc.tests);
             stat_add(&st->march_iterations, sc.iters);
@@ -622,10 +788,20 @@ __global__ __launch_bounds__(BLOCK) void shadow_sep_kernel(const FrameArgs a, do
     shadow_tile_sep<NR, CMP>(a.sh, smap, blockIdx.x, blockIdx.y, diag);
 }
 
-template <bool FUSED, bool COUNT>
+template <bool FUSED, bool COUNT, bool RT>
 __global__ __launch_bounds__(BLOCK) void eye_pass_kernel(const FrameArgs a, const double* __restrict__ smap,
-                                                         float4* __restrict__ out, StatsK* __restrict__ st) {
-    eye_tile<FUSED, COUNT>(a.ey, a.sh, smap, out, blockIdx.x, blockIdx.y, st);
+                                                         float4* __restrict__ out, StatsK* __restrict__ st,
+                                                         const RtK* __restrict__ rt) {
+    eye_tile<FUSED, COUNT, RT>(a.ey, a.sh, smap, out, blockIdx.x, blockIdx.y, st, rt);
+}
+
+// launch_rt_upload: one 8-byte word per thread from the kernarg copy.
+__global__ void rt_upload_kernel(const RtK k, RtK* __restrict__ dst) {
+    constexpr int N = (int)(sizeof(RtK) / sizeof(uint64_t));
+    static_assert(sizeof(RtK) % sizeof(uint64_t) == 0, "RtK size");
+    const uint64_t* src = reinterpret_cast<const uint64_t*>(&k);
+    uint64_t* d = reinterpret_cast<uint64_t*>(dst);
+    for (int i = threadIdx.x; i < N; i += blockDim.x) d[i] = src[i];
 }
 
 // Timing diagnostic only (RTM_DIAG_EYE=1): the eye pass's stores without its work.
@@ -657,7 +833,7 @@ __global__ __launch_bounds__(BLOCK) void frame_pipe_kernel(const FrameArgs a, do
             shadow_tile_generic<false>(a.sh, smap_w, t % sh_gx, t / sh_gx, nullptr);
     } else {
         const int t = (int)(b - s_before);
-        eye_tile<false, false>(a.ey, a.sh, smap_r, out, t % eye_gx, t / eye_gx, nullptr);
+        eye_tile<false, false, false>(a.ey, a.sh, smap_r, out, t % eye_gx, t / eye_gx, nullptr, nullptr);
     }
 }
 
@@ -718,6 +894,30 @@ __global__ __launch_bounds__(BLOCK) void vp_march_kernel(const MarchArgs a, doub
     if (!(zb == z0)) zbuf[idx] = zb;
 }
 
+// Viewport::processRaytracingRays (main.rs:569-642) against the viewport's
+// current zBuffer / G-buffer.
+__global__ __launch_bounds__(BLOCK) void vp_trace_kernel(const TraceArgs a, double* __restrict__ zbuf,
+                                                         double* __restrict__ gh, int32_t* __restrict__ gid,
+                                                         double* __restrict__ gn) {
+    const int xi = blockIdx.x * TILE_X + (threadIdx.x & (TILE_X - 1));
+    const int yi = blockIdx.y * TILE_Y + (threadIdx.x >> 6);
+    if (xi >= a.W || yi >= a.H) return;
+    const int64_t idx = (int64_t)yi * a.W + xi;
+    double o[3], d[3];
+    cam_ray(a.cam, ndc(xi, a.W), ndc(yi, a.H), o, d);
+    RtHit hit;
+    hit.kind = 0;
+    hit.id = 0;
+    trace_pixel(a.rt, o, d, zbuf[idx], hit);
+    if (hit.kind) {
+        zbuf[idx] = hit.t;
+        gh[idx] = hit.t;
+        gid[idx] = (hit.kind == 2 ? GID_PLANE : GID_CYLINDER) | hit.id;
+        if (hit.kind == 3)
+            for (int k = 0; k < 3; ++k) gn[3 * idx + k] = hit.n[k];
+    }
+}
+
 // renderColorImage (main.rs:710-902) from a G-buffer.
 __global__ __launch_bounds__(BLOCK) void vp_shade_kernel(const ShadeArgs a, const double* __restrict__ szbuf,
                                                          const double* __restrict__ gh,
@@ -728,9 +928,9 @@ __global__ __launch_bounds__(BLOCK) void vp_shade_kernel(const ShadeArgs a, cons
     if (xi >= a.W || yi >= a.H) return;
     const int64_t idx = (int64_t)yi * a.W + xi;
     float4 c = make_float4(0.0f, 0.2f, 0.2f, 1.0f);
-    const int32_t id = gid[idx];
-    if (id >= 0) {
-        const ShadeSphereK& s = a.shade[id];
+    const int32_t g = gid[idx];
+    if (g >= 0) {
+        const int32_t kind = g >> 16, id = g & 0xFFFF;
         const double s01 = ndc(xi, a.W), u01 = ndc(yi, a.H);
         double o[3], d[3];
         cam_ray(a.eye, s01, u01, o, d);
@@ -740,9 +940,41 @@ __global__ __launch_bounds__(BLOCK) void vp_shade_kernel(const ShadeArgs a, cons
         } else {
             for (int k = 0; k < 3; ++k) view[k] = d[k] * -1.0;  // retViewDirOfPixel == -ray dir
         }
-        const double depth = gz[idx] - gh[idx] * s.r;
-        const double wx = o[0] + d[0] * depth, wy = o[1] + d[1] * depth, wz = o[2] + d[2] * depth;
-        const double nx = (wx - s.px) * s.inv_r, ny = (wy - s.py) * s.inv_r, nz = (wz - s.pz) * s.inv_r;
+        double wx, wy, wz, nx, ny, nz, cr, cg, cb;
+        if (kind == 0) {
+            const ShadeSphereK& s = a.shade[id];
+            const double depth = gz[idx] - gh[idx] * s.r;
+            wx = o[0] + d[0] * depth;
+            wy = o[1] + d[1] * depth;
+            wz = o[2] + d[2] * depth;
+            nx = (wx - s.px) * s.inv_r;
+            ny = (wy - s.py) * s.inv_r;
+            nz = (wz - s.pz) * s.inv_r;
+            cr = s.cr;
+            cg = s.cg;
+            cb = s.cb;
+        } else {
+            const double depth = gh[idx];  // rayT
+            wx = o[0] + d[0] * depth;
+            wy = o[1] + d[1] * depth;
+            wz = o[2] + d[2] * depth;
+            if (kind == 1) {
+                const PlaneK& p = a.rt->pl[id];
+                nx = p.nx;
+                ny = p.ny;
+                nz = p.nz;
+                cr = p.cr;
+                cg = p.cg;
+                cb = p.cb;
+            } else {
+                nx = a.gn[3 * idx];
+                ny = a.gn[3 * idx + 1];
+                nz = a.gn[3 * idx + 2];
+                cr = a.rt->cy[id].cr;
+                cg = a.rt->cy[id].cg;
+                cb = a.rt->cy[id].cb;
+            }
+        }
         const double Lx = 1.0 * -1.0, Ly = 0.0 * -1.0, Lz = 0.0 * -1.0;
         const double diffuse = fmax(nx * Lx + ny * Ly + nz * Lz, 0.0);
         const double k2 = -2.0 * (Lx * nx + Ly * ny + Lz * nz);
@@ -764,9 +996,9 @@ __global__ __launch_bounds__(BLOCK) void vp_shade_kernel(const ShadeArgs a, cons
         if (ty >= 0 && ty < a.Hs && tx >= 0 && tx < a.Ws) dsm = szbuf[ty * a.Ws + tx];
         const double lm = (dsm > qz - 0.0) ? 1.0 : 0.25;
         const double base = diffuse + sp;
-        c.x = (float)((base * lm) * s.cr);
-        c.y = (float)((base * lm) * s.cg);
-        c.z = (float)((base * lm) * s.cb);
+        c.x = (float)((base * lm) * cr);
+        c.y = (float)((base * lm) * cg);
+        c.z = (float)((base * lm) * cb);
     }
     out[idx] = c;
 }
@@ -858,7 +1090,8 @@ int launch_shadow_pass(const FrameArgs& a, double* smap, void* stream, StatsK* s
     return launched();
 }
 
-int launch_eye_pass(const FrameArgs& a, const double* smap, float* out, void* stream, StatsK* stats) {
+int launch_eye_pass(const FrameArgs& a, const double* smap, float* out, void* stream, StatsK* stats,
+                    const RtK* rt) {
     hipStream_t s = (hipStream_t)stream;
     dim3 g = grid_for(a.ey.W, a.ey.row_end - a.ey.row_begin);
     float4* o = reinterpret_cast<float4*>(out);
@@ -867,14 +1100,24 @@ int launch_eye_pass(const FrameArgs& a, const double* smap, float* out, void* st
         hipLaunchKernelGGL(eye_store_only_kernel, g, dim3(BLOCK), 0, s, a, o);
         return launched();
     }
-    if (fused && stats)
-        hipLaunchKernelGGL((eye_pass_kernel<true, true>), g, dim3(BLOCK), 0, s, a, smap, o, stats);
-    else if (fused)
-        hipLaunchKernelGGL((eye_pass_kernel<true, false>), g, dim3(BLOCK), 0, s, a, smap, o, stats);
-    else if (stats)
-        hipLaunchKernelGGL((eye_pass_kernel<false, true>), g, dim3(BLOCK), 0, s, a, smap, o, stats);
-    else
-        hipLaunchKernelGGL((eye_pass_kernel<false, false>), g, dim3(BLOCK), 0, s, a, smap, o, stats);
+#define RTM_EYE(F, C, R) hipLaunchKernelGGL((eye_pass_kernel<F, C, R>), g, dim3(BLOCK), 0, s, a, smap, o, stats, rt)
+    if (rt) {
+        if (fused && stats) RTM_EYE(true, true, true);
+        else if (fused) RTM_EYE(true, false, true);
+        else if (stats) RTM_EYE(false, true, true);
+        else RTM_EYE(false, false, true);
+    } else {
+        if (fused && stats) RTM_EYE(true, true, false);
+        else if (fused) RTM_EYE(true, false, false);
+        else if (stats) RTM_EYE(false, true, false);
+        else RTM_EYE(false, false, false);
+    }
+#undef RTM_EYE
+    return launched();
+}
+
+int launch_rt_upload(const RtK& k, RtK* dst, void* stream) {
+    hipLaunchKernelGGL(rt_upload_kernel, dim3(1), dim3(512), 0, (hipStream_t)stream, k, dst);
     return launched();
 }
 
@@ -919,6 +1162,11 @@ int launch_vp_shade(const ShadeArgs& a, const double* szbuf, const double* gh, c
                     float* out, void* stream) {
     hipLaunchKernelGGL(vp_shade_kernel, grid_for(a.W, a.H), dim3(BLOCK), 0, (hipStream_t)stream, a, szbuf, gh, gz,
                        gid, reinterpret_cast<float4*>(out));
+    return launched();
+}
+
+int launch_vp_trace(const TraceArgs& a, double* zbuf, double* gh, int32_t* gid, double* gn, void* stream) {
+    hipLaunchKernelGGL(vp_trace_kernel, grid_for(a.W, a.H), dim3(BLOCK), 0, (hipStream_t)stream, a, zbuf, gh, gid, gn);
     return launched();
 }
 

@@ -4,6 +4,7 @@ Reference surface (src/main.rs) -> this module:
     Viewport{rasterized, zBuffer, face, camera}   main.rs:426-439  -> Viewport
     Viewport::rasterize(&Scene)                   main.rs:445      -> Viewport.rasterize
     Viewport::processRaymarchingRays()            main.rs:551      -> Viewport.processRaymarchingRays
+    Viewport::processRaytracingRays(&Scene)       main.rs:569      -> Viewport.processRaytracingRays
     renderColorImage(&Scene,&Viewport,&Viewport)  main.rs:710      -> renderColorImage
     writeColorImage(&Map2d<Color32>, &path)       main.rs:660      -> writeColorImage / Context.write_ppm
     the whole two-viewport frame of a scene script (main.rs:1533-1628) -> render_frame / Context.render_async
@@ -192,6 +193,12 @@ class Viewport:
         sc, keep = scene.to_c()
         lib = _lib()
         abi.check(lib, lib.rtm_viewport_rasterize(self._h, C.byref(sc)), "rtm_viewport_rasterize")
+
+    def processRaytracingRays(self, scene: Scene):  # main.rs:569
+        sc, keep = scene.to_c()
+        lib = _lib()
+        abi.check(lib, lib.rtm_viewport_process_raytracing_rays(self._h, C.byref(sc)),
+                  "rtm_viewport_process_raytracing_rays")
 
     def processRaymarchingRays(self, patches=(REFERENCE_PATCH,), steps: int = REFERENCE_MARCH_STEPS):  # main.rs:551
         arr = (abi.rtm_patch * max(len(patches), 1))()

@@ -8,6 +8,7 @@ are on Linux) and passed to the device as data.
 from __future__ import annotations
 
 import ctypes as C
+import dataclasses
 import math
 from dataclasses import dataclass, field
 from typing import List
@@ -28,6 +29,25 @@ class PrimitiveSphere:  # main.rs:343-349
     shading: Shading
     pos: tuple
     r: float
+
+
+@dataclass
+class PrimitiveCirclePlane:  # main.rs:370-380
+    id: int
+    shading: Shading
+    radius: float
+    pos: tuple
+    n: tuple
+
+
+@dataclass
+class PrimitiveCappedCylinder:  # main.rs:382-391
+    id: int
+    shading: Shading
+    pA: tuple
+    pB: tuple
+    radiusA: float
+    radiusB: float
 
 
 @dataclass
@@ -74,9 +94,11 @@ class Camera:  # main.rs:1887-1898 (resolution comes from the viewport)
 
 
 @dataclass
-class Scene:  # main.rs:404-410 (spheres + implicit patches: the hot path's primitives)
+class Scene:  # main.rs:404-410 (+ the implicit patches the march path takes as data)
     spherePrimitives: List[PrimitiveSphere] = field(default_factory=list)
     patches: List[Bilinear] = field(default_factory=list)
+    circlePlanePrimitives: List[PrimitiveCirclePlane] = field(default_factory=list)
+    cappedCylinderPrimitives: List[PrimitiveCappedCylinder] = field(default_factory=list)
 
     def to_c(self):
         """Returns (rtm_scene, keepalive) — keep the second value alive while
@@ -92,12 +114,31 @@ class Scene:  # main.rs:404-410 (spheres + implicit patches: the hot path's prim
         for i, p in enumerate(self.patches):
             pat[i].a0, pat[i].b0 = float(p._0.a), float(p._0.b)
             pat[i].a1, pat[i].b1 = float(p._1.a), float(p._1.b)
+        npl, ncy = len(self.circlePlanePrimitives), len(self.cappedCylinderPrimitives)
+        pl = (abi.rtm_circle_plane * max(npl, 1))()
+        for i, q in enumerate(self.circlePlanePrimitives):
+            pl[i].id = int(q.id)
+            pl[i].pos[:] = [float(v) for v in q.pos]
+            pl[i].n[:] = [float(v) for v in q.n]
+            pl[i].radius = float(q.radius)
+            pl[i].color[:] = [float(q.shading.colorR), float(q.shading.colorG), float(q.shading.colorB)]
+        cy = (abi.rtm_capped_cylinder * max(ncy, 1))()
+        for i, q in enumerate(self.cappedCylinderPrimitives):
+            cy[i].id = int(q.id)
+            cy[i].pa[:] = [float(v) for v in q.pA]
+            cy[i].pb[:] = [float(v) for v in q.pB]
+            cy[i].ra, cy[i].rb = float(q.radiusA), float(q.radiusB)
+            cy[i].color[:] = [float(q.shading.colorR), float(q.shading.colorG), float(q.shading.colorB)]
         sc = abi.rtm_scene()
         sc.spheres = C.cast(sph, C.POINTER(abi.rtm_sphere))
         sc.patches = C.cast(pat, C.POINTER(abi.rtm_patch))
         sc.n_spheres = ns
         sc.n_patches = npch
-        return sc, (sph, pat)
+        sc.circle_planes = C.cast(pl, C.POINTER(abi.rtm_circle_plane))
+        sc.capped_cylinders = C.cast(cy, C.POINTER(abi.rtm_capped_cylinder))
+        sc.n_circle_planes = npl
+        sc.n_capped_cylinders = ncy
+        return sc, (sph, pat, pl, cy)
 
 
 # ---- cameras of the orthographic test scenes ----
@@ -174,3 +215,76 @@ CONFIGS = {
     5: dict(width=7680, height=4320, steps=128, scene=scene_b, flags=0,
             desc="7680x4320, 16 spheres + 2 implicits, 128 march steps"),
 }
+
+
+# ---- testscene_raytracingPlane0 (main.rs:910-1046): main()'s default scene ----
+def normalize(v) -> tuple:
+    """normalize (main.rs:105-108): v.scale(1.0 / |v|), |v| = sqrt((x*x + y*y) + z*z)."""
+    m = math.sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2])
+    inv = 1.0 / m
+    return (v[0] * inv, v[1] * inv, v[2] * inv)
+
+
+def perspective_eye_camera() -> Camera:
+    """viewport0's PERSPECTIVE camera at the origin looking along +z (main.rs:1016-1027)."""
+    return Camera(PERSPECTIVE, (0.0, 0.0, 0.0), (0.0, 0.0, 1.0), (0.0, 1.0, 0.0), (1.0, 0.0, 0.0))
+
+
+# the circle plane testscene_raytracingPlane0 has commented out (main.rs:916-929)
+REFERENCE_CIRCLE_PLANE = PrimitiveCirclePlane(0, Shading(0.02, 0.02, 1.0), 0.5, (0.01, 0.01, 2.0),
+                                              normalize((-1.0, 0.0, 1.0)))
+# its one capped cylinder (main.rs:931-943)
+REFERENCE_CAPPED_CYLINDER = PrimitiveCappedCylinder(0, Shading(1.0, 0.02, 0.02), (0.01, 10.01, 10.01),
+                                                    (0.01, 0.01, 10.01), 0.3, 0.2)
+# both shadow passes are commented out (main.rs:998-1003): the shadow map stays +INF
+RAYTRACING_FLAGS = abi.RTM_FLAG_NO_MARCH | abi.RTM_FLAG_NO_SHADOW_RASTER
+
+
+def raytracing_plane0(with_plane: bool = False) -> Scene:
+    """testscene_raytracingPlane0's scene: one capped cylinder (and, with
+    with_plane, the circle plane the reference has commented out).  Render with
+    perspective_eye_camera(), shadow_camera() and RAYTRACING_FLAGS."""
+    return Scene([], [], [dataclasses.replace(REFERENCE_CIRCLE_PLANE)] if with_plane else [],
+                 [dataclasses.replace(REFERENCE_CAPPED_CYLINDER)])
+
+
+_COLORS_R = [(1.0, 0.02, 0.02), (0.02, 0.02, 1.0), (0.2, 0.9, 0.2), (0.9, 0.9, 0.2), (0.9, 0.2, 0.9)]
+
+
+def scene_r_bench() -> Scene:
+    """Scene R-bench (row f-1 measurement, synthetic): the
+    reference's cylinder and circle plane plus a ring of 8 capped cylinders
+    around the view axis and 3 more discs, one a backdrop covering most of the
+    frame, so most eye rays test and hit several primitives."""
+    cyl = [dataclasses.replace(REFERENCE_CAPPED_CYLINDER)]
+    for i in range(8):
+        a = 2.0 * math.pi * i / 8.0
+        c = (1.5 * math.cos(a), 1.5 * math.sin(a), 5.0)
+        h = (0.4 * math.cos(a + 1.0), 0.4 * math.sin(a + 1.0), -0.8)
+        cyl.append(PrimitiveCappedCylinder(
+            i + 1, Shading(*_COLORS_R[i % 5]), (c[0] + h[0], c[1] + h[1], c[2] + h[2]),
+            (c[0] - h[0], c[1] - h[1], c[2] - h[2]), 0.25 + 0.05 * (i % 3), 0.15 + 0.05 * (i % 2)))
+    planes = [
+        dataclasses.replace(REFERENCE_CIRCLE_PLANE),
+        PrimitiveCirclePlane(1, Shading(0.9, 0.9, 0.2), 16.0, (0.0, 0.0, 12.0), normalize((0.2, 0.1, -1.0))),
+        PrimitiveCirclePlane(2, Shading(0.2, 0.9, 0.2), 1.2, (-1.5, -1.0, 7.0), normalize((0.5, 0.3, -1.0))),
+        PrimitiveCirclePlane(3, Shading(0.9, 0.2, 0.9), 0.9, (1.2, 1.4, 6.0), normalize((-0.4, -0.6, -1.0))),
+    ]
+    return Scene([], [], planes, cyl)
+
+
+def mixed_rt(frame: int = 100) -> Scene:
+    """Scene A-bench frame `frame` plus two circle planes and two capped cylinders
+    in front of the orthographic eye camera: ray-traced hits compete with
+    rasterized spheres in the eye zBuffer (main.rs:592, 633) and are shadowed by
+    the spheres + patch shadow map (tests only; parity of the mixed frame)."""
+    s = scene_a_bench(frame)
+    s.circlePlanePrimitives = [
+        PrimitiveCirclePlane(0, Shading(0.2, 0.9, 0.2), 0.4, (0.3, -0.3, 0.3), normalize((-1.0, 0.2, 0.1))),
+        PrimitiveCirclePlane(1, Shading(0.9, 0.9, 0.2), 0.25, (0.05, 0.35, -0.45), normalize((-1.0, -0.5, 0.3))),
+    ]
+    s.cappedCylinderPrimitives = [
+        PrimitiveCappedCylinder(0, Shading(0.9, 0.2, 0.9), (0.0, -0.6, -0.5), (0.2, 0.5, -0.3), 0.1, 0.15),
+        PrimitiveCappedCylinder(1, Shading(1.0, 0.02, 0.02), (-0.1, 0.1, 0.3), (0.5, 0.1, 0.9), 0.12, 0.12),
+    ]
+    return s

@@ -4,10 +4,12 @@
  * Drop-in boundary for the CPU render loop of PtrMan/2018RustRayTracer
  * (reference: src/main.rs).  The reference has no FFI; the seams this ABI
  * replaces are the three Rust calls its scene drivers make
- * (testscene_closelyOrbitingSphere, main.rs:1568-1628):
+ * (testscene_closelyOrbitingSphere, main.rs:1568-1628; testscene_raytracingPlane0,
+ * main.rs:1033-1045):
  *
  *   Viewport::rasterize(&mut self, &Scene)              main.rs:445-547
  *   Viewport::processRaymarchingRays(&mut self)         main.rs:551-565
+ *   Viewport::processRaytracingRays(&mut self, &Scene)  main.rs:569-642
  *   renderColorImage(&Scene, &Viewport, &Viewport)      main.rs:710-902
  *
  * Two API levels:
@@ -39,11 +41,13 @@
 extern "C" {
 #endif
 
-#define RTM_ABI_VERSION 1
+#define RTM_ABI_VERSION 2
 
 /* ---- limits: scene constants travel as kernel arguments (SGPR path) ---- */
 #define RTM_MAX_SPHERES 16
 #define RTM_MAX_PATCHES 4
+#define RTM_MAX_CIRCLE_PLANES 16
+#define RTM_MAX_CAPPED_CYLINDERS 16
 #define RTM_MAX_DIM 32768
 
 /* ---- status codes ---- */
@@ -93,14 +97,43 @@ typedef struct rtm_camera {
     double side[3]; /* sideNormalized */
 } rtm_camera;
 
-/* Scene (main.rs:404-410) restricted to the hot path: spheres + implicit patches.
- * The reference marches one hard-coded patch (main.rs:2024-2031); n_patches
- * patches are marched in order, each with a strict-min depth update (main.rs:559). */
+/* PrimitiveCirclePlane (main.rs:370-380): a disc of `radius` around `pos` in the
+ * plane through `pos` with normal `n`.  88 bytes. */
+typedef struct rtm_circle_plane {
+    int64_t id;      /* index into the circle-plane array: renderColorImage shades a hit with
+                        circlePlanePrimitives[id]'s colour and normal (main.rs:773-776) */
+    double pos[3];   /* pos: the disc centre (Plane.center, main.rs:578-581) */
+    double n[3];     /* n: plane normal, used as given (the scenes normalise it, main.rs:913-914) */
+    double radius;
+    double color[3]; /* shading colorR, colorG, colorB */
+} rtm_circle_plane;
+
+/* PrimitiveCappedCylinder (main.rs:382-391): a capped cone from pA (radius
+ * radiusA) to pB (radius radiusB), intersected by iCappedCone (main.rs:2889-2959). 96 bytes. */
+typedef struct rtm_capped_cylinder {
+    int64_t id;      /* index into the cylinder array (shading lookup, main.rs:791) */
+    double pa[3];    /* pA */
+    double pb[3];    /* pB */
+    double ra, rb;   /* radiusA, radiusB */
+    double color[3];
+} rtm_capped_cylinder;
+
+/* Scene (main.rs:404-410).  Spheres are rasterized and patches marched (the
+ * reference marches one hard-coded patch, main.rs:2024-2031; here n_patches
+ * patches are marched in order, each with a strict-min depth update, main.rs:559).
+ * Circle planes and capped cylinders are ray traced into the eye viewport after
+ * its rasterize (processRaytracingRays, main.rs:569-642); the reference never
+ * traces them into the shadow map (main.rs:998-1003).  ABI v2 added the last
+ * four fields. */
 typedef struct rtm_scene {
     const rtm_sphere* spheres;
     const rtm_patch* patches;
     int32_t n_spheres;
     int32_t n_patches;
+    const rtm_circle_plane* circle_planes;
+    const rtm_capped_cylinder* capped_cylinders;
+    int32_t n_circle_planes;
+    int32_t n_capped_cylinders;
 } rtm_scene;
 
 /* Per-call statistics (filled by rtm_render_stats on the GPU). */
@@ -113,6 +146,8 @@ typedef struct rtm_stats {
     int64_t march_iterations;          /* loop iterations executed by raymarchPatch, all texels/patches */
     int64_t march_hits;                /* texels*patches where the march returned Some(t) */
     int64_t march_in_range;            /* texels*patches whose start is inside the [0,1]^2 domain */
+    int64_t eye_circle_plane_pixels;   /* eye pixels whose front surface is a circle plane */
+    int64_t eye_capped_cylinder_pixels; /* ... a capped cylinder */
 } rtm_stats;
 
 /* ---- library ---- */
@@ -124,6 +159,9 @@ int32_t rtm_device_count(void);
 /* ---- context (one per device; owns the stream, the shadow map and events) ---- */
 typedef struct rtm_ctx rtm_ctx;
 int rtm_ctx_create(int32_t device, rtm_ctx** out);
+/* Drains the stream and frees the context.  Viewports created on it stay
+ * valid handles: every call on them then fails (RTM_ERR_INVALID) except
+ * rtm_viewport_destroy, which still frees them. */
 void rtm_ctx_destroy(rtm_ctx* ctx);
 /* hipStream_t the context enqueues on (as void*) */
 void* rtm_ctx_stream(rtm_ctx* ctx);
@@ -144,8 +182,12 @@ int rtm_ctx_kernel_ms_history(rtm_ctx* ctx, float* shadow_pass_ms, float* eye_pa
 
 /* ---- whole frame, host output (blocking) ----
  * Equivalent of: shadow viewport (ORTHO, face BACK, zBuffer=+INF) rasterize +
- * processRaymarchingRays; eye viewport (face FRONT) rasterize; renderColorImage
- * (main.rs:1568-1628).  out_rgba: width*height*4 floats. Uses a per-thread
+ * processRaymarchingRays; eye viewport (face FRONT) rasterize +
+ * processRaytracingRays; renderColorImage (main.rs:1568-1628, 1033-1045).
+ * Cameras: the shadow camera must be ORTHOGONAL (Camera::project asserts it,
+ * main.rs:1949); the eye camera may be PERSPECTIVE only in a scene without
+ * spheres (perspective sphere projection is BASELINE row f-3 ->
+ * RTM_ERR_UNSUPPORTED).  out_rgba: width*height*4 floats. Uses a per-thread
  * default context on device 0. */
 int rtm_render(const rtm_scene* scene, const rtm_camera* eye, const rtm_camera* shadow,
                int32_t width, int32_t height, int32_t march_steps, int32_t flags,
@@ -204,9 +246,14 @@ typedef struct rtm_viewport rtm_viewport;
 int rtm_viewport_create(rtm_ctx* ctx, int32_t width, int32_t height, int32_t face,
                         const rtm_camera* camera, rtm_viewport** out);
 void rtm_viewport_destroy(rtm_viewport* vp);
-/* Viewport::rasterize (main.rs:445): ORTHOGONAL cameras only (perspective
- * projection is BASELINE "next" row f-3 -> RTM_ERR_UNSUPPORTED). */
+/* Viewport::rasterize (main.rs:445): spheres need an ORTHOGONAL camera
+ * (perspective projection is BASELINE "next" row f-3 -> RTM_ERR_UNSUPPORTED);
+ * a scene without spheres is a no-op for either camera type. */
 int rtm_viewport_rasterize(rtm_viewport* vp, const rtm_scene* scene);
+/* Viewport::processRaytracingRays (main.rs:569-642): every pixel's camera ray
+ * against the circle planes, then the capped cylinders, in scene order; a hit
+ * with 0 <= t <= zBuffer replaces the pixel's surface and depth. */
+int rtm_viewport_process_raytracing_rays(rtm_viewport* vp, const rtm_scene* scene);
 /* Viewport::processRaymarchingRays (main.rs:551) generalised: the reference's
  * hard-coded patch {0.1,0.1,0.1,0.1} and 500 steps (main.rs:2024-2031) become
  * arguments; patches are marched in order. */

@@ -52,6 +52,11 @@ def lib():
         L.rtmo_viewport_read_zbuffer.argtypes = [P, C.POINTER(C.c_double)]
         L.rtmo_calc_ray_plane.restype = C.c_int
         L.rtmo_calc_ray_plane.argtypes = [C.POINTER(C.c_double)] * 4 + [C.POINTER(C.c_double)]
+        L.rtmo_viewport_process_raytracing_rays.restype = C.c_int
+        L.rtmo_viewport_process_raytracing_rays.argtypes = [P, C.POINTER(_abi.rtm_scene)]
+        L.rtmo_icapped_cone.restype = None
+        L.rtmo_icapped_cone.argtypes = [C.POINTER(C.c_double)] * 4 + [C.c_double, C.c_double,
+                                                                       C.POINTER(C.c_double)]
         L.rtmo_encode_scan.restype = C.c_int64
         L.rtmo_encode_scan.argtypes = [C.POINTER(C.c_float), C.c_int32]
         L.rtmo_write_ppm.restype = C.c_int64
@@ -102,6 +107,12 @@ class Viewport:
         if rc != 0:
             raise RuntimeError(f"rtmo_viewport_rasterize: {rc}")
 
+    def processRaytracingRays(self, scene):
+        sc, keep = scene.to_c()
+        rc = lib().rtmo_viewport_process_raytracing_rays(self._h, C.byref(sc))
+        if rc != 0:
+            raise RuntimeError(f"rtmo_viewport_process_raytracing_rays: {rc}")
+
     def processRaymarchingRays(self, patches, steps):
         arr = (_abi.rtm_patch * max(len(patches), 1))()
         for i, p in enumerate(patches):
@@ -135,6 +146,14 @@ def calc_ray_plane(origin, direction, plane_n, plane_center):
     t = C.c_double()
     ok = lib().rtmo_calc_ray_plane(*arrs, C.byref(t))
     return t.value if ok else None
+
+
+def icapped_cone(ro, rd, pa, pb, ra, rb):
+    """iCappedCone (main.rs:2889-2959): (t, (nx, ny, nz))."""
+    arrs = [(C.c_double * 3)(*map(float, v)) for v in (ro, rd, pa, pb)]
+    out = (C.c_double * 4)()
+    lib().rtmo_icapped_cone(*arrs, float(ra), float(rb), out)
+    return out[0], (out[1], out[2], out[3])
 
 
 def encode_rgb8(rgba):

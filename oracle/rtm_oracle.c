@@ -202,12 +202,18 @@ static double calcOthoDistanceByAbsPosition(const ProjectedSphere* s, Vec2 p) {
     return calcEllipseDistToCenter(rel, s->axisA, s->axisB);
 }
 
-/* G-buffer entry: Option<PixelSurfaceInfo::RasterizedSphere{relativeHeight,id,z}> (main.rs:136-150) */
+/* G-buffer entry: Option<PixelSurfaceInfo> (main.rs:136-150):
+ *   RasterizedSphere{relativeHeight, id, z}            kind GK_SPHERE
+ *   RaytracedCirlcePlaneIntersection{id, rayT}          kind GK_PLANE
+ *   RaytracedCappedCylinderIntersection{id, rayT, n}    kind GK_CYLINDER */
+enum { GK_SPHERE = 1, GK_PLANE = 2, GK_CYLINDER = 3 };
 typedef struct {
-    int32_t some;
+    int32_t some; /* kind, 0 = None */
     int64_t id;
     double relativeHeight;
     double z;
+    double rayT;
+    Vec3 n;
 } GEntry;
 
 typedef struct {
@@ -222,6 +228,7 @@ typedef struct {
     int64_t eye_hits[RTM_MAX_SPHERES];
     int64_t eye_hit_pixels, lit_pixels, eye_sphere_tests, shadow_sphere_tests;
     int64_t march_iterations, march_hits, march_in_range;
+    int64_t eye_circle_plane_pixels, eye_capped_cylinder_pixels;
 } Counts; /* layout == rtm_stats */
 
 /* rasterizeSphere (main.rs:249-331).  Pixel loop over rows [y0,y1).  The
@@ -265,7 +272,7 @@ static void rasterizeSphere(const ProjectedSphere* ps, double r, Viewport* vp, i
             double depth = calcZValueOfProjectedSphere(ps->z, relativeHeight * r, vp->face);
             int64_t idx = yi * vp->W + xi;
             if (depth < vp->zBuffer[idx]) {
-                vp->rasterized[idx].some = 1;
+                vp->rasterized[idx].some = GK_SPHERE;
                 vp->rasterized[idx].id = ps->id;
                 vp->rasterized[idx].relativeHeight = relativeHeight;
                 vp->rasterized[idx].z = ps->z;
@@ -275,9 +282,12 @@ static void rasterizeSphere(const ProjectedSphere* ps, double r, Viewport* vp, i
     }
 }
 
-/* Viewport::rasterize, ORTHOGONAL branch (main.rs:445-471, 540-542) over rows [y0,y1). */
+/* Viewport::rasterize, ORTHOGONAL branch (main.rs:445-471, 540-542) over rows [y0,y1).
+ * The PERSPECTIVE branch (main.rs:473-530, row f-3) is not restated: with no
+ * spheres it does nothing, otherwise RTM_ERR_UNSUPPORTED. */
 static int viewport_rasterize(Viewport* vp, const rtm_scene* scene, int flags, int64_t y0, int64_t y1,
                               int64_t* tests) {
+    if (scene->n_spheres == 0) return RTM_OK;
     if (vp->camera.type != RTM_CAMERA_ORTHOGONAL) return RTM_ERR_UNSUPPORTED;
     for (int32_t i = 0; i < scene->n_spheres; i++) {
         const rtm_sphere* s = &scene->spheres[i];
@@ -387,6 +397,117 @@ static void viewport_process_raymarching_rays(Viewport* vp, const rtm_patch* pat
 }
 
 /* ------------------------------------------------------------------ */
+/* L2 ray-traced primitives (row f-1: main.rs:569-642, 2390-2408, 2884-2974) */
+/* ------------------------------------------------------------------ */
+/* calcRayPlane (main.rs:2398-2408); returns 1 and *t on Some */
+static int calcRayPlane(Vec3 rayOrigin, Vec3 rayDir, Vec3 planeN, Vec3 planeCenter, double* t) {
+    double denom = dot(planeN, rayDir);
+    if (fabs(denom) > 0.0001) {
+        *t = dot(v3_sub(planeCenter, rayOrigin), planeN) / denom;
+        return 1;
+    }
+    return 0;
+}
+
+/* dot2 (main.rs:2884-2886), inversesqrt (main.rs:2963-2965), sign (main.rs:2967-2974) */
+static double dot2(Vec3 v) { return dot(v, v); }
+static double inversesqrt(double v) { return 1.0 / sqrt(v); }
+static double sign_of(double v) { return v >= 0.0 ? 1.0 : -1.0; }
+
+/* iCappedCone (main.rs:2889-2959; Inigo Quilez's capped-cone intersector
+ * restated in the reference's f64 operation order).  Returns (t, normal);
+ * t = -1 and normal = (-1,-1,-1) on a miss. */
+static double iCappedCone(Vec3 ro, Vec3 rd, Vec3 pa, Vec3 pb, double ra, double rb, Vec3* nOut) {
+    Vec3 ba = v3_sub(pb, pa);
+    Vec3 oa = v3_sub(ro, pa);
+    Vec3 ob = v3_sub(ro, pb);
+    double baba = dot(ba, ba);
+    double rdba = dot(rd, ba);
+    double oaba = dot(oa, ba);
+    double obba = dot(ob, ba);
+    /* caps */
+    if (oaba < 0.0) {
+        if (dot2(v3_sub(v3_scale(oa, rdba), v3_scale(rd, oaba))) < ra * ra * rdba * rdba) {
+            *nOut = v3_scale(ba, -inversesqrt(baba));
+            return -oaba / rdba;
+        }
+    } else if (obba > 0.0) {
+        double t = -obba / rdba;
+        if (dot2(v3_add(ob, v3_scale(rd, t))) < rb * rb) {
+            *nOut = v3_scale(ba, inversesqrt(baba));
+            return t;
+        }
+    }
+    /* body */
+    double rr = rb - ra;
+    double hy = baba + rr * rr;
+    Vec3 oc = v3_sub(v3_scale(oa, rb), v3_scale(ob, ra));
+    double ocba = dot(oc, ba);
+    double ocrd = dot(oc, rd);
+    double ococ = dot(oc, oc);
+    double k2 = baba * baba - hy * rdba * rdba;
+    double k1 = baba * baba * ocrd - hy * rdba * ocba;
+    double k0 = baba * baba * ococ - hy * ocba * ocba;
+    double h = k1 * k1 - k2 * k0;
+    if (h < 0.0) {
+        *nOut = v3(-1.0, -1.0, -1.0);
+        return -1.0;
+    }
+    double t = (-k1 - sign_of(rr) * sqrt(h)) / (k2 * rr);
+    double y = oaba + rdba * t;
+    if (y > 0.0 && y < baba) {
+        Vec3 insideNormalize = v3_sub(v3_scale(v3_sub(v3_scale(v3_add(oa, v3_scale(rd, t)), baba), v3_scale(ba, rr * ra)), baba),
+                                      v3_scale(ba, hy * y));
+        *nOut = normalize(insideNormalize);
+        return t;
+    }
+    *nOut = v3(-1.0, -1.0, -1.0);
+    return -1.0;
+}
+
+/* Viewport::processRaytracingRays (main.rs:569-642) over rows [y0,y1) */
+static void viewport_process_raytracing_rays(Viewport* vp, const rtm_scene* scene, int64_t y0, int64_t y1) {
+    for (int64_t yi = y0; yi < y1; yi++) {
+        for (int64_t xi = 0; xi < vp->W; xi++) {
+            Vec3 o, d;
+            calcRayOriginAndDirection(&vp->camera, xi, yi, &o, &d);
+            int64_t idx = yi * vp->W + xi;
+            for (int32_t i = 0; i < scene->n_circle_planes; i++) {
+                const rtm_circle_plane* pl = &scene->circle_planes[i];
+                Vec3 n = v3(pl->n[0], pl->n[1], pl->n[2]);
+                Vec3 c = v3(pl->pos[0], pl->pos[1], pl->pos[2]);
+                double t;
+                if (!calcRayPlane(o, d, n, c, &t)) continue;
+                if (t < 0.0) continue;                   /* behind the camera */
+                if (t > vp->zBuffer[idx]) continue;      /* behind a known intersection */
+                Vec3 p = v3_add(o, v3_scale(d, t));
+                double distance = v3_magnitude(v3_sub(p, c));
+                if (distance > pl->radius) continue;
+                GEntry* g = &vp->rasterized[idx];
+                g->some = GK_PLANE;
+                g->id = pl->id;
+                g->rayT = t;
+                vp->zBuffer[idx] = t;
+            }
+            for (int32_t i = 0; i < scene->n_capped_cylinders; i++) {
+                const rtm_capped_cylinder* cy = &scene->capped_cylinders[i];
+                Vec3 n;
+                double t = iCappedCone(o, d, v3(cy->pa[0], cy->pa[1], cy->pa[2]), v3(cy->pb[0], cy->pb[1], cy->pb[2]),
+                                       cy->ra, cy->rb, &n);
+                if (t < 0.0) continue;
+                if (t > vp->zBuffer[idx]) continue;
+                GEntry* g = &vp->rasterized[idx];
+                g->some = GK_CYLINDER;
+                g->id = cy->id;
+                g->rayT = t;
+                g->n = n;
+                vp->zBuffer[idx] = t;
+            }
+        }
+    }
+}
+
+/* ------------------------------------------------------------------ */
 /* L3 shading (main.rs:155-173, 709-902, 2872-2875)                    */
 /* ------------------------------------------------------------------ */
 /* reflect (main.rs:2872-2875) — sign-flipped as written */
@@ -401,15 +522,29 @@ static void renderColorImage(const rtm_scene* scene, const Viewport* vp, const V
             double r = 0.0, g = 0.2, b = 0.2;
             if (iPixel->some) {
                 Vec3 viewDir = retViewDirOfPixel(&vp->camera, ix, iy);
-                const rtm_sphere* prim = &scene->spheres[iPixel->id];
-                /* calcDepth (main.rs:155-165) */
-                double rMulHeight = iPixel->relativeHeight * prim->r;
-                double depth = calcZValueOfProjectedSphere(iPixel->z, rMulHeight, RTM_FACE_FRONT);
+                Vec3 worldPosition, normal;
+                const double* color;
                 Vec3 o, d;
                 calcRayOriginAndDirection(&vp->camera, ix, iy, &o, &d);
-                Vec3 worldPosition = v3_add(o, v3_scale(d, depth));
-                Vec3 diffOfPositionToCenter = v3_sub(worldPosition, v3(prim->pos[0], prim->pos[1], prim->pos[2]));
-                Vec3 normal = v3_scale(diffOfPositionToCenter, 1.0 / prim->r);
+                if (iPixel->some == GK_SPHERE) { /* main.rs:731-755 */
+                    const rtm_sphere* prim = &scene->spheres[iPixel->id];
+                    /* calcDepth (main.rs:155-165) */
+                    double rMulHeight = iPixel->relativeHeight * prim->r;
+                    double depth = calcZValueOfProjectedSphere(iPixel->z, rMulHeight, RTM_FACE_FRONT);
+                    worldPosition = v3_add(o, v3_scale(d, depth));
+                    Vec3 diffOfPositionToCenter = v3_sub(worldPosition, v3(prim->pos[0], prim->pos[1], prim->pos[2]));
+                    normal = v3_scale(diffOfPositionToCenter, 1.0 / prim->r);
+                    color = prim->color;
+                } else if (iPixel->some == GK_PLANE) { /* main.rs:761-777; calcDepth = rayT (main.rs:166-168) */
+                    worldPosition = v3_add(o, v3_scale(d, iPixel->rayT));
+                    const rtm_circle_plane* pl = &scene->circle_planes[iPixel->id];
+                    color = pl->color;
+                    normal = v3(pl->n[0], pl->n[1], pl->n[2]);
+                } else { /* main.rs:779-795; calcDepth = rayT (main.rs:169-171) */
+                    worldPosition = v3_add(o, v3_scale(d, iPixel->rayT));
+                    color = scene->capped_cylinders[iPixel->id].color;
+                    normal = iPixel->n;
+                }
 
                 Vec3 incommingLightDir = v3(1.0, 0.0, 0.0);
                 Vec3 invertedIncommingLightDir = v3_scale(incommingLightDir, -1.0);
@@ -431,12 +566,15 @@ static void renderColorImage(const rtm_scene* scene, const Viewport* vp, const V
                 int inLight = depthFromShadowMap > projectedPosition.z - bias;
                 if (!inLight) lightMagnitude = 0.25;
 
-                r = (diffuse + specularMagnitude) * lightMagnitude * prim->color[0];
-                g = (diffuse + specularMagnitude) * lightMagnitude * prim->color[1];
-                b = (diffuse + specularMagnitude) * lightMagnitude * prim->color[2];
+                r = (diffuse + specularMagnitude) * lightMagnitude * color[0];
+                g = (diffuse + specularMagnitude) * lightMagnitude * color[1];
+                b = (diffuse + specularMagnitude) * lightMagnitude * color[2];
                 if (cnt) {
                     cnt->eye_hit_pixels++;
-                    if (iPixel->id >= 0 && iPixel->id < RTM_MAX_SPHERES) cnt->eye_hits[iPixel->id]++;
+                    if (iPixel->some == GK_SPHERE && iPixel->id >= 0 && iPixel->id < RTM_MAX_SPHERES)
+                        cnt->eye_hits[iPixel->id]++;
+                    if (iPixel->some == GK_PLANE) cnt->eye_circle_plane_pixels++;
+                    if (iPixel->some == GK_CYLINDER) cnt->eye_capped_cylinder_pixels++;
                     if (inLight) cnt->lit_pixels++;
                 }
             }
@@ -458,6 +596,15 @@ static int validate_scene(const rtm_scene* scene) {
     if (scene->n_patches > 0 && !scene->patches) return RTM_ERR_INVALID;
     for (int32_t i = 0; i < scene->n_spheres; i++)
         if (scene->spheres[i].id < 0 || scene->spheres[i].id >= scene->n_spheres) return RTM_ERR_INVALID;
+    if (scene->n_circle_planes < 0 || scene->n_capped_cylinders < 0) return RTM_ERR_INVALID;
+    if (scene->n_circle_planes > 0 && !scene->circle_planes) return RTM_ERR_INVALID;
+    if (scene->n_capped_cylinders > 0 && !scene->capped_cylinders) return RTM_ERR_INVALID;
+    for (int32_t i = 0; i < scene->n_circle_planes; i++)
+        if (scene->circle_planes[i].id < 0 || scene->circle_planes[i].id >= scene->n_circle_planes)
+            return RTM_ERR_INVALID;
+    for (int32_t i = 0; i < scene->n_capped_cylinders; i++)
+        if (scene->capped_cylinders[i].id < 0 || scene->capped_cylinders[i].id >= scene->n_capped_cylinders)
+            return RTM_ERR_INVALID;
     return RTM_OK;
 }
 
@@ -488,7 +635,8 @@ int rtmo_render(const rtm_scene* scene, const rtm_camera* eye, const rtm_camera*
     int rc = validate_scene(scene);
     if (rc) return rc;
     if (!eye || !shadow || !out_rgba || W <= 0 || H <= 0 || steps < 0) return RTM_ERR_INVALID;
-    if (eye->type != RTM_CAMERA_ORTHOGONAL || shadow->type != RTM_CAMERA_ORTHOGONAL) return RTM_ERR_UNSUPPORTED;
+    if (shadow->type != RTM_CAMERA_ORTHOGONAL) return RTM_ERR_UNSUPPORTED;
+    if (eye->type != RTM_CAMERA_ORTHOGONAL && scene->n_spheres > 0) return RTM_ERR_UNSUPPORTED;
     Viewport vs, ve;
     viewport_init(&vs, W, H, RTM_FACE_BACK, shadow);
     viewport_init(&ve, W, H, RTM_FACE_FRONT, eye);
@@ -515,6 +663,7 @@ int rtmo_render(const rtm_scene* scene, const rtm_camera* eye, const rtm_camera*
                     viewport_process_raymarching_rays(&vs, scene->patches, scene->n_patches, steps, y0, y1, &c);
             } else if (pass == 1) {
                 viewport_rasterize(&ve, scene, flags, y0, y1, &c.eye_sphere_tests);
+                viewport_process_raytracing_rays(&ve, scene, y0, y1);
             } else {
                 renderColorImage(scene, &ve, &vs, out_rgba, y0, y1, &c);
             }
@@ -560,6 +709,13 @@ int rtmo_viewport_rasterize(rtmo_viewport* v, const rtm_scene* scene, int32_t fl
     return viewport_rasterize(&v->vp, scene, flags, 0, v->vp.H, NULL);
 }
 
+int rtmo_viewport_process_raytracing_rays(rtmo_viewport* v, const rtm_scene* scene) {
+    int rc = validate_scene(scene);
+    if (rc) return rc;
+    viewport_process_raytracing_rays(&v->vp, scene, 0, v->vp.H);
+    return RTM_OK;
+}
+
 int rtmo_viewport_process_raymarching_rays(rtmo_viewport* v, const rtm_patch* patches, int32_t n, int32_t steps) {
     if (n < 0 || (n > 0 && !patches) || steps < 0) return RTM_ERR_INVALID;
     viewport_process_raymarching_rays(&v->vp, patches, n, steps, 0, v->vp.H, NULL);
@@ -581,20 +737,24 @@ int rtmo_viewport_read_zbuffer(const rtmo_viewport* v, double* out) {
     return RTM_OK;
 }
 
-/* ---- row f-1 helpers, pinned by the reference's own unit test ---- */
+/* ---- row f-1 helpers (calcRayPlane is pinned by the reference's own unit test) ---- */
 /* calcRayPlane (main.rs:2398-2408); returns 1 and *t on Some */
 int rtmo_calc_ray_plane(const double origin[3], const double dir[3], const double plane_n[3],
                         const double plane_center[3], double* t) {
-    Vec3 n = v3(plane_n[0], plane_n[1], plane_n[2]);
-    Vec3 d = v3(dir[0], dir[1], dir[2]);
-    double denom = dot(n, d);
-    if (fabs(denom) > 0.0001) {
-        Vec3 c = v3(plane_center[0], plane_center[1], plane_center[2]);
-        Vec3 o = v3(origin[0], origin[1], origin[2]);
-        *t = dot(v3_sub(c, o), n) / denom;
-        return 1;
-    }
-    return 0;
+    return calcRayPlane(v3(origin[0], origin[1], origin[2]), v3(dir[0], dir[1], dir[2]),
+                        v3(plane_n[0], plane_n[1], plane_n[2]), v3(plane_center[0], plane_center[1], plane_center[2]), t);
+}
+
+/* iCappedCone (main.rs:2889-2959): out4 = (t, n.x, n.y, n.z) */
+void rtmo_icapped_cone(const double ro[3], const double rd[3], const double pa[3], const double pb[3], double ra,
+                       double rb, double out4[4]) {
+    Vec3 n;
+    double t = iCappedCone(v3(ro[0], ro[1], ro[2]), v3(rd[0], rd[1], rd[2]), v3(pa[0], pa[1], pa[2]),
+                           v3(pb[0], pb[1], pb[2]), ra, rb, &n);
+    out4[0] = t;
+    out4[1] = n.x;
+    out4[2] = n.y;
+    out4[3] = n.z;
 }
 
 

@@ -62,6 +62,45 @@ def overlapping():
     return [(0, (0.0, 0.0, 0.0), 0.5, (0.02, 0.02, 1.0)), (1, (0.0, 0.0, 0.5), 0.5, (1.0, 1.0, 1.0))], []
 
 
+# ---- row f-1: testscene_raytracingPlane0 (main.rs:910-1046) ----
+PERSP_CAM = dict(type=1, pos=(0.0, 0.0, 0.0), dir=(0.0, 0.0, 1.0), up=(0.0, 1.0, 0.0), side=(1.0, 0.0, 0.0))
+
+
+def _normalize(v):
+    m = math.sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2])
+    inv = 1.0 / m
+    return (v[0] * inv, v[1] * inv, v[2] * inv)
+
+
+# (id, pos, n, radius, color) / (id, pA, pB, ra, rb, color)
+REF_PLANE = (0, (0.01, 0.01, 2.0), _normalize((-1.0, 0.0, 1.0)), 0.5, (0.02, 0.02, 1.0))
+REF_CYL = (0, (0.01, 10.01, 10.01), (0.01, 0.01, 10.01), 0.3, 0.2, (1.0, 0.02, 0.02))
+
+
+def rbench():
+    cols = [(1.0, 0.02, 0.02), (0.02, 0.02, 1.0), (0.2, 0.9, 0.2), (0.9, 0.9, 0.2), (0.9, 0.2, 0.9)]
+    cyl = [REF_CYL]
+    for i in range(8):
+        a = 2.0 * math.pi * i / 8.0
+        c = (1.5 * math.cos(a), 1.5 * math.sin(a), 5.0)
+        h = (0.4 * math.cos(a + 1.0), 0.4 * math.sin(a + 1.0), -0.8)
+        cyl.append((i + 1, (c[0] + h[0], c[1] + h[1], c[2] + h[2]), (c[0] - h[0], c[1] - h[1], c[2] - h[2]),
+                    0.25 + 0.05 * (i % 3), 0.15 + 0.05 * (i % 2), cols[i % 5]))
+    planes = [REF_PLANE,
+              (1, (0.0, 0.0, 12.0), _normalize((0.2, 0.1, -1.0)), 16.0, (0.9, 0.9, 0.2)),
+              (2, (-1.5, -1.0, 7.0), _normalize((0.5, 0.3, -1.0)), 1.2, (0.2, 0.9, 0.2)),
+              (3, (1.2, 1.4, 6.0), _normalize((-0.4, -0.6, -1.0)), 0.9, (0.9, 0.2, 0.9))]
+    return planes, cyl
+
+
+# ray-traced primitives seen by the orthographic eye camera of the orbit scene
+# (a disc and a cone crossing the spheres' depth range; same as tests' scenes.mixed_rt)
+MIXED_PLANES = [(0, (0.3, -0.3, 0.3), _normalize((-1.0, 0.2, 0.1)), 0.4, (0.2, 0.9, 0.2)),
+                (1, (0.05, 0.35, -0.45), _normalize((-1.0, -0.5, 0.3)), 0.25, (0.9, 0.9, 0.2))]
+MIXED_CYLS = [(0, (0.0, -0.6, -0.5), (0.2, 0.5, -0.3), 0.1, 0.15, (0.9, 0.2, 0.9)),
+              (1, (-0.1, 0.1, 0.3), (0.5, 0.1, 0.9), 0.12, 0.12, (1.0, 0.02, 0.02))]
+
+
 # ---------------- restatement ----------------
 def signum(v):  # Rust f64::signum
     return np.where(np.isnan(v), v, np.copysign(1.0, v))
@@ -76,6 +115,86 @@ def grid(W, H):
 
 def dot(a, b):
     return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]
+
+
+def rays(cam, W, H):
+    """Camera::calcRayOriginAndDirection (main.rs:1902-1942) for every pixel."""
+    s, u = grid(W, H)
+    if cam["type"] == 0:
+        o = [(cam["pos"][k] + cam["side"][k] * s) + cam["up"][k] * u for k in range(3)]
+        d = [np.full(s.shape, cam["dir"][k]) for k in range(3)]
+    else:
+        v = [(cam["dir"][k] + cam["side"][k] * (s * 1.0)) + cam["up"][k] * (u * 1.0) for k in range(3)]
+        m = np.sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2])
+        inv = 1.0 / m
+        o = [np.full(s.shape, cam["pos"][k]) for k in range(3)]
+        d = [v[k] * inv for k in range(3)]
+    return o, d
+
+
+def icapped_cone(ro, rd, pa, pb, ra, rb):
+    """iCappedCone (main.rs:2889-2959) vectorised; branches become masks."""
+    with np.errstate(all="ignore"):
+        ba = [pb[k] - pa[k] for k in range(3)]
+        oa = [ro[k] - pa[k] for k in range(3)]
+        ob = [ro[k] - pb[k] for k in range(3)]
+        baba = dot(ba, ba)
+        rdba = dot(rd, ba)
+        oaba = dot(oa, ba)
+        obba = dot(ob, ba)
+        isq = 1.0 / math.sqrt(baba)
+        w = [oa[k] * rdba - rd[k] * oaba for k in range(3)]
+        capA = (oaba < 0.0) & (dot(w, w) < ra * ra * rdba * rdba)
+        tA = -oaba / rdba
+        tB = -obba / rdba
+        w = [ob[k] + rd[k] * tB for k in range(3)]
+        capB = ~(oaba < 0.0) & (obba > 0.0) & (dot(w, w) < rb * rb)
+        rr = rb - ra
+        hy = baba + rr * rr
+        oc = [oa[k] * rb - ob[k] * ra for k in range(3)]
+        ocba, ocrd, ococ = dot(oc, ba), dot(oc, rd), dot(oc, oc)
+        k2 = baba * baba - hy * rdba * rdba
+        k1 = baba * baba * ocrd - hy * rdba * ocba
+        k0 = baba * baba * ococ - hy * ocba * ocba
+        h = k1 * k1 - k2 * k0
+        sg = 1.0 if rr >= 0.0 else -1.0
+        tb = (-k1 - sg * np.sqrt(np.where(h < 0.0, 0.0, h))) / (k2 * rr)
+        y = oaba + rdba * tb
+        body = ~capA & ~capB & ~(h < 0.0) & (y > 0.0) & (y < baba)
+        inside = [((oa[k] + rd[k] * tb) * baba - ba[k] * (rr * ra)) * baba - ba[k] * (hy * y) for k in range(3)]
+        m = np.sqrt(inside[0] * inside[0] + inside[1] * inside[1] + inside[2] * inside[2])
+        inv = 1.0 / m
+        nb = [inside[k] * inv for k in range(3)]
+        t = np.where(capA, tA, np.where(capB, tB, np.where(body, tb, -1.0)))
+        n = [np.where(capA, ba[k] * -isq, np.where(capB, ba[k] * isq, np.where(body, nb[k], -1.0)))
+             for k in range(3)]
+    return t, n
+
+
+def raytrace(cam, planes, cyls, W, H, zbuf, g):
+    """processRaytracingRays (main.rs:569-642): planes then cylinders, in order."""
+    o, d = rays(cam, W, H)
+    with np.errstate(all="ignore"):
+        for (pid, c, n, radius, _col) in planes:
+            denom = dot(n, d)
+            t = dot([c[k] - o[k] for k in range(3)], n) / denom
+            P = [o[k] + d[k] * t for k in range(3)]
+            q = [P[k] - c[k] for k in range(3)]
+            dist = np.sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2])
+            win = (np.abs(denom) > 0.0001) & ~(t < 0.0) & ~(t > zbuf) & ~(dist > radius)
+            zbuf[win] = t[win]
+            g["kind"][win] = 2
+            g["id"][win] = pid
+            g["t"][win] = t[win]
+        for (cid, pa, pb, ra, rb, _col) in cyls:
+            t, n = icapped_cone(o, d, pa, pb, ra, rb)
+            win = ~(t < 0.0) & ~(t > zbuf)
+            zbuf[win] = t[win]
+            g["kind"][win] = 3
+            g["id"][win] = cid
+            g["t"][win] = t[win]
+            for k in range(3):
+                g["n%d" % k][win] = n[k][win]
 
 
 def rasterize(cam, spheres, W, H, face, zbuf, gbuf):
@@ -101,6 +220,7 @@ def rasterize(cam, spheres, W, H, face, zbuf, gbuf):
         win = cov & (depth < zbuf)
         zbuf[win] = depth[win]
         if gbuf is not None:
+            gbuf["kind"][win] = 1
             gbuf["id"][win] = sid
             gbuf["h"][win] = h[win]
             gbuf["z"][win] = z
@@ -139,39 +259,52 @@ def march(cam, patches, W, H, steps, zbuf):
         zbuf[upd] = hit_t[upd]
 
 
-def render(spheres, patches, W, H, steps, no_march=False, no_sraster=False):
+def render(spheres, patches, W, H, steps, no_march=False, no_sraster=False, planes=(), cyls=(), eye=EYE_CAM):
     zs = np.full((H, W), np.inf)
     if not no_sraster:
         rasterize(SHADOW_CAM, spheres, W, H, 1, zs, None)
     if not no_march:
         march(SHADOW_CAM, patches, W, H, steps, zs)
     ze = np.full((H, W), np.inf)
-    g = dict(id=np.full((H, W), -1, np.int64), h=np.zeros((H, W)), z=np.zeros((H, W)))
-    rasterize(EYE_CAM, spheres, W, H, 0, ze, g)
+    g = dict(kind=np.zeros((H, W), np.int64), id=np.full((H, W), -1, np.int64), h=np.zeros((H, W)),
+             z=np.zeros((H, W)), t=np.zeros((H, W)), n0=np.zeros((H, W)), n1=np.zeros((H, W)),
+             n2=np.zeros((H, W)))
+    if spheres:
+        assert eye["type"] == 0
+        rasterize(eye, spheres, W, H, 0, ze, g)
+    raytrace(eye, planes, cyls, W, H, ze, g)
     # renderColorImage (main.rs:710-902)
     img = np.zeros((H, W, 4), np.float32)
     img[..., 1] = np.float32(0.2)
     img[..., 2] = np.float32(0.2)
     img[..., 3] = 1.0
-    hit = g["id"] >= 0
+    hit = g["kind"] > 0
     if hit.any():
+        kind = g["kind"][hit]
         ids = g["id"][hit]
-        prm = {sid: (pos, r, col) for (sid, pos, r, col) in spheres}
-        R = np.array([prm[i][1] for i in ids])
-        P = np.array([prm[i][0] for i in ids])
-        COL = np.array([prm[i][2] for i in ids])
-        depth = g["z"][hit] - g["h"][hit] * R
-        s, u = grid(W, H)
-        s, u = s[hit], u[hit]
-        cam = EYE_CAM
-        o = [(cam["pos"][k] + cam["side"][k] * s) + cam["up"][k] * u for k in range(3)]
-        wp = [o[k] + cam["dir"][k] * depth for k in range(3)]
-        n = [(wp[k] - P[:, k]) * (1.0 / R) for k in range(3)]
+        o, d = rays(eye, W, H)
+        o, d = [a[hit] for a in o], [a[hit] for a in d]
+        sprm = {sid: (pos, r, col) for (sid, pos, r, col) in spheres}
+        pprm = {pid: (n, col) for (pid, _c, n, _r, col) in planes}
+        cprm = {cid: col for (cid, _a, _b, _ra, _rb, col) in cyls}
+        sph = kind == 1
+        R = np.array([sprm[i][1] if k == 1 else 1.0 for i, k in zip(ids, kind)])
+        P = np.array([sprm[i][0] if k == 1 else (0.0, 0.0, 0.0) for i, k in zip(ids, kind)]).reshape(-1, 3)
+        COL = np.array([sprm[i][2] if k == 1 else pprm[i][1] if k == 2 else cprm[i]
+                        for i, k in zip(ids, kind)]).reshape(-1, 3)
+        # calcDepth (main.rs:155-173)
+        depth = np.where(sph, g["z"][hit] - g["h"][hit] * R, g["t"][hit])
+        wp = [o[k] + d[k] * depth for k in range(3)]
+        PN = np.array([pprm[i][0] if k == 2 else (0.0, 0.0, 0.0) for i, k in zip(ids, kind)]).reshape(-1, 3)
+        n = [np.where(sph, (wp[k] - P[:, k]) * (1.0 / R), np.where(kind == 2, PN[:, k], g["n%d" % k][hit]))
+             for k in range(3)]
+        cam = eye
         L = (1.0 * -1.0, 0.0 * -1.0, 0.0 * -1.0)
         diffuse = np.fmax(n[0] * L[0] + n[1] * L[1] + n[2] * L[2], 0.0)
         k2 = -2.0 * (L[0] * n[0] + L[1] * n[1] + L[2] * n[2])
         Rv = [L[k] - n[k] * k2 for k in range(3)]
-        view = [cam["dir"][k] * -1.0 for k in range(3)]
+        # retViewDirOfPixel (main.rs:1981-2013)
+        view = [cam["dir"][k] * -1.0 for k in range(3)] if cam["type"] == 0 else [d[k] * -1.0 for k in range(3)]
         sp = np.fmax(view[0] * Rv[0] + view[1] * Rv[1] + view[2] * Rv[2], 0.0)
         with np.errstate(over="ignore"):
             for _ in range(5):
@@ -198,9 +331,14 @@ def render(spheres, patches, W, H, steps, no_march=False, no_sraster=False):
             img[hit, 0] = ((base * lm) * COL[:, 0]).astype(np.float32)
             img[hit, 1] = ((base * lm) * COL[:, 1]).astype(np.float32)
             img[hit, 2] = ((base * lm) * COL[:, 2]).astype(np.float32)
-        stats = dict(eye_hits=[int((ids == i).sum()) for i in range(len(spheres))], lit=int(lit.sum()))
+        stats = dict(eye_hits=[int(((ids == i) & sph).sum()) for i in range(len(spheres))], lit=int(lit.sum()))
+        if planes or cyls:
+            stats["plane_px"] = int((kind == 2).sum())
+            stats["cyl_px"] = int((kind == 3).sum())
     else:
         stats = dict(eye_hits=[0] * len(spheres), lit=0)
+        if planes or cyls:
+            stats["plane_px"] = stats["cyl_px"] = 0
     return img, zs, stats
 
 
@@ -228,6 +366,19 @@ CASES = [
     ("sceneb_640x360_k128", scene_b, 640, 360, 128, 0, False),
 ]
 
+# row f-1 cases: (name, spheres, patches, planes, cyls, eye, W, H, steps, flags, small)
+RT_CASES = [
+    ("rt_plane0_64", [], [], [], [REF_CYL], PERSP_CAM, 64, 64, 0, 3, True),
+    ("rt_plane0_withplane_96x80", [], [], [REF_PLANE], [REF_CYL], PERSP_CAM, 96, 80, 0, 3, True),
+    ("rt_rbench_128x72", [], [], *rbench(), PERSP_CAM, 128, 72, 0, 3, True),
+    ("rt_mixed_orbit_96", *orbit_scene(100, [BENCH_PATCH]), MIXED_PLANES, MIXED_CYLS, EYE_CAM, 96, 96, 64, 0, True),
+    ("rt_plane0_512", [], [], [], [REF_CYL], PERSP_CAM, 512, 512, 0, 3, False),
+    ("rt_plane0_withplane_512", [], [], [REF_PLANE], [REF_CYL], PERSP_CAM, 512, 512, 0, 3, False),
+    ("rt_rbench_640x360", [], [], *rbench(), PERSP_CAM, 640, 360, 0, 3, False),
+    ("rt_mixed_orbit_320x180", *orbit_scene(100, [BENCH_PATCH]), MIXED_PLANES, MIXED_CYLS, EYE_CAM, 320, 180, 64,
+     0, False),
+]
+
 
 def main():
     # pin against SURVEY.md §8c-3 before writing anything
@@ -246,6 +397,16 @@ def main():
         img, zs, st = render(sph, pat, W, H, K, no_march=bool(flags & 1), no_sraster=bool(flags & 2))
         golden[name] = dict(width=W, height=H, steps=K, flags=flags, rgba_sha256=sha_full(img),
                             shadow_sha256=sha_full(zs), eye_hits=st["eye_hits"], lit_pixels=st["lit"])
+        if small:
+            fixtures[name + "__rgba"] = img
+            fixtures[name + "__shadow"] = zs
+        print(name, golden[name]["rgba_sha256"][:16], st)
+    for name, sph, pat, planes, cyls, eye, W, H, K, flags, small in RT_CASES:
+        img, zs, st = render(sph, pat, W, H, K, no_march=bool(flags & 1), no_sraster=bool(flags & 2),
+                             planes=planes, cyls=cyls, eye=eye)
+        golden[name] = dict(width=W, height=H, steps=K, flags=flags, rgba_sha256=sha_full(img),
+                            shadow_sha256=sha_full(zs), eye_hits=st["eye_hits"], lit_pixels=st["lit"],
+                            circle_plane_pixels=st["plane_px"], capped_cylinder_pixels=st["cyl_px"])
         if small:
             fixtures[name + "__rgba"] = img
             fixtures[name + "__shadow"] = zs

@@ -42,7 +42,35 @@ def test_struct_sizes(rtm):
     assert C.sizeof(abi.rtm_sphere) == 64
     assert C.sizeof(abi.rtm_camera) == 104
     assert C.sizeof(abi.rtm_patch) == 32
-    assert C.sizeof(abi.rtm_scene) == 24
+    assert C.sizeof(abi.rtm_circle_plane) == 88
+    assert C.sizeof(abi.rtm_capped_cylinder) == 96
+    assert C.sizeof(abi.rtm_scene) == 48
+
+
+def test_struct_layout_matches_header(rtm, tmp_path):
+    """Every ctypes struct's size and field offsets == the C compiler's view of include/rtm.h."""
+    import subprocess
+    abi = rtm.abi
+    structs = [abi.rtm_sphere, abi.rtm_patch, abi.rtm_camera, abi.rtm_circle_plane, abi.rtm_capped_cylinder,
+               abi.rtm_scene, abi.rtm_stats]
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "rtm.h"', "int main(void) {"]
+    for st in structs:
+        n = st.__name__
+        lines.append(f'printf("{n} %zu\\n", sizeof({n}));')
+        for f, _ in st._fields_:
+            lines.append(f'printf("{n}.{f} %zu\\n", offsetof({n}, {f}));')
+    lines.append("return 0; }")
+    src = tmp_path / "probe.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "probe"
+    subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
+    got = dict(l.split() for l in subprocess.run([str(exe)], check=True, capture_output=True,
+                                                   text=True).stdout.splitlines())
+    for st in structs:
+        n = st.__name__
+        assert int(got[n]) == C.sizeof(st), n
+        for f, _ in st._fields_:
+            assert int(got[f"{n}.{f}"]) == getattr(st, f).offset, (n, f)
 
 
 def test_abi_version_and_device_count(rtm):

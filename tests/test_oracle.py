@@ -17,6 +17,19 @@ def sha16(img):
     return hashlib.sha256(np.ascontiguousarray(img[:, :, :3]).tobytes()).hexdigest()[:16]
 
 
+def _case(scenes, name):
+    """(scene, eye camera) of a golden case."""
+    if name.startswith("rt_plane0_withplane"):
+        return scenes.raytracing_plane0(True), scenes.perspective_eye_camera()
+    if name.startswith("rt_plane0"):
+        return scenes.raytracing_plane0(), scenes.perspective_eye_camera()
+    if name.startswith("rt_rbench"):
+        return scenes.scene_r_bench(), scenes.perspective_eye_camera()
+    if name.startswith("rt_mixed_orbit"):
+        return scenes.mixed_rt(100), scenes.eye_camera()
+    return _scene_for(scenes, name), scenes.eye_camera()
+
+
 def _scene_for(scenes, name):
     if name.startswith("orbit_f0"):
         return scenes.closely_orbiting_sphere(0)
@@ -63,12 +76,16 @@ def _golden():
 @pytest.mark.parametrize("name", sorted(_golden().keys()))
 def test_oracle_matches_golden(oracle, scenes, name):
     g = _golden()[name]
-    r = oracle.render(_scene_for(scenes, name), scenes.eye_camera(), scenes.shadow_camera(), g["width"],
-                      g["height"], g["steps"], g["flags"], nthreads=4, want_shadow=True, want_stats=True)
+    scene, eye = _case(scenes, name)
+    r = oracle.render(scene, eye, scenes.shadow_camera(), g["width"], g["height"], g["steps"], g["flags"],
+                      nthreads=4, want_shadow=True, want_stats=True)
     assert hashlib.sha256(np.ascontiguousarray(r["rgba"]).tobytes()).hexdigest() == g["rgba_sha256"]
     assert hashlib.sha256(np.ascontiguousarray(r["shadow"]).tobytes()).hexdigest() == g["shadow_sha256"]
     assert r["stats"]["eye_hits"][:len(g["eye_hits"])] == g["eye_hits"]
     assert r["stats"]["lit_pixels"] == g["lit_pixels"]
+    if "circle_plane_pixels" in g:
+        assert r["stats"]["eye_circle_plane_pixels"] == g["circle_plane_pixels"]
+        assert r["stats"]["eye_capped_cylinder_pixels"] == g["capped_cylinder_pixels"]
 
 
 def test_oracle_matches_fixture_arrays(oracle, scenes):
@@ -77,8 +94,9 @@ def test_oracle_matches_fixture_arrays(oracle, scenes):
     assert len(names) >= 6
     for name in names:
         g = _golden()[name]
-        r = oracle.render(_scene_for(scenes, name), scenes.eye_camera(), scenes.shadow_camera(), g["width"],
-                          g["height"], g["steps"], g["flags"], want_shadow=True)
+        scene, eye = _case(scenes, name)
+        r = oracle.render(scene, eye, scenes.shadow_camera(), g["width"], g["height"], g["steps"], g["flags"],
+                          want_shadow=True)
         assert bits_equal(r["rgba"], fx[name + "__rgba"]), (name, first_mismatch(r["rgba"], fx[name + "__rgba"]))
         assert bits_equal(r["shadow"], fx[name + "__shadow"]), name
 
@@ -134,9 +152,74 @@ def test_no_march_and_no_raster_flags(oracle, scenes):
 
 
 def test_perspective_frame_is_unsupported(oracle, scenes):
-    persp = scenes.Camera(scenes.PERSPECTIVE, (0, 0, 0), (0, 0, 1), (0, 1, 0), (1, 0, 0))
+    """Spheres under a PERSPECTIVE eye camera need projectSphere (row f-3)."""
+    persp = scenes.perspective_eye_camera()
     with pytest.raises(RuntimeError):
         oracle.render(scenes.scene_a_bench(), persp, scenes.shadow_camera(), 16, 16, 8, 0)
+    # ... a sphere-free scene (testscene_raytracingPlane0) is fine
+    oracle.render(scenes.raytracing_plane0(), persp, scenes.shadow_camera(), 16, 16, 0, scenes.RAYTRACING_FLAGS)
+
+
+def test_raytracing_plane0_kats(oracle, scenes):
+    """testscene_raytracingPlane0 at the reference's 512x512: the cylinder covers
+    3257 pixels (independent numpy restatement: tests/golden/gen_golden.py), all
+    lit (the shadow map stays +INF), the rest is background."""
+    r = oracle.render(scenes.raytracing_plane0(), scenes.perspective_eye_camera(), scenes.shadow_camera(),
+                      512, 512, 0, scenes.RAYTRACING_FLAGS, want_stats=True)
+    st = r["stats"]
+    assert st["eye_capped_cylinder_pixels"] == st["eye_hit_pixels"] == st["lit_pixels"] == 3257
+    img = r["rgba"]
+    # the cylinder is above the view axis (pA.y = 10.01): no hit in the lower half
+    assert np.all(img[:256, :, 0] == 0.0) and np.all(img[:256, :, 1] == np.float32(0.2))
+
+
+def test_icapped_cone_known_answers(oracle):
+    """iCappedCone (main.rs:2889-2959) on analytic cases."""
+    # straight at cap A of a unit cylinder along z: t = 5, n = -ba/|ba| (signed zeros as computed)
+    t, n = oracle.icapped_cone((0, 0, -5), (0, 0, 1), (0, 0, 0), (0, 0, 1), 0.5, 0.5)
+    assert t == 5.0 and n == (-0.0, -0.0, -1.0)
+    # cap B from above: t = 4
+    t, n = oracle.icapped_cone((0, 0, 5), (0, 0, -1), (0, 0, 0), (0, 0, 1), 0.5, 0.5)
+    assert t == 4.0 and n == (0.0, 0.0, 1.0)
+    # body of a cone: radius 0.25 halfway up -> t ~ 4.75, normal tilted by the slope 0.1
+    t, n = oracle.icapped_cone((-5, 0, 0.5), (1, 0, 0), (0, 0, 0), (0, 0, 1), 0.3, 0.2)
+    assert abs(t - 4.75) < 1e-12 and abs(n[0] + 1 / np.sqrt(1.01)) < 1e-12 and abs(n[2] - 0.1 / np.sqrt(1.01)) < 1e-12
+    # miss: (-1, -1, -1, -1)
+    assert oracle.icapped_cone((-5, 3, 0.5), (1, 0, 0), (0, 0, 0), (0, 0, 1), 0.3, 0.2) == (-1.0, (-1.0, -1.0, -1.0))
+
+
+def test_icapped_cone_matches_independent_restatement(oracle):
+    """C oracle == numpy restatement (gen_golden.icapped_cone) bit for bit on random rays."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("gen_golden", os.path.join(GOLD, "gen_golden.py"))
+    gg = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(gg)
+    rng = np.random.default_rng(0x2018)
+    for _ in range(8):
+        pa, pb = rng.uniform(-1, 1, 3), rng.uniform(-1, 1, 3)
+        ra, rb = rng.uniform(0.05, 0.6, 2)
+        ro = rng.uniform(-3, 3, (200, 3))
+        rd = rng.normal(size=(200, 3))
+        rd /= np.linalg.norm(rd, axis=1, keepdims=True)
+        t_np, n_np = gg.icapped_cone([ro[:, k] for k in range(3)], [rd[:, k] for k in range(3)], pa, pb, ra, rb)
+        for i in range(200):
+            t, n = oracle.icapped_cone(ro[i], rd[i], pa, pb, ra, rb)
+            assert np.float64(t).tobytes() == np.float64(t_np[i]).tobytes(), i
+            assert all(np.float64(n[k]).tobytes() == np.float64(n_np[k][i]).tobytes() for k in range(3)), i
+
+
+def test_staged_raytracing_equals_frame(oracle, scenes):
+    """rasterize + processRaytracingRays + renderColorImage == the frame (mixed scene)."""
+    scene = scenes.mixed_rt(100)
+    vp1 = oracle.Viewport(120, 90, scenes.EnumFace.BACK, scenes.shadow_camera())
+    vp1.rasterize(scene)
+    vp1.processRaymarchingRays(scene.patches, 64)
+    vp0 = oracle.Viewport(120, 90, scenes.EnumFace.FRONT, scenes.eye_camera())
+    vp0.rasterize(scene)
+    vp0.processRaytracingRays(scene)
+    img = oracle.render_color_image(scene, vp0, vp1)
+    r = oracle.render(scene, scenes.eye_camera(), scenes.shadow_camera(), 120, 90, 64, 0)
+    assert bits_equal(img, r["rgba"])
 
 
 def test_encode_rgb8_ppm_pixel_rule(oracle):
