@@ -382,7 +382,7 @@ struct rtm_ctx {
     bool enc_tab_ready = false;
     uint64_t tab_key = 0;
     int64_t tab_nt = 0, tab_nz = 0, tab_nd = 0;
-    int32_t tab_w = 0, tab_h = 0, tab_np = 0;
+    int32_t tab_w = 0, tab_h = 0, tab_np = 0, tab_zmono = 0;
     bool tab_hast = false, tab_sep = false;
 };
 
@@ -471,6 +471,15 @@ int ensure_tables(rtm_ctx* ctx, int32_t steps, int32_t W, int32_t H, const rtm_c
             }
             if (nt == 0) with_z = false;
         }
+        int32_t zmono = 0;  // the search march needs a monotone table (re-checked, not assumed)
+        if (with_z) {
+            bool up = true, down = true;
+            for (int64_t k = 0; k + 1 < nt; ++k) {
+                up = up && zt[(size_t)k + 1] >= zt[(size_t)k];
+                down = down && zt[(size_t)k + 1] <= zt[(size_t)k];
+            }
+            zmono = up ? 1 : (down ? -1 : 0);
+        }
         std::vector<double> colx;
         double cy = 0.0;
         const bool with_sep = with_z && n_patches > 0 && separable(march_cam, W, colx, &cy);
@@ -522,6 +531,7 @@ int ensure_tables(rtm_ctx* ctx, int32_t steps, int32_t W, int32_t H, const rtm_c
         ctx->tab_w = W;
         ctx->tab_h = H;
         ctx->tab_np = n_patches;
+        ctx->tab_zmono = zmono;
     }
     const double* base = (const double*)ctx->tabs.p;
     const int64_t nt2 = ctx->tab_nt, nz2 = ctx->tab_nz;
@@ -529,6 +539,7 @@ int ensure_tables(rtm_ctx* ctx, int32_t steps, int32_t W, int32_t H, const rtm_c
     out->nx = base + nt2;
     out->ny = base + nt2 + W;
     out->z = nz2 ? base + nt2 + W + H : nullptr;
+    out->zmono = nz2 ? ctx->tab_zmono : 0;
     if (ctx->tab_sep) {
         out->py = base + nt2 + W + H + nz2;
         out->d0 = out->py + H;

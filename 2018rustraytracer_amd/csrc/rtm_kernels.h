@@ -64,6 +64,8 @@ struct PatchK {
 //   dd[k*W + i]    = (_1.a + (_1.b - _1.a) * p.x(i)) - d0 (main.rs:2075, 2077 diff)
 //   ok[i] / ok[W+j] = inRange01(p.x(i)) / inRange01(p.y(j)) (main.rs:2249)
 //   so the surface depth is D = d0 + dd * py (main.rs:2077, one mul + one add).
+// z_{k+1} = fl(z_k + step.z) is monotone in k (rounding is monotone), which the
+// host re-checks entry by entry before setting zmono.
 struct Tables {
     const double* t;   // steps entries, or nullptr when steps > RTM_T_TABLE_MAX
     const double* nx;  // W entries
@@ -73,6 +75,8 @@ struct Tables {
     const double* d0;  // n_patches*W
     const double* dd;  // n_patches*W
     const int32_t* ok; // W + H
+    int32_t zmono;     // z table (first `steps` entries) is non-decreasing (+1) / non-increasing (-1)
+    int32_t pad;
 };
 #define RTM_T_TABLE_MAX 65536
 

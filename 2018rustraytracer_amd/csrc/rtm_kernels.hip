@@ -452,6 +452,11 @@ __device__ __forceinline__ void shadow_tile_generic(const ShadowPart& a, double*
 
 // One 8-step chunk of the shared-z march for NR rows: lt[r] += #(z_k < D[r]);
 // returns true when no lane is still marching in any row (wave early-out).
+// March modes of the separable shadow tile (identical results):
+constexpr int MARCH_SIGN = 0;    // 8-step chunks, sign bit of fl(z_k - D)
+constexpr int MARCH_CMP = 1;     // 8-step chunks, compare z_k < D
+constexpr int MARCH_SEARCH = 2;  // first crossing located in the monotone z table
+
 template <int NR, bool CMP>
 __device__ __forceinline__ bool chunk8(const double (&z)[8], const double (&D)[NR], int (&lt)[NR],
                                        const unsigned (&inrb)[NR], const unsigned (&eposb)[NR]) {
@@ -470,16 +475,79 @@ __device__ __forceinline__ bool chunk8(const double (&z)[8], const double (&D)[N
     return !__any(cont != 0u);
 }
 
+// First crossing of a texel's march in the monotone shared z table
+// (MARCH_SEARCH).  With P(k) = [z_k < D] xor inc, P is false...false true...true
+// over k (z non-decreasing: inc, P(k) = z_k >= D; non-increasing: P(k) = z_k < D),
+// and P(0) false is exactly "z_0 on the entry side", so the reference's first
+// hit step is the first k with P(k) (none if there is no such k < steps).
+// The index is guessed from z_k ~ z_0 + k*sz and verified against the table
+// (P(f-1) false, P(f) true); a failed guess falls back to a binary search, so
+// the result never depends on the guess.  Returns steps for "no hit".
+__device__ __forceinline__ int first_crossing(cdouble* zt, double D, double oz, double inv_sz, bool inc, int steps) {
+    if ((oz < D) != inc) return steps;  // P(0): already past the surface, and z only moves away
+    double g = (D - oz) * inv_sz;
+    g = fmin(fmax(g, 0.0), (double)steps);  // NaN -> 0
+    int f = (int)ceil(g);
+    const bool ok = (f == 0 || ((zt[f - 1] < D) == inc)) && (f == steps || ((zt[f] < D) != inc));
+    if (!ok) {
+        int lo = 0, hi = steps;
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if ((zt[mid] < D) != inc) hi = mid;
+            else lo = mid + 1;
+        }
+        f = lo;
+    }
+    return f;
+}
+
+// first_crossing over the workgroup's LDS copy of the table: T[k] = (z_k, t_k)
+// for k <= steps, so one 16-byte read at the guessed index yields both the
+// verification value and the hit's t (main.rs:2264).
+constexpr int SEARCH_LDS_MAX_STEPS = 2048;  // 32 KiB of LDS at most
+__device__ __forceinline__ int first_crossing_lds(const double2* T, double D, double oz, double inv_sz, bool inc,
+                                                  int steps, double& t) {
+    if ((oz < D) != inc) return steps;
+    double g = (D - oz) * inv_sz;
+    g = fmin(fmax(g, 0.0), (double)steps);  // NaN -> 0
+    int f = (int)ceil(g);
+    const double2 e = T[f];
+    const double zp = T[f > 0 ? f - 1 : 0].x;
+    const bool ok = (f == 0 || ((zp < D) == inc)) && (f == steps || ((e.x < D) != inc));
+    if (ok) {
+        t = e.y;
+        return f;
+    }
+    int lo = 0, hi = steps;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if ((T[mid].x < D) != inc) hi = mid;
+        else lo = mid + 1;
+    }
+    t = T[lo].y;
+    return lo;
+}
+
 // Shadow tile for the separable axis-aligned shadow camera with a shared z
 // sequence (the BASELINE scenes): 64 x (TILE_Y*NR) texels, NR rows per wave, so
 // every lane runs NR independent march chains (ILP against VALU and load
-// latency), the 8-step table chunks are prefetched one chunk ahead, and each
-// step is the sign bit of fl(z_k - D) (D finite and nonzero on this path, so
-// that bit is exactly [z_k < D], see march_axis).  If any lane's D is not
-// finite/nonzero the wave takes the exact per-texel loop instead.
-template <int NR, bool CMP = false>
+// latency).  MARCH_SEARCH (default when the host proved the z table monotone)
+// locates each chain's first crossing directly (first_crossing); the chunk
+// modes walk the table in 8-step chunks, prefetched one chunk ahead, each step
+// the sign bit of fl(z_k - D) or the compare z_k < D (D finite and nonzero on
+// this path, so both are exactly the class test, see march_axis).  If any
+// lane's D is not finite/nonzero the wave takes the exact per-texel loop instead.
+template <int NR, int MODE>
 __device__ __forceinline__ void shadow_tile_sep(const ShadowPart& a, double* __restrict__ smap, int bx, int by,
-                                                int diag) {
+                                                int diag, double2* lds_zt = nullptr) {
+    constexpr bool CMP = MODE == MARCH_CMP;
+    // MARCH_SEARCH with lds_zt: stage (z_k, t_k), k <= steps, in LDS once per workgroup
+    const bool use_lds = MODE == MARCH_SEARCH && lds_zt != nullptr;
+    if (use_lds) {
+        for (int k = threadIdx.x; k <= a.steps; k += BLOCK)
+            lds_zt[k] = make_double2(a.tab.z[k], k < a.steps ? a.tab.t[k] : 0.0);
+        __syncthreads();
+    }
     const int lane = threadIdx.x & (TILE_X - 1);
     const int xb = bx * TILE_X;
     const int xi = xb + lane;
@@ -530,7 +598,20 @@ __device__ __forceinline__ void shadow_tile_sep(const ShadowPart& a, double* __r
                 fast = fast && (!inr[r] || (fabs(D[r]) < INFINITY && D[r] != 0.0));
             }
             int cnt[NR];
-            if (__all(fast)) {
+            double tl[NR];  // t of the hit step (LDS search only)
+            if (MODE == MARCH_SEARCH && use_lds && __all(fast)) {
+                const bool inc = a.tab.zmono > 0;
+                const double inv_sz = 1.0 / sz;
+#pragma unroll
+                for (int r = 0; r < NR; ++r)
+                    cnt[r] = inr[r] ? first_crossing_lds(lds_zt, D[r], oz, inv_sz, inc, steps, tl[r]) : steps;
+            } else if (MODE == MARCH_SEARCH && __all(fast)) {
+                cdouble* zt = (cdouble*)a.tab.z;
+                const bool inc = a.tab.zmono > 0;
+                const double inv_sz = 1.0 / sz;
+#pragma unroll
+                for (int r = 0; r < NR; ++r) cnt[r] = inr[r] ? first_crossing(zt, D[r], oz, inv_sz, inc, steps) : steps;
+            } else if (MODE != MARCH_SEARCH && __all(fast)) {
                 cdouble* zt = (cdouble*)a.tab.z;  // padded by 8 entries past `steps`
                 unsigned eposb[NR], inrb[NR];
                 bool epos[NR];
@@ -605,7 +686,13 @@ __device__ __forceinline__ void shadow_tile_sep(const ShadowPart& a, double* __r
 #pragma unroll
                 for (int r = 0; r < NR; ++r) cnt[r] = steps;
             }
-            if (steps > 0) {
+            if (MODE == MARCH_SEARCH && use_lds && __all(fast)) {
+#pragma unroll
+                for (int r = 0; r < NR; ++r) {
+                    const bool hit = cnt[r] < steps;
+                    zb[r] = (hit && tl[r] < zb[r]) ? tl[r] : zb[r];
+                }
+            } else if (steps > 0) {
                 // t of the first hit step (branch-free: clamped table index + select)
 #pragma unroll
                 for (int r = 0; r < NR; ++r) {
@@ -783,9 +870,11 @@ __global__ __launch_bounds__(BLOCK) void shadow_pass_kernel(const FrameArgs a, d
     shadow_tile_generic<COUNT>(a.sh, smap, blockIdx.x, blockIdx.y, st);
 }
 
-template <int NR, bool CMP>
-__global__ __launch_bounds__(BLOCK) void shadow_sep_kernel(const FrameArgs a, double* __restrict__ smap, int diag) {
-    shadow_tile_sep<NR, CMP>(a.sh, smap, blockIdx.x, blockIdx.y, diag);
+template <int NR, int MODE>
+__global__ __launch_bounds__(BLOCK) void shadow_sep_kernel(const FrameArgs a, double* __restrict__ smap, int diag,
+                                                           int lds) {
+    extern __shared__ double2 lds_zt[];
+    shadow_tile_sep<NR, MODE>(a.sh, smap, blockIdx.x, blockIdx.y, diag, lds ? lds_zt : nullptr);
 }
 
 template <bool FUSED, bool COUNT, bool RT>
@@ -828,7 +917,7 @@ __global__ __launch_bounds__(BLOCK) void frame_pipe_kernel(const FrameArgs a, do
     if (s_after > s_before) {
         const int t = (int)s_before;
         if (SEP)
-            shadow_tile_sep<NR>(a.sh, smap_w, t % sh_gx, t / sh_gx, 0);
+            shadow_tile_sep<NR, MARCH_CMP>(a.sh, smap_w, t % sh_gx, t / sh_gx, 0);
         else
             shadow_tile_generic<false>(a.sh, smap_w, t % sh_gx, t / sh_gx, nullptr);
     } else {
@@ -1053,24 +1142,38 @@ static int sep_rows() {
 
 static bool use_sep(const ShadowPart& s) { return sep_rows() > 0 && s.tab.d0 && s.tab.z && s.tab.t; }
 
-// Per-step test of the shared-z march: a compare (default; 47.1 vs 52.9 us for
-// the sign bit of fl(z - D) at config 3, profiles/r01_ab_cmp.txt) or the sign
-// bit (RTM_SEP_CMP=0) — identical results.
-static int sep_cmp() {
+// March mode of the separable shadow tile: the first-crossing search when the
+// z table is monotone (default), else 8-step chunks with a compare per step
+// (47.1 vs 52.9 us for the sign bit at config 3, profiles/r01_ab_cmp.txt).
+// RTM_SEP_MODE=0/1/2 forces sign/compare/search for A/B runs (search only when
+// the table allows it) — identical results.
+static int sep_mode(const ShadowPart& sh) {
     static int v = [] {
-        const char* e = getenv("RTM_SEP_CMP");
-        return e ? atoi(e) : 1;
+        const char* e = getenv("RTM_SEP_MODE");
+        return e ? atoi(e) : -1;
     }();
-    return v;
+    const int want = v < 0 ? MARCH_SEARCH : v;
+    return (want == MARCH_SEARCH && sh.tab.zmono == 0) ? MARCH_CMP : want;
 }
 
 template <int NR>
 static void launch_sep(const FrameArgs& a, double* smap, hipStream_t s) {
     dim3 g((unsigned)((a.sh.W + TILE_X - 1) / TILE_X), (unsigned)((a.sh.H + TILE_Y * NR - 1) / (TILE_Y * NR)));
-    if (sep_cmp())
-        hipLaunchKernelGGL((shadow_sep_kernel<NR, true>), g, dim3(BLOCK), 0, s, a, smap, diag_mode());
+    const int mode = sep_mode(a.sh);
+    // LDS-staged table for the search (RTM_SEP_LDS=0 disables it for A/B runs)
+    static const bool lds_on = [] {
+        const char* e = getenv("RTM_SEP_LDS");
+        return !e || atoi(e) != 0;
+    }();
+    const bool march = !(a.sh.flags & RTM_FLAG_NO_MARCH) && a.sh.n_patches > 0 && a.sh.steps > 0;
+    const int lds = (mode == MARCH_SEARCH && lds_on && march && a.sh.steps <= SEARCH_LDS_MAX_STEPS) ? 1 : 0;
+    const size_t smem = lds ? sizeof(double2) * (size_t)(a.sh.steps + 1) : 0;
+    if (mode == MARCH_SEARCH)
+        hipLaunchKernelGGL((shadow_sep_kernel<NR, MARCH_SEARCH>), g, dim3(BLOCK), smem, s, a, smap, diag_mode(), lds);
+    else if (mode == MARCH_CMP)
+        hipLaunchKernelGGL((shadow_sep_kernel<NR, MARCH_CMP>), g, dim3(BLOCK), 0, s, a, smap, diag_mode(), 0);
     else
-        hipLaunchKernelGGL((shadow_sep_kernel<NR, false>), g, dim3(BLOCK), 0, s, a, smap, diag_mode());
+        hipLaunchKernelGGL((shadow_sep_kernel<NR, MARCH_SIGN>), g, dim3(BLOCK), 0, s, a, smap, diag_mode(), 0);
 }
 
 int launch_shadow_pass(const FrameArgs& a, double* smap, void* stream, StatsK* stats) {

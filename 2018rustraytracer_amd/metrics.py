@@ -18,6 +18,12 @@ off for bit parity).  Per-unit figures:
                  84 per hit pixel         (ray, world pos, normal, Lambert,
                                            reflect, powi(32), shadow projection)
 
+  ray-traced primitives (row f-1), per eye pixel, common path:
+                 12 ray origin (ORTHOGONAL) / 24 normalised ray dir (PERSPECTIVE)
+                 33 per circle plane      (calcRayPlane 15, hit point + radius test 18)
+                 88 per capped cylinder   (iCappedCone: projections 22, cap test ~16,
+                                           body quadratic 50)
+
 HBM bytes the two-kernel design must move:
   shadow pass    8 B per texel            (f64 shadow-map store)
   eye pass       16 B per pixel           (RGBA f32 store)
@@ -43,6 +49,10 @@ SEP_PER_ITER = 1
 EYE_PER_SPHERE = 4
 EYE_PER_COVER = 21
 EYE_PER_HIT = 84
+RT_RAY_ORTHO = 12
+RT_RAY_PERSP = 24
+RT_PER_PLANE = 33
+RT_PER_CYL = 88
 
 
 def shared_z_separable(shadow_cam) -> bool:
@@ -55,7 +65,8 @@ def shared_z_separable(shadow_cam) -> bool:
 
 
 def frame_work(stats: dict, width: int, height: int, n_spheres: int, n_patches: int, flags: int = 0,
-               fused: bool = False, sep: bool = False) -> dict:
+               fused: bool = False, sep: bool = False, n_planes: int = 0, n_cyls: int = 0,
+               perspective: bool = False) -> dict:
     px = width * height
     no_march = bool(flags & 0x1)
     no_sraster = bool(flags & 0x2)
@@ -70,6 +81,9 @@ def frame_work(stats: dict, width: int, height: int, n_spheres: int, n_patches: 
             sh_ops += texels * n_patches * SHADOW_PER_PATCH + SHADOW_PER_ITER * stats["march_iterations"]
     eye_ops = (px * EYE_PER_SPHERE * n_spheres + EYE_PER_COVER * stats["eye_sphere_tests"]
                + EYE_PER_HIT * stats["eye_hit_pixels"])
+    if n_planes or n_cyls:
+        eye_ops += px * ((RT_RAY_PERSP if perspective else RT_RAY_ORTHO) + RT_PER_PLANE * n_planes
+                         + RT_PER_CYL * n_cyls)
     sh_bytes = 0 if fused else 8 * px
     eye_bytes = 16 * px + (0 if fused else 8 * stats["eye_hit_pixels"])
     return dict(shadow_pass=dict(ops=sh_ops, bytes=sh_bytes),

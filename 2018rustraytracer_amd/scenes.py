@@ -202,19 +202,6 @@ def overlapping_spheres() -> Scene:
 
 OVERLAPPING_FLAGS = abi.RTM_FLAG_NO_MARCH | abi.RTM_FLAG_NO_SHADOW_RASTER
 
-# BASELINE.json configs -> (width, height, march_steps, scene factory, flags)
-CONFIGS = {
-    1: dict(width=256, height=256, steps=0, scene=lambda: closely_orbiting_sphere(100),
-            flags=abi.RTM_FLAG_NO_MARCH, desc="256x256, 3 spheres, no ray-march (CPU plumbing)"),
-    2: dict(width=1920, height=1080, steps=32, scene=scene_a_bench, flags=0,
-            desc="1920x1080, 3 spheres + 1 implicit, 32 march steps"),
-    3: dict(width=3840, height=2160, steps=64, scene=scene_a_bench, flags=0,
-            desc="3840x2160, 3 spheres + 1 implicit, 64 march steps"),
-    4: dict(width=7680, height=4320, steps=64, scene=scene_a_bench, flags=0,
-            desc="7680x4320, 3 spheres + 1 implicit, 64 march steps"),
-    5: dict(width=7680, height=4320, steps=128, scene=scene_b, flags=0,
-            desc="7680x4320, 16 spheres + 2 implicits, 128 march steps"),
-}
 
 
 # ---- testscene_raytracingPlane0 (main.rs:910-1046): main()'s default scene ----
@@ -288,3 +275,26 @@ def mixed_rt(frame: int = 100) -> Scene:
         PrimitiveCappedCylinder(1, Shading(1.0, 0.02, 0.02), (-0.1, 0.1, 0.3), (0.5, 0.1, 0.9), 0.12, 0.12),
     ]
     return s
+
+
+# BASELINE.json configs 1-5 (+ row f-1 workloads 6-7):
+# width, height, march_steps, scene factory, flags, eye camera factory (default eye_camera)
+CONFIGS = {
+    1: dict(width=256, height=256, steps=0, scene=lambda: closely_orbiting_sphere(100),
+            flags=abi.RTM_FLAG_NO_MARCH, desc="256x256, 3 spheres, no ray-march (CPU plumbing)"),
+    2: dict(width=1920, height=1080, steps=32, scene=scene_a_bench, flags=0,
+            desc="1920x1080, 3 spheres + 1 implicit, 32 march steps"),
+    3: dict(width=3840, height=2160, steps=64, scene=scene_a_bench, flags=0,
+            desc="3840x2160, 3 spheres + 1 implicit, 64 march steps"),
+    4: dict(width=7680, height=4320, steps=64, scene=scene_a_bench, flags=0,
+            desc="7680x4320, 3 spheres + 1 implicit, 64 march steps"),
+    5: dict(width=7680, height=4320, steps=128, scene=scene_b, flags=0,
+            desc="7680x4320, 16 spheres + 2 implicits, 128 march steps"),
+    # row f-1 measurement workloads, PERSPECTIVE eye camera
+    6: dict(width=3840, height=2160, steps=0, scene=scene_r_bench, flags=RAYTRACING_FLAGS,
+            eye=perspective_eye_camera,
+            desc="3840x2160, Scene R-bench: 9 capped cylinders + 4 circle planes, perspective (row f-1)"),
+    7: dict(width=512, height=512, steps=0, scene=raytracing_plane0, flags=RAYTRACING_FLAGS,
+            eye=perspective_eye_camera,
+            desc="512x512, testscene_raytracingPlane0 as main() renders it (row f-1)"),
+}

@@ -27,6 +27,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "Mpixels/s at 3840×2160, 64 march steps; 1/2/4/8-GPU scaling"
+# configs 6/7 measure BASELINE "next" row f-1 (ray-traced primitives), not the headline
+METRIC_F1 = "Mpixels/s, ray-traced circle planes + capped cylinders (row f-1)"
 
 
 def parse():
@@ -34,7 +36,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--config", type=int, default=3)
+    ap.add_argument("--config", type=int, default=3, help="scenes.CONFIGS id: 1-5 BASELINE, 6-7 row f-1")
     ap.add_argument("--mode", choices=["frames", "tile-gather"], default="frames")
     ap.add_argument("--fused", action="store_true", help="evaluate shadow texels on demand (same image)")
     ap.add_argument("--per-frame-calls", action="store_true",
@@ -57,7 +59,7 @@ def _latest_traffic(cfg_id: int, kernel: str):
     return None
 
 
-def cpu_baseline(scene, eye, shadow, w, h, k, flags, threads):
+def cpu_baseline(scene, eye, shadow, w, h, k, flags, threads, what):
     """The CPU oracle (f64 C restatement of main.rs) on the host cores, rank 0 only."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle  # checker / CPU baseline only
@@ -70,7 +72,7 @@ def cpu_baseline(scene, eye, shadow, w, h, k, flags, threads):
         dt = time.perf_counter() - t0
         best = dt if best is None else min(best, dt)
     return dict(value=round(w * h / best / 1e6, 3), unit="Mpixels/s", cores=threads, kind="port",
-                sample=f"full {w}x{h} frame, K={k}, Scene A-bench frame 100, best of 2, {threads} thread(s)",
+                sample=f"full {w}x{h} frame, K={k}, {what}, best of 2, {threads} thread(s)",
                 seconds_per_frame=round(best, 3))
 
 
@@ -95,7 +97,7 @@ def main():
     # tile-gather: each band evaluates only the shadow texels it reads (no cross-rank shadow map)
     fused = a.fused or a.mode == "tile-gather"
     flags = cfg["flags"] | (rtm.abi.RTM_FLAG_FUSED_SHADOW if fused else 0)
-    eye, shadow = sc.eye_camera(), sc.shadow_camera()
+    eye, shadow = cfg.get("eye", sc.eye_camera)(), sc.shadow_camera()
     ctx = rtm.Context(local)
     # kernel durations: HIP events on every TIMING_STRIDE-th frame of the timed region
     # (an event is a barrier packet; timing every frame would cost ~15% throughput)
@@ -103,8 +105,8 @@ def main():
     ctx.set_timing_capacity(max(1, a.steps // timing_stride))
 
     def scene_for(frame_index: int):
-        if a.config == 5:
-            return sc.scene_b()
+        if a.config in (5, 6, 7):
+            return cfg["scene"]()  # static scenes
         if a.config == 1:
             return sc.closely_orbiting_sphere(100 + frame_index)
         return sc.scene_a_bench(100 + frame_index)
@@ -208,7 +210,9 @@ def main():
         band_h = rows[1] - rows[0]
         st = ctx.stats(s0, eye, shadow, W, H, K, flags)
         work = metrics.frame_work(st, W, H, len(s0.spherePrimitives), len(s0.patches), flags, fused=fused,
-                                  sep=metrics.shared_z_separable(shadow))
+                                  sep=metrics.shared_z_separable(shadow), n_planes=len(s0.circlePlanePrimitives),
+                                  n_cyls=len(s0.cappedCylinderPrimitives),
+                                  perspective=eye.type_ == sc.PERSPECTIVE)
         if band_h != H:  # rank 0 renders one band: scale the frame's work to it (approximate)
             for kk in work.values():
                 kk["ops"] = int(kk["ops"] * band_h / H)
@@ -226,7 +230,7 @@ def main():
             roof_other = (metrics.roofline(other, work, other_ms, _latest_traffic(a.config, other))
                           if other_ms > 0 else None)
         res = {
-            "metric": METRIC,
+            "metric": METRIC if a.config <= 5 else METRIC_F1,
             "value": round(value, 2),
             "unit": "Mpixels/s",
             "n_gpus": world,
@@ -237,8 +241,9 @@ def main():
             "scaling": "weak" if a.mode == "frames" else "strong",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": "synthetic: Scene A-bench (SURVEY.md §8d-2) animation frames 100+i, f64 scene built on host"
-                    if a.config in (2, 3, 4) else "synthetic: SURVEY.md §8d-2 scene",
+            "data": ("synthetic: Scene A-bench (SURVEY.md §8d-2) animation frames 100+i, f64 scene built on host"
+                     if a.config in (2, 3, 4) else "synthetic: SURVEY.md §8d-2 scene" if a.config <= 5
+                     else "synthetic: row f-1 scene (scenes.py), f64 scene built on host"),
             "config": {"workload": cfg["desc"], "config_id": a.config, "width": W, "height": H,
                        "march_steps": K, "mode": a.mode, "shadow": "fused" if fused else "two-pass",
                        "pipelined": pipelined,
@@ -252,10 +257,12 @@ def main():
                          "frame_kernel_ms": round(avg_sh + avg_eye, 5)}),
             "roofline": roof,
             "roofline_other_kernel": roof_other,
-            "parity": "bit-exact vs CPU oracle (tests/test_gpu_parity.py)",
+            "parity": ("bit-exact vs CPU oracle (tests/test_gpu_parity.py)" if a.config <= 5
+                       else "bit-exact vs CPU oracle (tests/test_raytrace.py)"),
         }
         if world == 1 and not a.no_cpu_baseline:
-            res["cpu_baseline"] = cpu_baseline(s0, eye, shadow, W, H, K, flags, a.cpu_threads)
+            what = ("Scene A-bench frame 100" if a.config in (2, 3, 4) else cfg["desc"].split(", ", 1)[1])
+            res["cpu_baseline"] = cpu_baseline(s0, eye, shadow, W, H, K, flags, a.cpu_threads, what)
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()
