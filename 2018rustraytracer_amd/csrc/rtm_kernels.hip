@@ -122,13 +122,42 @@ __device__ __forceinline__ int hit_class_mask(double v0) {
 // finite nonzero D, class(z - D) is POS iff z >= D (z - D is +0 when z == D)
 // and NEG iff z < D, so each step is one compare against a scalar-loaded table
 // entry.  Otherwise each step is fl(z - D) + a class test, exactly as written.
+// First crossing of a texel's march in the monotone shared z table
+// (MARCH_SEARCH).  With P(k) = [z_k < D] xor inc, P is false...false true...true
+// over k (z non-decreasing: inc, P(k) = z_k >= D; non-increasing: P(k) = z_k < D),
+// and P(0) false is exactly "z_0 on the entry side", so the reference's first
+// hit step is the first k with P(k) (none if there is no such k < steps).
+// The index is guessed from z_k ~ z_0 + k*sz and verified against the table
+// (P(f-1) false, P(f) true); a failed guess falls back to a binary search, so
+// the result never depends on the guess.  Returns steps for "no hit".
+__device__ __forceinline__ int first_crossing(cdouble* zt, double D, double oz, double inv_sz, bool inc, int steps) {
+    if ((oz < D) != inc) return steps;  // P(0): already past the surface, and z only moves away
+    double g = (D - oz) * inv_sz;
+    g = fmin(fmax(g, 0.0), (double)steps);  // NaN -> 0
+    int f = (int)ceil(g);
+    const bool ok = (f == 0 || ((zt[f - 1] < D) == inc)) && (f == steps || ((zt[f] < D) != inc));
+    if (!ok) {
+        int lo = 0, hi = steps;
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if ((zt[mid] < D) != inc) hi = mid;
+            else lo = mid + 1;
+        }
+        f = lo;
+    }
+    return f;
+}
+
 template <bool COUNT>
 __device__ __forceinline__ MarchResult march_axis(double D, bool inr0, double oz, double sz, int steps,
                                                   const Tables& tb) {
     MarchResult r{false, 0.0, 0};
     int cnt = inr0 ? 0 : steps;
     const bool fast_ok = tb.z != nullptr && (!inr0 || (fabs(D) < INFINITY && D != 0.0));
-    if (__any(inr0) && __all(fast_ok)) {
+    if (tb.zmono != 0 && __all(fast_ok)) {
+        // monotone table (host-checked): locate the first crossing directly
+        if (inr0) cnt = first_crossing((cdouble*)tb.z, D, oz, 1.0 / sz, tb.zmono > 0, steps);
+    } else if (__any(inr0) && __all(fast_ok)) {
         cdouble* zt = (cdouble*)tb.z;
         const bool epos = !(oz < D);  // entry class POS <=> z0 >= D
         int lt = 0;                   // #steps with z_k < D
@@ -473,32 +502,6 @@ __device__ __forceinline__ bool chunk8(const double (&z)[8], const double (&D)[N
         cont |= inrb[r] & (last ^ eposb[r]);
     }
     return !__any(cont != 0u);
-}
-
-// First crossing of a texel's march in the monotone shared z table
-// (MARCH_SEARCH).  With P(k) = [z_k < D] xor inc, P is false...false true...true
-// over k (z non-decreasing: inc, P(k) = z_k >= D; non-increasing: P(k) = z_k < D),
-// and P(0) false is exactly "z_0 on the entry side", so the reference's first
-// hit step is the first k with P(k) (none if there is no such k < steps).
-// The index is guessed from z_k ~ z_0 + k*sz and verified against the table
-// (P(f-1) false, P(f) true); a failed guess falls back to a binary search, so
-// the result never depends on the guess.  Returns steps for "no hit".
-__device__ __forceinline__ int first_crossing(cdouble* zt, double D, double oz, double inv_sz, bool inc, int steps) {
-    if ((oz < D) != inc) return steps;  // P(0): already past the surface, and z only moves away
-    double g = (D - oz) * inv_sz;
-    g = fmin(fmax(g, 0.0), (double)steps);  // NaN -> 0
-    int f = (int)ceil(g);
-    const bool ok = (f == 0 || ((zt[f - 1] < D) == inc)) && (f == steps || ((zt[f] < D) != inc));
-    if (!ok) {
-        int lo = 0, hi = steps;
-        while (lo < hi) {
-            const int mid = (lo + hi) >> 1;
-            if ((zt[mid] < D) != inc) hi = mid;
-            else lo = mid + 1;
-        }
-        f = lo;
-    }
-    return f;
 }
 
 // first_crossing over the workgroup's LDS copy of the table: T[k] = (z_k, t_k)
