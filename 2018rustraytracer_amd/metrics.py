@@ -14,6 +14,12 @@ off for bit parity).  Per-unit figures:
     z_k is one host table for all texels, so per texel:
                  19 per covering sphere, 4 per patch (D: mul+add, entry compare,
                  min), 1 per march iteration (the compare z_k < D)
+    ... and when the host proved that table monotone (every BASELINE scene) the
+    implemented march is a first-crossing search, constant work per texel and
+    patch, no per-iteration term:
+                 10 per patch (D: 2, entry compare, index guess (D - z0)/sz with
+                 clamp + ceil: 5, two verifying compares) — also the work of a
+                 fused (on-demand) shadow texel
   eye pixel      4 per sphere (cull)      + 21 per covering sphere (incl. z-test)
                  84 per hit pixel         (ray, world pos, normal, Lambert,
                                            reflect, powi(32), shadow projection)
@@ -46,6 +52,7 @@ SHADOW_PER_PATCH = 32
 SHADOW_PER_ITER = 3
 SEP_PER_PATCH = 4
 SEP_PER_ITER = 1
+SEARCH_PER_PATCH = 10
 EYE_PER_SPHERE = 4
 EYE_PER_COVER = 21
 EYE_PER_HIT = 84
@@ -66,7 +73,8 @@ def shared_z_separable(shadow_cam) -> bool:
 
 def frame_work(stats: dict, width: int, height: int, n_spheres: int, n_patches: int, flags: int = 0,
                fused: bool = False, sep: bool = False, n_planes: int = 0, n_cyls: int = 0,
-               perspective: bool = False) -> dict:
+               perspective: bool = False, search: bool = False) -> dict:
+    """search: the march is the first-crossing search (monotone shared z table)."""
     px = width * height
     no_march = bool(flags & 0x1)
     no_sraster = bool(flags & 0x2)
@@ -75,7 +83,9 @@ def frame_work(stats: dict, width: int, height: int, n_spheres: int, n_patches: 
     if not no_sraster:
         sh_ops += (0 if sep else texels * SHADOW_PER_SPHERE * n_spheres) + SHADOW_PER_COVER * stats["shadow_sphere_tests"]
     if not no_march:
-        if sep and not fused:
+        if search:
+            sh_ops += texels * n_patches * SEARCH_PER_PATCH
+        elif sep and not fused:
             sh_ops += texels * n_patches * SEP_PER_PATCH + SEP_PER_ITER * stats["march_iterations"]
         else:
             sh_ops += texels * n_patches * SHADOW_PER_PATCH + SHADOW_PER_ITER * stats["march_iterations"]
