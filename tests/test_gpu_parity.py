@@ -326,3 +326,33 @@ def test_pipelined_frames_scene_b_8k(rtm, oracle, scenes, gpu_ctx):
     want = oracle.render(frames[0], scenes.eye_camera(), scenes.shadow_camera(), w, h, k, 0, nthreads=NT)["rgba"]
     for o in outs:
         assert bits_equal(o.cpu().numpy(), want)
+
+
+def test_pipelined_launch_in_subprocess(rtm, scenes):
+    """RTM_PIPELINE=1 (read once per process): the software-pipelined launch
+    (shadow pass of frame i + eye pass of frame i-1 in one grid) is opt-in, so
+    it runs in a child process here, against frame-by-frame rtm_render."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = r'''
+import importlib, sys
+import numpy as np, torch
+sys.path.insert(0, %r)
+rtm = importlib.import_module("2018rustraytracer_amd")
+sc = importlib.import_module("2018rustraytracer_amd.scenes")
+ctx = rtm.Context(0)
+for frames, w, h, k in (([sc.scene_a_bench(100 + 3 * i) for i in range(4)], 1920, 1080, 64),
+                        ([sc.scene_b(), sc.scene_b()], 640, 480, 128)):
+    outs = [torch.empty((h, w, 4), dtype=torch.float32, device="cuda") for _ in frames]
+    torch.cuda.synchronize()
+    ctx.render_frames_async(frames, sc.eye_camera(), sc.shadow_camera(), w, h, k, 0, [o.data_ptr() for o in outs])
+    ctx.synchronize()
+    for s, o in zip(frames, outs):
+        want = rtm.render_frame(s, sc.eye_camera(), sc.shadow_camera(), w, h, k, 0)
+        assert np.array_equal(o.cpu().numpy().view(np.uint32), want.view(np.uint32))
+print("pipelined ok")
+''' % root
+    env = dict(os.environ, RTM_PIPELINE="1")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0 and "pipelined ok" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
