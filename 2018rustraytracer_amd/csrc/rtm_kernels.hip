@@ -886,7 +886,7 @@ __device__ __forceinline__ void shadow_tile_lean2(const ShadowPart& a, double* _
                     const double d = sqrt(pa[c] * pa[c] + pb * pb);
                     const double h = sqrt(1.0 - d * d);
                     const double depth = sp.z + h * sp.r;
-                    zb[r][c] = (d < 1.0 && depth < zb[r][c]) ? depth : zb[r][c];
+                    zb[r][c] = ((d < 1.0) & (depth < zb[r][c])) ? depth : zb[r][c];
                 }
             }
         }
@@ -939,12 +939,16 @@ __device__ __forceinline__ void shadow_tile_lean2(const ShadowPart& a, double* _
                     const int f = (int)ceil(g);
                     const double2 e = T[f];
                     const double zp = T[f - 1].x;
+                    // bitwise & | on the predicates: no short-circuit, so no divergent
+                    // branches (and the t read is not sunk into one)
                     const bool okA = INC ? (zp < Dv) : !(zp < Dv);
                     const bool okB = INC ? !(e.x < Dv) : (e.x < Dv);
                     const bool entry = INC ? (oz < Dv) : !(oz < Dv);
-                    const bool hit = inr && fastD && okA && okB && f < steps;
-                    zb[r][c] = (hit && e.y < zb[r][c]) ? e.y : zb[r][c];
-                    slow |= (inr && (!fastD || (entry && !(okA && (f == steps || okB))))) ? (1u << (r * CW + c)) : 0u;
+                    const bool hit = inr & fastD & okA & okB & (f < steps);
+                    const double ty = e.y;
+                    zb[r][c] = (hit & (ty < zb[r][c])) ? ty : zb[r][c];
+                    const bool sl = inr & (!fastD | (entry & !(okA & ((f == steps) | okB))));
+                    slow |= sl ? (1u << (r * CW + c)) : 0u;
                 }
             }
             if (__any(slow != 0u)) {

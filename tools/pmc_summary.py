@@ -15,7 +15,7 @@ from collections import defaultdict
 
 
 def short(name):
-    m = re.search(r"(shadow_pass_kernel|shadow_sep_kernel|eye_pass_kernel|frame_pipe_kernel|rt_upload_kernel|"
+    m = re.search(r"(shadow_\w+_kernel|eye_pass_kernel|frame_pipe_kernel|rt_upload_kernel|"
                   r"vp_\w+_kernel|fill_kernel|encode_rgb8_kernel|ppm_\w+_kernel)(<[^>]*>)?", name)
     return (m.group(1) + (m.group(2) or "")) if m else name[:60]
 
@@ -55,7 +55,8 @@ def main():
         if "SQ_INSTS_VALU" in d and "SQ_WAVES" in d and d["SQ_WAVES"]:
             d["valu_insts_per_wave"] = d["SQ_INSTS_VALU"] / d["SQ_WAVES"]
             d["salu_insts_per_wave"] = d.get("SQ_INSTS_SALU", 0) / d["SQ_WAVES"]
-        name = ("shadow_pass" if (k.startswith("shadow_pass_kernel<false") or k.startswith("shadow_sep_kernel")) else
+        timed_shadow = k.startswith("shadow_") and not k.startswith("shadow_pass_kernel<true")  # (<true>: stats)
+        name = ("shadow_pass" if timed_shadow else
                 "eye_pass" if k.startswith("eye_pass_kernel<false, false") else
                 "eye_pass_fused" if k.startswith("eye_pass_kernel<true, false") else k)
         out["kernels"][name] = d
