@@ -134,6 +134,116 @@ RasterSphereK project_sphere(const rtm_camera& c, const rtm_sphere& s, int32_t W
     return k;
 }
 
+// ---- PERSPECTIVE sphere projection (row f-3) ----
+// nalgebra 0.16 semantics (Cargo.toml nalgebra = "^0.16.12"): Matrix4::new is
+// row-major; a fixed 4x4 product is one gemv per output column, y_i = v0*m_i0
+// then y_i = v_j*m_ij + 1*y_i (axpy), zero terms included; Perspective3::new =
+// identity, set_fovy, set_aspect, set_znear_and_zfar, m33 = 0, m32 = -1.
+struct M44 {
+    double m[4][4];
+};
+
+M44 m44_identity() {
+    M44 r{};
+    for (int i = 0; i < 4; ++i) r.m[i][i] = 1.0;
+    return r;
+}
+
+void m44_gemv(const M44& a, const double x[4], double y[4]) {
+    for (int i = 0; i < 4; ++i) y[i] = x[0] * a.m[i][0];
+    for (int j = 1; j < 4; ++j)
+        for (int i = 0; i < 4; ++i) y[i] = x[j] * a.m[i][j] + 1.0 * y[i];
+}
+
+M44 m44_mul(const M44& a, const M44& b) {
+    M44 r{};
+    for (int j = 0; j < 4; ++j) {
+        const double x[4] = {b.m[0][j], b.m[1][j], b.m[2][j], b.m[3][j]};
+        double y[4];
+        m44_gemv(a, x, y);
+        for (int i = 0; i < 4; ++i) r.m[i][j] = y[i];
+    }
+    return r;
+}
+
+// Viewport::rasterize, PERSPECTIVE branch (main.rs:473-524) for one sphere, and
+// projectSphere (main.rs:2796-2837).  The aspect (512 as f64)/(512 as f64)
+// (main.rs:496) generalises to W/H.  tan is the platform libm's (Rust f64::tan).
+RasterSphereK project_sphere_persp(const rtm_camera& c, const rtm_sphere& s, int32_t W, int32_t H, PerspSphK& q) {
+    RasterSphereK k{};
+    const double diff[3] = {s.pos[0] - c.pos[0], s.pos[1] - c.pos[1], s.pos[2] - c.pos[2]};
+    k.z = dot3(c.dir, diff);  // calcDepthOfProjectedPoint (main.rs:1962-1978)
+    k.r = s.r;
+    k.id = (int32_t)s.id;
+    M44 rel{};  // relativeGlobalToCamera (main.rs:484-489)
+    for (int i = 0; i < 3; ++i) {
+        rel.m[0][i] = c.side[i];
+        rel.m[1][i] = c.up[i];
+        rel.m[2][i] = c.dir[i];
+    }
+    rel.m[3][3] = 1.0;
+    const double d4[4] = {diff[0], diff[1], diff[2], 1.0};
+    double local[4];
+    m44_gemv(rel, d4, local);  // mul(&relativeGlobalToCamera, &(pos - camera.position)) (main.rs:492)
+    const double fov = 3.14 / 2.0;
+    M44 p = m44_identity();  // Perspective3::new(W/H, fov, 0.1, 1000.0).to_homogeneous() (main.rs:496-499)
+    const double old_m22 = p.m[1][1];
+    p.m[1][1] = 1.0 / std::tan(fov / 2.0);
+    p.m[0][0] = p.m[0][0] * (p.m[1][1] / old_m22);
+    p.m[0][0] = p.m[1][1] / ((double)W / (double)H);
+    p.m[2][2] = (1000.0 + 0.1) / (0.1 - 1000.0);
+    p.m[2][3] = 1000.0 * 0.1 * 2.0 / (0.1 - 1000.0);
+    p.m[3][3] = 0.0;
+    p.m[3][2] = -1.0;
+    M44 refl = m44_identity();  // new_nonuniform_scaling(&Vector3::new(1.0, 1.0, -1.0)) (main.rs:503)
+    refl.m[2][2] = -1.0;
+    const M44 cam = m44_mul(p, refl);  // perspectiveMat * reflectionZMat (main.rs:506)
+    // projectSphere(&Vec4(local, r), &cameraMat, fov)
+    const double l4[4] = {local[0], local[1], local[2], 1.0};
+    double o[4];
+    m44_gemv(cam, l4, o);
+    const double r2 = s.r * s.r;
+    const double z2 = o[2] * o[2];
+    const double l2 = o[0] * o[0] + o[1] * o[1] + o[2] * o[2];
+    const double sa = fov * std::sqrt(-r2 * (r2 - l2) / ((l2 - z2) * (r2 - z2) * (r2 - z2)));
+    const double sb = fov * std::sqrt(-r2 * (r2 - l2) / ((l2 - z2) * (r2 - z2) * (r2 - l2)));
+    const double axa[2] = {o[0] * sa, o[1] * sa};
+    const double axb[2] = {-o[1] * sb, o[0] * sb};
+    const double sc = fov * o[2] / (z2 - r2);
+    q.cx = o[0] * sc;
+    q.cy = o[1] * sc;
+    // calcEllipseDistToCenter's normalized() / magnitude() (main.rs:2849-2850, 2098-2109)
+    q.mA = std::sqrt(axa[0] * axa[0] + axa[1] * axa[1]);
+    q.mB = std::sqrt(axb[0] * axb[0] + axb[1] * axb[1]);
+    const double iA = 1.0 / q.mA, iB = 1.0 / q.mB;
+    q.nAx = axa[0] * iA;
+    q.nAy = axa[1] * iA;
+    q.nBx = axb[0] * iB;
+    q.nBy = axb[1] * iB;
+    k.cx = q.cx;
+    k.cy = q.cy;
+    k.n = 0.0;
+    k.m = q.mA;
+    // The axes are perpendicular, so d < 1 implies |rel| < max(mA, mB): each
+    // coordinate is within R of the centre (1e-6 relative margin for the
+    // rounding of the unit axes).  Non-finite or zero axes cover nothing.
+    k.ix0 = k.iy0 = 1;
+    k.ix1 = k.iy1 = 0;
+    const bool ok = std::isfinite(q.mA) && std::isfinite(q.mB) && q.mA > 0.0 && q.mB > 0.0 && std::isfinite(q.cx) &&
+                    std::isfinite(q.cy) && std::isfinite(q.nAx) && std::isfinite(q.nAy) && std::isfinite(q.nBx) &&
+                    std::isfinite(q.nBy);
+    if (ok) {
+        const double R = std::max(q.mA, q.mB) * (1.0 + 1e-6);
+        pixel_range(q.cx, R, W, &k.ix0, &k.ix1);
+        pixel_range(q.cy, R, H, &k.iy0, &k.iy1);
+        if (k.ix0 > k.ix1 || k.iy0 > k.iy1) {
+            k.ix0 = k.iy0 = 1;
+            k.ix1 = k.iy1 = 0;
+        }
+    }
+    return k;
+}
+
 ShadeSphereK shade_sphere(const rtm_sphere& s) {
     ShadeSphereK k{};
     k.px = s.pos[0];
@@ -199,6 +309,24 @@ int validate_scene(const rtm_scene* scene) {
             return fail(RTM_ERR_INVALID, "capped cylinder %d has id %lld outside [0,%d)", i,
                         (long long)scene->capped_cylinders[i].id, nc);
     return RTM_OK;
+}
+
+// What a frame needs beyond FrameArgs, in device memory: its ray-traced
+// primitives (row f-1) and the eye's PERSPECTIVE sphere projections (row f-3).
+struct FrameExtra {
+    RtK rt;
+    PerspK psp;
+    bool has_rt = false, has_psp = false;
+};
+
+bool build_rt(const rtm_scene* scene, RtK& k);
+
+void build_extra(const rtm_scene* scene, const rtm_camera* eye, int32_t W, int32_t H, FrameExtra& x) {
+    x.has_rt = build_rt(scene, x.rt);
+    std::memset(&x.psp, 0, sizeof x.psp);
+    x.has_psp = eye->type != RTM_CAMERA_ORTHOGONAL && scene->n_spheres > 0;
+    if (x.has_psp)
+        for (int i = 0; i < scene->n_spheres; ++i) (void)project_sphere_persp(*eye, scene->spheres[i], W, H, x.psp.s[i]);
 }
 
 // Ray-traced primitives of a (validated) scene, with iCappedCone's
@@ -273,13 +401,13 @@ int build_frame(FrameArgs& a, const rtm_scene* scene, const rtm_camera* eye, con
     // and a PERSPECTIVE eye is exact (testscene_raytracingPlane0, main.rs:1016).
     if (shadow->type != RTM_CAMERA_ORTHOGONAL)
         return fail(RTM_ERR_UNSUPPORTED, "frame path needs an ORTHOGONAL shadow camera");
-    if (eye->type != RTM_CAMERA_ORTHOGONAL && scene->n_spheres > 0)
-        return fail(RTM_ERR_UNSUPPORTED, "spheres under a PERSPECTIVE eye camera need projectSphere (row f-3)");
     std::memset(&a, 0, sizeof a);
     ShadowPart& sh = a.sh;
     EyePart& ey = a.ey;
+    PerspSphK unused;
     for (int i = 0; i < scene->n_spheres; ++i) {
-        ey.sph[i] = project_sphere(*eye, scene->spheres[i], W, H);
+        ey.sph[i] = eye->type == RTM_CAMERA_ORTHOGONAL ? project_sphere(*eye, scene->spheres[i], W, H)
+                                                       : project_sphere_persp(*eye, scene->spheres[i], W, H, unused);
         sh.sph[i] = project_sphere(*shadow, scene->spheres[i], W, H);
         ey.shade[i] = shade_sphere(scene->spheres[i]);
     }
@@ -378,6 +506,7 @@ struct rtm_ctx {
     DevBuf enc_rgb, enc_rows, enc_text;  // writeColorImage scratch
     DevBuf enc_tab;                      // EncodeTable on the device (t | bucket)
     DevBuf rtk;                          // RtK of the frame being enqueued (row f-1)
+    DevBuf pspk;                         // PerspK of the frame being enqueued (row f-3)
     std::vector<rtm_viewport*> viewports;  // live viewports (orphaned when the context goes first)
     bool enc_tab_ready = false;
     uint64_t tab_key = 0;
@@ -601,11 +730,21 @@ int upload_rt(rtm_ctx* ctx, const RtK& rt, const RtK** dev) {
     return RTM_OK;
 }
 
-int enqueue_frame(rtm_ctx* ctx, FrameArgs& a, const RtK* rt_host, float* out_dev, StatsK* stats) {
+int upload_persp(rtm_ctx* ctx, const PerspK& k, const PerspK** dev) {
+    int rc = ctx->pspk.ensure(sizeof(PerspK), ctx->device);
+    if (rc) return rc;
+    if ((rc = launch_persp_upload(k, (PerspK*)ctx->pspk.p, ctx->stream))) return fail(rc, "upload launch failed");
+    *dev = (const PerspK*)ctx->pspk.p;
+    return RTM_OK;
+}
+
+int enqueue_frame(rtm_ctx* ctx, FrameArgs& a, const FrameExtra* x, float* out_dev, StatsK* stats) {
     int rc;
     if ((rc = frame_tables(ctx, a))) return rc;
     const RtK* rt = nullptr;
-    if (rt_host && (rc = upload_rt(ctx, *rt_host, &rt))) return rc;
+    const PerspK* psp = nullptr;
+    if (x && x->has_rt && (rc = upload_rt(ctx, x->rt, &rt))) return rc;
+    if (x && x->has_psp && (rc = upload_persp(ctx, x->psp, &psp))) return rc;
     const bool fused = (a.ey.flags & RTM_FLAG_FUSED_SHADOW) != 0;
     hipStream_t s = ctx->stream;
     double* smap = nullptr;
@@ -624,7 +763,7 @@ int enqueue_frame(rtm_ctx* ctx, FrameArgs& a, const RtK* rt_host, float* out_dev
         ctx->have_shadow_pass = false;
     }
     if (slot) HIP_TRY(hipEventRecord(slot->ev[2], s));
-    if ((rc = launch_eye_pass(a, smap, out_dev, s, stats, rt))) return fail(rc, "eye pass launch failed");
+    if ((rc = launch_eye_pass(a, smap, out_dev, s, stats, rt, psp))) return fail(rc, "eye pass launch failed");
     if (slot) {
         HIP_TRY(hipEventRecord(slot->ev[3], s));
         slot->shadow = !fused;
@@ -645,11 +784,7 @@ rtm_ctx* default_ctx(int* rc) {
     return c.get();
 }
 
-int check_ortho_raster(const rtm_camera& c, const rtm_scene* scene) {
-    if (c.type != RTM_CAMERA_ORTHOGONAL && scene->n_spheres > 0)
-        return fail(RTM_ERR_UNSUPPORTED, "rasterize: perspective projectSphere (main.rs:473-530) is not on this path");
-    return RTM_OK;
-}
+
 
 }  // namespace
 
@@ -775,10 +910,10 @@ int rtm_render_async(rtm_ctx* ctx, const rtm_scene* scene, const rtm_camera* eye
         return fail(RTM_ERR_INVALID, "row range [%d,%d) outside [0,%d)", row_begin, row_end, height);
     a.ey.row_begin = row_begin;
     a.ey.row_end = row_end;
-    RtK rt;
-    const bool has_rt = build_rt(scene, rt);
+    FrameExtra x;
+    build_extra(scene, eye, width, height, x);
     DeviceGuard g(ctx->device);
-    return enqueue_frame(ctx, a, has_rt ? &rt : nullptr, out_rgba_dev, nullptr);
+    return enqueue_frame(ctx, a, &x, out_rgba_dev, nullptr);
 }
 
 const double* rtm_ctx_shadow_map(rtm_ctx* ctx) {
@@ -793,12 +928,13 @@ int rtm_render_frames_async(rtm_ctx* ctx, int32_t n_frames, const rtm_scene* sce
     for (int32_t i = 0; i < n_frames; ++i)
         if (!out_rgba_dev[i]) return fail(RTM_ERR_INVALID, "out_rgba_dev[%d] is NULL", i);
     std::vector<FrameArgs> f((size_t)n_frames);
-    std::vector<RtK> rt((size_t)n_frames);
+    std::vector<FrameExtra> ex((size_t)n_frames);
     bool any_rt = false;
     for (int32_t i = 0; i < n_frames; ++i) {
         int rc = build_frame(f[(size_t)i], &scenes[i], eye, shadow, width, height, march_steps, flags);
         if (rc) return rc;
-        any_rt |= build_rt(&scenes[i], rt[(size_t)i]);
+        build_extra(&scenes[i], eye, width, height, ex[(size_t)i]);
+        any_rt |= ex[(size_t)i].has_rt || ex[(size_t)i].has_psp;
     }
     DeviceGuard g(ctx->device);
     // The pipelined launch (shadow pass of frame i + eye pass of frame i-1) is
@@ -811,15 +947,14 @@ int rtm_render_frames_async(rtm_ctx* ctx, int32_t n_frames, const rtm_scene* sce
     }();
     // The pipeline shares one table set: every frame must have the same patches
     // (the cameras are shared by construction).  Otherwise render frame by frame.
-    // (frames with ray-traced primitives always take the two-kernel path)
+    // (frames with ray-traced primitives or perspective spheres always take the two-kernel path)
     bool same = pipeline_on && !any_rt && (flags & RTM_FLAG_FUSED_SHADOW) == 0 && n_frames > 1;
     for (int32_t i = 1; same && i < n_frames; ++i)
         same = f[(size_t)i].sh.n_patches == f[0].sh.n_patches &&
                std::memcmp(f[(size_t)i].sh.patch, f[0].sh.patch, sizeof(PatchK) * (size_t)f[0].sh.n_patches) == 0;
     if (!same) {
         for (int32_t i = 0; i < n_frames; ++i) {
-            const RtK* r = rt[(size_t)i].n_pl + rt[(size_t)i].n_cy > 0 ? &rt[(size_t)i] : nullptr;
-            int rc = enqueue_frame(ctx, f[(size_t)i], r, out_rgba_dev[i], nullptr);
+            int rc = enqueue_frame(ctx, f[(size_t)i], &ex[(size_t)i], out_rgba_dev[i], nullptr);
             if (rc) return rc;
         }
         return RTM_OK;
@@ -888,12 +1023,12 @@ int rtm_render(const rtm_scene* scene, const rtm_camera* eye, const rtm_camera* 
     if (rc) return rc;
     rtm_ctx* ctx = default_ctx(&rc);
     if (!ctx) return rc;
-    RtK rt;
-    const bool has_rt = build_rt(scene, rt);
+    FrameExtra x;
+    build_extra(scene, eye, width, height, x);
     DeviceGuard g(ctx->device);
     const size_t bytes = sizeof(float) * 4 * (size_t)width * (size_t)height;
     if ((rc = ctx->out.ensure(bytes, ctx->device))) return rc;
-    if ((rc = enqueue_frame(ctx, a, has_rt ? &rt : nullptr, (float*)ctx->out.p, nullptr))) return rc;
+    if ((rc = enqueue_frame(ctx, a, &x, (float*)ctx->out.p, nullptr))) return rc;
     HIP_TRY(hipMemcpyAsync(out_rgba, ctx->out.p, bytes, hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(hipStreamSynchronize(ctx->stream));
     return RTM_OK;
@@ -905,14 +1040,14 @@ int rtm_render_stats(rtm_ctx* ctx, const rtm_scene* scene, const rtm_camera* eye
     FrameArgs a;
     int rc = build_frame(a, scene, eye, shadow, width, height, march_steps, flags);
     if (rc) return rc;
-    RtK rt;
-    const bool has_rt = build_rt(scene, rt);
+    FrameExtra x;
+    build_extra(scene, eye, width, height, x);
     DeviceGuard g(ctx->device);
     const size_t bytes = sizeof(float) * 4 * (size_t)width * (size_t)height;
     if ((rc = ctx->out.ensure(bytes, ctx->device))) return rc;
     if ((rc = ctx->stats.ensure(sizeof(StatsK), ctx->device))) return rc;
     HIP_TRY(hipMemsetAsync(ctx->stats.p, 0, sizeof(StatsK), ctx->stream));
-    if ((rc = enqueue_frame(ctx, a, has_rt ? &rt : nullptr, (float*)ctx->out.p, (StatsK*)ctx->stats.p))) return rc;
+    if ((rc = enqueue_frame(ctx, a, &x, (float*)ctx->out.p, (StatsK*)ctx->stats.p))) return rc;
     HIP_TRY(hipMemcpyAsync(out, ctx->stats.p, sizeof(StatsK), hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(hipStreamSynchronize(ctx->stream));
     return RTM_OK;
@@ -1041,11 +1176,14 @@ void rtm_viewport_destroy(rtm_viewport* vp) {
 int rtm_viewport_rasterize(rtm_viewport* vp, const rtm_scene* scene) {
     if (!vp || !vp->ctx) return fail(RTM_ERR_INVALID, "viewport is NULL or its context was destroyed");
     int rc;
-    if ((rc = validate_scene(scene)) || (rc = check_ortho_raster(vp->cam, scene))) return rc;
+    if ((rc = validate_scene(scene))) return rc;
     if (scene->n_spheres == 0) return RTM_OK;  // main.rs:447: nothing to project
     RasterArgs a;
     std::memset(&a, 0, sizeof a);
-    for (int i = 0; i < scene->n_spheres; ++i) a.sph[i] = project_sphere(vp->cam, scene->spheres[i], vp->W, vp->H);
+    a.persp = vp->cam.type != RTM_CAMERA_ORTHOGONAL;
+    for (int i = 0; i < scene->n_spheres; ++i)
+        a.sph[i] = a.persp ? project_sphere_persp(vp->cam, scene->spheres[i], vp->W, vp->H, a.psp[i])
+                           : project_sphere(vp->cam, scene->spheres[i], vp->W, vp->H);
     a.n_spheres = scene->n_spheres;
     a.face = vp->face;
     a.W = vp->W;

@@ -144,10 +144,27 @@ struct RtK {
 static_assert(sizeof(PlaneK) == 88 && sizeof(CylK) == 152, "RtK layout");
 static_assert(sizeof(RtK) + sizeof(void*) <= 4096, "RtK must fit the upload kernel's kernarg segment");
 
+// One sphere as seen by a PERSPECTIVE camera (row f-3; Viewport::rasterize,
+// main.rs:473-524 + projectSphere, main.rs:2796-2837): the ellipse centre and
+// its two (perpendicular, not axis-aligned) axes as calcEllipseDistToCenter uses
+// them (main.rs:2848-2852): n = axis.normalized(), m = axis.magnitude().
+// z, r, id and the pixel ranges stay in the RasterSphereK of the same index.
+struct PerspSphK {
+    double cx, cy;
+    double nAx, nAy, nBx, nBy;
+    double mA, mB;
+};
+struct PerspK {
+    PerspSphK s[RTM_MAX_SPHERES];
+};
+static_assert(sizeof(PerspK) + sizeof(void*) <= 4096, "PerspK must fit the upload kernel's kernarg segment");
+
 // Reference-seam kernels (one per reference function).
 struct RasterArgs {
     RasterSphereK sph[RTM_MAX_SPHERES];
+    PerspSphK psp[RTM_MAX_SPHERES];  // used when persp != 0
     int32_t n_spheres, face, W, H;
+    int32_t persp, pad;
 };
 
 struct MarchArgs {
@@ -187,12 +204,15 @@ static_assert(sizeof(StatsK) == sizeof(rtm_stats), "StatsK layout");
 
 // Launchers (rtm_kernels.hip).  All asynchronous on `stream`.
 int launch_shadow_pass(const FrameArgs& a, double* smap, void* stream, StatsK* stats);
-// rt != nullptr: the frame has ray-traced primitives (device RtK, see launch_rt_upload).
+// rt / psp != nullptr: the frame has ray-traced primitives / a PERSPECTIVE eye
+// with spheres (device RtK / PerspK, see launch_upload); either selects the
+// general eye kernel.
 int launch_eye_pass(const FrameArgs& a, const double* smap, float* out, void* stream, StatsK* stats,
-                    const RtK* rt = nullptr);
-// Stream-ordered copy of a host RtK into device memory (a kernel, so the host
-// copy is consumed at launch: no pinned staging, no host synchronisation).
+                    const RtK* rt = nullptr, const PerspK* psp = nullptr);
+// Stream-ordered copy of a host struct into device memory (a kernel, so the
+// host copy is consumed at launch: no pinned staging, no host synchronisation).
 int launch_rt_upload(const RtK& k, RtK* dst, void* stream);
+int launch_persp_upload(const PerspK& k, PerspK* dst, void* stream);
 // Software-pipelined frame step: the shadow pass of a.sh into smap_w and the eye
 // pass of a.ey (the previous frame) from smap_r into out, in ONE launch whose
 // workgroups interleave the two roles (VALU-bound and HBM-store-bound tiles

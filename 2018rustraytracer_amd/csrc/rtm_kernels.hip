@@ -66,6 +66,21 @@ __device__ __forceinline__ bool may_cover(const RasterSphereK& s, int xb, int xe
     return y >= s.iy0 && y <= s.iy1 && xe >= s.ix0 && xb <= s.ix1;
 }
 
+// Coverage under a PERSPECTIVE camera (row f-3): the same test with the general
+// ellipse axes of projectSphere (main.rs:2848-2852, 2098-2109).
+__device__ __forceinline__ bool cover_persp(const PerspSphK& s, double x, double y, double& h) {
+    const double relx = x - s.cx;
+    const double rely = y - s.cy;
+    const double pa = (relx * s.nAx + rely * s.nAy) / s.mA;
+    const double pb = (relx * s.nBx + rely * s.nBy) / s.mB;
+    const double d = sqrt(pa * pa + pb * pb);
+    if (d < 1.0) {
+        h = sqrt(1.0 - d * d);
+        return true;
+    }
+    return false;
+}
+
 // Sphere coverage of one pixel (projectSphereAtZBuffer, main.rs:176-195):
 // calcOthoDistanceByAbsPosition -> calcEllipseDistToCenter -> calcHeightOfSphereOnUnit.
 __device__ __forceinline__ bool cover(const RasterSphereK& s, double x, double y, double& h) {
@@ -1026,7 +1041,7 @@ __global__ __launch_bounds__(BLOCK) void shadow_lean_kernel(const FrameArgs a, d
 template <bool FUSED, bool COUNT, bool RT>
 __device__ __forceinline__ void eye_tile(const EyePart& a, const ShadowPart& sh, const double* __restrict__ smap,
                                          float4* __restrict__ out, int bx, int by, StatsK* __restrict__ st,
-                                         const RtK* __restrict__ rt) {
+                                         const RtK* __restrict__ rt, const PerspK* __restrict__ psp = nullptr) {
     const int xb = bx * TILE_X;
     const int xi = xb + (threadIdx.x & (TILE_X - 1));
     const int yl = __builtin_amdgcn_readfirstlane(by * TILE_Y + (threadIdx.x >> 6));
@@ -1044,7 +1059,8 @@ __device__ __forceinline__ void eye_tile(const EyePart& a, const ShadowPart& sh,
         for (int i = 0; i < a.n_spheres; ++i) {
             if (!may_cover(a.sph[i], xb, xb + TILE_X - 1, yi)) continue;
             double h;
-            if (cover(a.sph[i], x, y, h)) {
+            // (RT variant only: a PERSPECTIVE eye with spheres, row f-3; psp is wave-uniform)
+            if ((RT && psp) ? cover_persp(psp->s[i], x, y, h) : cover(a.sph[i], x, y, h)) {
                 if (COUNT) ++n_tests;
                 const double depth = a.sph[i].z - h * a.sph[i].r;  // EnumFace::FRONT (main.rs:239)
                 if (depth < best) {
@@ -1061,7 +1077,7 @@ __device__ __forceinline__ void eye_tile(const EyePart& a, const ShadowPart& sh,
         double o[3], d[3];
         if (RT) {
             cam_ray(a.eye, x, y, o, d);
-            trace_pixel(rt, o, d, best, hit);
+            if (rt) trace_pixel(rt, o, d, best, hit);
         }
         float4 c = make_float4(0.0f, 0.2f, 0.2f, 1.0f);  // (0.0, 0.2, 0.2) as f32 (main.rs:718-720)
         if (hit.kind) {
@@ -1189,14 +1205,15 @@ __global__ __launch_bounds__(BLOCK) void shadow_sep_kernel(const FrameArgs a, do
 template <bool FUSED, bool COUNT, bool RT>
 __global__ __launch_bounds__(BLOCK) void eye_pass_kernel(const FrameArgs a, const double* __restrict__ smap,
                                                          float4* __restrict__ out, StatsK* __restrict__ st,
-                                                         const RtK* __restrict__ rt) {
-    eye_tile<FUSED, COUNT, RT>(a.ey, a.sh, smap, out, blockIdx.x, blockIdx.y, st, rt);
+                                                         const RtK* __restrict__ rt, const PerspK* __restrict__ psp) {
+    eye_tile<FUSED, COUNT, RT>(a.ey, a.sh, smap, out, blockIdx.x, blockIdx.y, st, rt, psp);
 }
 
-// launch_rt_upload: one 8-byte word per thread from the kernarg copy.
-__global__ void rt_upload_kernel(const RtK k, RtK* __restrict__ dst) {
-    constexpr int N = (int)(sizeof(RtK) / sizeof(uint64_t));
-    static_assert(sizeof(RtK) % sizeof(uint64_t) == 0, "RtK size");
+// launch_*_upload: one 8-byte word per thread from the kernarg copy.
+template <class T>
+__global__ void upload_kernel(const T k, T* __restrict__ dst) {
+    constexpr int N = (int)(sizeof(T) / sizeof(uint64_t));
+    static_assert(sizeof(T) % sizeof(uint64_t) == 0, "upload size");
     const uint64_t* src = reinterpret_cast<const uint64_t*>(&k);
     uint64_t* d = reinterpret_cast<uint64_t*>(dst);
     for (int i = threadIdx.x; i < N; i += blockDim.x) d[i] = src[i];
@@ -1260,7 +1277,7 @@ __global__ __launch_bounds__(BLOCK) void vp_rasterize_kernel(const RasterArgs a,
     for (int i = 0; i < a.n_spheres; ++i) {
         if (!may_cover(a.sph[i], xb, xb + TILE_X - 1, yi)) continue;
         double h;
-        if (cover(a.sph[i], x, y, h)) {
+        if (a.persp ? cover_persp(a.psp[i], x, y, h) : cover(a.sph[i], x, y, h)) {
             const double hr = h * a.sph[i].r;
             const double depth = a.face == RTM_FACE_FRONT ? a.sph[i].z - hr : a.sph[i].z + hr;
             if (depth < zb) {
@@ -1570,7 +1587,7 @@ int launch_shadow_pass(const FrameArgs& a, double* smap, void* stream, StatsK* s
 }
 
 int launch_eye_pass(const FrameArgs& a, const double* smap, float* out, void* stream, StatsK* stats,
-                    const RtK* rt) {
+                    const RtK* rt, const PerspK* psp) {
     hipStream_t s = (hipStream_t)stream;
     dim3 g = grid_for(a.ey.W, a.ey.row_end - a.ey.row_begin);
     float4* o = reinterpret_cast<float4*>(out);
@@ -1579,8 +1596,9 @@ int launch_eye_pass(const FrameArgs& a, const double* smap, float* out, void* st
         hipLaunchKernelGGL(eye_store_only_kernel, g, dim3(BLOCK), 0, s, a, o);
         return launched();
     }
-#define RTM_EYE(F, C, R) hipLaunchKernelGGL((eye_pass_kernel<F, C, R>), g, dim3(BLOCK), 0, s, a, smap, o, stats, rt)
-    if (rt) {
+#define RTM_EYE(F, C, R) \
+    hipLaunchKernelGGL((eye_pass_kernel<F, C, R>), g, dim3(BLOCK), 0, s, a, smap, o, stats, rt, psp)
+    if (rt || psp) {
         if (fused && stats) RTM_EYE(true, true, true);
         else if (fused) RTM_EYE(true, false, true);
         else if (stats) RTM_EYE(false, true, true);
@@ -1596,7 +1614,12 @@ int launch_eye_pass(const FrameArgs& a, const double* smap, float* out, void* st
 }
 
 int launch_rt_upload(const RtK& k, RtK* dst, void* stream) {
-    hipLaunchKernelGGL(rt_upload_kernel, dim3(1), dim3(512), 0, (hipStream_t)stream, k, dst);
+    hipLaunchKernelGGL(upload_kernel<RtK>, dim3(1), dim3(512), 0, (hipStream_t)stream, k, dst);
+    return launched();
+}
+
+int launch_persp_upload(const PerspK& k, PerspK* dst, void* stream) {
+    hipLaunchKernelGGL(upload_kernel<PerspK>, dim3(1), dim3(256), 0, (hipStream_t)stream, k, dst);
     return launched();
 }
 

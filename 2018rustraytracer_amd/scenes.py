@@ -298,3 +298,23 @@ CONFIGS = {
             eye=perspective_eye_camera,
             desc="512x512, testscene_raytracingPlane0 as main() renders it (row f-1)"),
 }
+
+
+# ---- row f-3: testscene_perspectiveSimple1/2 (main.rs:1059-1316) ----
+def perspective_simple1() -> Scene:
+    """testscene_perspectiveSimple1 (main.rs:1059-1182): one sphere in front of
+    the PERSPECTIVE eye camera at the origin; no shadow pass (main.rs:1115-1120).
+    Render with perspective_eye_camera(), shadow_camera(), RAYTRACING_FLAGS."""
+    return Scene([PrimitiveSphere(0, Shading(0.02, 0.02, 1.0), (0.01, 0.01, 4.0), 0.5)], [])
+
+
+def perspective_simple2() -> Scene:
+    """testscene_perspectiveSimple2 (main.rs:1184-1316): two spheres; render with
+    perspective_simple2_camera()."""
+    return Scene([PrimitiveSphere(0, Shading(0.02, 0.02, 1.0), (0.01, 0.01, 4.0), 0.5),
+                  PrimitiveSphere(1, Shading(0.02, 1.0, 0.02), (0.01, 0.01, 6.0), 0.5)], [])
+
+
+def perspective_simple2_camera() -> Camera:
+    """viewport0's camera of testscene_perspectiveSimple2 (main.rs:1283-1295)."""
+    return Camera(PERSPECTIVE, (0.0, 1.5, 0.0), (0.0, 0.0, 1.0), (0.0, 1.0, 0.0), (1.0, 0.0, 0.0))

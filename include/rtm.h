@@ -53,7 +53,7 @@ extern "C" {
 /* ---- status codes ---- */
 #define RTM_OK 0
 #define RTM_ERR_INVALID -1     /* bad argument (null, size, id out of range, ...) */
-#define RTM_ERR_UNSUPPORTED -2 /* valid in the reference but not on this path (perspective rasterize) */
+#define RTM_ERR_UNSUPPORTED -2 /* valid in the reference but not on this path (a non-orthographic shadow camera) */
 #define RTM_ERR_HIP -3         /* a HIP runtime call failed */
 #define RTM_ERR_NO_DEVICE -4   /* no usable gfx950 device */
 #define RTM_ERR_OOM -5         /* device allocation failed */
@@ -185,10 +185,11 @@ int rtm_ctx_kernel_ms_history(rtm_ctx* ctx, float* shadow_pass_ms, float* eye_pa
  * processRaymarchingRays; eye viewport (face FRONT) rasterize +
  * processRaytracingRays; renderColorImage (main.rs:1568-1628, 1033-1045).
  * Cameras: the shadow camera must be ORTHOGONAL (Camera::project asserts it,
- * main.rs:1949); the eye camera may be PERSPECTIVE only in a scene without
- * spheres (perspective sphere projection is BASELINE row f-3 ->
- * RTM_ERR_UNSUPPORTED).  out_rgba: width*height*4 floats. Uses a per-thread
- * default context on device 0. */
+ * main.rs:1949 -> RTM_ERR_UNSUPPORTED); the eye camera may be ORTHOGONAL or
+ * PERSPECTIVE (spheres then project through nalgebra's Perspective3 and
+ * projectSphere, main.rs:473-530, 2796-2837, with the aspect 512/512
+ * generalised to width/height).  out_rgba: width*height*4 floats. Uses a
+ * per-thread default context on device 0. */
 int rtm_render(const rtm_scene* scene, const rtm_camera* eye, const rtm_camera* shadow,
                int32_t width, int32_t height, int32_t march_steps, int32_t flags,
                float* out_rgba);
@@ -246,9 +247,9 @@ typedef struct rtm_viewport rtm_viewport;
 int rtm_viewport_create(rtm_ctx* ctx, int32_t width, int32_t height, int32_t face,
                         const rtm_camera* camera, rtm_viewport** out);
 void rtm_viewport_destroy(rtm_viewport* vp);
-/* Viewport::rasterize (main.rs:445): spheres need an ORTHOGONAL camera
- * (perspective projection is BASELINE "next" row f-3 -> RTM_ERR_UNSUPPORTED);
- * a scene without spheres is a no-op for either camera type. */
+/* Viewport::rasterize (main.rs:445): ORTHOGONAL (main.rs:452-471) or
+ * PERSPECTIVE (main.rs:473-524) projection of every sphere, then
+ * rasterizeSphere into the viewport's zBuffer / G-buffer. */
 int rtm_viewport_rasterize(rtm_viewport* vp, const rtm_scene* scene);
 /* Viewport::processRaytracingRays (main.rs:569-642): every pixel's camera ray
  * against the circle planes, then the capped cylinders, in scene order; a hit

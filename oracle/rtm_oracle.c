@@ -282,13 +282,139 @@ static void rasterizeSphere(const ProjectedSphere* ps, double r, Viewport* vp, i
     }
 }
 
-/* Viewport::rasterize, ORTHOGONAL branch (main.rs:445-471, 540-542) over rows [y0,y1).
- * The PERSPECTIVE branch (main.rs:473-530, row f-3) is not restated: with no
- * spheres it does nothing, otherwise RTM_ERR_UNSUPPORTED. */
+/* ---- PERSPECTIVE sphere projection (row f-3, main.rs:473-530, 2796-2837) ----
+ * nalgebra (Cargo.toml: nalgebra = "^0.16.12"; not in /root/reference, no
+ * Cargo.lock) is restated from its published 0.16 source:
+ *   Matrix4::new(m11, m12, …) takes its 16 elements row by row;
+ *   Matrix * Matrix / Vector (fixed 4x4) = gemm → per output column one gemv,
+ *     y_i = v_0*m_i0, then y_i = v_j*m_ij + 1*y_i for j = 1..3 (axpy), i.e.
+ *     ((m_i0 v_0 + m_i1 v_1) + m_i2 v_2) + m_i3 v_3, zero terms included;
+ *   Perspective3::new(aspect, fovy, znear, zfar): identity, then set_fovy
+ *     (m11 = 1 / tan(fovy / 2); m00 = m00 * (m11 / old m11)), set_aspect
+ *     (m00 = m11 / aspect), set_znear_and_zfar (m22 = (zfar + znear) /
+ *     (znear - zfar); m23 = zfar * znear * 2 / (znear - zfar)), m33 = 0, m32 = -1;
+ *   Matrix4::new_nonuniform_scaling(v) = identity with the diagonal v.
+ * tan is the platform libm's, as Rust's f64::tan.  No reference output exists
+ * for this branch: parity unpinned, cross-checked against the
+ * independent restatement in tests/golden/gen_golden.py. */
+typedef struct { double m[4][4]; } M44;
+
+static M44 m44_identity(void) {
+    M44 r;
+    memset(&r, 0, sizeof r);
+    for (int i = 0; i < 4; i++) r.m[i][i] = 1.0;
+    return r;
+}
+
+/* nalgebra gemv: y = a * x (fixed 4x4, column-by-column axpy) */
+static void m44_gemv(const M44* a, const double x[4], double y[4]) {
+    for (int i = 0; i < 4; i++) y[i] = x[0] * a->m[i][0];
+    for (int j = 1; j < 4; j++)
+        for (int i = 0; i < 4; i++) y[i] = x[j] * a->m[i][j] + 1.0 * y[i];
+}
+
+/* nalgebra gemm: r = a * b, one gemv per column of b */
+static M44 m44_mul(const M44* a, const M44* b) {
+    M44 r;
+    for (int j = 0; j < 4; j++) {
+        double x[4] = {b->m[0][j], b->m[1][j], b->m[2][j], b->m[3][j]}, y[4];
+        m44_gemv(a, x, y);
+        for (int i = 0; i < 4; i++) r.m[i][j] = y[i];
+    }
+    return r;
+}
+
+/* mul (main.rs:2321-2326): (m * (v, 1.0)).xyz */
+static Vec3 m44_mul_point(const M44* m, Vec3 v) {
+    double x[4] = {v.x, v.y, v.z, 1.0}, y[4];
+    m44_gemv(m, x, y);
+    return v3(y[0], y[1], y[2]);
+}
+
+/* Perspective3::new(aspect, fovy, znear, zfar).to_homogeneous() */
+static M44 perspective3(double aspect, double fovy, double znear, double zfar) {
+    M44 p = m44_identity();
+    double old_m22 = p.m[1][1];
+    p.m[1][1] = 1.0 / tan(fovy / 2.0);
+    p.m[0][0] = p.m[0][0] * (p.m[1][1] / old_m22);
+    p.m[0][0] = p.m[1][1] / aspect;
+    p.m[2][2] = (zfar + znear) / (znear - zfar);
+    p.m[2][3] = zfar * znear * 2.0 / (znear - zfar);
+    p.m[3][3] = 0.0;
+    p.m[3][2] = -1.0;
+    return p;
+}
+
+/* projectSphere (main.rs:2796-2837): center and the two ellipse axes */
+static void projectSphere(const double sphere[4], const M44* cameraMat, double fle, Vec2* center, Vec2* axa,
+                          Vec2* axb) {
+    Vec3 o = m44_mul_point(cameraMat, v3(sphere[0], sphere[1], sphere[2]));
+    double r2 = sphere[3] * sphere[3];
+    double z2 = o.z * o.z;
+    double l2 = dot(o, o);
+    *axa = v2_scale(v2(o.x, o.y), fle * sqrt(-r2 * (r2 - l2) / ((l2 - z2) * (r2 - z2) * (r2 - z2))));
+    *axb = v2_scale(v2(-o.y, o.x), fle * sqrt(-r2 * (r2 - l2) / ((l2 - z2) * (r2 - z2) * (r2 - l2))));
+    *center = v2_scale(v2(o.x, o.y), fle * o.z / (z2 - r2));
+}
+
+/* Viewport::rasterize's per-sphere projection, PERSPECTIVE branch (main.rs:473-524).
+ * The image aspect generalises (512 as f64) / (512 as f64) (main.rs:496) to W / H. */
+void rtmo_project_sphere_perspective(const rtm_camera* cam, int32_t W, int32_t H, const double pos[3], double r,
+                                     double out[6]) {
+    Camera c = camera_from(cam, W, H);
+    M44 rel;
+    memset(&rel, 0, sizeof rel);
+    rel.m[0][0] = c.side.x; rel.m[0][1] = c.side.y; rel.m[0][2] = c.side.z;
+    rel.m[1][0] = c.up.x;   rel.m[1][1] = c.up.y;   rel.m[1][2] = c.up.z;
+    rel.m[2][0] = c.dir.x;  rel.m[2][1] = c.dir.y;  rel.m[2][2] = c.dir.z;
+    rel.m[3][3] = 1.0;
+    Vec3 local = m44_mul_point(&rel, v3_sub(v3(pos[0], pos[1], pos[2]), c.pos));
+    double fov = 3.14 / 2.0;
+    M44 persp = perspective3((double)W / (double)H, fov, 0.1, 1000.0);
+    M44 refl = m44_identity();
+    refl.m[2][2] = -1.0;  /* new_nonuniform_scaling(&Vector3::new(1.0, 1.0, -1.0)) */
+    M44 cameraMat = m44_mul(&persp, &refl);
+    double sphere4[4] = {local.x, local.y, local.z, r};
+    Vec2 center, axa, axb;
+    projectSphere(sphere4, &cameraMat, fov, &center, &axa, &axb);
+    out[0] = center.x;
+    out[1] = center.y;
+    out[2] = axa.x;
+    out[3] = axa.y;
+    out[4] = axb.x;
+    out[5] = axb.y;
+}
+
+/* Viewport::rasterize (main.rs:445-547) over rows [y0,y1): ORTHOGONAL
+ * (main.rs:452-471) or PERSPECTIVE (main.rs:473-524, row f-3) projection,
+ * then rasterizeSphere (main.rs:540-542). */
 static int viewport_rasterize(Viewport* vp, const rtm_scene* scene, int flags, int64_t y0, int64_t y1,
                               int64_t* tests) {
     if (scene->n_spheres == 0) return RTM_OK;
-    if (vp->camera.type != RTM_CAMERA_ORTHOGONAL) return RTM_ERR_UNSUPPORTED;
+    if (vp->camera.type != RTM_CAMERA_ORTHOGONAL) {
+        rtm_camera cc;
+        memset(&cc, 0, sizeof cc);
+        cc.type = vp->camera.type;
+        cc.pos[0] = vp->camera.pos.x; cc.pos[1] = vp->camera.pos.y; cc.pos[2] = vp->camera.pos.z;
+        cc.dir[0] = vp->camera.dir.x; cc.dir[1] = vp->camera.dir.y; cc.dir[2] = vp->camera.dir.z;
+        cc.up[0] = vp->camera.up.x;   cc.up[1] = vp->camera.up.y;   cc.up[2] = vp->camera.up.z;
+        cc.side[0] = vp->camera.side.x; cc.side[1] = vp->camera.side.y; cc.side[2] = vp->camera.side.z;
+        for (int32_t i = 0; i < scene->n_spheres; i++) {
+            const rtm_sphere* s = &scene->spheres[i];
+            Vec3 pos = v3(s->pos[0], s->pos[1], s->pos[2]);
+            double pr[6];
+            rtmo_project_sphere_perspective(&cc, (int32_t)vp->W, (int32_t)vp->H, s->pos, s->r, pr);
+            ProjectedSphere ps;
+            ps.id = s->id;
+            ps.z = calcDepthOfProjectedPoint(&vp->camera, pos);
+            ps.center = v2(pr[0], pr[1]);
+            ps.r = s->r;
+            ps.axisA = v2(pr[2], pr[3]);
+            ps.axisB = v2(pr[4], pr[5]);
+            rasterizeSphere(&ps, ps.r, vp, flags, y0, y1, tests);
+        }
+        return RTM_OK;
+    }
     for (int32_t i = 0; i < scene->n_spheres; i++) {
         const rtm_sphere* s = &scene->spheres[i];
         Vec3 pos = v3(s->pos[0], s->pos[1], s->pos[2]);
@@ -636,7 +762,6 @@ int rtmo_render(const rtm_scene* scene, const rtm_camera* eye, const rtm_camera*
     if (rc) return rc;
     if (!eye || !shadow || !out_rgba || W <= 0 || H <= 0 || steps < 0) return RTM_ERR_INVALID;
     if (shadow->type != RTM_CAMERA_ORTHOGONAL) return RTM_ERR_UNSUPPORTED;
-    if (eye->type != RTM_CAMERA_ORTHOGONAL && scene->n_spheres > 0) return RTM_ERR_UNSUPPORTED;
     Viewport vs, ve;
     viewport_init(&vs, W, H, RTM_FACE_BACK, shadow);
     viewport_init(&ve, W, H, RTM_FACE_FRONT, eye);

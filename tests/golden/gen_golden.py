@@ -197,18 +197,80 @@ def raytrace(cam, planes, cyls, W, H, zbuf, g):
                 g["n%d" % k][win] = n[k][win]
 
 
+# ---- row f-3: perspective projection (main.rs:473-530, 2796-2837; nalgebra 0.16) ----
+def _gemv(a, x):
+    """nalgebra fixed 4x4 gemv: y_i = v0*m_i0, then y_i = v_j*m_ij + 1*y_i."""
+    y = [x[0] * a[i][0] for i in range(4)]
+    for j in range(1, 4):
+        y = [x[j] * a[i][j] + 1.0 * y[i] for i in range(4)]
+    return y
+
+
+def _mm(a, b):
+    cols = [_gemv(a, [b[0][j], b[1][j], b[2][j], b[3][j]]) for j in range(4)]
+    return [[cols[j][i] for j in range(4)] for i in range(4)]
+
+
+def _perspective3(aspect, fovy, znear, zfar):
+    p = [[1.0 if i == j else 0.0 for j in range(4)] for i in range(4)]
+    old = p[1][1]
+    p[1][1] = 1.0 / math.tan(fovy / 2.0)            # set_fovy
+    p[0][0] = p[0][0] * (p[1][1] / old)
+    p[0][0] = p[1][1] / aspect                       # set_aspect
+    p[2][2] = (zfar + znear) / (znear - zfar)        # set_znear_and_zfar
+    p[2][3] = zfar * znear * 2.0 / (znear - zfar)
+    p[3][3] = 0.0
+    p[3][2] = -1.0
+    return p
+
+
+def project_perspective(cam, W, H, pos, r):
+    """(center, axisA, axisB) of a sphere seen by a PERSPECTIVE camera."""
+    rel = [[cam["side"][0], cam["side"][1], cam["side"][2], 0.0], [cam["up"][0], cam["up"][1], cam["up"][2], 0.0],
+           [cam["dir"][0], cam["dir"][1], cam["dir"][2], 0.0], [0.0, 0.0, 0.0, 1.0]]
+    diff = [pos[k] - cam["pos"][k] for k in range(3)]
+    local = _gemv(rel, diff + [1.0])[:3]
+    fov = 3.14 / 2.0
+    refl = [[1.0 if i == j else 0.0 for j in range(4)] for i in range(4)]
+    refl[2][2] = -1.0
+    cm = _mm(_perspective3(float(W) / float(H), fov, 0.1, 1000.0), refl)
+    o = _gemv(cm, local + [1.0])[:3]
+    r2 = r * r
+    z2 = o[2] * o[2]
+    l2 = (o[0] * o[0] + o[1] * o[1]) + o[2] * o[2]
+
+    def safe_sqrt(v):
+        return math.sqrt(v) if v >= 0.0 else float("nan")
+
+    with np.errstate(all="ignore"):
+        sa = fle_sqrt = fov * safe_sqrt(-r2 * (r2 - l2) / ((l2 - z2) * (r2 - z2) * (r2 - z2)))
+        sb = fov * safe_sqrt(-r2 * (r2 - l2) / ((l2 - z2) * (r2 - z2) * (r2 - l2)))
+    del fle_sqrt
+    axa = (o[0] * sa, o[1] * sa)
+    axb = (-o[1] * sb, o[0] * sb)
+    sc = fov * o[2] / (z2 - r2)
+    return (o[0] * sc, o[1] * sc), axa, axb
+
+
 def rasterize(cam, spheres, W, H, face, zbuf, gbuf):
-    """Viewport::rasterize, orthographic (main.rs:445-547), no bbox."""
+    """Viewport::rasterize (main.rs:445-547), orthographic or perspective, no bbox."""
     x, y = grid(W, H)
     for (sid, pos, r, _col) in spheres:
         diff = tuple(pos[k] - cam["pos"][k] for k in range(3))
         z = dot(cam["dir"], diff)
-        cx, cy = dot(diff, cam["side"]), dot(diff, cam["up"])
-        # calcEllipseDistToCenter with axisA=(r,0), axisB=(0,r)
-        mA = math.sqrt(r * r + 0.0 * 0.0)
-        nA = (r * (1.0 / mA), 0.0 * (1.0 / mA))
-        mB = math.sqrt(0.0 * 0.0 + r * r)
-        nB = (0.0 * (1.0 / mB), r * (1.0 / mB))
+        if cam["type"] == 0:
+            cx, cy = dot(diff, cam["side"]), dot(diff, cam["up"])
+            axA, axB = (r, 0.0), (0.0, r)
+        else:
+            (cx, cy), axA, axB = project_perspective(cam, W, H, pos, r)
+        # calcEllipseDistToCenter: Vec2::normalized = v.scale(1/|v|), |v| = sqrt(x*x + y*y)
+        mA = math.sqrt(axA[0] * axA[0] + axA[1] * axA[1]) if not any(map(math.isnan, axA)) else float("nan")
+        mB = math.sqrt(axB[0] * axB[0] + axB[1] * axB[1]) if not any(map(math.isnan, axB)) else float("nan")
+        with np.errstate(all="ignore"):
+            iA = np.float64(1.0) / np.float64(mA)
+            iB = np.float64(1.0) / np.float64(mB)
+        nA = (axA[0] * iA, axA[1] * iA)
+        nB = (axB[0] * iB, axB[1] * iB)
         relx, rely = x - cx, y - cy
         with np.errstate(all="ignore"):
             pa = (relx * nA[0] + rely * nA[1]) / mA
@@ -270,7 +332,6 @@ def render(spheres, patches, W, H, steps, no_march=False, no_sraster=False, plan
              z=np.zeros((H, W)), t=np.zeros((H, W)), n0=np.zeros((H, W)), n1=np.zeros((H, W)),
              n2=np.zeros((H, W)))
     if spheres:
-        assert eye["type"] == 0
         rasterize(eye, spheres, W, H, 0, ze, g)
     raytrace(eye, planes, cyls, W, H, ze, g)
     # renderColorImage (main.rs:710-902)
@@ -367,7 +428,16 @@ CASES = [
 ]
 
 # row f-1 cases: (name, spheres, patches, planes, cyls, eye, W, H, steps, flags, small)
+P1 = [(0, (0.01, 0.01, 4.0), 0.5, (0.02, 0.02, 1.0))]
+P2 = P1 + [(1, (0.01, 0.01, 6.0), 0.5, (0.02, 1.0, 0.02))]
+PERSP2_CAM = dict(PERSP_CAM, pos=(0.0, 1.5, 0.0))
+
 RT_CASES = [
+    ("f3_persp1_96", P1, [], [], [], PERSP_CAM, 96, 96, 0, 3, True),
+    ("f3_persp2_80x64", P2, [], [], [], PERSP2_CAM, 80, 64, 0, 3, True),
+    ("f3_persp1_512", P1, [], [], [], PERSP_CAM, 512, 512, 0, 3, False),
+    ("f3_persp2_512", P2, [], [], [], PERSP2_CAM, 512, 512, 0, 3, False),
+    ("f3_persp2_rt_640x360", P2, [], [REF_PLANE], [REF_CYL], PERSP2_CAM, 640, 360, 0, 3, False),
     ("rt_plane0_64", [], [], [], [REF_CYL], PERSP_CAM, 64, 64, 0, 3, True),
     ("rt_plane0_withplane_96x80", [], [], [REF_PLANE], [REF_CYL], PERSP_CAM, 96, 80, 0, 3, True),
     ("rt_rbench_128x72", [], [], *rbench(), PERSP_CAM, 128, 72, 0, 3, True),
@@ -406,7 +476,7 @@ def main():
                              planes=planes, cyls=cyls, eye=eye)
         golden[name] = dict(width=W, height=H, steps=K, flags=flags, rgba_sha256=sha_full(img),
                             shadow_sha256=sha_full(zs), eye_hits=st["eye_hits"], lit_pixels=st["lit"],
-                            circle_plane_pixels=st["plane_px"], capped_cylinder_pixels=st["cyl_px"])
+                            circle_plane_pixels=st.get("plane_px", 0), capped_cylinder_pixels=st.get("cyl_px", 0))
         if small:
             fixtures[name + "__rgba"] = img
             fixtures[name + "__shadow"] = zs

@@ -92,7 +92,8 @@ def test_argument_validation_without_gpu(rtm, scenes):
     assert lib.rtm_render(C.byref(sc), C.byref(e), C.byref(s), 2, 2, 1, 0x80, out) == abi.RTM_ERR_INVALID
     assert b"flags" in lib.rtm_last_error()
     p = scenes.Camera(scenes.PERSPECTIVE, (0, 0, 0), (0, 0, 1), (0, 1, 0), (1, 0, 0)).to_c()
-    assert lib.rtm_render(C.byref(sc), C.byref(p), C.byref(s), 2, 2, 1, 0, out) == abi.RTM_ERR_UNSUPPORTED
+    # a perspective shadow camera: Camera::project asserts ORTHOGONAL (main.rs:1949)
+    assert lib.rtm_render(C.byref(sc), C.byref(e), C.byref(p), 2, 2, 1, 0, out) == abi.RTM_ERR_UNSUPPORTED
     h = C.c_void_p()
     rc = lib.rtm_ctx_create(0, C.byref(h))
     if lib.rtm_device_count() == 0:

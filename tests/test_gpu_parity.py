@@ -249,8 +249,8 @@ def test_degenerate_spheres(rtm, oracle, scenes):
 def test_error_codes(rtm, scenes):
     abi = rtm.abi
     persp = scenes.Camera(scenes.PERSPECTIVE, (0, 0, 0), (0, 0, 1), (0, 1, 0), (1, 0, 0))
-    with pytest.raises(abi.RtmError) as e:
-        rtm.render_frame(scenes.scene_a_bench(), persp, scenes.shadow_camera(), 64, 64, 10)
+    with pytest.raises(abi.RtmError) as e:  # Camera::project asserts ORTHOGONAL (main.rs:1949)
+        rtm.render_frame(scenes.scene_a_bench(), scenes.eye_camera(), persp, 64, 64, 10)
     assert e.value.code == abi.RTM_ERR_UNSUPPORTED
     with pytest.raises(abi.RtmError) as e:
         rtm.render_frame(scenes.scene_a_bench(), scenes.eye_camera(), scenes.shadow_camera(), 0, 64, 10)

@@ -27,6 +27,15 @@ def _case(scenes, name):
         return scenes.scene_r_bench(), scenes.perspective_eye_camera()
     if name.startswith("rt_mixed_orbit"):
         return scenes.mixed_rt(100), scenes.eye_camera()
+    if name.startswith("f3_persp1"):
+        return scenes.perspective_simple1(), scenes.perspective_eye_camera()
+    if name.startswith("f3_persp2_rt"):
+        s = scenes.perspective_simple2()
+        s.circlePlanePrimitives = [scenes.dataclasses.replace(scenes.REFERENCE_CIRCLE_PLANE)]
+        s.cappedCylinderPrimitives = [scenes.dataclasses.replace(scenes.REFERENCE_CAPPED_CYLINDER)]
+        return s, scenes.perspective_simple2_camera()
+    if name.startswith("f3_persp2"):
+        return scenes.perspective_simple2(), scenes.perspective_simple2_camera()
     return _scene_for(scenes, name), scenes.eye_camera()
 
 
@@ -151,13 +160,24 @@ def test_no_march_and_no_raster_flags(oracle, scenes):
     assert r["stats"]["lit_pixels"] == r["stats"]["eye_hit_pixels"]
 
 
-def test_perspective_frame_is_unsupported(oracle, scenes):
-    """Spheres under a PERSPECTIVE eye camera need projectSphere (row f-3)."""
-    persp = scenes.perspective_eye_camera()
+def test_perspective_shadow_camera_is_unsupported(oracle, scenes):
+    """Camera::project asserts an ORTHOGONAL camera (main.rs:1949)."""
     with pytest.raises(RuntimeError):
-        oracle.render(scenes.scene_a_bench(), persp, scenes.shadow_camera(), 16, 16, 8, 0)
-    # ... a sphere-free scene (testscene_raytracingPlane0) is fine
-    oracle.render(scenes.raytracing_plane0(), persp, scenes.shadow_camera(), 16, 16, 0, scenes.RAYTRACING_FLAGS)
+        oracle.render(scenes.scene_a_bench(), scenes.eye_camera(), scenes.perspective_eye_camera(), 16, 16, 8, 0)
+
+
+def test_perspective_simple_kats(oracle, scenes):
+    """testscene_perspectiveSimple1/2 at 512x512 (row f-3): per-sphere pixel
+    counts shared with the independent numpy restatement; the disc of scene 1
+    is centred (the sphere sits on the view axis up to 0.01)."""
+    r = oracle.render(scenes.perspective_simple1(), scenes.perspective_eye_camera(), scenes.shadow_camera(),
+                      512, 512, 0, scenes.RAYTRACING_FLAGS, want_stats=True)
+    assert r["stats"]["eye_hits"][:1] == [8949]
+    ys, xs = np.nonzero(r["rgba"][..., 1] != np.float32(0.2))
+    assert (xs.min(), xs.max(), ys.min(), ys.max()) == (204, 310, 204, 310)
+    r = oracle.render(scenes.perspective_simple2(), scenes.perspective_simple2_camera(), scenes.shadow_camera(),
+                      512, 512, 0, scenes.RAYTRACING_FLAGS, want_stats=True)
+    assert r["stats"]["eye_hits"][:2] == [9607, 2185]
 
 
 def test_raytracing_plane0_kats(oracle, scenes):

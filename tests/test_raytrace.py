@@ -37,12 +37,21 @@ def _case(scenes, name):
         return scenes.raytracing_plane0(), scenes.perspective_eye_camera()
     if name.startswith("rt_rbench"):
         return scenes.scene_r_bench(), scenes.perspective_eye_camera()
+    if name.startswith("f3_persp1"):
+        return scenes.perspective_simple1(), scenes.perspective_eye_camera()
+    if name.startswith("f3_persp2_rt"):
+        s = scenes.perspective_simple2()
+        s.circlePlanePrimitives = [scenes.dataclasses.replace(scenes.REFERENCE_CIRCLE_PLANE)]
+        s.cappedCylinderPrimitives = [scenes.dataclasses.replace(scenes.REFERENCE_CAPPED_CYLINDER)]
+        return s, scenes.perspective_simple2_camera()
+    if name.startswith("f3_persp2"):
+        return scenes.perspective_simple2(), scenes.perspective_simple2_camera()
     return scenes.mixed_rt(100), scenes.eye_camera()
 
 
 def _rt_golden():
     with open(os.path.join(GOLD, "golden.json")) as f:
-        return {k: v for k, v in json.load(f)["cases"].items() if k.startswith("rt_")}
+        return {k: v for k, v in json.load(f)["cases"].items() if k.startswith(("rt_", "f3_"))}
 
 
 @pytest.mark.parametrize("name", sorted(_rt_golden().keys()))
@@ -236,11 +245,10 @@ def test_degenerate_primitives(rtm, oracle, scenes):
 
 def test_raytrace_error_codes(rtm, scenes, gpu_ctx):
     abi = rtm.abi
-    # spheres under a perspective eye: projectSphere is row f-3
-    s = scenes.raytracing_plane0()
-    s.spherePrimitives = [scenes.PrimitiveSphere(0, scenes.Shading(1, 1, 1), (0, 0, 3), 0.5)]
+    # a perspective shadow camera: Camera::project asserts ORTHOGONAL (main.rs:1949)
     with pytest.raises(abi.RtmError) as e:
-        rtm.render_frame(s, scenes.perspective_eye_camera(), scenes.shadow_camera(), 64, 64, 0)
+        rtm.render_frame(scenes.raytracing_plane0(), scenes.perspective_eye_camera(),
+                         scenes.perspective_eye_camera(), 64, 64, 0)
     assert e.value.code == abi.RTM_ERR_UNSUPPORTED
     # id out of range (the reference would index past the array and panic)
     s = scenes.raytracing_plane0(True)
