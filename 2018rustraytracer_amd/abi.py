@@ -11,11 +11,12 @@ import os
 _PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_PKG_DIR, "librtm.so")
 
-RTM_ABI_VERSION = 2
+RTM_ABI_VERSION = 3
 RTM_MAX_SPHERES = 16
 RTM_MAX_PATCHES = 4
 RTM_MAX_CIRCLE_PLANES = 16
 RTM_MAX_CAPPED_CYLINDERS = 16
+RTM_MAX_SDFS = 8
 RTM_MAX_DIM = 32768
 
 RTM_OK = 0
@@ -59,12 +60,19 @@ class rtm_capped_cylinder(C.Structure):
                 ("rb", C.c_double), ("color", C.c_double * 3)]
 
 
+class rtm_sdf(C.Structure):
+    _fields_ = [("id", C.c_int64), ("box_center", C.c_double * 3), ("tri_anchor", C.c_double * 3),
+                ("aabb_center", C.c_double * 3), ("aabb_extent", C.c_double * 3), ("color", C.c_double * 3),
+                ("max_steps", C.c_int32), ("reserved", C.c_int32)]
+
+
 class rtm_scene(C.Structure):
     _fields_ = [("spheres", C.POINTER(rtm_sphere)), ("patches", C.POINTER(rtm_patch)),
                 ("n_spheres", C.c_int32), ("n_patches", C.c_int32),
                 ("circle_planes", C.POINTER(rtm_circle_plane)),
                 ("capped_cylinders", C.POINTER(rtm_capped_cylinder)),
-                ("n_circle_planes", C.c_int32), ("n_capped_cylinders", C.c_int32)]
+                ("n_circle_planes", C.c_int32), ("n_capped_cylinders", C.c_int32),
+                ("sdfs", C.POINTER(rtm_sdf)), ("n_sdfs", C.c_int32), ("reserved", C.c_int32)]
 
 
 class rtm_stats(C.Structure):
@@ -72,7 +80,8 @@ class rtm_stats(C.Structure):
                 ("lit_pixels", C.c_int64), ("eye_sphere_tests", C.c_int64),
                 ("shadow_sphere_tests", C.c_int64), ("march_iterations", C.c_int64),
                 ("march_hits", C.c_int64), ("march_in_range", C.c_int64),
-                ("eye_circle_plane_pixels", C.c_int64), ("eye_capped_cylinder_pixels", C.c_int64)]
+                ("eye_circle_plane_pixels", C.c_int64), ("eye_capped_cylinder_pixels", C.c_int64),
+                ("eye_sdf_pixels", C.c_int64), ("sdf_distance_evals", C.c_int64)]
 
     def as_dict(self) -> dict:
         d = {name: getattr(self, name) for name, _ in self._fields_ if name != "eye_hits"}
@@ -85,8 +94,9 @@ assert C.sizeof(rtm_patch) == 32
 assert C.sizeof(rtm_camera) == 104
 assert C.sizeof(rtm_circle_plane) == 88
 assert C.sizeof(rtm_capped_cylinder) == 96
-assert C.sizeof(rtm_scene) == 48
-assert C.sizeof(rtm_stats) == 8 * (RTM_MAX_SPHERES + 9)
+assert C.sizeof(rtm_sdf) == 136
+assert C.sizeof(rtm_scene) == 64
+assert C.sizeof(rtm_stats) == 8 * (RTM_MAX_SPHERES + 11)
 
 # (name, restype, argtypes) for every symbol include/rtm.h declares.
 _P = C.c_void_p

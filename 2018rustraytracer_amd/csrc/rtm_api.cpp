@@ -308,6 +308,15 @@ int validate_scene(const rtm_scene* scene) {
         if (scene->capped_cylinders[i].id < 0 || scene->capped_cylinders[i].id >= nc)
             return fail(RTM_ERR_INVALID, "capped cylinder %d has id %lld outside [0,%d)", i,
                         (long long)scene->capped_cylinders[i].id, nc);
+    const int ns = scene->n_sdfs;
+    if (ns < 0 || ns > RTM_MAX_SDFS) return fail(RTM_ERR_INVALID, "n_sdfs=%d outside [0,%d]", ns, RTM_MAX_SDFS);
+    if (ns > 0 && !scene->sdfs) return fail(RTM_ERR_INVALID, "sdfs is NULL");
+    for (int i = 0; i < ns; ++i) {
+        if (scene->sdfs[i].id < 0 || scene->sdfs[i].id >= ns)
+            return fail(RTM_ERR_INVALID, "sdf %d has id %lld outside [0,%d)", i, (long long)scene->sdfs[i].id, ns);
+        if (scene->sdfs[i].max_steps < 0)
+            return fail(RTM_ERR_INVALID, "sdf %d has max_steps=%d", i, scene->sdfs[i].max_steps);
+    }
     return RTM_OK;
 }
 
@@ -316,13 +325,16 @@ int validate_scene(const rtm_scene* scene) {
 struct FrameExtra {
     RtK rt;
     PerspK psp;
-    bool has_rt = false, has_psp = false;
+    SdfTabK sdf;
+    bool has_rt = false, has_psp = false, has_sdf = false;
 };
 
 bool build_rt(const rtm_scene* scene, RtK& k);
+bool build_sdf(const rtm_scene* scene, SdfTabK& k);
 
 void build_extra(const rtm_scene* scene, const rtm_camera* eye, int32_t W, int32_t H, FrameExtra& x) {
     x.has_rt = build_rt(scene, x.rt);
+    x.has_sdf = build_sdf(scene, x.sdf);
     std::memset(&x.psp, 0, sizeof x.psp);
     x.has_psp = eye->type != RTM_CAMERA_ORTHOGONAL && scene->n_spheres > 0;
     if (x.has_psp)
@@ -371,6 +383,51 @@ bool build_rt(const rtm_scene* scene, RtK& k) {
         c.id = (int32_t)q.id;
     }
     return k.n_pl + k.n_cy > 0;
+}
+
+// SDF primitives (row f-4) with udTriangleSingle's point-independent terms
+// (entry.frag:318-321, 436), computed as oracle/rtm_oracle.c's sdf_geom does.
+bool build_sdf(const rtm_scene* scene, SdfTabK& k) {
+    std::memset(&k, 0, sizeof k);
+    k.n = scene->n_sdfs;
+    auto cross = [](const double x[3], const double y[3], double r[3]) {  // GLSL cross
+        r[0] = x[1] * y[2] - y[1] * x[2];
+        r[1] = x[2] * y[0] - y[2] * x[0];
+        r[2] = x[0] * y[1] - y[0] * x[1];
+    };
+    auto dot = [](const double x[3], const double y[3]) { return x[0] * y[0] + x[1] * y[1] + x[2] * y[2]; };
+    static const double o1[3] = {0.8, 0.8, 0.8}, o2[3] = {1.3, 0.8, 0.8}, o3[3] = {1.0, 0.7, 0.2};
+    for (int i = 0; i < k.n; ++i) {
+        const rtm_sdf& q = scene->sdfs[i];
+        SdfK& g = k.s[i];
+        for (int j = 0; j < 3; ++j) {
+            g.box[j] = q.box_center[j];
+            g.v1[j] = q.tri_anchor[j] + o1[j];
+            g.v2[j] = q.tri_anchor[j] + o2[j];
+            g.v3[j] = q.tri_anchor[j] + o3[j];
+            g.ac[j] = q.aabb_center[j];
+            g.ae[j] = q.aabb_extent[j];
+        }
+        for (int j = 0; j < 3; ++j) {
+            g.e21[j] = g.v2[j] - g.v1[j];
+            g.e32[j] = g.v3[j] - g.v2[j];
+            g.e13[j] = g.v1[j] - g.v3[j];
+        }
+        cross(g.e21, g.e13, g.nor);
+        cross(g.e21, g.nor, g.c1);
+        cross(g.e32, g.nor, g.c2);
+        cross(g.e13, g.nor, g.c3);
+        g.d21 = dot(g.e21, g.e21);
+        g.d32 = dot(g.e32, g.e32);
+        g.d13 = dot(g.e13, g.e13);
+        g.dnor = dot(g.nor, g.nor);
+        g.cr = q.color[0];
+        g.cg = q.color[1];
+        g.cb = q.color[2];
+        g.id = (int32_t)q.id;
+        g.steps = q.max_steps;
+    }
+    return k.n > 0;
 }
 
 int validate_camera(const rtm_camera* c, const char* what) {
@@ -507,6 +564,7 @@ struct rtm_ctx {
     DevBuf enc_tab;                      // EncodeTable on the device (t | bucket)
     DevBuf rtk;                          // RtK of the frame being enqueued (row f-1)
     DevBuf pspk;                         // PerspK of the frame being enqueued (row f-3)
+    DevBuf sdfk;                         // SdfTabK of the frame being enqueued (row f-4)
     std::vector<rtm_viewport*> viewports;  // live viewports (orphaned when the context goes first)
     bool enc_tab_ready = false;
     uint64_t tab_key = 0;
@@ -520,8 +578,8 @@ struct rtm_viewport {
     int32_t W = 0, H = 0, face = 0;
     rtm_camera cam{};
     DevBuf zbuf, gh, gz, gid;
-    DevBuf gn;  // capped-cylinder hit normals (3 f64 per pixel), allocated by the first trace
-    int32_t traced_pl = 0, traced_cy = 0;  // max primitive counts traced into the G-buffer
+    DevBuf gn;  // capped-cylinder / SDF hit normals (3 f64 per pixel), allocated by the first trace
+    int32_t traced_pl = 0, traced_cy = 0, traced_sdf = 0;  // max primitive counts traced into the G-buffer
     int32_t raster_sp = 0;                 // ... and rasterized
 };
 
@@ -738,13 +796,21 @@ int upload_persp(rtm_ctx* ctx, const PerspK& k, const PerspK** dev) {
     return RTM_OK;
 }
 
+int upload_sdf(rtm_ctx* ctx, const SdfTabK& k, const SdfTabK** dev) {
+    int rc = ctx->sdfk.ensure(sizeof(SdfTabK), ctx->device);
+    if (rc) return rc;
+    if ((rc = launch_sdf_upload(k, (SdfTabK*)ctx->sdfk.p, ctx->stream))) return fail(rc, "sdf upload launch failed");
+    *dev = (const SdfTabK*)ctx->sdfk.p;
+    return RTM_OK;
+}
+
 int enqueue_frame(rtm_ctx* ctx, FrameArgs& a, const FrameExtra* x, float* out_dev, StatsK* stats) {
     int rc;
     if ((rc = frame_tables(ctx, a))) return rc;
-    const RtK* rt = nullptr;
-    const PerspK* psp = nullptr;
-    if (x && x->has_rt && (rc = upload_rt(ctx, x->rt, &rt))) return rc;
-    if (x && x->has_psp && (rc = upload_persp(ctx, x->psp, &psp))) return rc;
+    DevTabs tabs{nullptr, nullptr, nullptr};
+    if (x && x->has_rt && (rc = upload_rt(ctx, x->rt, &tabs.rt))) return rc;
+    if (x && x->has_psp && (rc = upload_persp(ctx, x->psp, &tabs.psp))) return rc;
+    if (x && x->has_sdf && (rc = upload_sdf(ctx, x->sdf, &tabs.sdf))) return rc;
     const bool fused = (a.ey.flags & RTM_FLAG_FUSED_SHADOW) != 0;
     hipStream_t s = ctx->stream;
     double* smap = nullptr;
@@ -763,7 +829,7 @@ int enqueue_frame(rtm_ctx* ctx, FrameArgs& a, const FrameExtra* x, float* out_de
         ctx->have_shadow_pass = false;
     }
     if (slot) HIP_TRY(hipEventRecord(slot->ev[2], s));
-    if ((rc = launch_eye_pass(a, smap, out_dev, s, stats, rt, psp))) return fail(rc, "eye pass launch failed");
+    if ((rc = launch_eye_pass(a, smap, out_dev, s, stats, tabs))) return fail(rc, "eye pass launch failed");
     if (slot) {
         HIP_TRY(hipEventRecord(slot->ev[3], s));
         slot->shadow = !fused;
@@ -934,7 +1000,7 @@ int rtm_render_frames_async(rtm_ctx* ctx, int32_t n_frames, const rtm_scene* sce
         int rc = build_frame(f[(size_t)i], &scenes[i], eye, shadow, width, height, march_steps, flags);
         if (rc) return rc;
         build_extra(&scenes[i], eye, width, height, ex[(size_t)i]);
-        any_rt |= ex[(size_t)i].has_rt || ex[(size_t)i].has_psp;
+        any_rt |= ex[(size_t)i].has_rt || ex[(size_t)i].has_psp || ex[(size_t)i].has_sdf;
     }
     DeviceGuard g(ctx->device);
     // The pipelined launch (shadow pass of frame i + eye pass of frame i-1) is
@@ -947,7 +1013,7 @@ int rtm_render_frames_async(rtm_ctx* ctx, int32_t n_frames, const rtm_scene* sce
     }();
     // The pipeline shares one table set: every frame must have the same patches
     // (the cameras are shared by construction).  Otherwise render frame by frame.
-    // (frames with ray-traced primitives or perspective spheres always take the two-kernel path)
+    // (frames with ray-traced primitives, SDFs or perspective spheres always take the two-kernel path)
     bool same = pipeline_on && !any_rt && (flags & RTM_FLAG_FUSED_SHADOW) == 0 && n_frames > 1;
     for (int32_t i = 1; same && i < n_frames; ++i)
         same = f[(size_t)i].sh.n_patches == f[0].sh.n_patches &&
@@ -1201,7 +1267,9 @@ int rtm_viewport_process_raytracing_rays(rtm_viewport* vp, const rtm_scene* scen
     int rc;
     if ((rc = validate_scene(scene))) return rc;
     RtK k;
-    if (!build_rt(scene, k)) return RTM_OK;  // no circle planes, no cylinders: nothing to trace
+    SdfTabK sk;
+    const bool has_rt = build_rt(scene, k), has_sdf = build_sdf(scene, sk);
+    if (!has_rt && !has_sdf) return RTM_OK;  // no circle planes, cylinders or SDFs: nothing to trace
     rtm_ctx* ctx = vp->ctx;
     DeviceGuard g(ctx->device);
     if ((rc = vp->gn.ensure(sizeof(double) * 3 * (size_t)vp->W * (size_t)vp->H, ctx->device))) return rc;
@@ -1210,12 +1278,14 @@ int rtm_viewport_process_raytracing_rays(rtm_viewport* vp, const rtm_scene* scen
     a.cam = cam_k(vp->cam);
     a.W = vp->W;
     a.H = vp->H;
-    if ((rc = upload_rt(ctx, k, &a.rt))) return rc;
+    if (has_rt && (rc = upload_rt(ctx, k, &a.rt))) return rc;
+    if (has_sdf && (rc = upload_sdf(ctx, sk, &a.sdf))) return rc;
     if ((rc = launch_vp_trace(a, (double*)vp->zbuf.p, (double*)vp->gh.p, (int32_t*)vp->gid.p, (double*)vp->gn.p,
                               ctx->stream)))
         return fail(rc, "trace launch failed");
     vp->traced_pl = std::max(vp->traced_pl, k.n_pl);
     vp->traced_cy = std::max(vp->traced_cy, k.n_cy);
+    vp->traced_sdf = std::max(vp->traced_sdf, sk.n);
     return RTM_OK;
 }
 
@@ -1254,10 +1324,11 @@ int rtm_render_color_image(const rtm_scene* scene, const rtm_viewport* vp, const
     // the G-buffer may hold ids of every primitive traced into it: the reference
     // indexes the scene's arrays with them and panics when out of range (main.rs:773, 791)
     if (vp->traced_pl > scene->n_circle_planes || vp->traced_cy > scene->n_capped_cylinders ||
-        vp->raster_sp > scene->n_spheres)
-        return fail(RTM_ERR_INVALID, "scene has fewer spheres/circle planes/cylinders (%d/%d/%d) than the viewport "
-                    "holds (%d/%d/%d)", scene->n_spheres, scene->n_circle_planes, scene->n_capped_cylinders,
-                    vp->raster_sp, vp->traced_pl, vp->traced_cy);
+        vp->traced_sdf > scene->n_sdfs || vp->raster_sp > scene->n_spheres)
+        return fail(RTM_ERR_INVALID, "scene has fewer spheres/circle planes/cylinders/sdfs (%d/%d/%d/%d) than the "
+                    "viewport holds (%d/%d/%d/%d)", scene->n_spheres, scene->n_circle_planes,
+                    scene->n_capped_cylinders, scene->n_sdfs, vp->raster_sp, vp->traced_pl, vp->traced_cy,
+                    vp->traced_sdf);
     ShadeArgs a;
     std::memset(&a, 0, sizeof a);
     for (int i = 0; i < scene->n_spheres; ++i) a.shade[i] = shade_sphere(scene->spheres[i]);
@@ -1273,8 +1344,13 @@ int rtm_render_color_image(const rtm_scene* scene, const rtm_viewport* vp, const
     const size_t bytes = sizeof(float) * 4 * (size_t)vp->W * (size_t)vp->H;
     if ((rc = ctx->out.ensure(bytes, ctx->device))) return rc;
     RtK k;
+    SdfTabK sk;
     if (build_rt(scene, k)) {  // shading lookups circlePlanePrimitives[id] / cappedCylinderPrimitives[id]
         if ((rc = upload_rt(ctx, k, &a.rt))) return rc;
+        a.gn = (const double*)vp->gn.p;
+    }
+    if (build_sdf(scene, sk)) {  // ... and the SDF colours (row f-4)
+        if ((rc = upload_sdf(ctx, sk, &a.sdf))) return rc;
         a.gn = (const double*)vp->gn.p;
     }
     if ((rc = launch_vp_shade(a, (const double*)shadow_vp->zbuf.p, (const double*)vp->gh.p, (const double*)vp->gz.p,

@@ -159,6 +159,33 @@ struct PerspK {
 };
 static_assert(sizeof(PerspK) + sizeof(void*) <= 4096, "PerspK must fit the upload kernel's kernarg segment");
 
+// The GL preview's SDF implicit surface (row f-4, entry.frag:416-442, 842-905),
+// with udTriangleSingle's point-independent terms precomputed on the host in
+// the restatement's operation order (oracle/rtm_oracle.c).
+struct SdfK {
+    double box[3];                       // descriptor vecs[0]
+    double v1[3], v2[3], v3[3];          // triangle
+    double e21[3], e32[3], e13[3];       // v2-v1, v3-v2, v1-v3
+    double nor[3];                       // cross(v21, v13)
+    double c1[3], c2[3], c3[3];          // cross(v21,nor), cross(v32,nor), cross(v13,nor)
+    double d21, d32, d13, dnor;          // dot2 of the edges and of nor
+    double ac[3], ae[3];                 // AABB centre / extent
+    double cr, cg, cb;
+    int32_t id, steps;
+};
+struct SdfTabK {
+    SdfK s[RTM_MAX_SDFS];
+    int32_t n, pad;
+};
+static_assert(sizeof(SdfTabK) + sizeof(void*) <= 4096, "SdfTabK must fit the upload kernel's kernarg segment");
+
+// The device tables a frame may carry beside FrameArgs (each nullptr when absent).
+struct DevTabs {
+    const RtK* rt;        // circle planes + capped cylinders (f-1)
+    const PerspK* psp;    // PERSPECTIVE eye sphere projections (f-3)
+    const SdfTabK* sdf;   // SDF implicit surfaces (f-4)
+};
+
 // Reference-seam kernels (one per reference function).
 struct RasterArgs {
     RasterSphereK sph[RTM_MAX_SPHERES];
@@ -180,25 +207,29 @@ struct ShadeArgs {
     int32_t W, H, Ws, Hs;
     int32_t n_spheres, pad;
     const RtK* rt;      // plane / cylinder shading constants (device; nullptr: none)
-    const double* gn;   // cylinder hit normals, 3 per pixel (nullptr: none)
+    const double* gn;   // cylinder / SDF hit normals, 3 per pixel (nullptr: none)
+    const SdfTabK* sdf; // SDF shading constants (device; nullptr: none)
 };
 
 struct TraceArgs {      // processRaytracingRays of one viewport
     CamK cam;
     int32_t W, H;
     const RtK* rt;
+    const SdfTabK* sdf;
 };
 
-// Staged G-buffer id encoding: sphere id | GID_PLANE | GID_CYLINDER (kind in bits 16+).
+// Staged G-buffer id encoding: sphere id | GID_PLANE | GID_CYLINDER | GID_SDF (kind in bits 16+).
 constexpr int32_t GID_PLANE = 1 << 16;
 constexpr int32_t GID_CYLINDER = 2 << 16;
+constexpr int32_t GID_SDF = 3 << 16;
 
 // Device counters for rtm_render_stats (layout == rtm_stats).
 struct StatsK {
     unsigned long long eye_hits[RTM_MAX_SPHERES];
     unsigned long long eye_hit_pixels, lit_pixels, eye_sphere_tests, shadow_sphere_tests;
     unsigned long long march_iterations, march_hits, march_in_range;
-    unsigned long long eye_circle_plane_pixels, eye_capped_cylinder_pixels;
+    unsigned long long eye_circle_plane_pixels, eye_capped_cylinder_pixels, eye_sdf_pixels;
+    unsigned long long sdf_distance_evals;
 };
 static_assert(sizeof(StatsK) == sizeof(rtm_stats), "StatsK layout");
 
@@ -208,11 +239,12 @@ int launch_shadow_pass(const FrameArgs& a, double* smap, void* stream, StatsK* s
 // with spheres (device RtK / PerspK, see launch_upload); either selects the
 // general eye kernel.
 int launch_eye_pass(const FrameArgs& a, const double* smap, float* out, void* stream, StatsK* stats,
-                    const RtK* rt = nullptr, const PerspK* psp = nullptr);
+                    const DevTabs& tabs = DevTabs{nullptr, nullptr, nullptr});
 // Stream-ordered copy of a host struct into device memory (a kernel, so the
 // host copy is consumed at launch: no pinned staging, no host synchronisation).
 int launch_rt_upload(const RtK& k, RtK* dst, void* stream);
 int launch_persp_upload(const PerspK& k, PerspK* dst, void* stream);
+int launch_sdf_upload(const SdfTabK& k, SdfTabK* dst, void* stream);
 // Software-pipelined frame step: the shadow pass of a.sh into smap_w and the eye
 // pass of a.ey (the previous frame) from smap_r into out, in ONE launch whose
 // workgroups interleave the two roles (VALU-bound and HBM-store-bound tiles

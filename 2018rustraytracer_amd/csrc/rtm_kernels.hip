@@ -369,18 +369,160 @@ __device__ __forceinline__ double icapped(const CylK& c, const double ro[3], con
     return -1.0;
 }
 
+// ---- row f-4: the GL preview's SDF, the f64 restatement of oracle/rtm_oracle.c ----
+// min/max: NaN-ignoring with +0 > -0 (a NaN a gives b, a NaN b gives a; a tie
+// gives a unless the signs of zero decide); sign: GLSL (0 for 0 and NaN).  All
+// branch-free: the predicates combine with bitwise ops into one select, so the
+// march loop stays straight-line code (nested ternaries compiled to exec-mask
+// branches, ~4x the instructions).
+__device__ __forceinline__ double fmax_d(double a, double b) {
+    const bool take_a = !(a != a) & ((a > b) | (b != b) | ((a == b) & !__builtin_signbit(a)));
+    return take_a ? a : b;
+}
+__device__ __forceinline__ double fmin_d(double a, double b) {
+    const bool take_a = !(a != a) & ((a < b) | (b != b) | ((a == b) & __builtin_signbit(a)));
+    return take_a ? a : b;
+}
+// fmax_d(x, +0.0) and fmin_d(x, +0.0)
+__device__ __forceinline__ double fmax0_d(double x) { return x > 0.0 ? x : 0.0; }
+__device__ __forceinline__ double fmin0_d(double x) { return (__builtin_signbit(x) & !(x != x)) ? x : 0.0; }
+// fmin_d(fmax_d(x, 0.0), 1.0)
+__device__ __forceinline__ double clamp01_d(double x) {
+    const double v = x > 0.0 ? x : 0.0;
+    return v < 1.0 ? v : 1.0;
+}
+__device__ __forceinline__ int gsign_i(double x) { return (int)(x > 0.0) - (int)(x < 0.0); }
+__device__ __forceinline__ double dot3d(const double a[3], const double b[3]) {
+    return a[0] * b[0] + a[1] * b[1] + a[2] * b[2];
+}
+
+// distanceFn0 (entry.frag:416-442): sdBox (290-298) union udTriangleSingle (312-340), - 0.2
+__device__ __forceinline__ double sdf_dist(const SdfK& g, const double p[3]) {
+    double dd[3], m[3];
+    for (int k = 0; k < 3; ++k) {
+        dd[k] = fabs(p[k] - g.box[k]) - (k == 0 ? 0.4 : 0.2);
+        m[k] = fmax0_d(dd[k]);
+    }
+    const double d0 = fmin0_d(fmax_d(dd[0], fmax_d(dd[1], dd[2]))) + sqrt(dot3d(m, m));
+    double p1[3], p2[3], p3[3];
+    for (int k = 0; k < 3; ++k) {
+        p1[k] = p[k] - g.v1[k];
+        p2[k] = p[k] - g.v2[k];
+        p3[k] = p[k] - g.v3[k];
+    }
+    double d1;
+    // (the sum of three signs is a small integer: exact in f64 and in int)
+    if (gsign_i(dot3d(g.c1, p1)) + gsign_i(dot3d(g.c2, p2)) + gsign_i(dot3d(g.c3, p3)) < 2) {
+        const double s1 = clamp01_d(dot3d(g.e21, p1) / g.d21);
+        const double s2 = clamp01_d(dot3d(g.e32, p2) / g.d32);
+        const double s3 = clamp01_d(dot3d(g.e13, p3) / g.d13);
+        double e1[3], e2[3], e3[3];
+        for (int k = 0; k < 3; ++k) {
+            e1[k] = g.e21[k] * s1 - p1[k];
+            e2[k] = g.e32[k] * s2 - p2[k];
+            e3[k] = g.e13[k] * s3 - p3[k];
+        }
+        d1 = fmin_d(fmin_d(dot3d(e1, e1), dot3d(e2, e2)), dot3d(e3, e3));
+    } else {
+        const double dn = dot3d(g.nor, p1);
+        d1 = dn * dn / g.dnor;
+    }
+    double d2 = fmin_d(d0, d1);
+    d2 -= 0.2;
+    return d2;
+}
+
+// Both sBox calls of one trace (entry.frag:85-110, 857-859) with txx =
+// translate(-centre), sharing the per-ray m = 1/rd (hoisted by the caller).
+// The second call's ray is -rd: 1/(-x) == -(1/x), (-m)*roo == -(m*roo) and
+// |-m| == |m| exactly in IEEE arithmetic, so its t1 = -n' - k' is n - k bit for
+// bit.  Returns false on the first call's miss (tN > tF || tF < 0).
+__device__ __forceinline__ bool sdf_slabs(const double ro[3], const double m[3], const double am[3], const SdfK& g,
+                                          double& tIn, double& tOut) {
+    double t1[3], t2[3], u1[3];
+    for (int k = 0; k < 3; ++k) {
+        const double roo = ro[k] - g.ac[k];
+        const double n = m[k] * roo;
+        const double kk = am[k] * g.ae[k];
+        t1[k] = -n - kk;
+        t2[k] = -n + kk;
+        u1[k] = n - kk;
+    }
+    const double tN = fmax_d(fmax_d(t1[0], t1[1]), t1[2]);
+    const double tF = fmin_d(fmin_d(t2[0], t2[1]), t2[2]);
+    tIn = (tN > tF || tF < 0.0) ? -1.0 : tN;
+    tOut = -fmax_d(fmax_d(u1[0], u1[1]), u1[2]);
+    return tIn >= 0.0;
+}
+
+// The implicit-surface branch of bvhProcessLeafHit (entry.frag:842-905):
+// t of the hit or -1, and the sdNormalFast normal.  m = 1/rd, am = |m|.
+__device__ __forceinline__ double sdf_trace(const SdfK& g, const double ro[3], const double rd[3], const double m[3],
+                                            const double am[3], double n[3], uint32_t& evals) {
+    double tIn, tOut;
+    if (!sdf_slabs(ro, m, am, g, tIn, tOut)) return -1.0;
+    double t = tIn;
+    bool hit = false;
+    for (int step = 0; step < g.steps; ++step) {
+        const double p[3] = {ro[0] + rd[0] * t, ro[1] + rd[1] * t, ro[2] + rd[2] * t};
+        const double dist = sdf_dist(g, p);
+        ++evals;
+        if (dist < 0.03) {
+            hit = true;
+            break;
+        }
+        if (t > tOut) break;
+        t += dist;
+    }
+    if (!hit) return -1.0;
+    evals += 4;
+    const double p[3] = {ro[0] + rd[0] * t, ro[1] + rd[1] * t, ro[2] + rd[2] * t};
+    const double h = 0.001;
+    const double ks[4][3] = {{1.0, -1.0, -1.0}, {-1.0, -1.0, 1.0}, {-1.0, 1.0, -1.0}, {1.0, 1.0, 1.0}};
+    double tap[4];
+    for (int j = 0; j < 4; ++j) {
+        const double q[3] = {p[0] + ks[j][0] * h, p[1] + ks[j][1] * h, p[2] + ks[j][2] * h};
+        tap[j] = sdf_dist(g, q);
+    }
+    double v[3];
+    for (int k = 0; k < 3; ++k) v[k] = ((ks[0][k] * tap[0] + ks[1][k] * tap[1]) + ks[2][k] * tap[2]) + ks[3][k] * tap[3];
+    const double inv = 1.0 / sqrt(dot3d(v, v));
+    for (int k = 0; k < 3; ++k) n[k] = v[k] * inv;
+    return t;
+}
+
 // The ray-traced part of one eye pixel: planes, then cylinders, in scene order
-// (main.rs:573-638).  zb is the depth after the sphere rasterize; kind/rid/t/n
-// are updated in place when a primitive takes the pixel.
+// (main.rs:573-638), then the row f-4 SDFs.  zb is the depth after the sphere
+// rasterize; kind/rid/t/n are updated in place when a primitive takes the pixel.
 struct RtHit {
-    int kind;  // 0 none, 1 sphere, 2 circle plane, 3 capped cylinder
+    int kind;  // 0 none, 1 sphere, 2 circle plane, 3 capped cylinder, 4 SDF
     int id;
     double t;
     double n[3];
 };
 
+__device__ __forceinline__ void trace_sdfs(const SdfTabK* __restrict__ sdf, const double o[3], const double d[3],
+                                           double zb, RtHit& hit, uint32_t& evals) {
+    const int ns = sdf->n;
+    const double m[3] = {1.0 / d[0], 1.0 / d[1], 1.0 / d[2]};
+    const double am[3] = {fabs(m[0]), fabs(m[1]), fabs(m[2])};
+    for (int i = 0; i < ns; ++i) {
+        double n[3];
+        const double t = sdf_trace(sdf->s[i], o, d, m, am, n, evals);
+        if (!(t > 0.0) || !(t < zb)) continue;  // the shader's acceptance (entry.frag:908-917)
+        hit.kind = 4;
+        hit.id = sdf->s[i].id;
+        hit.t = t;
+        hit.n[0] = n[0];
+        hit.n[1] = n[1];
+        hit.n[2] = n[2];
+        zb = t;
+    }
+}
+
 __device__ __forceinline__ void trace_pixel(const RtK* __restrict__ rt, const double o[3], const double d[3],
-                                            double zb, RtHit& hit) {
+                                            double& zb_io, RtHit& hit) {
+    double zb = zb_io;
     const int npl = rt->n_pl, ncy = rt->n_cy;
     for (int i = 0; i < npl; ++i) {
         double t;
@@ -404,6 +546,7 @@ __device__ __forceinline__ void trace_pixel(const RtK* __restrict__ rt, const do
         hit.n[2] = n[2];
         zb = t;
     }
+    zb_io = zb;
 }
 
 // ---- statistics (rtm_render_stats only; never in the timed kernels) ----
@@ -1038,10 +1181,16 @@ __global__ __launch_bounds__(BLOCK) void shadow_lean_kernel(const FrameArgs a, d
 // [+ processRaytracingRays when RT, main.rs:1035] + renderColorImage
 // (main.rs:714-898).  FUSED evaluates the looked-up shadow texel on demand from
 // `sh` (same frame) instead of reading `smap`.
-template <bool FUSED, bool COUNT, bool RT>
+// RT: 0 spheres only, 1 + ray-traced planes/cylinders and PERSPECTIVE spheres,
+// 2 + SDFs (its own instantiation: the sphere-trace loop's registers would
+// otherwise lower the occupancy of every ray-traced frame).
+template <bool FUSED, bool COUNT, int RT>
 __device__ __forceinline__ void eye_tile(const EyePart& a, const ShadowPart& sh, const double* __restrict__ smap,
                                          float4* __restrict__ out, int bx, int by, StatsK* __restrict__ st,
-                                         const RtK* __restrict__ rt, const PerspK* __restrict__ psp = nullptr) {
+                                         const DevTabs tabs) {
+    const RtK* __restrict__ rt = tabs.rt;
+    const PerspK* __restrict__ psp = tabs.psp;
+    const SdfTabK* __restrict__ sdf = tabs.sdf;
     const int xb = bx * TILE_X;
     const int xi = xb + (threadIdx.x & (TILE_X - 1));
     const int yl = __builtin_amdgcn_readfirstlane(by * TILE_Y + (threadIdx.x >> 6));
@@ -1050,6 +1199,7 @@ __device__ __forceinline__ void eye_tile(const EyePart& a, const ShadowPart& sh,
     unsigned long long n_tests = 0, n_hit = 0, n_lit = 0;
     ShadowCounts sc;
     int hit_kind = 0, hit_id = -1;
+    uint32_t n_evals = 0;
     if (live) {
         const double x = a.nx[xi];
         const double y = a.ny[yi];
@@ -1077,7 +1227,9 @@ __device__ __forceinline__ void eye_tile(const EyePart& a, const ShadowPart& sh,
         double o[3], d[3];
         if (RT) {
             cam_ray(a.eye, x, y, o, d);
-            if (rt) trace_pixel(rt, o, d, best, hit);
+            double zb = best;
+            if (rt) trace_pixel(rt, o, d, zb, hit);
+            if (RT == 2) trace_sdfs(sdf, o, d, zb, hit, n_evals);
         }
         float4 c = make_float4(0.0f, 0.2f, 0.2f, 1.0f);  // (0.0, 0.2, 0.2) as f32 (main.rs:718-720)
         if (hit.kind) {
@@ -1108,14 +1260,19 @@ __device__ __forceinline__ void eye_tile(const EyePart& a, const ShadowPart& sh,
                     cr = p.cr;
                     cg = p.cg;
                     cb = p.cb;
-                } else {
-                    const CylK& q = rt->cy[hit.id];
+                } else {  // capped cylinder or SDF: the normal came with the hit
                     nx = hit.n[0];
                     ny = hit.n[1];
                     nz = hit.n[2];
-                    cr = q.cr;
-                    cg = q.cg;
-                    cb = q.cb;
+                    if (hit.kind == 3) {
+                        cr = rt->cy[hit.id].cr;
+                        cg = rt->cy[hit.id].cg;
+                        cb = rt->cy[hit.id].cb;
+                    } else if (RT == 2) {
+                        cr = sdf->s[hit.id].cr;
+                        cg = sdf->s[hit.id].cg;
+                        cb = sdf->s[hit.id].cb;
+                    }
                 }
             }
             // light (1,0,0).scale(-1.0) (main.rs:810-813)
@@ -1179,6 +1336,10 @@ __device__ __forceinline__ void eye_tile(const EyePart& a, const ShadowPart& sh,
         if (RT) {
             stat_add(&st->eye_circle_plane_pixels, hit_kind == 2);
             stat_add(&st->eye_capped_cylinder_pixels, hit_kind == 3);
+            if (RT == 2) {
+                stat_add(&st->eye_sdf_pixels, hit_kind == 4);
+                stat_add(&st->sdf_distance_evals, n_evals);
+            }
         }
         if (FUSED) {
             stat_add(&st->shadow_sphere_tests, sc.tests);
@@ -1202,11 +1363,11 @@ __global__ __launch_bounds__(BLOCK) void shadow_sep_kernel(const FrameArgs a, do
     shadow_tile_sep<NR, MODE>(a.sh, smap, blockIdx.x, blockIdx.y, diag, lds ? lds_zt : nullptr);
 }
 
-template <bool FUSED, bool COUNT, bool RT>
+template <bool FUSED, bool COUNT, int RT>
 __global__ __launch_bounds__(BLOCK) void eye_pass_kernel(const FrameArgs a, const double* __restrict__ smap,
                                                          float4* __restrict__ out, StatsK* __restrict__ st,
-                                                         const RtK* __restrict__ rt, const PerspK* __restrict__ psp) {
-    eye_tile<FUSED, COUNT, RT>(a.ey, a.sh, smap, out, blockIdx.x, blockIdx.y, st, rt, psp);
+                                                         const DevTabs tabs) {
+    eye_tile<FUSED, COUNT, RT>(a.ey, a.sh, smap, out, blockIdx.x, blockIdx.y, st, tabs);
 }
 
 // launch_*_upload: one 8-byte word per thread from the kernarg copy.
@@ -1253,7 +1414,8 @@ __global__ __launch_bounds__(BLOCK) void frame_pipe_kernel(const FrameArgs a, do
             shadow_tile_generic<false>(a.sh, smap_w, t % sh_gx, t / sh_gx, nullptr);
     } else {
         const int t = (int)(b - s_before);
-        eye_tile<false, false, false>(a.ey, a.sh, smap_r, out, t % eye_gx, t / eye_gx, nullptr, nullptr);
+        eye_tile<false, false, 0>(a.ey, a.sh, smap_r, out, t % eye_gx, t / eye_gx, nullptr,
+                                      DevTabs{nullptr, nullptr, nullptr});
     }
 }
 
@@ -1328,12 +1490,15 @@ __global__ __launch_bounds__(BLOCK) void vp_trace_kernel(const TraceArgs a, doub
     RtHit hit;
     hit.kind = 0;
     hit.id = 0;
-    trace_pixel(a.rt, o, d, zbuf[idx], hit);
+    double zb = zbuf[idx];
+    if (a.rt) trace_pixel(a.rt, o, d, zb, hit);
+    uint32_t evals = 0;
+    if (a.sdf) trace_sdfs(a.sdf, o, d, zb, hit, evals);
     if (hit.kind) {
         zbuf[idx] = hit.t;
         gh[idx] = hit.t;
-        gid[idx] = (hit.kind == 2 ? GID_PLANE : GID_CYLINDER) | hit.id;
-        if (hit.kind == 3)
+        gid[idx] = (hit.kind == 2 ? GID_PLANE : hit.kind == 3 ? GID_CYLINDER : GID_SDF) | hit.id;
+        if (hit.kind >= 3)
             for (int k = 0; k < 3; ++k) gn[3 * idx + k] = hit.n[k];
     }
 }
@@ -1390,9 +1555,15 @@ __global__ __launch_bounds__(BLOCK) void vp_shade_kernel(const ShadeArgs a, cons
                 nx = a.gn[3 * idx];
                 ny = a.gn[3 * idx + 1];
                 nz = a.gn[3 * idx + 2];
-                cr = a.rt->cy[id].cr;
-                cg = a.rt->cy[id].cg;
-                cb = a.rt->cy[id].cb;
+                if (kind == 2) {
+                    cr = a.rt->cy[id].cr;
+                    cg = a.rt->cy[id].cg;
+                    cb = a.rt->cy[id].cb;
+                } else {
+                    cr = a.sdf->s[id].cr;
+                    cg = a.sdf->s[id].cg;
+                    cb = a.sdf->s[id].cb;
+                }
             }
         }
         const double Lx = 1.0 * -1.0, Ly = 0.0 * -1.0, Lz = 0.0 * -1.0;
@@ -1587,7 +1758,7 @@ int launch_shadow_pass(const FrameArgs& a, double* smap, void* stream, StatsK* s
 }
 
 int launch_eye_pass(const FrameArgs& a, const double* smap, float* out, void* stream, StatsK* stats,
-                    const RtK* rt, const PerspK* psp) {
+                    const DevTabs& tabs) {
     hipStream_t s = (hipStream_t)stream;
     dim3 g = grid_for(a.ey.W, a.ey.row_end - a.ey.row_begin);
     float4* o = reinterpret_cast<float4*>(out);
@@ -1597,17 +1768,22 @@ int launch_eye_pass(const FrameArgs& a, const double* smap, float* out, void* st
         return launched();
     }
 #define RTM_EYE(F, C, R) \
-    hipLaunchKernelGGL((eye_pass_kernel<F, C, R>), g, dim3(BLOCK), 0, s, a, smap, o, stats, rt, psp)
-    if (rt || psp) {
-        if (fused && stats) RTM_EYE(true, true, true);
-        else if (fused) RTM_EYE(true, false, true);
-        else if (stats) RTM_EYE(false, true, true);
-        else RTM_EYE(false, false, true);
+    hipLaunchKernelGGL((eye_pass_kernel<F, C, R>), g, dim3(BLOCK), 0, s, a, smap, o, stats, tabs)
+    if (tabs.sdf) {
+        if (fused && stats) RTM_EYE(true, true, 2);
+        else if (fused) RTM_EYE(true, false, 2);
+        else if (stats) RTM_EYE(false, true, 2);
+        else RTM_EYE(false, false, 2);
+    } else if (tabs.rt || tabs.psp) {
+        if (fused && stats) RTM_EYE(true, true, 1);
+        else if (fused) RTM_EYE(true, false, 1);
+        else if (stats) RTM_EYE(false, true, 1);
+        else RTM_EYE(false, false, 1);
     } else {
-        if (fused && stats) RTM_EYE(true, true, false);
-        else if (fused) RTM_EYE(true, false, false);
-        else if (stats) RTM_EYE(false, true, false);
-        else RTM_EYE(false, false, false);
+        if (fused && stats) RTM_EYE(true, true, 0);
+        else if (fused) RTM_EYE(true, false, 0);
+        else if (stats) RTM_EYE(false, true, 0);
+        else RTM_EYE(false, false, 0);
     }
 #undef RTM_EYE
     return launched();
@@ -1620,6 +1796,11 @@ int launch_rt_upload(const RtK& k, RtK* dst, void* stream) {
 
 int launch_persp_upload(const PerspK& k, PerspK* dst, void* stream) {
     hipLaunchKernelGGL(upload_kernel<PerspK>, dim3(1), dim3(256), 0, (hipStream_t)stream, k, dst);
+    return launched();
+}
+
+int launch_sdf_upload(const SdfTabK& k, SdfTabK* dst, void* stream) {
+    hipLaunchKernelGGL(upload_kernel<SdfTabK>, dim3(1), dim3(512), 0, (hipStream_t)stream, k, dst);
     return launched();
 }
 

@@ -60,6 +60,14 @@ RT_RAY_ORTHO = 12
 RT_RAY_PERSP = 24
 RT_PER_PLANE = 33
 RT_PER_CYL = 88
+# row f-4 (entry.frag distanceFn0 + the sphere-tracing leaf, restated in f64):
+# per (pixel, SDF): two sBox slab tests + the loop set-up; per distanceFn0
+# evaluation: sdBox 19 + udTriangleSingle's sign test 30 + its edge branch 59
+# (the usual one) + union/offset 2 + the march step's p = ro + rd*t, compare and
+# advance 8; per SDF hit: the 4-tap normal's offsets/combination/normalize.
+SDF_PER_TRACE = 48
+SDF_PER_EVAL = 118
+SDF_PER_HIT = 31
 
 
 def shared_z_separable(shadow_cam) -> bool:
@@ -73,7 +81,7 @@ def shared_z_separable(shadow_cam) -> bool:
 
 def frame_work(stats: dict, width: int, height: int, n_spheres: int, n_patches: int, flags: int = 0,
                fused: bool = False, sep: bool = False, n_planes: int = 0, n_cyls: int = 0,
-               perspective: bool = False, search: bool = False) -> dict:
+               perspective: bool = False, search: bool = False, n_sdfs: int = 0) -> dict:
     """search: the march is the first-crossing search (monotone shared z table)."""
     px = width * height
     no_march = bool(flags & 0x1)
@@ -91,9 +99,10 @@ def frame_work(stats: dict, width: int, height: int, n_spheres: int, n_patches: 
             sh_ops += texels * n_patches * SHADOW_PER_PATCH + SHADOW_PER_ITER * stats["march_iterations"]
     eye_ops = (px * EYE_PER_SPHERE * n_spheres + EYE_PER_COVER * stats["eye_sphere_tests"]
                + EYE_PER_HIT * stats["eye_hit_pixels"])
-    if n_planes or n_cyls:
+    if n_planes or n_cyls or n_sdfs:
         eye_ops += px * ((RT_RAY_PERSP if perspective else RT_RAY_ORTHO) + RT_PER_PLANE * n_planes
-                         + RT_PER_CYL * n_cyls)
+                         + RT_PER_CYL * n_cyls + SDF_PER_TRACE * n_sdfs)
+        eye_ops += SDF_PER_EVAL * stats.get("sdf_distance_evals", 0) + SDF_PER_HIT * stats.get("eye_sdf_pixels", 0)
     sh_bytes = 0 if fused else 8 * px
     eye_bytes = 16 * px + (0 if fused else 8 * stats["eye_hit_pixels"])
     return dict(shadow_pass=dict(ops=sh_ops, bytes=sh_bytes),

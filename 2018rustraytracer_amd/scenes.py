@@ -51,6 +51,17 @@ class PrimitiveCappedCylinder:  # main.rs:382-391
 
 
 @dataclass
+class PrimitiveSdf:  # the GL preview's implicit surface (entry.frag:842-947), row f-4
+    id: int
+    shading: Shading
+    box_center: tuple = (3.0, 0.0, 5.0)    # descriptor vecs[0] (entry.frag:878)
+    tri_anchor: tuple = (3.5, 0.0, 6.0)    # descriptor vecs[2] (entry.frag:880)
+    aabb_center: tuple = (3.0, 0.0, 5.0)   # entry.frag:850
+    aabb_extent: tuple = (3.0, 3.0, 3.0)   # entry.frag:851
+    max_steps: int = 180                   # entry.frag:887
+
+
+@dataclass
 class Linear:  # main.rs:2134-2137
     a: float
     b: float
@@ -99,6 +110,7 @@ class Scene:  # main.rs:404-410 (+ the implicit patches the march path takes as 
     patches: List[Bilinear] = field(default_factory=list)
     circlePlanePrimitives: List[PrimitiveCirclePlane] = field(default_factory=list)
     cappedCylinderPrimitives: List[PrimitiveCappedCylinder] = field(default_factory=list)
+    sdfPrimitives: List[PrimitiveSdf] = field(default_factory=list)
 
     def to_c(self):
         """Returns (rtm_scene, keepalive) — keep the second value alive while
@@ -138,7 +150,19 @@ class Scene:  # main.rs:404-410 (+ the implicit patches the march path takes as 
         sc.capped_cylinders = C.cast(cy, C.POINTER(abi.rtm_capped_cylinder))
         sc.n_circle_planes = npl
         sc.n_capped_cylinders = ncy
-        return sc, (sph, pat, pl, cy)
+        nsd = len(self.sdfPrimitives)
+        sd = (abi.rtm_sdf * max(nsd, 1))()
+        for i, q in enumerate(self.sdfPrimitives):
+            sd[i].id = int(q.id)
+            sd[i].box_center[:] = [float(v) for v in q.box_center]
+            sd[i].tri_anchor[:] = [float(v) for v in q.tri_anchor]
+            sd[i].aabb_center[:] = [float(v) for v in q.aabb_center]
+            sd[i].aabb_extent[:] = [float(v) for v in q.aabb_extent]
+            sd[i].color[:] = [float(q.shading.colorR), float(q.shading.colorG), float(q.shading.colorB)]
+            sd[i].max_steps = int(q.max_steps)
+        sc.sdfs = C.cast(sd, C.POINTER(abi.rtm_sdf))
+        sc.n_sdfs = nsd
+        return sc, (sph, pat, pl, cy, sd)
 
 
 # ---- cameras of the orthographic test scenes ----
@@ -297,6 +321,11 @@ CONFIGS = {
     7: dict(width=512, height=512, steps=0, scene=raytracing_plane0, flags=RAYTRACING_FLAGS,
             eye=perspective_eye_camera,
             desc="512x512, testscene_raytracingPlane0 as main() renders it (row f-1)"),
+    # row f-4: Scene S-bench (8 preview SDFs + a backdrop circle plane); the
+    # factories are defined below, hence the lambdas
+    8: dict(width=3840, height=2160, steps=0, scene=lambda: sdf_bench_scene(), flags=RAYTRACING_FLAGS,
+            eye=lambda: sdf_eye_camera(),
+            desc="3840x2160, Scene S-bench: 8 GL-preview SDFs + 1 circle plane, perspective (row f-4)"),
 }
 
 
@@ -318,3 +347,42 @@ def perspective_simple2() -> Scene:
 def perspective_simple2_camera() -> Camera:
     """viewport0's camera of testscene_perspectiveSimple2 (main.rs:1283-1295)."""
     return Camera(PERSPECTIVE, (0.0, 1.5, 0.0), (0.0, 0.0, 1.0), (0.0, 1.0, 0.0), (1.0, 0.0, 0.0))
+
+
+# ---- row f-4: the GL preview's SDF implicit surface (entry.frag:842-947) ----
+PREVIEW_SDF = PrimitiveSdf(0, Shading(0.9, 0.6, 0.2))  # the shader's one instance, its own constants
+
+
+def sdf_eye_camera() -> Camera:
+    """PERSPECTIVE eye outside the preview SDF's AABB (x 0..6, y -3..3, z 2..8), looking along +z."""
+    return Camera(PERSPECTIVE, (3.0, 0.3, 0.5), (0.0, 0.0, 1.0), (0.0, 1.0, 0.0), (1.0, 0.0, 0.0))
+
+
+def sdf_preview_scene() -> Scene:
+    """The preview shader's implicit surface alone (tests; render with
+    sdf_eye_camera(), shadow_camera(), RAYTRACING_FLAGS)."""
+    return Scene([], [], [], [], [dataclasses.replace(PREVIEW_SDF)])
+
+
+def sdf_bench_scene() -> Scene:
+    """Scene S-bench (row f-4 measurement, synthetic): 8 copies of the preview
+    SDF, each with its own AABB, in a 4 x 2 grid in front of sdf_eye_camera(),
+    plus the reference's circle plane as a backdrop."""
+    sdfs = []
+    for i in range(8):
+        dx, dy = -2.25 + 1.5 * (i % 4), -0.9 + 1.8 * (i // 4)
+        base = (3.0 + dx, dy, 5.0 + 0.25 * i)
+        sdfs.append(PrimitiveSdf(i, Shading(*_COLORS_R[i % 5]), base, (base[0] + 0.5, base[1], base[2] + 1.0),
+                                 base, (1.6, 1.4, 2.0)))
+    back = PrimitiveCirclePlane(0, Shading(0.2, 0.2, 0.25), 30.0, (3.0, 0.0, 12.0), (0.0, 0.0, -1.0))
+    return Scene([], [], [back], [], sdfs)
+
+
+def mixed_sdf(frame: int = 100) -> Scene:
+    """Scene A-bench plus one preview SDF beside the spheres, in front of the
+    orthographic eye camera (tests: SDF hits against sphere depths and under
+    the spheres + patch shadow map)."""
+    s = scene_a_bench(frame)
+    s.sdfPrimitives = [PrimitiveSdf(0, Shading(0.9, 0.6, 0.2), (0.4, -0.3, 0.0), (-1.0, -1.2, -1.2),
+                                    (0.4, -0.3, 0.0), (1.0, 1.0, 1.0), 120)]
+    return s

@@ -29,6 +29,7 @@ sys.path.insert(0, ROOT)
 METRIC = "Mpixels/s at 3840×2160, 64 march steps; 1/2/4/8-GPU scaling"
 # configs 6/7 measure BASELINE "next" row f-1 (ray-traced primitives), not the headline
 METRIC_F1 = "Mpixels/s, ray-traced circle planes + capped cylinders (row f-1)"
+METRIC_F4 = "Mpixels/s, sphere-traced GL-preview SDFs (row f-4)"
 
 
 def parse():
@@ -36,7 +37,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--config", type=int, default=3, help="scenes.CONFIGS id: 1-5 BASELINE, 6-7 row f-1")
+    ap.add_argument("--config", type=int, default=3, help="scenes.CONFIGS id: 1-5 BASELINE, 6-7 row f-1, 8 row f-4")
     ap.add_argument("--mode", choices=["frames", "tile-gather"], default="frames")
     ap.add_argument("--fused", action="store_true", help="evaluate shadow texels on demand (same image)")
     ap.add_argument("--per-frame-calls", action="store_true",
@@ -119,7 +120,7 @@ def main():
     ctx.set_timing_capacity(max(1, a.steps // timing_stride))
 
     def scene_for(frame_index: int):
-        if a.config in (5, 6, 7):
+        if a.config >= 5:
             return cfg["scene"]()  # static scenes
         if a.config == 1:
             return sc.closely_orbiting_sphere(100 + frame_index)
@@ -252,7 +253,8 @@ def main():
                                   sep=sep, n_planes=len(s0.circlePlanePrimitives),
                                   n_cyls=len(s0.cappedCylinderPrimitives),
                                   perspective=eye.type_ == sc.PERSPECTIVE,
-                                  search=sep and os.environ.get("RTM_SEP_MODE", "2") == "2")
+                                  search=sep and os.environ.get("RTM_SEP_MODE", "2") == "2",
+                                  n_sdfs=len(s0.sdfPrimitives))
         if band_h != H:  # rank 0 renders one band: scale the frame's work to it (approximate)
             for kk in work.values():
                 kk["ops"] = int(kk["ops"] * band_h / H)
@@ -270,7 +272,7 @@ def main():
             roof_other = (metrics.roofline(other, work, other_ms, _latest_traffic(a.config, other))
                           if other_ms > 0 else None)
         res = {
-            "metric": METRIC if a.config <= 5 else METRIC_F1,
+            "metric": METRIC if a.config <= 5 else METRIC_F1 if a.config <= 7 else METRIC_F4,
             "value": round(value, 2),
             "unit": "Mpixels/s",
             "n_gpus": world,
@@ -283,7 +285,8 @@ def main():
             "dtype": "f64",
             "data": ("synthetic: Scene A-bench (SURVEY.md §8d-2) animation frames 100+i, f64 scene built on host"
                      if a.config in (2, 3, 4) else "synthetic: SURVEY.md §8d-2 scene" if a.config <= 5
-                     else "synthetic: row f-1 scene (scenes.py), f64 scene built on host"),
+                     else "synthetic: row f-1 scene (scenes.py), f64 scene built on host" if a.config <= 7
+                     else "synthetic: row f-4 Scene S-bench (scenes.py), f64 scene built on host"),
             "config": {"workload": cfg["desc"], "config_id": a.config, "width": W, "height": H,
                        "march_steps": K, "mode": a.mode, "shadow": "fused" if fused else "two-pass",
                        "pipelined": pipelined,

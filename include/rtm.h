@@ -41,13 +41,14 @@
 extern "C" {
 #endif
 
-#define RTM_ABI_VERSION 2
+#define RTM_ABI_VERSION 3
 
 /* ---- limits: scene constants travel as kernel arguments (SGPR path) ---- */
 #define RTM_MAX_SPHERES 16
 #define RTM_MAX_PATCHES 4
 #define RTM_MAX_CIRCLE_PLANES 16
 #define RTM_MAX_CAPPED_CYLINDERS 16
+#define RTM_MAX_SDFS 8
 #define RTM_MAX_DIM 32768
 
 /* ---- status codes ---- */
@@ -118,13 +119,34 @@ typedef struct rtm_capped_cylinder {
     double color[3];
 } rtm_capped_cylinder;
 
+/* The signed-distance implicit surface of the reference's GL preview (BASELINE
+ * row f-4; entry.frag:842-947 sphere trace, 416-442 distanceFn0, 290-298 sdBox,
+ * 312-340 udTriangleSingle, 85-110 sBox, 356-364 sdNormalFast): the union of a
+ * box of half-extents (0.4, 0.2, 0.2) centred at box_center and the triangle
+ * tri_anchor + {(0.8,0.8,0.8), (1.3,0.8,0.8), (1.0,0.7,0.2)} (udTriangleSingle's
+ * SQUARED distance, as written), thickened by 0.2; sphere-traced from the ray's
+ * entry into the axis-aligned box aabb_center +- aabb_extent, hit when the
+ * distance drops below 0.03, at most max_steps steps (the shader: 180).  The
+ * shader runs it in f32 on the GPU; here it is restated in f64 (parity against
+ * the oracle's restatement, not against main.rs).  136 bytes. */
+typedef struct rtm_sdf {
+    int64_t id;             /* index into the sdf array (shading lookup) */
+    double box_center[3];   /* descriptor vecs[0] (entry.frag:878) */
+    double tri_anchor[3];   /* descriptor vecs[2] (entry.frag:880) */
+    double aabb_center[3];  /* entry.frag:850 */
+    double aabb_extent[3];  /* entry.frag:851 */
+    double color[3];
+    int32_t max_steps;      /* entry.frag:887: 180 */
+    int32_t reserved;
+} rtm_sdf;
+
 /* Scene (main.rs:404-410).  Spheres are rasterized and patches marched (the
  * reference marches one hard-coded patch, main.rs:2024-2031; here n_patches
  * patches are marched in order, each with a strict-min depth update, main.rs:559).
  * Circle planes and capped cylinders are ray traced into the eye viewport after
  * its rasterize (processRaytracingRays, main.rs:569-642); the reference never
- * traces them into the shadow map (main.rs:998-1003).  ABI v2 added the last
- * four fields. */
+ * traces them into the shadow map (main.rs:998-1003).  ABI v2 added the
+ * primitive fields, v3 the SDFs. */
 typedef struct rtm_scene {
     const rtm_sphere* spheres;
     const rtm_patch* patches;
@@ -134,6 +156,9 @@ typedef struct rtm_scene {
     const rtm_capped_cylinder* capped_cylinders;
     int32_t n_circle_planes;
     int32_t n_capped_cylinders;
+    const rtm_sdf* sdfs; /* ABI v3: traced after the cylinders (row f-4) */
+    int32_t n_sdfs;
+    int32_t reserved;
 } rtm_scene;
 
 /* Per-call statistics (filled by rtm_render_stats on the GPU). */
@@ -148,6 +173,8 @@ typedef struct rtm_stats {
     int64_t march_in_range;            /* texels*patches whose start is inside the [0,1]^2 domain */
     int64_t eye_circle_plane_pixels;   /* eye pixels whose front surface is a circle plane */
     int64_t eye_capped_cylinder_pixels; /* ... a capped cylinder */
+    int64_t eye_sdf_pixels;            /* ... an SDF implicit surface (row f-4) */
+    int64_t sdf_distance_evals;        /* distanceFn0 calls of the eye's SDF traces (march steps + 4 normal taps per hit) */
 } rtm_stats;
 
 /* ---- library ---- */

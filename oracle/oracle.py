@@ -57,6 +57,10 @@ def lib():
         L.rtmo_icapped_cone.restype = None
         L.rtmo_icapped_cone.argtypes = [C.POINTER(C.c_double)] * 4 + [C.c_double, C.c_double,
                                                                        C.POINTER(C.c_double)]
+        L.rtmo_sdf_distance.restype = C.c_double
+        L.rtmo_sdf_distance.argtypes = [C.POINTER(_abi.rtm_sdf), C.POINTER(C.c_double)]
+        L.rtmo_sdf_trace.restype = C.c_double
+        L.rtmo_sdf_trace.argtypes = [C.POINTER(_abi.rtm_sdf)] + [C.POINTER(C.c_double)] * 3 + [C.POINTER(C.c_int64)]
         L.rtmo_encode_scan.restype = C.c_int64
         L.rtmo_encode_scan.argtypes = [C.POINTER(C.c_float), C.c_int32]
         L.rtmo_write_ppm.restype = C.c_int64
@@ -180,3 +184,26 @@ def write_ppm(rgba):
     n = lib().rtmo_write_ppm(_fp(rgba, C.c_float), w, h, buf, cap)
     assert n >= 0
     return buf.raw[:n]
+
+
+def sdf_distance(scene_sdf, p):
+    """distanceFn0 (entry.frag:416-442) of one scenes.PrimitiveSdf at point p."""
+    sc, keep = _sdf_c(scene_sdf)
+    return lib().rtmo_sdf_distance(C.byref(sc), (C.c_double * 3)(*map(float, p)))
+
+
+def sdf_trace(scene_sdf, ro, rd, want_evals=False):
+    """The preview's sphere trace (entry.frag:842-905): (t or -1, normal[, distanceFn0 calls])."""
+    sc, keep = _sdf_c(scene_sdf)
+    n = (C.c_double * 3)()
+    ev = C.c_int64(0)
+    t = lib().rtmo_sdf_trace(C.byref(sc), (C.c_double * 3)(*map(float, ro)), (C.c_double * 3)(*map(float, rd)), n,
+                             C.byref(ev))
+    return (t, tuple(n), ev.value) if want_evals else (t, tuple(n))
+
+
+def _sdf_c(q):
+    from importlib import import_module
+    scenes = import_module("2018rustraytracer_amd.scenes")
+    sc, keep = scenes.Scene([], [], [], [], [q]).to_c()
+    return sc.sdfs[0], keep

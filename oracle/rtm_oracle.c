@@ -206,7 +206,7 @@ static double calcOthoDistanceByAbsPosition(const ProjectedSphere* s, Vec2 p) {
  *   RasterizedSphere{relativeHeight, id, z}            kind GK_SPHERE
  *   RaytracedCirlcePlaneIntersection{id, rayT}          kind GK_PLANE
  *   RaytracedCappedCylinderIntersection{id, rayT, n}    kind GK_CYLINDER */
-enum { GK_SPHERE = 1, GK_PLANE = 2, GK_CYLINDER = 3 };
+enum { GK_SPHERE = 1, GK_PLANE = 2, GK_CYLINDER = 3, GK_SDF = 4 };
 typedef struct {
     int32_t some; /* kind, 0 = None */
     int64_t id;
@@ -228,7 +228,8 @@ typedef struct {
     int64_t eye_hits[RTM_MAX_SPHERES];
     int64_t eye_hit_pixels, lit_pixels, eye_sphere_tests, shadow_sphere_tests;
     int64_t march_iterations, march_hits, march_in_range;
-    int64_t eye_circle_plane_pixels, eye_capped_cylinder_pixels;
+    int64_t eye_circle_plane_pixels, eye_capped_cylinder_pixels, eye_sdf_pixels;
+    int64_t sdf_distance_evals;
 } Counts; /* layout == rtm_stats */
 
 /* rasterizeSphere (main.rs:249-331).  Pixel loop over rows [y0,y1).  The
@@ -591,8 +592,160 @@ static double iCappedCone(Vec3 ro, Vec3 rd, Vec3 pa, Vec3 pb, double ra, double 
     return -1.0;
 }
 
+/* ---- row f-4: the GL preview's SDF implicit surface, restated in f64 ----
+ * entry.frag is GLSL (f32, implementation-defined min/max/normalize); this
+ * restatement fixes the f64 semantics the GPU kernels share:
+ *   min/max: NaN-ignoring, +0 > -0;  sign: GLSL (0 for 0 and NaN);
+ *   cross(x, y) = (x.y y.z - y.y x.z, x.z y.x - y.z x.x, x.x y.y - y.x x.y) (GLSL spec);
+ *   normalize(v) = v * (1 / sqrt(dot(v, v)));  dot = (x + y) + z;
+ *   sBox's translate(-c) applied as ro - c, rd unchanged. */
+static double fmax_d(double a, double b) {
+    if (isnan(a)) return b;
+    if (isnan(b)) return a;
+    if (a > b) return a;
+    if (b > a) return b;
+    return signbit(a) ? b : a;
+}
+static double fmin_d(double a, double b) {
+    if (isnan(a)) return b;
+    if (isnan(b)) return a;
+    if (a < b) return a;
+    if (b < a) return b;
+    return signbit(a) ? a : b;
+}
+static double glsl_sign(double x) { return x > 0.0 ? 1.0 : (x < 0.0 ? -1.0 : 0.0); }
+static Vec3 cross3(Vec3 x, Vec3 y) {
+    return v3(x.y * y.z - y.y * x.z, x.z * y.x - y.z * x.x, x.x * y.y - y.x * x.y);
+}
+
+typedef struct {
+    Vec3 box;                  /* descriptor vecs[0] */
+    Vec3 v1, v2, v3;           /* triangle (entry.frag:436) */
+    Vec3 v21, v32, v13, nor;   /* udTriangleSingle's point-independent terms (entry.frag:318-321) */
+    Vec3 c1, c2, c3;           /* cross(v21,nor), cross(v32,nor), cross(v13,nor) */
+    double d21, d32, d13, dnor;
+} SdfGeom;
+
+static void sdf_geom(const rtm_sdf* s, SdfGeom* g) {
+    Vec3 a = v3(s->tri_anchor[0], s->tri_anchor[1], s->tri_anchor[2]);
+    g->box = v3(s->box_center[0], s->box_center[1], s->box_center[2]);
+    g->v1 = v3_add(a, v3(0.8, 0.8, 0.8));
+    g->v2 = v3_add(a, v3(1.3, 0.8, 0.8));
+    g->v3 = v3_add(a, v3(1.0, 0.7, 0.2));
+    g->v21 = v3_sub(g->v2, g->v1);
+    g->v32 = v3_sub(g->v3, g->v2);
+    g->v13 = v3_sub(g->v1, g->v3);
+    g->nor = cross3(g->v21, g->v13);
+    g->c1 = cross3(g->v21, g->nor);
+    g->c2 = cross3(g->v32, g->nor);
+    g->c3 = cross3(g->v13, g->nor);
+    g->d21 = dot(g->v21, g->v21);
+    g->d32 = dot(g->v32, g->v32);
+    g->d13 = dot(g->v13, g->v13);
+    g->dnor = dot(g->nor, g->nor);
+}
+
+/* sdBox (entry.frag:290-298) */
+static double sdBox(Vec3 p, Vec3 b) {
+    Vec3 d = v3(fabs(p.x) - b.x, fabs(p.y) - b.y, fabs(p.z) - b.z);
+    Vec3 m = v3(fmax_d(d.x, 0.0), fmax_d(d.y, 0.0), fmax_d(d.z, 0.0));
+    return fmin_d(fmax_d(d.x, fmax_d(d.y, d.z)), 0.0) + sqrt(dot(m, m));
+}
+
+/* udTriangleSingle (entry.frag:312-340): the SQUARED distance */
+static double udTriangleSingle(const SdfGeom* g, Vec3 p) {
+    Vec3 p1 = v3_sub(p, g->v1), p2 = v3_sub(p, g->v2), p3 = v3_sub(p, g->v3);
+    if (glsl_sign(dot(g->c1, p1)) + glsl_sign(dot(g->c2, p2)) + glsl_sign(dot(g->c3, p3)) < 2.0) {
+        Vec3 e1 = v3_sub(v3_scale(g->v21, fmin_d(fmax_d(dot(g->v21, p1) / g->d21, 0.0), 1.0)), p1);
+        Vec3 e2 = v3_sub(v3_scale(g->v32, fmin_d(fmax_d(dot(g->v32, p2) / g->d32, 0.0), 1.0)), p2);
+        Vec3 e3 = v3_sub(v3_scale(g->v13, fmin_d(fmax_d(dot(g->v13, p3) / g->d13, 0.0), 1.0)), p3);
+        return fmin_d(fmin_d(dot(e1, e1), dot(e2, e2)), dot(e3, e3));
+    }
+    double dn = dot(g->nor, p1);
+    return dn * dn / g->dnor;
+}
+
+/* distanceFn0 (entry.frag:416-442) */
+static double distanceFn0(const SdfGeom* g, Vec3 p) {
+    double d0 = sdBox(v3_sub(p, g->box), v3(0.4, 0.2, 0.2));
+    double d1 = udTriangleSingle(g, p);
+    double d2 = fmin_d(d0, d1);
+    d2 -= 0.2;
+    return d2;
+}
+
+/* sBox (entry.frag:85-110) with txx = translate(-center) */
+static double sBox(Vec3 ro, Vec3 rd, Vec3 center, Vec3 rad, int checkFirstIntersection) {
+    Vec3 roo = v3_sub(ro, center);
+    Vec3 m = v3(1.0 / rd.x, 1.0 / rd.y, 1.0 / rd.z);
+    Vec3 n = v3(m.x * roo.x, m.y * roo.y, m.z * roo.z);
+    Vec3 k = v3(fabs(m.x) * rad.x, fabs(m.y) * rad.y, fabs(m.z) * rad.z);
+    Vec3 t1 = v3(-n.x - k.x, -n.y - k.y, -n.z - k.z);
+    Vec3 t2 = v3(-n.x + k.x, -n.y + k.y, -n.z + k.z);
+    double tN = fmax_d(fmax_d(t1.x, t1.y), t1.z);
+    double tF = fmin_d(fmin_d(t2.x, t2.y), t2.z);
+    if (checkFirstIntersection && (tN > tF || tF < 0.0)) return -1.0;
+    return tN;
+}
+
+/* The implicit-surface branch of bvhProcessLeafHit (entry.frag:842-917): t of
+ * the hit or -1, and the sdNormalFast normal (entry.frag:356-364, 893-905). */
+static double traceSdf(const rtm_sdf* s, const SdfGeom* g, Vec3 ro, Vec3 rd, Vec3* nOut, int64_t* evals) {
+    Vec3 c = v3(s->aabb_center[0], s->aabb_center[1], s->aabb_center[2]);
+    Vec3 e = v3(s->aabb_extent[0], s->aabb_extent[1], s->aabb_extent[2]);
+    double tIn = sBox(ro, rd, c, e, 1);
+    if (!(tIn >= 0.0)) return -1.0;
+    double tOut = -sBox(ro, v3(-rd.x, -rd.y, -rd.z), c, e, 0);
+    double t = tIn;
+    int hit = 0;
+    for (int32_t stepI = 0; stepI < s->max_steps; stepI++) {
+        Vec3 p = v3_add(ro, v3_scale(rd, t));
+        double distance = distanceFn0(g, p);
+        if (evals) ++*evals;
+        if (distance < 0.03) {
+            hit = 1;
+            break;
+        }
+        if (t > tOut) break;
+        t += distance;
+    }
+    if (!hit) return -1.0;
+    if (evals) *evals += 4;
+    Vec3 p = v3_add(ro, v3_scale(rd, t));
+    const double h = 0.001;
+    double pnn = distanceFn0(g, v3_add(p, v3(1.0 * h, -1.0 * h, -1.0 * h)));
+    double nnp = distanceFn0(g, v3_add(p, v3(-1.0 * h, -1.0 * h, 1.0 * h)));
+    double npn = distanceFn0(g, v3_add(p, v3(-1.0 * h, 1.0 * h, -1.0 * h)));
+    double ppp = distanceFn0(g, v3_add(p, v3(1.0 * h, 1.0 * h, 1.0 * h)));
+    Vec3 v = v3(((1.0 * pnn + -1.0 * nnp) + -1.0 * npn) + 1.0 * ppp,
+                ((-1.0 * pnn + -1.0 * nnp) + 1.0 * npn) + 1.0 * ppp,
+                ((-1.0 * pnn + 1.0 * nnp) + -1.0 * npn) + 1.0 * ppp);
+    *nOut = normalize(v);
+    return t;
+}
+
+/* test hooks */
+double rtmo_sdf_distance(const rtm_sdf* s, const double p[3]) {
+    SdfGeom g;
+    sdf_geom(s, &g);
+    return distanceFn0(&g, v3(p[0], p[1], p[2]));
+}
+double rtmo_sdf_trace(const rtm_sdf* s, const double ro[3], const double rd[3], double n[3], int64_t* evals) {
+    SdfGeom g;
+    sdf_geom(s, &g);
+    Vec3 nn = v3(0.0, 0.0, 0.0);
+    double t = traceSdf(s, &g, v3(ro[0], ro[1], ro[2]), v3(rd[0], rd[1], rd[2]), &nn, evals);
+    n[0] = nn.x;
+    n[1] = nn.y;
+    n[2] = nn.z;
+    return t;
+}
+
 /* Viewport::processRaytracingRays (main.rs:569-642) over rows [y0,y1) */
-static void viewport_process_raytracing_rays(Viewport* vp, const rtm_scene* scene, int64_t y0, int64_t y1) {
+static void viewport_process_raytracing_rays(Viewport* vp, const rtm_scene* scene, int64_t y0, int64_t y1,
+                                             int64_t* evals) {
+    SdfGeom geoms[RTM_MAX_SDFS];
+    for (int32_t i = 0; i < scene->n_sdfs && i < RTM_MAX_SDFS; i++) sdf_geom(&scene->sdfs[i], &geoms[i]);
     for (int64_t yi = y0; yi < y1; yi++) {
         for (int64_t xi = 0; xi < vp->W; xi++) {
             Vec3 o, d;
@@ -625,6 +778,18 @@ static void viewport_process_raytracing_rays(Viewport* vp, const rtm_scene* scen
                 GEntry* g = &vp->rasterized[idx];
                 g->some = GK_CYLINDER;
                 g->id = cy->id;
+                g->rayT = t;
+                g->n = n;
+                vp->zBuffer[idx] = t;
+            }
+            for (int32_t i = 0; i < scene->n_sdfs; i++) {
+                /* row f-4, after the cylinders; the shader's acceptance: 0 < t < depth (entry.frag:908-917) */
+                Vec3 n;
+                double t = traceSdf(&scene->sdfs[i], &geoms[i], o, d, &n, evals);
+                if (!(t > 0.0) || !(t < vp->zBuffer[idx])) continue;
+                GEntry* g = &vp->rasterized[idx];
+                g->some = GK_SDF;
+                g->id = scene->sdfs[i].id;
                 g->rayT = t;
                 g->n = n;
                 vp->zBuffer[idx] = t;
@@ -666,9 +831,13 @@ static void renderColorImage(const rtm_scene* scene, const Viewport* vp, const V
                     const rtm_circle_plane* pl = &scene->circle_planes[iPixel->id];
                     color = pl->color;
                     normal = v3(pl->n[0], pl->n[1], pl->n[2]);
-                } else { /* main.rs:779-795; calcDepth = rayT (main.rs:169-171) */
+                } else if (iPixel->some == GK_CYLINDER) { /* main.rs:779-795; calcDepth = rayT (main.rs:169-171) */
                     worldPosition = v3_add(o, v3_scale(d, iPixel->rayT));
                     color = scene->capped_cylinders[iPixel->id].color;
+                    normal = iPixel->n;
+                } else { /* row f-4: shaded like the cylinder kind, with the sdNormalFast normal */
+                    worldPosition = v3_add(o, v3_scale(d, iPixel->rayT));
+                    color = scene->sdfs[iPixel->id].color;
                     normal = iPixel->n;
                 }
 
@@ -701,6 +870,7 @@ static void renderColorImage(const rtm_scene* scene, const Viewport* vp, const V
                         cnt->eye_hits[iPixel->id]++;
                     if (iPixel->some == GK_PLANE) cnt->eye_circle_plane_pixels++;
                     if (iPixel->some == GK_CYLINDER) cnt->eye_capped_cylinder_pixels++;
+                    if (iPixel->some == GK_SDF) cnt->eye_sdf_pixels++;
                     if (inLight) cnt->lit_pixels++;
                 }
             }
@@ -730,6 +900,10 @@ static int validate_scene(const rtm_scene* scene) {
             return RTM_ERR_INVALID;
     for (int32_t i = 0; i < scene->n_capped_cylinders; i++)
         if (scene->capped_cylinders[i].id < 0 || scene->capped_cylinders[i].id >= scene->n_capped_cylinders)
+            return RTM_ERR_INVALID;
+    if (scene->n_sdfs < 0 || scene->n_sdfs > RTM_MAX_SDFS || (scene->n_sdfs > 0 && !scene->sdfs)) return RTM_ERR_INVALID;
+    for (int32_t i = 0; i < scene->n_sdfs; i++)
+        if (scene->sdfs[i].id < 0 || scene->sdfs[i].id >= scene->n_sdfs || scene->sdfs[i].max_steps < 0)
             return RTM_ERR_INVALID;
     return RTM_OK;
 }
@@ -788,7 +962,7 @@ int rtmo_render(const rtm_scene* scene, const rtm_camera* eye, const rtm_camera*
                     viewport_process_raymarching_rays(&vs, scene->patches, scene->n_patches, steps, y0, y1, &c);
             } else if (pass == 1) {
                 viewport_rasterize(&ve, scene, flags, y0, y1, &c.eye_sphere_tests);
-                viewport_process_raytracing_rays(&ve, scene, y0, y1);
+                viewport_process_raytracing_rays(&ve, scene, y0, y1, &c.sdf_distance_evals);
             } else {
                 renderColorImage(scene, &ve, &vs, out_rgba, y0, y1, &c);
             }
@@ -837,7 +1011,7 @@ int rtmo_viewport_rasterize(rtmo_viewport* v, const rtm_scene* scene, int32_t fl
 int rtmo_viewport_process_raytracing_rays(rtmo_viewport* v, const rtm_scene* scene) {
     int rc = validate_scene(scene);
     if (rc) return rc;
-    viewport_process_raytracing_rays(&v->vp, scene, 0, v->vp.H);
+    viewport_process_raytracing_rays(&v->vp, scene, 0, v->vp.H, NULL);
     return RTM_OK;
 }
 

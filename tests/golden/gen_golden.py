@@ -171,8 +171,113 @@ def icapped_cone(ro, rd, pa, pb, ra, rb):
     return t, n
 
 
-def raytrace(cam, planes, cyls, W, H, zbuf, g):
-    """processRaytracingRays (main.rs:569-642): planes then cylinders, in order."""
+# ---- row f-4: the GL preview's SDF (entry.frag), f64 restatement, vectorised ----
+def _fmax(a, b):
+    a, b = np.broadcast_arrays(np.asarray(a, np.float64), np.asarray(b, np.float64))
+    return np.where(np.isnan(a), b, np.where(np.isnan(b), a, np.where(a > b, a, np.where(b > a, b,
+                    np.where(np.signbit(a), b, a)))))
+
+
+def _fmin(a, b):
+    a, b = np.broadcast_arrays(np.asarray(a, np.float64), np.asarray(b, np.float64))
+    return np.where(np.isnan(a), b, np.where(np.isnan(b), a, np.where(a < b, a, np.where(b < a, b,
+                    np.where(np.signbit(a), a, b)))))
+
+
+def _gsign(x):
+    return np.where(x > 0.0, 1.0, np.where(x < 0.0, -1.0, 0.0))
+
+
+def _cross(x, y):
+    return (x[1] * y[2] - y[1] * x[2], x[2] * y[0] - y[2] * x[0], x[0] * y[1] - y[0] * x[1])
+
+
+def _sub3(a, b):
+    return tuple(a[k] - b[k] for k in range(3))
+
+
+def _sdf_geom(sd):
+    _id, box, tri, _c, _e, _col, _steps = sd
+    v1 = tuple(tri[k] + (0.8, 0.8, 0.8)[k] for k in range(3))
+    v2 = tuple(tri[k] + (1.3, 0.8, 0.8)[k] for k in range(3))
+    v3 = tuple(tri[k] + (1.0, 0.7, 0.2)[k] for k in range(3))
+    v21, v32, v13 = _sub3(v2, v1), _sub3(v3, v2), _sub3(v1, v3)
+    nor = _cross(v21, v13)
+    return dict(box=box, v=(v1, v2, v3), e=(v21, v32, v13), nor=nor,
+                c=(_cross(v21, nor), _cross(v32, nor), _cross(v13, nor)),
+                d=(dot(v21, v21), dot(v32, v32), dot(v13, v13)), dnor=dot(nor, nor))
+
+
+def _dist(g, p):
+    """distanceFn0 (entry.frag:416-442) at points p (3 arrays)."""
+    with np.errstate(all="ignore"):
+        q = _sub3(p, g["box"])
+        dd = [np.abs(q[k]) - (0.4, 0.2, 0.2)[k] for k in range(3)]
+        m = [_fmax(dd[k], 0.0) for k in range(3)]
+        d0 = _fmin(_fmax(dd[0], _fmax(dd[1], dd[2])), 0.0) + np.sqrt(dot(m, m))
+        ps = [_sub3(p, g["v"][i]) for i in range(3)]
+        inside = (_gsign(dot(g["c"][0], ps[0])) + _gsign(dot(g["c"][1], ps[1])) + _gsign(dot(g["c"][2], ps[2]))) < 2.0
+        es = []
+        for i in range(3):
+            cl = _fmin(_fmax(dot(g["e"][i], ps[i]) / g["d"][i], 0.0), 1.0)
+            e = [g["e"][i][k] * cl - ps[i][k] for k in range(3)]
+            es.append(dot(e, e))
+        edges = _fmin(_fmin(es[0], es[1]), es[2])
+        dn = dot(g["nor"], ps[0])
+        face = dn * dn / g["dnor"]
+        d1 = np.where(inside, edges, face)
+        return _fmin(d0, d1) - 0.2
+
+
+def _sbox(ro, rd, c, e, check):
+    with np.errstate(all="ignore"):
+        roo = _sub3(ro, c)
+        m = [1.0 / rd[k] for k in range(3)]
+        n = [m[k] * roo[k] for k in range(3)]
+        kk = [np.abs(m[k]) * e[k] for k in range(3)]
+        t1 = [-n[k] - kk[k] for k in range(3)]
+        t2 = [-n[k] + kk[k] for k in range(3)]
+        tN = _fmax(_fmax(t1[0], t1[1]), t1[2])
+        tF = _fmin(_fmin(t2[0], t2[1]), t2[2])
+        if check:
+            tN = np.where((tN > tF) | (tF < 0.0), -1.0, tN)
+        return tN
+
+
+def trace_sdf(sd, ro, rd):
+    """entry.frag:842-905 per pixel: (t or -1, normal)."""
+    g = _sdf_geom(sd)
+    c, e, steps = sd[3], sd[4], sd[6]
+    tIn = _sbox(ro, rd, c, e, True)
+    ok = tIn >= 0.0
+    tOut = -_sbox(ro, tuple(-rd[k] for k in range(3)), c, e, False)
+    t = np.where(ok, tIn, 0.0)
+    active = ok.copy()
+    hit = np.zeros(ok.shape, bool)
+    for _ in range(steps):
+        if not active.any():
+            break
+        p = tuple(ro[k] + rd[k] * t for k in range(3))
+        dist = _dist(g, p)
+        newhit = active & (dist < 0.03)
+        hit |= newhit
+        active &= ~newhit
+        active &= ~(t > tOut)
+        t = np.where(active, t + dist, t)
+    p = tuple(ro[k] + rd[k] * t for k in range(3))
+    h = 0.001
+    ks = ((1.0, -1.0, -1.0), (-1.0, -1.0, 1.0), (-1.0, 1.0, -1.0), (1.0, 1.0, 1.0))
+    taps = [_dist(g, tuple(p[k] + (s[k] * h) for k in range(3))) for s in ks]
+    v = [((ks[0][k] * taps[0] + ks[1][k] * taps[1]) + ks[2][k] * taps[2]) + ks[3][k] * taps[3] for k in range(3)]
+    with np.errstate(all="ignore"):
+        inv = 1.0 / np.sqrt(dot(v, v))
+    n = [v[k] * inv for k in range(3)]
+    return np.where(hit, t, -1.0), n
+
+
+def raytrace(cam, planes, cyls, W, H, zbuf, g, sdfs=()):
+    """processRaytracingRays (main.rs:569-642): planes then cylinders, in order
+    (then the row f-4 SDFs, accepted for 0 < t < depth)."""
     o, d = rays(cam, W, H)
     with np.errstate(all="ignore"):
         for (pid, c, n, radius, _col) in planes:
@@ -192,6 +297,15 @@ def raytrace(cam, planes, cyls, W, H, zbuf, g):
             zbuf[win] = t[win]
             g["kind"][win] = 3
             g["id"][win] = cid
+            g["t"][win] = t[win]
+            for k in range(3):
+                g["n%d" % k][win] = n[k][win]
+        for sd in sdfs:
+            t, n = trace_sdf(sd, o, d)
+            win = (t > 0.0) & (t < zbuf)
+            zbuf[win] = t[win]
+            g["kind"][win] = 4
+            g["id"][win] = sd[0]
             g["t"][win] = t[win]
             for k in range(3):
                 g["n%d" % k][win] = n[k][win]
@@ -321,7 +435,8 @@ def march(cam, patches, W, H, steps, zbuf):
         zbuf[upd] = hit_t[upd]
 
 
-def render(spheres, patches, W, H, steps, no_march=False, no_sraster=False, planes=(), cyls=(), eye=EYE_CAM):
+def render(spheres, patches, W, H, steps, no_march=False, no_sraster=False, planes=(), cyls=(), eye=EYE_CAM,
+           sdfs=()):
     zs = np.full((H, W), np.inf)
     if not no_sraster:
         rasterize(SHADOW_CAM, spheres, W, H, 1, zs, None)
@@ -333,7 +448,7 @@ def render(spheres, patches, W, H, steps, no_march=False, no_sraster=False, plan
              n2=np.zeros((H, W)))
     if spheres:
         rasterize(eye, spheres, W, H, 0, ze, g)
-    raytrace(eye, planes, cyls, W, H, ze, g)
+    raytrace(eye, planes, cyls, W, H, ze, g, sdfs)
     # renderColorImage (main.rs:710-902)
     img = np.zeros((H, W, 4), np.float32)
     img[..., 1] = np.float32(0.2)
@@ -348,10 +463,11 @@ def render(spheres, patches, W, H, steps, no_march=False, no_sraster=False, plan
         sprm = {sid: (pos, r, col) for (sid, pos, r, col) in spheres}
         pprm = {pid: (n, col) for (pid, _c, n, _r, col) in planes}
         cprm = {cid: col for (cid, _a, _b, _ra, _rb, col) in cyls}
+        sdprm = {sd[0]: sd[5] for sd in sdfs}
         sph = kind == 1
         R = np.array([sprm[i][1] if k == 1 else 1.0 for i, k in zip(ids, kind)])
         P = np.array([sprm[i][0] if k == 1 else (0.0, 0.0, 0.0) for i, k in zip(ids, kind)]).reshape(-1, 3)
-        COL = np.array([sprm[i][2] if k == 1 else pprm[i][1] if k == 2 else cprm[i]
+        COL = np.array([sprm[i][2] if k == 1 else pprm[i][1] if k == 2 else cprm[i] if k == 3 else sdprm[i]
                         for i, k in zip(ids, kind)]).reshape(-1, 3)
         # calcDepth (main.rs:155-173)
         depth = np.where(sph, g["z"][hit] - g["h"][hit] * R, g["t"][hit])
@@ -393,13 +509,11 @@ def render(spheres, patches, W, H, steps, no_march=False, no_sraster=False, plan
             img[hit, 1] = ((base * lm) * COL[:, 1]).astype(np.float32)
             img[hit, 2] = ((base * lm) * COL[:, 2]).astype(np.float32)
         stats = dict(eye_hits=[int(((ids == i) & sph).sum()) for i in range(len(spheres))], lit=int(lit.sum()))
-        if planes or cyls:
-            stats["plane_px"] = int((kind == 2).sum())
-            stats["cyl_px"] = int((kind == 3).sum())
+        stats["plane_px"] = int((kind == 2).sum())
+        stats["cyl_px"] = int((kind == 3).sum())
+        stats["sdf_px"] = int((kind == 4).sum())
     else:
-        stats = dict(eye_hits=[0] * len(spheres), lit=0)
-        if planes or cyls:
-            stats["plane_px"] = stats["cyl_px"] = 0
+        stats = dict(eye_hits=[0] * len(spheres), lit=0, plane_px=0, cyl_px=0, sdf_px=0)
     return img, zs, stats
 
 
@@ -428,6 +542,25 @@ CASES = [
 ]
 
 # row f-1 cases: (name, spheres, patches, planes, cyls, eye, W, H, steps, flags, small)
+# (id, box_center, tri_anchor, aabb_center, aabb_extent, color, max_steps): scenes.PREVIEW_SDF etc.
+SDF_PREVIEW = (0, (3.0, 0.0, 5.0), (3.5, 0.0, 6.0), (3.0, 0.0, 5.0), (3.0, 3.0, 3.0), (0.9, 0.6, 0.2), 180)
+SDF_CAM = dict(type=1, pos=(3.0, 0.3, 0.5), dir=(0.0, 0.0, 1.0), up=(0.0, 1.0, 0.0), side=(1.0, 0.0, 0.0))
+
+
+def sdf_bench():
+    cols = [(1.0, 0.02, 0.02), (0.02, 0.02, 1.0), (0.2, 0.9, 0.2), (0.9, 0.9, 0.2), (0.9, 0.2, 0.9)]
+    sdfs = []
+    for i in range(8):
+        dx, dy = -2.25 + 1.5 * (i % 4), -0.9 + 1.8 * (i // 4)
+        base = (3.0 + dx, dy, 5.0 + 0.25 * i)
+        sdfs.append((i, base, (base[0] + 0.5, base[1], base[2] + 1.0), base, (1.6, 1.4, 2.0), cols[i % 5], 180))
+    back = (0, (3.0, 0.0, 12.0), (0.0, 0.0, -1.0), 30.0, (0.2, 0.2, 0.25))
+    return [back], sdfs
+
+
+# an SDF beside the orbit scene's spheres, seen by its orthographic eye (scenes.mixed_sdf)
+SDF_MIXED = (0, (0.4, -0.3, 0.0), (-1.0, -1.2, -1.2), (0.4, -0.3, 0.0), (1.0, 1.0, 1.0), (0.9, 0.6, 0.2), 120)
+
 P1 = [(0, (0.01, 0.01, 4.0), 0.5, (0.02, 0.02, 1.0))]
 P2 = P1 + [(1, (0.01, 0.01, 6.0), 0.5, (0.02, 1.0, 0.02))]
 PERSP2_CAM = dict(PERSP_CAM, pos=(0.0, 1.5, 0.0))
@@ -438,6 +571,11 @@ RT_CASES = [
     ("f3_persp1_512", P1, [], [], [], PERSP_CAM, 512, 512, 0, 3, False),
     ("f3_persp2_512", P2, [], [], [], PERSP2_CAM, 512, 512, 0, 3, False),
     ("f3_persp2_rt_640x360", P2, [], [REF_PLANE], [REF_CYL], PERSP2_CAM, 640, 360, 0, 3, False),
+    ("f4_preview_96", [], [], [], [], SDF_CAM, 96, 96, 0, 3, True, [SDF_PREVIEW]),
+    ("f4_bench_128x72", [], [], sdf_bench()[0], [], SDF_CAM, 128, 72, 0, 3, True, sdf_bench()[1]),
+    ("f4_mixed_orbit_96", *orbit_scene(100, [BENCH_PATCH]), [], [], EYE_CAM, 96, 96, 64, 0, True, [SDF_MIXED]),
+    ("f4_preview_512", [], [], [], [], SDF_CAM, 512, 512, 0, 3, False, [SDF_PREVIEW]),
+    ("f4_bench_640x360", [], [], sdf_bench()[0], [], SDF_CAM, 640, 360, 0, 3, False, sdf_bench()[1]),
     ("rt_plane0_64", [], [], [], [REF_CYL], PERSP_CAM, 64, 64, 0, 3, True),
     ("rt_plane0_withplane_96x80", [], [], [REF_PLANE], [REF_CYL], PERSP_CAM, 96, 80, 0, 3, True),
     ("rt_rbench_128x72", [], [], *rbench(), PERSP_CAM, 128, 72, 0, 3, True),
@@ -453,12 +591,12 @@ RT_CASES = [
 def main():
     # pin against SURVEY.md §8c-3 before writing anything
     img0, _, st0 = render(*orbit_scene(0, [REF_PATCH]), 512, 512, 500)
-    assert st0 == dict(eye_hits=[8014, 6372, 659], lit=0), st0
+    assert (st0["eye_hits"], st0["lit"]) == ([8014, 6372, 659], 0), st0
     assert sha16(img0) == "cf557d736f83a4f6"
     assert img0[256, 384, :3].tolist() == [9265101144064.0, 9265101144064.0, 463255038328832.0]
     assert img0[300, 384, :3].tolist() == [3506.7421875, 3506.7421875, 175337.109375]
     img100, _, st100 = render(*orbit_scene(100, [REF_PATCH]), 512, 512, 500)
-    assert st100 == dict(eye_hits=[8245, 6580, 2059], lit=2059), st100
+    assert (st100["eye_hits"], st100["lit"]) == ([8245, 6580, 2059], 2059), st100
     assert sha16(img100) == "cb7008f728da5208"
 
     fixtures, golden = {}, {}
@@ -471,12 +609,15 @@ def main():
             fixtures[name + "__rgba"] = img
             fixtures[name + "__shadow"] = zs
         print(name, golden[name]["rgba_sha256"][:16], st)
-    for name, sph, pat, planes, cyls, eye, W, H, K, flags, small in RT_CASES:
+    for case in RT_CASES:
+        name, sph, pat, planes, cyls, eye, W, H, K, flags, small = case[:11]
+        sdfs = case[11] if len(case) > 11 else []
         img, zs, st = render(sph, pat, W, H, K, no_march=bool(flags & 1), no_sraster=bool(flags & 2),
-                             planes=planes, cyls=cyls, eye=eye)
+                             planes=planes, cyls=cyls, eye=eye, sdfs=sdfs)
         golden[name] = dict(width=W, height=H, steps=K, flags=flags, rgba_sha256=sha_full(img),
                             shadow_sha256=sha_full(zs), eye_hits=st["eye_hits"], lit_pixels=st["lit"],
-                            circle_plane_pixels=st.get("plane_px", 0), capped_cylinder_pixels=st.get("cyl_px", 0))
+                            circle_plane_pixels=st.get("plane_px", 0), capped_cylinder_pixels=st.get("cyl_px", 0),
+                            sdf_pixels=st.get("sdf_px", 0))
         if small:
             fixtures[name + "__rgba"] = img
             fixtures[name + "__shadow"] = zs

@@ -44,7 +44,8 @@ def test_struct_sizes(rtm):
     assert C.sizeof(abi.rtm_patch) == 32
     assert C.sizeof(abi.rtm_circle_plane) == 88
     assert C.sizeof(abi.rtm_capped_cylinder) == 96
-    assert C.sizeof(abi.rtm_scene) == 48
+    assert C.sizeof(abi.rtm_sdf) == 136
+    assert C.sizeof(abi.rtm_scene) == 64
 
 
 def test_struct_layout_matches_header(rtm, tmp_path):
@@ -52,7 +53,7 @@ def test_struct_layout_matches_header(rtm, tmp_path):
     import subprocess
     abi = rtm.abi
     structs = [abi.rtm_sphere, abi.rtm_patch, abi.rtm_camera, abi.rtm_circle_plane, abi.rtm_capped_cylinder,
-               abi.rtm_scene, abi.rtm_stats]
+               abi.rtm_sdf, abi.rtm_scene, abi.rtm_stats]
     lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "rtm.h"', "int main(void) {"]
     for st in structs:
         n = st.__name__

@@ -36,6 +36,12 @@ def _case(scenes, name):
         return s, scenes.perspective_simple2_camera()
     if name.startswith("f3_persp2"):
         return scenes.perspective_simple2(), scenes.perspective_simple2_camera()
+    if name.startswith("f4_preview"):
+        return scenes.sdf_preview_scene(), scenes.sdf_eye_camera()
+    if name.startswith("f4_bench"):
+        return scenes.sdf_bench_scene(), scenes.sdf_eye_camera()
+    if name.startswith("f4_mixed_orbit"):
+        return scenes.mixed_sdf(100), scenes.eye_camera()
     return _scene_for(scenes, name), scenes.eye_camera()
 
 
@@ -95,6 +101,8 @@ def test_oracle_matches_golden(oracle, scenes, name):
     if "circle_plane_pixels" in g:
         assert r["stats"]["eye_circle_plane_pixels"] == g["circle_plane_pixels"]
         assert r["stats"]["eye_capped_cylinder_pixels"] == g["capped_cylinder_pixels"]
+    if "sdf_pixels" in g:
+        assert r["stats"]["eye_sdf_pixels"] == g["sdf_pixels"]
 
 
 def test_oracle_matches_fixture_arrays(oracle, scenes):
@@ -249,3 +257,41 @@ def test_encode_rgb8_ppm_pixel_rule(oracle):
     assert out[0].tolist() == [0, int(np.float32(np.float32(0.5) ** np.float32(1 / 2.2)) * 255), 255] or out[0][0] == 0
     assert out[1][0] == 255 and out[1][1] == 0
     assert out[2][0] == 255
+
+
+def test_sdf_known_answers(oracle, scenes):
+    """The preview SDF (entry.frag:416-442, 842-905) restated in f64: distance
+    inside / outside the box, a trace straight at the box's front face (which
+    the thickening puts at z = 5 - 0.2 - 0.2), a ray that misses the AABB, a ray
+    from inside the AABB (the shader's tIn < 0 -> no hit, entry.frag:855-858)."""
+    q = scenes.PREVIEW_SDF
+    assert oracle.sdf_distance(q, (3.0, 0.0, 5.0)) == -0.4      # box centre: -0.2 (inside) - 0.2
+    assert abs(oracle.sdf_distance(q, (3.0, 0.0, 0.0)) - 4.6) < 1e-12
+    t, n = oracle.sdf_trace(q, (3.0, 0.05, 0.5), (0.0, 0.0, 1.0))
+    assert abs(t - 4.1) < 0.03 and n == (0.0, 0.0, -1.0)
+    assert oracle.sdf_trace(q, (3.0, 5.0, 0.5), (0.0, 0.0, 1.0))[0] == -1.0   # above the AABB
+    assert oracle.sdf_trace(q, (3.0, 0.0, 3.0), (0.0, 0.0, 1.0))[0] == -1.0   # starts inside the AABB
+
+
+def test_sdf_matches_independent_restatement(oracle, scenes):
+    """C oracle trace == numpy restatement (gen_golden.trace_sdf) bit for bit on random rays."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("gen_golden", os.path.join(GOLD, "gen_golden.py"))
+    gg = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(gg)
+    rng = np.random.default_rng(0x2018 + 4)
+    q = scenes.PREVIEW_SDF
+    sd = (0, q.box_center, q.tri_anchor, q.aabb_center, q.aabb_extent, (1.0, 1.0, 1.0), q.max_steps)
+    ro = np.stack([rng.uniform(1.0, 5.0, 300), rng.uniform(-1.0, 1.5, 300), rng.uniform(-1.0, 1.5, 300)], 1)
+    tgt = np.stack([rng.uniform(2.2, 5.0, 300), rng.uniform(-0.5, 1.0, 300), rng.uniform(4.5, 7.0, 300)], 1)
+    rd = tgt - ro
+    rd /= np.linalg.norm(rd, axis=1, keepdims=True)
+    t_np, n_np = gg.trace_sdf(sd, [ro[:, k] for k in range(3)], [rd[:, k] for k in range(3)])
+    hits = 0
+    for i in range(300):
+        t, n = oracle.sdf_trace(q, ro[i], rd[i])
+        assert np.float64(t).tobytes() == np.float64(t_np[i]).tobytes(), i
+        if t >= 0:
+            hits += 1
+            assert all(np.float64(n[k]).tobytes() == np.float64(n_np[k][i]).tobytes() for k in range(3)), i
+    assert hits > 50

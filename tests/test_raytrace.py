@@ -46,12 +46,18 @@ def _case(scenes, name):
         return s, scenes.perspective_simple2_camera()
     if name.startswith("f3_persp2"):
         return scenes.perspective_simple2(), scenes.perspective_simple2_camera()
+    if name.startswith("f4_preview"):
+        return scenes.sdf_preview_scene(), scenes.sdf_eye_camera()
+    if name.startswith("f4_bench"):
+        return scenes.sdf_bench_scene(), scenes.sdf_eye_camera()
+    if name.startswith("f4_mixed_orbit"):
+        return scenes.mixed_sdf(100), scenes.eye_camera()
     return scenes.mixed_rt(100), scenes.eye_camera()
 
 
 def _rt_golden():
     with open(os.path.join(GOLD, "golden.json")) as f:
-        return {k: v for k, v in json.load(f)["cases"].items() if k.startswith(("rt_", "f3_"))}
+        return {k: v for k, v in json.load(f)["cases"].items() if k.startswith(("rt_", "f3_", "f4_"))}
 
 
 @pytest.mark.parametrize("name", sorted(_rt_golden().keys()))
