@@ -10,6 +10,7 @@ with importlib.import_module("2018rustraytracer_amd").
 from . import abi, scenes  # noqa: F401
 from .abi import RtmError, load_library  # noqa: F401
 from .scenes import (Bilinear, Camera, EnumFace, Linear, PrimitiveCappedCylinder, PrimitiveCirclePlane,  # noqa: F401
-                     PrimitiveSphere, Scene, Shading, eye_camera, perspective_eye_camera, shadow_camera)
+                     PrimitiveSdf, PrimitiveSphere, Scene, Shading, eye_camera, perspective_eye_camera,
+                     shadow_camera)
 from .renderer import (Context, Viewport, device_count, encode_thresholds, renderColorImage,  # noqa: F401
-                       render_frame, writeColorImage)
+                       render_frame, render_frame_multi, writeColorImage)

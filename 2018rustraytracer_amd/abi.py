@@ -121,6 +121,8 @@ ABI_SYMBOLS = [
     ("rtm_render_frames_async", C.c_int, [_P, _I32, C.POINTER(rtm_scene), C.POINTER(rtm_camera),
                                           C.POINTER(rtm_camera), _I32, _I32, _I32, _I32, C.POINTER(_P)]),
     ("rtm_ctx_shadow_map", _P, [_P]),
+    ("rtm_render_multi", C.c_int, [C.POINTER(rtm_scene), C.POINTER(rtm_camera), C.POINTER(rtm_camera),
+                                   _I32, _I32, _I32, _I32, C.POINTER(C.c_float), _I32]),
     ("rtm_render_stats", C.c_int, [_P, C.POINTER(rtm_scene), C.POINTER(rtm_camera),
                                    C.POINTER(rtm_camera), _I32, _I32, _I32, _I32,
                                    C.POINTER(rtm_stats)]),

@@ -452,10 +452,8 @@ int build_frame(FrameArgs& a, const rtm_scene* scene, const rtm_camera* eye, con
     if (steps < 0) return fail(RTM_ERR_INVALID, "march_steps=%d < 0", steps);
     if (flags & ~(RTM_FLAG_NO_MARCH | RTM_FLAG_NO_SHADOW_RASTER | RTM_FLAG_FUSED_SHADOW))
         return fail(RTM_ERR_INVALID, "unknown flags 0x%x", flags);
-    // Camera::project asserts ORTHO (main.rs:1949) for the shadow lookup; the eye
-    // viewport rasterizes spheres orthographically only (perspective projectSphere
-    // is BASELINE "next" row f-3).  Without spheres the eye rasterize is a no-op
-    // and a PERSPECTIVE eye is exact (testscene_raytracingPlane0, main.rs:1016).
+    // Camera::project asserts ORTHO (main.rs:1949) for the shadow viewport and the
+    // shadow lookup; the eye may be PERSPECTIVE (spheres via project_sphere_persp, row f-3).
     if (shadow->type != RTM_CAMERA_ORTHOGONAL)
         return fail(RTM_ERR_UNSUPPORTED, "frame path needs an ORTHOGONAL shadow camera");
     std::memset(&a, 0, sizeof a);
@@ -838,11 +836,15 @@ int enqueue_frame(rtm_ctx* ctx, FrameArgs& a, const FrameExtra* x, float* out_de
     return RTM_OK;
 }
 
-rtm_ctx* default_ctx(int* rc) {
-    thread_local std::unique_ptr<rtm_ctx, void (*)(rtm_ctx*)> c(nullptr, rtm_ctx_destroy);
+// Per-thread default contexts, one per device (rtm_render: device 0; rtm_render_multi: 0..n-1).
+rtm_ctx* default_ctx(int* rc, int device = 0) {
+    using Ctx = std::unique_ptr<rtm_ctx, void (*)(rtm_ctx*)>;
+    thread_local std::vector<Ctx> cs;
+    while ((int)cs.size() <= device) cs.emplace_back(nullptr, rtm_ctx_destroy);
+    Ctx& c = cs[(size_t)device];
     if (!c) {
         rtm_ctx* p = nullptr;
-        *rc = rtm_ctx_create(0, &p);
+        *rc = rtm_ctx_create(device, &p);
         if (*rc) return nullptr;
         c.reset(p);
     }
@@ -1097,6 +1099,55 @@ int rtm_render(const rtm_scene* scene, const rtm_camera* eye, const rtm_camera* 
     if ((rc = enqueue_frame(ctx, a, &x, (float*)ctx->out.p, nullptr))) return rc;
     HIP_TRY(hipMemcpyAsync(out_rgba, ctx->out.p, bytes, hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(hipStreamSynchronize(ctx->stream));
+    return RTM_OK;
+}
+
+int rtm_render_multi(const rtm_scene* scene, const rtm_camera* eye, const rtm_camera* shadow, int32_t width,
+                     int32_t height, int32_t march_steps, int32_t flags, float* out_rgba, int32_t n_gpus) {
+    if (!out_rgba) return fail(RTM_ERR_INVALID, "out_rgba is NULL");
+    const int n_dev = rtm_device_count();
+    if (n_dev <= 0) return fail(RTM_ERR_NO_DEVICE, "no HIP device visible");
+    if (n_gpus < 1 || n_gpus > n_dev) return fail(RTM_ERR_INVALID, "n_gpus=%d outside [1,%d]", n_gpus, n_dev);
+    // Row bands, one per device.  With more than one device every band evaluates
+    // the shadow texels it reads (RTM_FLAG_FUSED_SHADOW: same image bits), so no
+    // device needs another's shadow map and there is no device-to-device exchange:
+    // each band goes straight from its device into its slice of the host frame.
+    const int32_t f = flags | (n_gpus > 1 ? RTM_FLAG_FUSED_SHADOW : 0);
+    FrameArgs a;
+    int rc = build_frame(a, scene, eye, shadow, width, height, march_steps, f);
+    if (rc) return rc;
+    FrameExtra x;
+    build_extra(scene, eye, width, height, x);
+    const int32_t band = (height + n_gpus - 1) / n_gpus;
+    std::vector<rtm_ctx*> ctxs((size_t)n_gpus, nullptr);
+    for (int d = 0; d < n_gpus; ++d) {
+        const int32_t r0 = std::min(height, d * band), r1 = std::min(height, (d + 1) * band);
+        if (r0 >= r1) continue;
+        rtm_ctx* ctx = default_ctx(&rc, d);
+        if (!ctx) return rc;
+        ctxs[(size_t)d] = ctx;
+        DeviceGuard g(ctx->device);
+        FrameArgs ad = a;
+        ad.ey.row_begin = r0;
+        ad.ey.row_end = r1;
+        const size_t bytes = sizeof(float) * 4 * (size_t)width * (size_t)(r1 - r0);
+        if ((rc = ctx->out.ensure(bytes, ctx->device))) return rc;
+        if ((rc = enqueue_frame(ctx, ad, &x, (float*)ctx->out.p, nullptr))) return rc;
+    }
+    for (int d = 0; d < n_gpus; ++d) {  // the bands' D2H copies, then wait for all devices
+        rtm_ctx* ctx = ctxs[(size_t)d];
+        if (!ctx) continue;
+        const int32_t r0 = std::min(height, d * band), r1 = std::min(height, (d + 1) * band);
+        DeviceGuard g(ctx->device);
+        HIP_TRY(hipMemcpyAsync(out_rgba + (size_t)r0 * (size_t)width * 4, ctx->out.p,
+                               sizeof(float) * 4 * (size_t)width * (size_t)(r1 - r0), hipMemcpyDeviceToHost,
+                               ctx->stream));
+    }
+    for (rtm_ctx* ctx : ctxs) {
+        if (!ctx) continue;
+        DeviceGuard g(ctx->device);
+        HIP_TRY(hipStreamSynchronize(ctx->stream));
+    }
     return RTM_OK;
 }
 

@@ -162,6 +162,19 @@ def render_frame(scene: Scene, eye: Camera, shadow: Camera, width: int, height: 
     return out
 
 
+def render_frame_multi(scene: Scene, eye: Camera, shadow: Camera, width: int, height: int, steps: int,
+                       flags: int = 0, n_gpus: int = 1) -> np.ndarray:
+    """rtm_render_multi: the frame as row bands on devices 0..n_gpus-1 of this
+    process, assembled in host memory, (height, width, 4) f32."""
+    out = np.empty((height, width, 4), np.float32)
+    sc, keep = scene.to_c()
+    e, s = eye.to_c(), shadow.to_c()
+    lib = _lib()
+    abi.check(lib, lib.rtm_render_multi(C.byref(sc), C.byref(e), C.byref(s), width, height, steps, flags,
+                                        out.ctypes.data_as(C.POINTER(C.c_float)), n_gpus), "rtm_render_multi")
+    return out
+
+
 def encode_thresholds() -> np.ndarray:
     """T[k] = least f32 v in [0,1] whose writeColorImage byte is >= k (T[0] = 0)."""
     t = (C.c_float * 256)()

@@ -220,6 +220,15 @@ int rtm_ctx_kernel_ms_history(rtm_ctx* ctx, float* shadow_pass_ms, float* eye_pa
 int rtm_render(const rtm_scene* scene, const rtm_camera* eye, const rtm_camera* shadow,
                int32_t width, int32_t height, int32_t march_steps, int32_t flags,
                float* out_rgba);
+/* The same frame on devices 0..n_gpus-1 of this process (SURVEY.md §8b-1's
+ * rtm_render_multi): row bands of ceil(height/n_gpus) rows, one per device,
+ * each evaluating the shadow texels it reads (RTM_FLAG_FUSED_SHADOW when
+ * n_gpus > 1: same image bits), each copied from its device straight into its
+ * slice of out_rgba.  Blocking.  n_gpus in [1, rtm_device_count()].  (The
+ * one-process-per-GPU form is rtm_render_async per rank, see bench.py.) */
+int rtm_render_multi(const rtm_scene* scene, const rtm_camera* eye, const rtm_camera* shadow,
+                     int32_t width, int32_t height, int32_t march_steps, int32_t flags,
+                     float* out_rgba, int32_t n_gpus);
 
 /* ---- whole frame, device output (asynchronous on ctx's stream) ----
  * Renders eye rows [row_begin, row_end) into out_rgba_dev (device memory,

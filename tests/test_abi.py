@@ -88,6 +88,7 @@ def test_argument_validation_without_gpu(rtm, scenes):
     e, s = scenes.eye_camera().to_c(), scenes.shadow_camera().to_c()
     out = (C.c_float * 16)()
     assert lib.rtm_render(None, C.byref(e), C.byref(s), 2, 2, 1, 0, out) == abi.RTM_ERR_INVALID
+    assert lib.rtm_render_multi(C.byref(sc), C.byref(e), C.byref(s), 2, 2, 1, 0, None, 1) == abi.RTM_ERR_INVALID
     assert lib.rtm_render(C.byref(sc), C.byref(e), C.byref(s), 0, 2, 1, 0, out) == abi.RTM_ERR_INVALID
     assert lib.rtm_render(C.byref(sc), C.byref(e), C.byref(s), 2, 2, -1, 0, out) == abi.RTM_ERR_INVALID
     assert lib.rtm_render(C.byref(sc), C.byref(e), C.byref(s), 2, 2, 1, 0x80, out) == abi.RTM_ERR_INVALID
@@ -100,6 +101,7 @@ def test_argument_validation_without_gpu(rtm, scenes):
     if lib.rtm_device_count() == 0:
         assert rc == abi.RTM_ERR_NO_DEVICE
         assert lib.rtm_render(C.byref(sc), C.byref(e), C.byref(s), 2, 2, 1, 0, out) == abi.RTM_ERR_NO_DEVICE
+        assert lib.rtm_render_multi(C.byref(sc), C.byref(e), C.byref(s), 2, 2, 1, 0, out, 1) == abi.RTM_ERR_NO_DEVICE
     else:
         assert rc == 0
         lib.rtm_ctx_destroy(h)

@@ -356,3 +356,22 @@ print("pipelined ok")
     env = dict(os.environ, RTM_PIPELINE="1")
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0 and "pipelined ok" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
+
+
+def test_render_multi(rtm, oracle, scenes):
+    """rtm_render_multi: row bands on devices 0..n-1 of this
+    process, assembled in host memory == rtm_render == the oracle.  On a
+    one-GPU box n = 1; n beyond the visible devices is rejected."""
+    abi = rtm.abi
+    n = rtm.device_count()
+    args = (scenes.scene_a_bench(), scenes.eye_camera(), scenes.shadow_camera(), 640, 361, 64)
+    want = _oracle(oracle, *args)["rgba"]
+    for k in range(1, n + 1):
+        got = rtm.render_frame_multi(*args, n_gpus=k)
+        assert bits_equal(got, want), (k, first_mismatch(got, want))
+    with pytest.raises(abi.RtmError) as e:
+        rtm.render_frame_multi(*args, n_gpus=n + 1)
+    assert e.value.code == abi.RTM_ERR_INVALID
+    with pytest.raises(abi.RtmError) as e:
+        rtm.render_frame_multi(*args, n_gpus=0)
+    assert e.value.code == abi.RTM_ERR_INVALID
