@@ -1025,12 +1025,24 @@ __device__ __forceinline__ void shadow_tile_lean2(const ShadowPart& a, double* _
         for (int c = 0; c < CW; ++c) zb[r][c] = INFINITY;
     // shadow viewport rasterize, face BACK (main.rs:1569, 243)
     if (!(a.flags & RTM_FLAG_NO_SHADOW_RASTER) && !(diag & 1)) {
-        double x[CW];
-#pragma unroll
-        for (int c = 0; c < CW; ++c) x[c] = a.tab.nx[xs[c]];
+        // the wave's sphere set first (bitwise tests: the four range words load
+        // together, no branch per word), so a tile no sphere reaches skips the
+        // raster, its column loads included
+        uint32_t live = 0u;
         for (int i = 0; i < a.n_spheres; ++i) {
             const RasterSphereK& sp = a.sph[i];
-            if (y0 + NR - 1 < sp.iy0 || y0 > sp.iy1 || xb + TW - 1 < sp.ix0 || xb > sp.ix1) continue;
+            const bool out = (y0 + NR - 1 < sp.iy0) | (y0 > sp.iy1) | (xb + TW - 1 < sp.ix0) | (xb > sp.ix1);
+            live |= out ? 0u : (1u << i);
+        }
+        double x[CW];
+        if (live) {
+#pragma unroll
+            for (int c = 0; c < CW; ++c) x[c] = a.tab.nx[xs[c]];
+        }
+        while (live) {
+            const int i = __builtin_ctz(live);
+            live &= live - 1u;
+            const RasterSphereK& sp = a.sph[i];
             double pa[CW];
 #pragma unroll
             for (int c = 0; c < CW; ++c) pa[c] = ((x[c] - sp.cx) * sp.n) / sp.m;
@@ -1130,6 +1142,15 @@ __device__ __forceinline__ void shadow_tile_lean2(const ShadowPart& a, double* _
         }
     }
     const bool vec = CW == 2 && (a.W % 2) == 0 && colv[CW - 1];  // x0 even: 16-byte aligned row pairs
+    if (diag & 4) {  // timing diagnostic: compute everything, store (almost) nothing
+        bool any = false;
+#pragma unroll
+        for (int r = 0; r < NR; ++r)
+#pragma unroll
+            for (int c = 0; c < CW; ++c) any |= zb[r][c] == -12345.0;
+        if (any) smap[0] = 0.0;
+        return;
+    }
 #pragma unroll
     for (int r = 0; r < NR; ++r) {
         if (y0 + r >= a.H) continue;

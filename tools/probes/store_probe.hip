@@ -34,6 +34,21 @@ __global__ void store_f64(double* __restrict__ out, double v) {
     }
 }
 
+__global__ void empty_kernel(float* out, int flag) {
+    if (flag == 12345) out[threadIdx.x] = 0.0f;
+}
+
+// a kernel that needs many VGPRs (live f64 values) but does no memory work
+__global__ void heavy_regs_kernel(float* out, int flag, double seed) {
+    double v[40];
+#pragma unroll
+    for (int i = 0; i < 40; ++i) v[i] = seed * (threadIdx.x + i);
+    double acc = 0.0;
+#pragma unroll
+    for (int i = 0; i < 40; ++i) acc += v[i] * v[(i + 7) % 40];
+    if (flag == 12345 || acc == -1.0) out[threadIdx.x] = (float)acc;
+}
+
 template <typename F>
 static float time_it(F f, int iters) {
     hipEvent_t a, b;
@@ -68,6 +83,12 @@ int main() {
         float us = time_it([&] { hipLaunchKernelGGL(store_f64<P>, g, dim3(B), 0, 0, o8, 1.0); }, 50);          \
         printf("f64   ppl=%d block=%4d waves=%7u  %7.2f us  %6.2f TB/s\n", P, B, g.x * g.y * (B / 64), us,   \
                mb8 / us / 1e6 * 1e6 / 1e6);                                                                    \
+    }
+    for (int wgs : {4050, 32400, 129600}) {
+        float us = time_it([&] { hipLaunchKernelGGL(empty_kernel, dim3(wgs), dim3(256), 0, 0, (float*)o4, 0); }, 50);
+        float us1 = time_it([&] { hipLaunchKernelGGL(empty_kernel, dim3(wgs), dim3(256), 1040, 0, (float*)o4, 0); }, 50);
+        float us2 = time_it([&] { hipLaunchKernelGGL(heavy_regs_kernel, dim3(wgs), dim3(256), 0, 0, (float*)o4, 0, 1.0); }, 50);
+        printf("empty kernel %6d WGs x 256: %6.2f us (with 1 KB dyn LDS %6.2f us; ~90-VGPR kernel %6.2f us)\n", wgs, us, us1, us2);
     }
     RGBA(1, 256) RGBA(2, 256) RGBA(4, 256) RGBA(8, 256) RGBA(1, 512) RGBA(1, 1024) RGBA(4, 1024)
     F64(1, 256) F64(2, 256) F64(4, 256) F64(8, 256) F64(4, 1024)
