@@ -979,6 +979,17 @@ __device__ __forceinline__ void shadow_tile_lean(const ShadowPart& a, double* __
     }
 }
 
+// Phase timestamps of the lean tile (timing diagnostic, RTM_DIAG_SHADOW bit 8):
+// s_memtime of lane 0 of every wave at 6 program points; read by
+// rtm_diag_shadow_phases (not part of include/rtm.h).
+__device__ unsigned long long g_phase[1 << 18];
+#define RTM_PHASE(k)                                                                                         \
+    if (diag & 8) {                                                                                          \
+        const unsigned long long t_ = __builtin_amdgcn_s_memtime();                                         \
+        const unsigned wid_ = ((blockIdx.y * gridDim.x + blockIdx.x) * (BLOCK / 64) + (threadIdx.x >> 6)); \
+        if ((threadIdx.x & 63) == 0 && wid_ * 8u + 8u <= (1u << 18)) g_phase[wid_ * 8u + (k)] = t_;        \
+    }
+
 // shadow_tile_lean with CW columns per lane (a wave covers 64*CW columns, so a
 // row's texels leave as one 16-byte store per lane when CW == 2) and the table
 // direction as a template parameter.  Per texel the search is: D (exact, 2
@@ -1006,6 +1017,7 @@ __device__ __forceinline__ void shadow_tile_lean2(const ShadowPart& a, double* _
     }
     const int steps = a.steps;
     const bool march = !(a.flags & RTM_FLAG_NO_MARCH) && !(diag & 2) && a.n_patches > 0 && steps > 0;
+    RTM_PHASE(0)
     // LDS table fill, split so its global loads are in flight during the sphere
     // raster below (which does not read it); written + barrier afterwards
     constexpr int FILL = 4;  // entries per thread held in registers (steps + 1 <= FILL * BLOCK)
@@ -1061,6 +1073,7 @@ __device__ __forceinline__ void shadow_tile_lean2(const ShadowPart& a, double* _
             }
         }
     }
+    RTM_PHASE(1)
     if (!FILLED && march) {
         if (fill_regs) {
 #pragma unroll
@@ -1074,6 +1087,7 @@ __device__ __forceinline__ void shadow_tile_lean2(const ShadowPart& a, double* _
         }
         __syncthreads();
     }
+    RTM_PHASE(2)
     if (march) {
         const double oz = ((cdouble*)a.tab.z)[0];
         const double sz = a.cam.dir[2] * 0.03;
@@ -1141,6 +1155,7 @@ __device__ __forceinline__ void shadow_tile_lean2(const ShadowPart& a, double* _
             }
         }
     }
+    RTM_PHASE(3)
     const bool vec = CW == 2 && (a.W % 2) == 0 && colv[CW - 1];  // x0 even: 16-byte aligned row pairs
     if (diag & 4) {  // timing diagnostic: compute everything, store (almost) nothing
         bool any = false;
@@ -1162,6 +1177,11 @@ __device__ __forceinline__ void shadow_tile_lean2(const ShadowPart& a, double* _
             for (int c = 0; c < CW; ++c)
                 if (colv[c]) row[x0 + c] = zb[r][c];
         }
+    }
+    RTM_PHASE(4)
+    if (diag & 8) {
+        __builtin_amdgcn_s_waitcnt(0);  // (diagnostic only: when this wave's stores have left)
+        RTM_PHASE(5)
     }
 }
 
@@ -1819,6 +1839,17 @@ int launch_persp_upload(const PerspK& k, PerspK* dst, void* stream) {
     hipLaunchKernelGGL(upload_kernel<PerspK>, dim3(1), dim3(256), 0, (hipStream_t)stream, k, dst);
     return launched();
 }
+
+}  // namespace rtm
+
+extern "C" int rtm_diag_shadow_phases(unsigned long long* out, int n) {
+    if (n > (1 << 18)) n = 1 << 18;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(rtm::g_phase), sizeof(unsigned long long) * (size_t)n) == hipSuccess
+               ? 0
+               : -1;
+}
+
+namespace rtm {
 
 int launch_sdf_upload(const SdfTabK& k, SdfTabK* dst, void* stream) {
     hipLaunchKernelGGL(upload_kernel<SdfTabK>, dim3(1), dim3(512), 0, (hipStream_t)stream, k, dst);
