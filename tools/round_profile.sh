@@ -1,0 +1,35 @@
+#!/bin/bash
+# One GPU-box session producing the round's evidence: GPU tests, smoke, bench
+# lines for configs 3 (headline), 6 (row f-1) and 8 (row f-4), rocprofv3
+# kernel-trace summaries of the same commands, and the PMC passes for config 3.
+# Every GPU step has its own limit; a crash/timeout/abort stops the script.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+ROOT=$(pwd)
+TAG=${TAG:-r01_v9}
+OUT=$ROOT/gpurun_out/$TAG
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+fatal() { local rc=$1; [ "$rc" -eq 124 ] || [ "$rc" -eq 137 ] || [ "$rc" -eq 134 ] || [ "$rc" -eq 139 ] || [ "$rc" -gt 128 ]; }
+step() {
+  local name=$1 limit=$2; shift 2
+  echo "=== $name ($(date +%T))" | tee -a "$OUT/status.txt"
+  timeout -k 10 "$limit" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "$name rc=$rc" | tee -a "$OUT/status.txt"
+  tail -3 "$OUT/$name.log"
+  if fatal $rc; then echo "FATAL in $name, stopping"; exit $rc; fi
+  return 0
+}
+[ "${SKIP_TESTS:-0}" = 1 ] || step pytest_gpu 900 python -m pytest tests -m gpu -q -p no:cacheprovider
+[ "${SKIP_TESTS:-0}" = 1 ] || step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
+step bench3 600 python bench.py
+step bench6 300 python bench.py --config 6 --no-alt
+step bench8 300 python bench.py --config 8 --no-alt
+step prof3 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof3" -o run --output-format csv -- python3 "$ROOT/bench.py" --steps 200 --warmup 20 --no-cpu-baseline --no-alt
+step prof6 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof6" -o run --output-format csv -- python3 "$ROOT/bench.py" --config 6 --steps 200 --warmup 20 --no-cpu-baseline --no-alt
+step prof8 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof8" -o run --output-format csv -- python3 "$ROOT/bench.py" --config 8 --steps 100 --warmup 10 --no-cpu-baseline --no-alt
+if [ "${PMC:-1}" = 1 ]; then
+  TAG=$TAG CFG=3 BENCH_ARGS="--no-alt" step pmc3 1200 bash tools/profile_pmc.sh
+fi
+echo done
