@@ -1092,18 +1092,22 @@ __device__ __forceinline__ void shadow_tile_lean2(const ShadowPart& a, double* _
         const double oz = ((cdouble*)a.tab.z)[0];
         const double sz = a.cam.dir[2] * 0.03;
         const double inv_sz = 1.0 / sz;
-        const double fsteps = (double)steps;
+        const float fsteps = (float)steps;
         bool colok[CW];
 #pragma unroll
         for (int c = 0; c < CW; ++c) colok[c] = colv[c] && a.tab.ok[xs[c]] != 0;
         for (int k = 0; k < a.n_patches; ++k) {
-            double d0[CW], dd[CW], g0[CW], g1[CW];
+            double d0[CW], dd[CW];
+            float g0[CW], g1[CW];
 #pragma unroll
             for (int c = 0; c < CW; ++c) {
                 d0[c] = a.tab.d0[k * a.W + xs[c]];
                 dd[c] = a.tab.dd[k * a.W + xs[c]];
-                g0[c] = (d0[c] - oz) * inv_sz;  // guess terms: (D - z0)/sz ~ g0 + g1*py
-                g1[c] = dd[c] * inv_sz;
+                // guess terms, f32: (D - z0)/sz ~ g0 + g1*py.  A guess only (the table
+                // verification below decides), so f32's ~1e-5-step error just sends
+                // the rare texel within it of a step boundary to the exact path.
+                g0[c] = (float)((d0[c] - oz) * inv_sz);
+                g1[c] = (float)(dd[c] * inv_sz);
             }
             unsigned slow = 0u;
             double D[NR][CW];
@@ -1112,6 +1116,7 @@ __device__ __forceinline__ void shadow_tile_lean2(const ShadowPart& a, double* _
                 const bool rowv = y0 + r < a.H;
                 const int yr = rowv ? y0 + r : y0;  // wave-uniform: scalar loads
                 const double py = ((cdouble*)a.tab.py)[yr];
+                const float pyf = (float)py;
                 const bool rowok = rowv && ((cint*)a.tab.ok)[a.W + yr] != 0;
 #pragma unroll
                 for (int c = 0; c < CW; ++c) {
@@ -1119,8 +1124,8 @@ __device__ __forceinline__ void shadow_tile_lean2(const ShadowPart& a, double* _
                     const double Dv = D[r][c];
                     const bool inr = rowok && colok[c];
                     const bool fastD = __builtin_amdgcn_class(Dv, 0x198);  // finite, nonzero
-                    const double g = fmin(fmax(__builtin_fma(g1[c], py, g0[c]), 1.0), fsteps);  // NaN -> 1
-                    const int f = (int)ceil(g);
+                    const float g = fminf(fmaxf(__builtin_fmaf(g1[c], pyf, g0[c]), 1.0f), fsteps);  // NaN -> 1
+                    const int f = (int)ceilf(g);
                     const double2 e = T[f];
                     const double zp = T[f - 1].x;
                     // bitwise & | on the predicates: no short-circuit, so no divergent
