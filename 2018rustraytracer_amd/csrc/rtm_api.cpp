@@ -481,6 +481,23 @@ int build_frame(FrameArgs& a, const rtm_scene* scene, const rtm_camera* eye, con
     ey.Ws = W;
     ey.Hs = H;
     ey.n_spheres = scene->n_spheres;
+    // union of the spheres' pixel ranges per viewport (empty: x0 > x1); a wave
+    // outside it skips the per-sphere culls
+    auto cull_union = [&](const RasterSphereK* sph, int32_t* x0, int32_t* x1, int32_t* y0, int32_t* y1) {
+        *x0 = *y0 = 1;
+        *x1 = *y1 = 0;
+        for (int i = 0; i < scene->n_spheres; ++i) {
+            const RasterSphereK& k = sph[i];
+            if (k.ix0 > k.ix1 || k.iy0 > k.iy1) continue;  // covers nothing
+            const bool first = *x0 > *x1;
+            *x0 = first ? k.ix0 : std::min(*x0, k.ix0);
+            *x1 = first ? k.ix1 : std::max(*x1, k.ix1);
+            *y0 = first ? k.iy0 : std::min(*y0, k.iy0);
+            *y1 = first ? k.iy1 : std::max(*y1, k.iy1);
+        }
+    };
+    cull_union(ey.sph, &ey.cull_x0, &ey.cull_x1, &ey.cull_y0, &ey.cull_y1);
+    cull_union(sh.sph, &sh.cull_x0, &sh.cull_x1, &sh.cull_y0, &sh.cull_y1);
     ey.flags = flags;
     ey.row_begin = 0;
     ey.row_end = H;

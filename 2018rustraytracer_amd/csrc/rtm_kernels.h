@@ -89,6 +89,7 @@ struct ShadowPart {
     int32_t W, H;                        // shadow map (== eye image dims)
     int32_t n_spheres, n_patches;
     int32_t steps, flags;
+    int32_t cull_x0, cull_x1, cull_y0, cull_y1;  // union of the spheres' pixel ranges (see EyePart)
 };
 
 // What the eye pass of one frame reads (eye viewport rasterize + renderColorImage).
@@ -102,6 +103,9 @@ struct EyePart {
     int32_t Ws, Hs;                      // shadow map
     int32_t n_spheres, flags;
     int32_t row_begin, row_end;
+    // union of the spheres' pixel ranges (empty: cull_x0 > cull_x1): a wave
+    // outside it skips the per-sphere culls
+    int32_t cull_x0, cull_x1, cull_y0, cull_y1;
 };
 
 // One launch's arguments: the shadow pass of frame i and the eye pass of frame

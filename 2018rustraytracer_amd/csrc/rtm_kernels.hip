@@ -66,6 +66,12 @@ __device__ __forceinline__ bool may_cover(const RasterSphereK& s, int xb, int xe
     return y >= s.iy0 && y <= s.iy1 && xe >= s.ix0 && xb <= s.ix1;
 }
 
+// Does the union of a viewport's sphere pixel ranges reach columns [xb, xe] of rows [ya, ye]?
+template <typename P>
+__device__ __forceinline__ bool union_may_cover(const P& a, int xb, int xe, int ya, int ye) {
+    return ye >= a.cull_y0 && ya <= a.cull_y1 && xe >= a.cull_x0 && xb <= a.cull_x1;
+}
+
 // Coverage under a PERSPECTIVE camera (row f-3): the same test with the general
 // ellipse axes of projectSphere (main.rs:2848-2852, 2098-2109).
 __device__ __forceinline__ bool cover_persp(const PerspSphK& s, double x, double y, double& h) {
@@ -571,7 +577,7 @@ template <bool COUNT>
 __device__ __forceinline__ double shadow_texel(const ShadowPart& a, int xi, int yi, int xb, int xe, int yw,
                                                ShadowCounts& c) {
     double zb = INFINITY;
-    if (!(a.flags & RTM_FLAG_NO_SHADOW_RASTER)) {
+    if (!(a.flags & RTM_FLAG_NO_SHADOW_RASTER) && union_may_cover(a, xb, xe, yw, yw)) {
         const double x = a.tab.nx[xi];
         const double y = a.tab.ny[yi];
         for (int i = 0; i < a.n_spheres; ++i) {
@@ -725,7 +731,8 @@ __device__ __forceinline__ void shadow_tile_sep(const ShadowPart& a, double* __r
         rowv[r] = y0 + r < a.H;
     }
     // shadow viewport rasterize, face BACK (main.rs:1569, 243)
-    if (!(a.flags & RTM_FLAG_NO_SHADOW_RASTER) && !(diag & 1)) {
+    if (!(a.flags & RTM_FLAG_NO_SHADOW_RASTER) && !(diag & 1) &&
+        union_may_cover(a, xb, xb + TILE_X - 1, y0, y0 + NR - 1)) {
         const double x = a.tab.nx[xs];
         for (int i = 0; i < a.n_spheres; ++i) {
             const RasterSphereK& sp = a.sph[i];
@@ -907,7 +914,8 @@ __device__ __forceinline__ void shadow_tile_lean(const ShadowPart& a, double* __
 #pragma unroll
     for (int r = 0; r < NR; ++r) zb[r] = INFINITY;
     // shadow viewport rasterize, face BACK (main.rs:1569, 243)
-    if (!(a.flags & RTM_FLAG_NO_SHADOW_RASTER) && !(diag & 1)) {
+    if (!(a.flags & RTM_FLAG_NO_SHADOW_RASTER) && !(diag & 1) &&
+        union_may_cover(a, xb, xb + TILE_X - 1, y0, y0 + NR - 1)) {
         const double x = a.tab.nx[xs];
         for (int i = 0; i < a.n_spheres; ++i) {
             const RasterSphereK& sp = a.sph[i];
@@ -1036,7 +1044,8 @@ __device__ __forceinline__ void shadow_tile_lean2(const ShadowPart& a, double* _
 #pragma unroll
         for (int c = 0; c < CW; ++c) zb[r][c] = INFINITY;
     // shadow viewport rasterize, face BACK (main.rs:1569, 243)
-    if (!(a.flags & RTM_FLAG_NO_SHADOW_RASTER) && !(diag & 1)) {
+    if (!(a.flags & RTM_FLAG_NO_SHADOW_RASTER) && !(diag & 1) &&
+        union_may_cover(a, xb, xb + TW - 1, y0, y0 + NR - 1)) {
         // the wave's sphere set first (bitwise tests: the four range words load
         // together, no branch per word), so a tile no sphere reaches skips the
         // raster, its column loads included
@@ -1252,7 +1261,8 @@ __device__ __forceinline__ void eye_tile(const EyePart& a, const ShadowPart& sh,
         // z-test over spheres in scene order, strict '<' against +INF init (main.rs:318)
         double best = INFINITY, bh = 0.0, bz = 0.0;
         int bid = -1;
-        for (int i = 0; i < a.n_spheres; ++i) {
+        const bool any_sphere = union_may_cover(a, xb, xb + TILE_X - 1, yi, yi);
+        for (int i = 0; any_sphere && i < a.n_spheres; ++i) {
             if (!may_cover(a.sph[i], xb, xb + TILE_X - 1, yi)) continue;
             double h;
             // (RT variant only: a PERSPECTIVE eye with spheres, row f-3; psp is wave-uniform)
