@@ -33,6 +33,10 @@ def lib():
         L = C.CDLL(LIB_PATH)
         P = C.c_void_p
         I = C.c_int32
+        L.rtmo_render_rows.restype = C.c_int
+        L.rtmo_render_rows.argtypes = [C.POINTER(_abi.rtm_scene), C.POINTER(_abi.rtm_camera),
+                                       C.POINTER(_abi.rtm_camera), I, I, I, I, I, I, C.POINTER(C.c_float),
+                                       C.POINTER(C.c_int64), C.POINTER(C.c_int64)]
         L.rtmo_render.restype = C.c_int
         L.rtmo_render.argtypes = [C.POINTER(_abi.rtm_scene), C.POINTER(_abi.rtm_camera),
                                   C.POINTER(_abi.rtm_camera), I, I, I, I, I,
@@ -92,6 +96,23 @@ def render(scene, eye, shadow, width, height, steps, flags=0, nthreads=1, want_s
     if rc != 0:
         raise RuntimeError(f"rtmo_render failed: {rc}")
     return dict(rgba=out, shadow=sh, stats=st.as_dict() if st is not None else None)
+
+
+def render_rows(scene, eye, shadow, width, height, steps, flags, row0, row1):
+    """Eye rows [row0, row1) of the frame, holding only those rows and the shadow
+    rows they look up (rtmo_render_rows): bit-identical to render()'s rows, at
+    sizes whose full frame would not fit the host.  Returns ((row1-row0, W, 4) f32,
+    (t0, t1) shadow rows computed)."""
+    L = lib()
+    sc, keep = scene.to_c()
+    ec, sc_cam = eye.to_c(), shadow.to_c()
+    out = np.empty((row1 - row0, width, 4), np.float32)
+    t0, t1 = C.c_int64(0), C.c_int64(0)
+    rc = L.rtmo_render_rows(C.byref(sc), C.byref(ec), C.byref(sc_cam), width, height, steps, flags, row0, row1,
+                            _fp(out, C.c_float), C.byref(t0), C.byref(t1))
+    if rc != 0:
+        raise RuntimeError(f"rtmo_render_rows failed: {rc}")
+    return out, (t0.value, t1.value)
 
 
 class Viewport:

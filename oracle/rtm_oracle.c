@@ -222,6 +222,9 @@ typedef struct {
     Camera camera;
     double* zBuffer; /* Map2d<f64> row-major y*W+x (main.rs:2351-2373) */
     GEntry* rasterized;
+    /* rows held: [y0, y0 + rows) (the whole viewport unless a row window was
+     * asked for, rtmo_render_rows); element (y, x) is at (y - y0) * W + x */
+    int64_t y0, rows;
 } Viewport;
 
 typedef struct {
@@ -271,7 +274,7 @@ static void rasterizeSphere(const ProjectedSphere* ps, double r, Viewport* vp, i
             if (!calcHeightOfSphereOnUnit(distanceToCenterUnit, &relativeHeight)) continue;
             if (tests) (*tests)++;
             double depth = calcZValueOfProjectedSphere(ps->z, relativeHeight * r, vp->face);
-            int64_t idx = yi * vp->W + xi;
+            int64_t idx = (yi - vp->y0) * vp->W + xi;
             if (depth < vp->zBuffer[idx]) {
                 vp->rasterized[idx].some = GK_SPHERE;
                 vp->rasterized[idx].id = ps->id;
@@ -515,7 +518,7 @@ static void viewport_process_raymarching_rays(Viewport* vp, const rtm_patch* pat
                 if (raymarchPatchDomainM11(pStart, dirN, steps, &patches[k], &rayDepth,
                                            cnt ? &cnt->march_iterations : NULL)) {
                     if (cnt) cnt->march_hits++;
-                    int64_t idx = yi * vp->W + xi;
+                    int64_t idx = (yi - vp->y0) * vp->W + xi;
                     if (rayDepth < vp->zBuffer[idx]) vp->zBuffer[idx] = rayDepth;
                 }
             }
@@ -750,7 +753,7 @@ static void viewport_process_raytracing_rays(Viewport* vp, const rtm_scene* scen
         for (int64_t xi = 0; xi < vp->W; xi++) {
             Vec3 o, d;
             calcRayOriginAndDirection(&vp->camera, xi, yi, &o, &d);
-            int64_t idx = yi * vp->W + xi;
+            int64_t idx = (yi - vp->y0) * vp->W + xi;
             for (int32_t i = 0; i < scene->n_circle_planes; i++) {
                 const rtm_circle_plane* pl = &scene->circle_planes[i];
                 Vec3 n = v3(pl->n[0], pl->n[1], pl->n[2]);
@@ -804,12 +807,14 @@ static void viewport_process_raytracing_rays(Viewport* vp, const rtm_scene* scen
 /* reflect (main.rs:2872-2875) — sign-flipped as written */
 static Vec3 reflect(Vec3 d, Vec3 n) { return v3_sub(d, v3_scale(n, -2.0 * dot(d, n))); }
 
-/* renderColorImage (main.rs:710-902) over rows [y0,y1) */
+/* renderColorImage (main.rs:710-902) over rows [y0,y1).  out holds the eye
+ * viewport's rows from vp->y0.  texrows (nullable): instead of shading, record
+ * the range of shadow-map rows the hit pixels look up (rtmo_render_rows). */
 static void renderColorImage(const rtm_scene* scene, const Viewport* vp, const Viewport* vps, float* out,
-                             int64_t y0, int64_t y1, Counts* cnt) {
+                             int64_t y0, int64_t y1, Counts* cnt, int64_t* texrows) {
     for (int64_t iy = y0; iy < y1; iy++) {
         for (int64_t ix = 0; ix < vp->W; ix++) {
-            const GEntry* iPixel = &vp->rasterized[iy * vp->W + ix];
+            const GEntry* iPixel = &vp->rasterized[(iy - vp->y0) * vp->W + ix];
             double r = 0.0, g = 0.2, b = 0.2;
             if (iPixel->some) {
                 Vec3 viewDir = retViewDirOfPixel(&vp->camera, ix, iy);
@@ -855,8 +860,17 @@ static void renderColorImage(const rtm_scene* scene, const Viewport* vp, const V
                 int64_t texX = wrap_add_i64(halfW, rust_as_i64(projectedPosition.x * (double)halfW));
                 int64_t texY = wrap_add_i64(halfH, rust_as_i64(projectedPosition.y * (double)halfH));
                 double depthFromShadowMap = INFINITY;
-                if (texY >= 0 && texY < vps->H && texX >= 0 && texX < vps->W)
-                    depthFromShadowMap = vps->zBuffer[texY * vps->W + texX];
+                if (texrows) {
+                    if (texY >= 0 && texY < vps->H && texX >= 0 && texX < vps->W) {
+                        if (texY < texrows[0]) texrows[0] = texY;
+                        if (texY > texrows[1]) texrows[1] = texY;
+                    }
+                    continue;
+                }
+                if (texY >= 0 && texY < vps->H && texX >= 0 && texX < vps->W) {
+                    if (texY < vps->y0 || texY >= vps->y0 + vps->rows) abort(); /* outside the row window */
+                    depthFromShadowMap = vps->zBuffer[(texY - vps->y0) * vps->W + texX];
+                }
                 double bias = 0.0;
                 int inLight = depthFromShadowMap > projectedPosition.z - bias;
                 if (!inLight) lightMagnitude = 0.25;
@@ -874,7 +888,8 @@ static void renderColorImage(const rtm_scene* scene, const Viewport* vp, const V
                     if (inLight) cnt->lit_pixels++;
                 }
             }
-            float* px = out + 4 * (iy * vp->W + ix);
+            if (texrows) continue;
+            float* px = out + 4 * ((iy - vp->y0) * vp->W + ix);
             px[0] = (float)r;
             px[1] = (float)g;
             px[2] = (float)b;
@@ -908,14 +923,21 @@ static int validate_scene(const rtm_scene* scene) {
     return RTM_OK;
 }
 
-static void viewport_init(Viewport* vp, int64_t W, int64_t H, int face, const rtm_camera* cam) {
+static void viewport_init_rows(Viewport* vp, int64_t W, int64_t H, int face, const rtm_camera* cam, int64_t y0,
+                               int64_t rows) {
     vp->W = W;
     vp->H = H;
     vp->face = face;
     vp->camera = camera_from(cam, W, H);
-    vp->zBuffer = (double*)malloc(sizeof(double) * (size_t)(W * H));
-    vp->rasterized = (GEntry*)calloc((size_t)(W * H), sizeof(GEntry));
-    for (int64_t i = 0; i < W * H; i++) vp->zBuffer[i] = INFINITY;
+    vp->y0 = y0;
+    vp->rows = rows;
+    vp->zBuffer = (double*)malloc(sizeof(double) * (size_t)(W * rows));
+    vp->rasterized = (GEntry*)calloc((size_t)(W * rows), sizeof(GEntry));
+    for (int64_t i = 0; i < W * rows; i++) vp->zBuffer[i] = INFINITY;
+}
+
+static void viewport_init(Viewport* vp, int64_t W, int64_t H, int face, const rtm_camera* cam) {
+    viewport_init_rows(vp, W, H, face, cam, 0, H);
 }
 
 static void viewport_free(Viewport* vp) {
@@ -964,7 +986,7 @@ int rtmo_render(const rtm_scene* scene, const rtm_camera* eye, const rtm_camera*
                 viewport_rasterize(&ve, scene, flags, y0, y1, &c.eye_sphere_tests);
                 viewport_process_raytracing_rays(&ve, scene, y0, y1, &c.sdf_distance_evals);
             } else {
-                renderColorImage(scene, &ve, &vs, out_rgba, y0, y1, &c);
+                renderColorImage(scene, &ve, &vs, out_rgba, y0, y1, &c, NULL);
             }
 #ifdef _OPENMP
 #pragma omp critical
@@ -978,6 +1000,45 @@ int rtmo_render(const rtm_scene* scene, const rtm_camera* eye, const rtm_camera*
     }
     if (out_shadow) memcpy(out_shadow, vs.zBuffer, sizeof(double) * (size_t)W * (size_t)H);
     if (stats) memcpy(stats, &total, sizeof total);
+    viewport_free(&vs);
+    viewport_free(&ve);
+    return RTM_OK;
+}
+
+/* Eye rows [r0, r1) of the W x H frame, without holding the whole frame: the
+ * eye viewport holds only those rows, and the shadow viewport only the rows
+ * [t0, t1] the band's hit pixels look up (found by a first shading pass that
+ * records texY instead of shading).  Same functions, same order: the rows are
+ * bit-identical to rtmo_render's.  For maximum-size parity checks (RTM_MAX_DIM),
+ * where the full frame would not fit the host.  out_rgba: (r1 - r0) * W * 4
+ * floats; t0_out, t1_out (nullable): the shadow rows computed (t1 < t0 when the
+ * band looks nothing up). */
+int rtmo_render_rows(const rtm_scene* scene, const rtm_camera* eye, const rtm_camera* shadow, int32_t W,
+                     int32_t H, int32_t steps, int32_t flags, int32_t r0, int32_t r1, float* out_rgba,
+                     int64_t* t0_out, int64_t* t1_out) {
+    int rc = validate_scene(scene);
+    if (rc) return rc;
+    if (!eye || !shadow || !out_rgba || W <= 0 || H <= 0 || steps < 0 || r0 < 0 || r1 > H || r0 >= r1)
+        return RTM_ERR_INVALID;
+    if (shadow->type != RTM_CAMERA_ORTHOGONAL) return RTM_ERR_UNSUPPORTED;
+    Viewport ve, vs;
+    viewport_init_rows(&ve, W, H, RTM_FACE_FRONT, eye, r0, r1 - r0);
+    viewport_rasterize(&ve, scene, flags, r0, r1, NULL);
+    viewport_process_raytracing_rays(&ve, scene, r0, r1, NULL);
+    int64_t tr[2] = {H, -1};
+    viewport_init_rows(&vs, W, H, RTM_FACE_BACK, shadow, 0, 0);  /* camera only, for the texel rows */
+    renderColorImage(scene, &ve, &vs, out_rgba, r0, r1, NULL, tr);
+    viewport_free(&vs);
+    const int64_t t0 = tr[1] >= tr[0] ? tr[0] : 0, t1 = tr[1] >= tr[0] ? tr[1] : -1;
+    viewport_init_rows(&vs, W, H, RTM_FACE_BACK, shadow, t0, t1 - t0 + 1);
+    if (t1 >= t0) {
+        if (!(flags & RTM_FLAG_NO_SHADOW_RASTER)) viewport_rasterize(&vs, scene, flags, t0, t1 + 1, NULL);
+        if (!(flags & RTM_FLAG_NO_MARCH))
+            viewport_process_raymarching_rays(&vs, scene->patches, scene->n_patches, steps, t0, t1 + 1, NULL);
+    }
+    renderColorImage(scene, &ve, &vs, out_rgba, r0, r1, NULL, NULL);
+    if (t0_out) *t0_out = t0;
+    if (t1_out) *t1_out = t1;
     viewport_free(&vs);
     viewport_free(&ve);
     return RTM_OK;
@@ -1026,7 +1087,7 @@ int rtmo_render_color_image(const rtm_scene* scene, const rtmo_viewport* v, cons
     if (rc) return rc;
     if (!v || !vs || !out) return RTM_ERR_INVALID;
     if (vs->vp.camera.type != RTM_CAMERA_ORTHOGONAL) return RTM_ERR_UNSUPPORTED;
-    renderColorImage(scene, &v->vp, &vs->vp, out, 0, v->vp.H, NULL);
+    renderColorImage(scene, &v->vp, &vs->vp, out, 0, v->vp.H, NULL, NULL);
     return RTM_OK;
 }
 

@@ -375,3 +375,47 @@ def test_render_multi(rtm, oracle, scenes):
     with pytest.raises(abi.RtmError) as e:
         rtm.render_frame_multi(*args, n_gpus=0)
     assert e.value.code == abi.RTM_ERR_INVALID
+
+
+@pytest.mark.parametrize("case", ["bench", "rbench", "thin"])
+def test_maximum_size_frames(rtm, oracle, scenes, gpu_ctx, case):
+    """RTM_MAX_DIM: a 32768 x 32768 frame (17 GB RGBA + 8.6 GB shadow map on
+    the device; element indices past 2^32) against the row-window oracle
+    (oracle.render_rows) on bands at the top, middle and bottom; the same rows
+    through row-band launches, two-pass and fused.  'thin': 32768 x 1 and
+    1 x 32768."""
+    import torch
+    abi = rtm.abi
+    M = abi.RTM_MAX_DIM
+    if case == "thin":
+        for w, h in ((M, 1), (1, M)):
+            args = (scenes.scene_a_bench(), scenes.eye_camera(), scenes.shadow_camera(), w, h, 64, 0)
+            got = rtm.render_frame(*args)
+            want = _oracle(oracle, *args)["rgba"]
+            assert bits_equal(got, want), (w, h, first_mismatch(got, want))
+        return
+    if case == "bench":
+        args = (scenes.scene_a_bench(), scenes.eye_camera(), scenes.shadow_camera(), M, M, 64, 0)
+    else:
+        args = (scenes.scene_r_bench(), scenes.perspective_eye_camera(), scenes.shadow_camera(), M, M, 0,
+                scenes.RAYTRACING_FLAGS)
+    scene, eye, shadow, W, H, K, flags = args
+    out = torch.empty((H, W, 4), dtype=torch.float32, device="cuda")
+    torch.cuda.synchronize()
+    gpu_ctx.render_async(scene, eye, shadow, W, H, K, flags, out.data_ptr())
+    gpu_ctx.synchronize()
+    bands = [(0, 2), (H // 2 - 3, H // 2 + 3), (H - 2, H)]
+    if case == "bench":
+        bands.append((H // 2 + 2500, H // 2 + 2504))  # through the spheres and their shadows
+    for r0, r1 in bands:
+        want, _ = oracle.render_rows(scene, eye, shadow, W, H, K, flags, r0, r1)
+        got = out[r0:r1].cpu().numpy()
+        assert bits_equal(got, want), (r0, r1, first_mismatch(got, want))
+        for f in (flags, flags | abi.RTM_FLAG_FUSED_SHADOW):
+            band = torch.empty((r1 - r0, W, 4), dtype=torch.float32, device="cuda")
+            torch.cuda.synchronize()
+            gpu_ctx.render_async(scene, eye, shadow, W, H, K, f, band.data_ptr(), r0, r1)
+            gpu_ctx.synchronize()
+            assert bits_equal(band.cpu().numpy(), want), (r0, r1, f)
+    del out
+    torch.cuda.empty_cache()

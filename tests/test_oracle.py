@@ -295,3 +295,23 @@ def test_sdf_matches_independent_restatement(oracle, scenes):
             hits += 1
             assert all(np.float64(n[k]).tobytes() == np.float64(n_np[k][i]).tobytes() for k in range(3)), i
     assert hits > 50
+
+
+@pytest.mark.parametrize("case", ["bench", "sceneb", "rbench", "sdf"])
+def test_render_rows_matches_full_frame(oracle, scenes, case):
+    """The row-window oracle (used for maximum-size GPU parity) reproduces the
+    full frame's rows bit for bit, shadow rows computed on demand."""
+    if case == "bench":
+        args = (scenes.scene_a_bench(), scenes.eye_camera(), scenes.shadow_camera(), 320, 181, 64, 0)
+    elif case == "sceneb":
+        args = (scenes.scene_b(), scenes.eye_camera(), scenes.shadow_camera(), 200, 150, 128, 0)
+    elif case == "rbench":
+        args = (scenes.scene_r_bench(), scenes.perspective_eye_camera(), scenes.shadow_camera(), 160, 90, 0,
+                scenes.RAYTRACING_FLAGS)
+    else:
+        args = (scenes.mixed_sdf(100), scenes.eye_camera(), scenes.shadow_camera(), 120, 96, 64, 0)
+    full = oracle.render(*args, nthreads=4)["rgba"]
+    H = args[4]
+    for r0, r1 in ((0, 1), (H // 2 - 3, H // 2 + 4), (H - 2, H), (0, H)):
+        rows, (t0, t1) = oracle.render_rows(*args, r0, r1)
+        assert rows.tobytes() == full[r0:r1].tobytes(), (case, r0, r1)
