@@ -585,6 +585,7 @@ struct rtm_ctx {
     uint64_t tab_key = 0;
     int64_t tab_nt = 0, tab_nz = 0, tab_nd = 0;
     int32_t tab_w = 0, tab_h = 0, tab_np = 0, tab_zmono = 0;
+    double tab_z0 = 0.0;
     bool tab_hast = false, tab_sep = false;
 };
 
@@ -734,6 +735,7 @@ int ensure_tables(rtm_ctx* ctx, int32_t steps, int32_t W, int32_t H, const rtm_c
         ctx->tab_h = H;
         ctx->tab_np = n_patches;
         ctx->tab_zmono = zmono;
+        ctx->tab_z0 = nz ? zt[0] : 0.0;
     }
     const double* base = (const double*)ctx->tabs.p;
     const int64_t nt2 = ctx->tab_nt, nz2 = ctx->tab_nz;
@@ -742,6 +744,7 @@ int ensure_tables(rtm_ctx* ctx, int32_t steps, int32_t W, int32_t H, const rtm_c
     out->ny = base + nt2 + W;
     out->z = nz2 ? base + nt2 + W + H : nullptr;
     out->zmono = nz2 ? ctx->tab_zmono : 0;
+    out->z0 = nz2 ? ctx->tab_z0 : 0.0;
     if (ctx->tab_sep) {
         out->py = base + nt2 + W + H + nz2;
         out->d0 = out->py + H;

@@ -77,6 +77,7 @@ struct Tables {
     const int32_t* ok; // W + H
     int32_t zmono;     // z table (first `steps` entries) is non-decreasing (+1) / non-increasing (-1)
     int32_t pad;
+    double z0;         // z[0] when z != nullptr (a kernarg copy: no dependent global load for it)
 };
 #define RTM_T_TABLE_MAX 65536
 

@@ -987,6 +987,13 @@ __device__ __forceinline__ void shadow_tile_lean(const ShadowPart& a, double* __
     }
 }
 
+__device__ __forceinline__ double readlane_f64(double v, int l) {
+    const uint64_t b = __double_as_longlong(v);
+    const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)b, l);
+    const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(b >> 32), l);
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+
 // Phase timestamps of the lean tile (timing diagnostic, RTM_DIAG_SHADOW bit 8):
 // s_memtime of lane 0 of every wave at 6 program points; read by
 // rtm_diag_shadow_phases (not part of include/rtm.h).
@@ -1008,7 +1015,7 @@ __device__ unsigned long long g_phase[1 << 18];
 //   okA = !P(z_{f-1}), okB = P(z_f), entry = !P(z_0)   (monotone P)
 //   hit  = inr & fastD & okA & okB & f < steps      -> t = t_f
 //   slow = inr & (!fastD | (entry & !(okA & (f == steps | okB))))  -> exact march_axis
-template <int NR, int CW, bool INC, bool FILLED = false>
+template <int NR, int CW, bool INC, bool FILLED = false, int FILLN = 4>
 __device__ __forceinline__ void shadow_tile_lean2(const ShadowPart& a, double* __restrict__ smap, int bx, int by,
                                                   double2* __restrict__ T, int diag) {
     constexpr int TW = TILE_X * CW;
@@ -1028,7 +1035,7 @@ __device__ __forceinline__ void shadow_tile_lean2(const ShadowPart& a, double* _
     RTM_PHASE(0)
     // LDS table fill, split so its global loads are in flight during the sphere
     // raster below (which does not read it); written + barrier afterwards
-    constexpr int FILL = 4;  // entries per thread held in registers (steps + 1 <= FILL * BLOCK)
+    constexpr int FILL = FILLN;  // entries per thread held in registers (steps + 1 <= FILL * BLOCK)
     double2 fv[FILL];
     const bool fill_regs = !FILLED && march && steps + 1 <= FILL * BLOCK;
     if (fill_regs) {
@@ -1036,6 +1043,40 @@ __device__ __forceinline__ void shadow_tile_lean2(const ShadowPart& a, double* _
         for (int u = 0; u < FILL; ++u) {
             const int k = threadIdx.x + u * BLOCK;
             if (k <= steps) fv[u] = make_double2(a.tab.z[k], k < steps ? a.tab.t[k] : 0.0);
+        }
+    }
+    // Every vector global load of the tile is issued here, before any store:
+    // loads and stores share vmcnt, so a load after a store would wait for that
+    // store's (long, under a full write stream) completion.
+    bool colok[CW];
+    double xcol[CW];       // shadow-camera NDC x of the columns (raster)
+    double h_d0[CW], h_dd[CW];  // patch 0's column terms
+    float h_g0[CW], h_g1[CW];
+    const double oz = a.tab.z0;
+    const double inv_sz = 1.0 / (a.cam.dir[2] * 0.03);
+#pragma unroll
+    for (int c = 0; c < CW; ++c) xcol[c] = a.tab.nx[xs[c]];
+    // the wave's row terms as one vector load (lane l: row yw + l), read back per
+    // row with readlane: no serial chain of scalar loads in the march
+    static_assert(NR <= TILE_X, "rows per wave");
+    double py_l = 0.0;
+    int ok_l = 0;
+    if (march) {
+        const int yl = min(y0 + (lane < NR ? lane : 0), a.H - 1);
+        py_l = a.tab.py[yl];
+        ok_l = a.tab.ok[a.W + yl];
+    }
+    if (march) {
+#pragma unroll
+        for (int c = 0; c < CW; ++c) {
+            colok[c] = colv[c] & (a.tab.ok[xs[c]] != 0);  // xs clamped: no branch
+            h_d0[c] = a.tab.d0[xs[c]];
+            h_dd[c] = a.tab.dd[xs[c]];
+            // guess terms, f32: (D - z0)/sz ~ g0 + g1*py.  A guess only (the table
+            // verification below decides), so f32's ~1e-5-step error just sends
+            // the rare texel within it of a step boundary to the exact path.
+            h_g0[c] = (float)((h_d0[c] - oz) * inv_sz);
+            h_g1[c] = (float)(h_dd[c] * inv_sz);
         }
     }
     double zb[NR][CW];
@@ -1055,11 +1096,7 @@ __device__ __forceinline__ void shadow_tile_lean2(const ShadowPart& a, double* _
             const bool out = (y0 + NR - 1 < sp.iy0) | (y0 > sp.iy1) | (xb + TW - 1 < sp.ix0) | (xb > sp.ix1);
             live |= out ? 0u : (1u << i);
         }
-        double x[CW];
-        if (live) {
-#pragma unroll
-            for (int c = 0; c < CW; ++c) x[c] = a.tab.nx[xs[c]];
-        }
+        const double* x = xcol;
         while (live) {
             const int i = __builtin_ctz(live);
             live &= live - 1u;
@@ -1072,9 +1109,19 @@ __device__ __forceinline__ void shadow_tile_lean2(const ShadowPart& a, double* _
                 const int y = y0 + r;
                 if (y >= a.H || y < sp.iy0 || y > sp.iy1) continue;  // wave-uniform
                 const double pb = ((((cdouble*)a.tab.ny)[y] - sp.cy) * sp.n) / sp.m;
+                double s2[CW];
+                bool in = false;
 #pragma unroll
                 for (int c = 0; c < CW; ++c) {
-                    const double d = sqrt(pa[c] * pa[c] + pb * pb);
+                    s2[c] = pa[c] * pa[c] + pb * pb;
+                    in |= s2[c] < 1.0;
+                }
+                // sqrt is monotone with sqrt(1) == 1, so d < 1 implies s2 < 1: a wave
+                // with no s2 < 1 has no covered texel in this row and skips both sqrts
+                if (!__any(in)) continue;
+#pragma unroll
+                for (int c = 0; c < CW; ++c) {
+                    const double d = sqrt(s2[c]);
                     const double h = sqrt(1.0 - d * d);
                     const double depth = sp.z + h * sp.r;
                     zb[r][c] = ((d < 1.0) & (depth < zb[r][c])) ? depth : zb[r][c];
@@ -1098,40 +1145,45 @@ __device__ __forceinline__ void shadow_tile_lean2(const ShadowPart& a, double* _
     }
     RTM_PHASE(2)
     if (march) {
-        const double oz = ((cdouble*)a.tab.z)[0];
         const double sz = a.cam.dir[2] * 0.03;
-        const double inv_sz = 1.0 / sz;
         const float fsteps = (float)steps;
-        bool colok[CW];
+        // per-row terms, patch-invariant (rows past H: row H-1's, masked by rowv)
+        double pyr[NR];
+        bool rowok[NR];
 #pragma unroll
-        for (int c = 0; c < CW; ++c) colok[c] = colv[c] && a.tab.ok[xs[c]] != 0;
+        for (int r = 0; r < NR; ++r) {
+            pyr[r] = readlane_f64(py_l, r);
+            rowok[r] = (y0 + r < a.H) & (__builtin_amdgcn_readlane(ok_l, r) != 0);
+        }
         for (int k = 0; k < a.n_patches; ++k) {
             double d0[CW], dd[CW];
             float g0[CW], g1[CW];
-#pragma unroll
-            for (int c = 0; c < CW; ++c) {
-                d0[c] = a.tab.d0[k * a.W + xs[c]];
-                dd[c] = a.tab.dd[k * a.W + xs[c]];
-                // guess terms, f32: (D - z0)/sz ~ g0 + g1*py.  A guess only (the table
-                // verification below decides), so f32's ~1e-5-step error just sends
-                // the rare texel within it of a step boundary to the exact path.
-                g0[c] = (float)((d0[c] - oz) * inv_sz);
-                g1[c] = (float)(dd[c] * inv_sz);
-            }
-            unsigned slow = 0u;
-            double D[NR][CW];
-#pragma unroll
-            for (int r = 0; r < NR; ++r) {
-                const bool rowv = y0 + r < a.H;
-                const int yr = rowv ? y0 + r : y0;  // wave-uniform: scalar loads
-                const double py = ((cdouble*)a.tab.py)[yr];
-                const float pyf = (float)py;
-                const bool rowok = rowv && ((cint*)a.tab.ok)[a.W + yr] != 0;
+            if (k == 0) {
 #pragma unroll
                 for (int c = 0; c < CW; ++c) {
-                    D[r][c] = d0[c] + dd[c] * py;
-                    const double Dv = D[r][c];
-                    const bool inr = rowok && colok[c];
+                    d0[c] = h_d0[c];
+                    dd[c] = h_dd[c];
+                    g0[c] = h_g0[c];
+                    g1[c] = h_g1[c];
+                }
+            } else {
+#pragma unroll
+                for (int c = 0; c < CW; ++c) {
+                    d0[c] = a.tab.d0[k * a.W + xs[c]];
+                    dd[c] = a.tab.dd[k * a.W + xs[c]];
+                    g0[c] = (float)((d0[c] - oz) * inv_sz);
+                    g1[c] = (float)(dd[c] * inv_sz);
+                }
+            }
+            unsigned slow = 0u;
+#pragma unroll
+            for (int r = 0; r < NR; ++r) {
+                const double py = pyr[r];
+                const float pyf = (float)py;
+#pragma unroll
+                for (int c = 0; c < CW; ++c) {
+                    const double Dv = d0[c] + dd[c] * py;
+                    const bool inr = rowok[r] & colok[c];
                     const bool fastD = __builtin_amdgcn_class(Dv, 0x198);  // finite, nonzero
                     const float g = fminf(fmaxf(__builtin_fmaf(g1[c], pyf, g0[c]), 1.0f), fsteps);  // NaN -> 1
                     const int f = (int)ceilf(g);
@@ -1154,11 +1206,18 @@ __device__ __forceinline__ void shadow_tile_lean2(const ShadowPart& a, double* _
 #pragma unroll 1
                 for (int q = 0; q < NR * CW; ++q) {
                     if (!((slow >> q) & 1u)) continue;
-                    double Dq = D[0][0];
+                    // D recomputed (same two ops, same bits) rather than held live
+                    // across the fast path: NR*CW*2 fewer VGPRs there
+                    const int qr = q / CW, qc = q % CW;
+                    double d0q = d0[0], ddq = dd[0], pyq = pyr[0];
 #pragma unroll
-                    for (int r = 0; r < NR; ++r)
+                    for (int c = 1; c < CW; ++c) {
+                        d0q = qc == c ? d0[c] : d0q;
+                        ddq = qc == c ? dd[c] : ddq;
+                    }
 #pragma unroll
-                        for (int c = 0; c < CW; ++c) Dq = q == r * CW + c ? D[r][c] : Dq;
+                    for (int r = 1; r < NR; ++r) pyq = qr == r ? pyr[r] : pyq;
+                    const double Dq = d0q + ddq * pyq;
                     MarchResult m = march_axis<false>(Dq, true, oz, sz, steps, a.tab);
 #pragma unroll
                     for (int r = 0; r < NR; ++r)
@@ -1219,12 +1278,33 @@ __global__ __launch_bounds__(BLOCK) void shadow_persist_kernel(const FrameArgs a
         shadow_tile_lean2<NR, CW, INC, true>(sh, smap, t % tiles_x, t / tiles_x, lds_zt, diag);
 }
 
-template <int NR, int CW, bool INC>
-__global__ __launch_bounds__(BLOCK) void shadow_lean2_kernel(const FrameArgs a, double* __restrict__ smap,
-                                                             int diag) {
-    extern __shared__ double2 lds_zt[];
-    shadow_tile_lean2<NR, CW, INC>(a.sh, smap, blockIdx.x, blockIdx.y, lds_zt, diag);
+// Tile row of workgroup row b (of n) with the rows [h0, h1] that the spheres'
+// pixel-range union reaches dispatched first: their waves carry the raster work,
+// and started last they would be the kernel's tail.
+__device__ __forceinline__ int hot_rows_first(int b, int n, int h0, int h1) {
+    if (h0 > h1) return b;
+    const int nh = h1 - h0 + 1;
+    if (b < nh) return h0 + b;
+    const int r = b - nh;
+    return r < h0 ? r : r + nh;
 }
+
+template <int NR, int CW, bool INC, int FILLN = 4>
+__global__ __launch_bounds__(BLOCK) void shadow_lean2_kernel(const FrameArgs a, double* __restrict__ smap, int diag,
+                                                             int hot) {
+    extern __shared__ double2 lds_zt[];
+    int by = blockIdx.y;
+    if (hot) {
+        constexpr int TR = TILE_Y * NR;
+        const int n = (int)gridDim.y;
+        const int h0 = max(a.sh.cull_y0, 0) / TR;
+        const int h1 = min(min(a.sh.cull_y1, a.sh.H - 1) / TR, n - 1);
+        const bool none = a.sh.cull_x0 > a.sh.cull_x1 || a.sh.cull_y0 > a.sh.cull_y1 || a.sh.cull_y1 < 0;
+        by = none ? by : hot_rows_first(by, n, h0, h1);
+    }
+    shadow_tile_lean2<NR, CW, INC, false, FILLN>(a.sh, smap, blockIdx.x, by, lds_zt, diag);
+}
+
 
 template <int NR>
 __global__ __launch_bounds__(BLOCK) void shadow_lean_kernel(const FrameArgs a, double* __restrict__ smap, int diag) {
@@ -1744,6 +1824,27 @@ static int lean_cols() {
     return v;
 }
 
+// Register-held LDS table entries of the lean tile: 1 per thread when the table
+// fits (RTM_LEAN_FILL=4 forces the 4-entry form for A/B runs).
+static bool lean_fill1() {
+    static bool v = [] {
+        const char* e = getenv("RTM_LEAN_FILL");
+        return !(e && atoi(e) == 4);
+    }();
+    return v;
+}
+
+
+// Sphere rows dispatched first (default; RTM_HOT=0 keeps the plain row order
+// for A/B runs).
+static bool lean_hot() {
+    static bool v = [] {
+        const char* e = getenv("RTM_HOT");
+        return !(e && atoi(e) == 0);
+    }();
+    return v;
+}
+
 template <int NR>
 static void launch_sep(const FrameArgs& a, double* smap, hipStream_t s) {
     dim3 g((unsigned)((a.sh.W + TILE_X - 1) / TILE_X), (unsigned)((a.sh.H + TILE_Y * NR - 1) / (TILE_Y * NR)));
@@ -1774,13 +1875,20 @@ static void launch_sep(const FrameArgs& a, double* smap, hipStream_t s) {
         const int tw = TILE_X * cw;
         dim3 g2((unsigned)((a.sh.W + tw - 1) / tw), g.y);
         const bool inc = a.sh.tab.zmono >= 0;  // (no march: either instantiation is exact)
-#define RTM_L2(C, I) hipLaunchKernelGGL((shadow_lean2_kernel<NR, C, I>), g2, dim3(BLOCK), lsm, s, a, smap, diag_mode())
-        if (cw == 2) {
-            if (inc) RTM_L2(2, true);
-            else RTM_L2(2, false);
+        // one register-held table entry per thread when the table fits one per thread
+        const bool fill1 = lean_fill1() && a.sh.steps + 1 <= BLOCK;
+        const int hot = lean_hot() ? 1 : 0;
+#define RTM_L2(C, I, F) \
+    hipLaunchKernelGGL((shadow_lean2_kernel<NR, C, I, F>), g2, dim3(BLOCK), lsm, s, a, smap, diag_mode(), hot)
+        if (cw == 2 && fill1) {
+            if (inc) RTM_L2(2, true, 1);
+            else RTM_L2(2, false, 1);
+        } else if (cw == 2) {
+            if (inc) RTM_L2(2, true, 4);
+            else RTM_L2(2, false, 4);
         } else {
-            if (inc) RTM_L2(1, true);
-            else RTM_L2(1, false);
+            if (inc) RTM_L2(1, true, 4);
+            else RTM_L2(1, false, 4);
         }
 #undef RTM_L2
     } else if (mode == MARCH_LEAN) {
