@@ -987,6 +987,8 @@ __device__ __forceinline__ void shadow_tile_lean(const ShadowPart& a, double* __
     }
 }
 
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
 __device__ __forceinline__ double readlane_f64(double v, int l) {
     const uint64_t b = __double_as_longlong(v);
     const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)b, l);
@@ -1322,13 +1324,15 @@ __global__ __launch_bounds__(BLOCK) void shadow_lean_kernel(const FrameArgs a, d
 template <bool FUSED, bool COUNT, int RT>
 __device__ __forceinline__ void eye_tile(const EyePart& a, const ShadowPart& sh, const double* __restrict__ smap,
                                          float4* __restrict__ out, int bx, int by, StatsK* __restrict__ st,
-                                         const DevTabs tabs) {
+                                         const DevTabs tabs, int wide = 0) {
     const RtK* __restrict__ rt = tabs.rt;
     const PerspK* __restrict__ psp = tabs.psp;
     const SdfTabK* __restrict__ sdf = tabs.sdf;
-    const int xb = bx * TILE_X;
+    // wide: the workgroup's 4 waves side by side in one row (256 x 1), else stacked (64 x 4)
+    const int wv = threadIdx.x >> 6;
+    const int xb = __builtin_amdgcn_readfirstlane((wide & 1) ? (bx * TILE_Y + wv) * TILE_X : bx * TILE_X);
     const int xi = xb + (threadIdx.x & (TILE_X - 1));
-    const int yl = __builtin_amdgcn_readfirstlane(by * TILE_Y + (threadIdx.x >> 6));
+    const int yl = __builtin_amdgcn_readfirstlane((wide & 1) ? by : by * TILE_Y + wv);
     const int yi = a.row_begin + yl;
     const bool live = xi < a.W && yi < a.row_end;
     unsigned long long n_tests = 0, n_hit = 0, n_lit = 0;
@@ -1462,7 +1466,10 @@ __device__ __forceinline__ void eye_tile(const EyePart& a, const ShadowPart& sh,
                 hit_id = hit.id;
             }
         }
-        out[(int64_t)yl * a.W + xi] = c;
+        if (wide & 2)  // non-temporal: the frame's stores do not allocate in the caches
+            __builtin_nontemporal_store(f32x4{c.x, c.y, c.z, c.w}, reinterpret_cast<f32x4*>(&out[(int64_t)yl * a.W + xi]));
+        else
+            out[(int64_t)yl * a.W + xi] = c;
     }
     if (COUNT) {
         stat_add(&st->eye_sphere_tests, n_tests);
@@ -1502,8 +1509,8 @@ __global__ __launch_bounds__(BLOCK) void shadow_sep_kernel(const FrameArgs a, do
 template <bool FUSED, bool COUNT, int RT>
 __global__ __launch_bounds__(BLOCK) void eye_pass_kernel(const FrameArgs a, const double* __restrict__ smap,
                                                          float4* __restrict__ out, StatsK* __restrict__ st,
-                                                         const DevTabs tabs) {
-    eye_tile<FUSED, COUNT, RT>(a.ey, a.sh, smap, out, blockIdx.x, blockIdx.y, st, tabs);
+                                                         const DevTabs tabs, int wide) {
+    eye_tile<FUSED, COUNT, RT>(a.ey, a.sh, smap, out, blockIdx.x, blockIdx.y, st, tabs, wide);
 }
 
 // launch_*_upload: one 8-byte word per thread from the kernarg copy.
@@ -1517,9 +1524,10 @@ __global__ void upload_kernel(const T k, T* __restrict__ dst) {
 }
 
 // Timing diagnostic only (RTM_DIAG_EYE=1): the eye pass's stores without its work.
-__global__ __launch_bounds__(BLOCK) void eye_store_only_kernel(const FrameArgs a, float4* __restrict__ out) {
-    const int xi = blockIdx.x * TILE_X + (threadIdx.x & (TILE_X - 1));
-    const int yl = blockIdx.y * TILE_Y + (threadIdx.x >> 6);
+__global__ __launch_bounds__(BLOCK) void eye_store_only_kernel(const FrameArgs a, float4* __restrict__ out, int wide) {
+    const int wv = threadIdx.x >> 6;
+    const int xi = ((wide & 1) ? (blockIdx.x * TILE_Y + wv) * TILE_X : blockIdx.x * TILE_X) + (threadIdx.x & (TILE_X - 1));
+    const int yl = (wide & 1) ? blockIdx.y : blockIdx.y * TILE_Y + wv;
     if (xi < a.ey.W && a.ey.row_begin + yl < a.ey.row_end)
         out[(int64_t)yl * a.ey.W + xi] = make_float4(0.0f, 0.2f, 0.2f, 1.0f);
 }
@@ -1921,18 +1929,32 @@ int launch_shadow_pass(const FrameArgs& a, double* smap, void* stream, StatsK* s
     return launched();
 }
 
+// Eye pass store/shape mode (RTM_EYE_MODE, for A/B runs): bit 0 = 256 x 1
+// workgroups instead of 64 x 4 (measured neutral), bit 1 = non-temporal frame
+// stores (default: the frame is not re-read, and at 7680x4320 its 531 MB would
+// otherwise evict the shadow map the pass gathers from: eye 120 -> 85 us).
+static int eye_wide() {
+    static int v = [] {
+        const char* e = getenv("RTM_EYE_MODE");
+        return e ? atoi(e) : 2;
+    }();
+    return v;
+}
+
 int launch_eye_pass(const FrameArgs& a, const double* smap, float* out, void* stream, StatsK* stats,
                     const DevTabs& tabs) {
     hipStream_t s = (hipStream_t)stream;
-    dim3 g = grid_for(a.ey.W, a.ey.row_end - a.ey.row_begin);
+    const int rows = a.ey.row_end - a.ey.row_begin;
+    const int wide = eye_wide();
+    dim3 g = (wide & 1) ? dim3((unsigned)((a.ey.W + BLOCK - 1) / BLOCK), (unsigned)rows) : grid_for(a.ey.W, rows);
     float4* o = reinterpret_cast<float4*>(out);
     const bool fused = (a.ey.flags & RTM_FLAG_FUSED_SHADOW) != 0;
     if (diag_eye()) {
-        hipLaunchKernelGGL(eye_store_only_kernel, g, dim3(BLOCK), 0, s, a, o);
+        hipLaunchKernelGGL(eye_store_only_kernel, g, dim3(BLOCK), 0, s, a, o, wide);
         return launched();
     }
 #define RTM_EYE(F, C, R) \
-    hipLaunchKernelGGL((eye_pass_kernel<F, C, R>), g, dim3(BLOCK), 0, s, a, smap, o, stats, tabs)
+    hipLaunchKernelGGL((eye_pass_kernel<F, C, R>), g, dim3(BLOCK), 0, s, a, smap, o, stats, tabs, wide)
     if (tabs.sdf) {
         if (fused && stats) RTM_EYE(true, true, 2);
         else if (fused) RTM_EYE(true, false, 2);
