@@ -1,12 +1,12 @@
 #!/bin/bash
 # One GPU-box session producing the round's evidence: GPU tests, smoke, bench
-# lines for configs 3 (headline), 6 (row f-1) and 8 (row f-4), rocprofv3
+# lines for configs 3 (headline), 4/5 (8K), 6 (row f-1) and 8 (row f-4), rocprofv3
 # kernel-trace summaries of the same commands, and the PMC passes for config 3.
 # Every GPU step has its own limit; a crash/timeout/abort stops the script.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 ROOT=$(pwd)
-TAG=${TAG:-r01_v9}
+TAG=${TAG:-r01_v11}
 OUT=$ROOT/gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
@@ -24,9 +24,12 @@ step() {
 [ "${SKIP_TESTS:-0}" = 1 ] || step pytest_gpu 900 python -m pytest tests -m gpu -q -p no:cacheprovider
 [ "${SKIP_TESTS:-0}" = 1 ] || step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 step bench3 600 python bench.py
+step bench4 300 python bench.py --config 4 --no-alt --no-cpu-baseline
+step bench5 300 python bench.py --config 5 --no-alt --no-cpu-baseline
 step bench6 300 python bench.py --config 6 --no-alt
 step bench8 300 python bench.py --config 8 --no-alt
 step prof3 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof3" -o run --output-format csv -- python3 "$ROOT/bench.py" --steps 200 --warmup 20 --no-cpu-baseline --no-alt
+step prof4 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof4" -o run --output-format csv -- python3 "$ROOT/bench.py" --config 4 --steps 100 --warmup 10 --no-cpu-baseline --no-alt
 step prof6 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof6" -o run --output-format csv -- python3 "$ROOT/bench.py" --config 6 --steps 200 --warmup 20 --no-cpu-baseline --no-alt
 step prof8 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof8" -o run --output-format csv -- python3 "$ROOT/bench.py" --config 8 --steps 100 --warmup 10 --no-cpu-baseline --no-alt
 if [ "${PMC:-1}" = 1 ]; then
