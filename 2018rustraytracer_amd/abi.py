@@ -9,7 +9,8 @@ import ctypes as C
 import os
 
 _PKG_DIR = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_PKG_DIR, "librtm.so")
+# RTM_LIB: another build of the same library (A/B timing runs only, tools/ab_bench.py)
+LIB_PATH = os.environ.get("RTM_LIB") or os.path.join(_PKG_DIR, "librtm.so")
 
 RTM_ABI_VERSION = 3
 RTM_MAX_SPHERES = 16

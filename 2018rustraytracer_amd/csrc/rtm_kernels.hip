@@ -66,6 +66,21 @@ __device__ __forceinline__ bool may_cover(const RasterSphereK& s, int xb, int xe
     return y >= s.iy0 && y <= s.iy1 && xe >= s.ix0 && xb <= s.ix1;
 }
 
+// The wave's sphere set: bit i set iff sphere i's pixel range can reach columns
+// [xb, xe] of rows [ya, ye].  Lane i tests sphere i (one vector load of the range
+// words) and a ballot gathers the bits, instead of a serial chain of per-sphere
+// scalar loads and compares.  Call with every lane of the wave active.
+__device__ __forceinline__ uint32_t wave_sphere_mask(const RasterSphereK* __restrict__ sph, int n, int xb, int xe,
+                                                     int ya, int ye) {
+    const int l = threadIdx.x & 63;
+    bool m = false;
+    if (l < n) {
+        const RasterSphereK& s = sph[l];
+        m = (ye >= s.iy0) & (ya <= s.iy1) & (xe >= s.ix0) & (xb <= s.ix1);
+    }
+    return (uint32_t)__ballot(m);
+}
+
 // Does the union of a viewport's sphere pixel ranges reach columns [xb, xe] of rows [ya, ye]?
 template <typename P>
 __device__ __forceinline__ bool union_may_cover(const P& a, int xb, int xe, int ya, int ye) {
@@ -1089,15 +1104,9 @@ __device__ __forceinline__ void shadow_tile_lean2(const ShadowPart& a, double* _
     // shadow viewport rasterize, face BACK (main.rs:1569, 243)
     if (!(a.flags & RTM_FLAG_NO_SHADOW_RASTER) && !(diag & 1) &&
         union_may_cover(a, xb, xb + TW - 1, y0, y0 + NR - 1)) {
-        // the wave's sphere set first (bitwise tests: the four range words load
-        // together, no branch per word), so a tile no sphere reaches skips the
-        // raster, its column loads included
-        uint32_t live = 0u;
-        for (int i = 0; i < a.n_spheres; ++i) {
-            const RasterSphereK& sp = a.sph[i];
-            const bool out = (y0 + NR - 1 < sp.iy0) | (y0 > sp.iy1) | (xb + TW - 1 < sp.ix0) | (xb > sp.ix1);
-            live |= out ? 0u : (1u << i);
-        }
+        // the wave's sphere set first (one ballot), so a tile no sphere reaches
+        // skips the raster
+        uint32_t live = wave_sphere_mask(a.sph, a.n_spheres, xb, xb + TW - 1, y0, y0 + NR - 1);
         const double* x = xcol;
         while (live) {
             const int i = __builtin_ctz(live);
@@ -1339,15 +1348,19 @@ __device__ __forceinline__ void eye_tile(const EyePart& a, const ShadowPart& sh,
     ShadowCounts sc;
     int hit_kind = 0, hit_id = -1;
     uint32_t n_evals = 0;
+    // the wave's spheres (all lanes active here); ascending bit order = scene order
+    uint32_t smask = union_may_cover(a, xb, xb + TILE_X - 1, yi, yi)
+                         ? wave_sphere_mask(a.sph, a.n_spheres, xb, xb + TILE_X - 1, yi, yi)
+                         : 0u;
     if (live) {
         const double x = a.nx[xi];
         const double y = a.ny[yi];
         // z-test over spheres in scene order, strict '<' against +INF init (main.rs:318)
         double best = INFINITY, bh = 0.0, bz = 0.0;
         int bid = -1;
-        const bool any_sphere = union_may_cover(a, xb, xb + TILE_X - 1, yi, yi);
-        for (int i = 0; any_sphere && i < a.n_spheres; ++i) {
-            if (!may_cover(a.sph[i], xb, xb + TILE_X - 1, yi)) continue;
+        while (smask) {
+            const int i = __builtin_ctz(smask);
+            smask &= smask - 1u;
             double h;
             // (RT variant only: a PERSPECTIVE eye with spheres, row f-3; psp is wave-uniform)
             if ((RT && psp) ? cover_persp(psp->s[i], x, y, h) : cover(a.sph[i], x, y, h)) {

@@ -27,12 +27,12 @@ ctx.set_timing_capacity(%(events)d)
 lib = rtm.load_library()
 scenes = [sc.scene_a_bench(100 + i) if %(cfg)d in (2, 3, 4) else cfg["scene"]() for i in range(%(n)d)]
 cs = [s.to_c() for s in scenes]
-e, s_ = sc.eye_camera().to_c(), sc.shadow_camera().to_c()
+e, s_ = cfg.get("eye", sc.eye_camera)().to_c(), sc.shadow_camera().to_c()
 out = torch.empty((H, W, 4), dtype=torch.float32, device="cuda")
 prep = ctx.prepare_frames(scenes)
 def run(n):
     if %(pipe)d:
-        ctx.render_frames_async(None, sc.eye_camera(), sc.shadow_camera(), W, H, K, flags, [out.data_ptr()] * n,
+        ctx.render_frames_async(None, cfg.get("eye", sc.eye_camera)(), sc.shadow_camera(), W, H, K, flags, [out.data_ptr()] * n,
                                 (prep[0], prep[1]) if n == len(scenes) else ctx.prepare_frames(scenes[:n]))
         return
     for i in range(n):
@@ -59,7 +59,7 @@ def main():
     for _ in range(rounds):
         for name, v in variants.items():
             env = dict(os.environ)
-            env.update(v.get("env", {}))
+            env.update({k: x.replace("__ROOT__", ROOT) for k, x in v.get("env", {}).items()})
             code = CHILD % dict(root=ROOT, cfg=cfg, flags=v.get("flags", 0), events=v.get("events", 200), n=200,
                                steps=v.get("steps", -1), pipe=1 if v.get("pipe") else 0)
             p = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
