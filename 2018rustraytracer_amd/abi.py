@@ -12,7 +12,7 @@ _PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 # RTM_LIB: another build of the same library (A/B timing runs only, tools/ab_bench.py)
 LIB_PATH = os.environ.get("RTM_LIB") or os.path.join(_PKG_DIR, "librtm.so")
 
-RTM_ABI_VERSION = 3
+RTM_ABI_VERSION = 4
 RTM_MAX_SPHERES = 16
 RTM_MAX_PATCHES = 4
 RTM_MAX_CIRCLE_PLANES = 16
@@ -82,7 +82,8 @@ class rtm_stats(C.Structure):
                 ("shadow_sphere_tests", C.c_int64), ("march_iterations", C.c_int64),
                 ("march_hits", C.c_int64), ("march_in_range", C.c_int64),
                 ("eye_circle_plane_pixels", C.c_int64), ("eye_capped_cylinder_pixels", C.c_int64),
-                ("eye_sdf_pixels", C.c_int64), ("sdf_distance_evals", C.c_int64)]
+                ("eye_sdf_pixels", C.c_int64), ("sdf_distance_evals", C.c_int64),
+                ("eye_plane_tests", C.c_int64), ("eye_cylinder_tests", C.c_int64)]
 
     def as_dict(self) -> dict:
         d = {name: getattr(self, name) for name, _ in self._fields_ if name != "eye_hits"}
@@ -97,7 +98,7 @@ assert C.sizeof(rtm_circle_plane) == 88
 assert C.sizeof(rtm_capped_cylinder) == 96
 assert C.sizeof(rtm_sdf) == 136
 assert C.sizeof(rtm_scene) == 64
-assert C.sizeof(rtm_stats) == 8 * (RTM_MAX_SPHERES + 11)
+assert C.sizeof(rtm_stats) == 8 * (RTM_MAX_SPHERES + 13)
 
 # (name, restype, argtypes) for every symbol include/rtm.h declares.
 _P = C.c_void_p

@@ -235,6 +235,7 @@ struct StatsK {
     unsigned long long march_iterations, march_hits, march_in_range;
     unsigned long long eye_circle_plane_pixels, eye_capped_cylinder_pixels, eye_sdf_pixels;
     unsigned long long sdf_distance_evals;
+    unsigned long long eye_plane_tests, eye_cylinder_tests;
 };
 static_assert(sizeof(StatsK) == sizeof(rtm_stats), "StatsK layout");
 

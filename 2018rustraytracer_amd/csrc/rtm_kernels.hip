@@ -541,11 +541,87 @@ __device__ __forceinline__ void trace_sdfs(const SdfTabK* __restrict__ sdf, cons
     }
 }
 
+// Per-wave cull of the ray-traced primitives under a PERSPECTIVE eye (all lanes
+// active).  The wave's rays (one row, columns [xb, xe]) leave the camera origin
+// inside a cone: axis the bisector of its two end rays, half-angle theta to
+// them.  Every hit a primitive can report lies within a bounding sphere (C, R):
+//   circle plane: |o + d t - pos| <= radius            -> (pos, radius)
+//   capped cone:  on the frustum between pa and pb     -> ((pa+pb)/2, |ba|/2 + max|r|)
+// and only at t >= 0 (both tests reject t < 0), so a primitive whose inflated
+// sphere lies outside the cone -- angle(axis, C - o) > theta + asin(R/|C - o|)
+// -- cannot be hit by any ray of the wave.  Inflation (R*1.001 + 1e-7, cosine
+// margin 1e-7) dwarfs the f64 rounding of the exact tests.  Kept (never culled):
+// non-finite data (every comparison is false), origins inside a sphere, and
+// near-cylinders (|rb - ra| < 1e-3 max|r|: the cone formula's cancellation, main.rs:2924-2936).
+__device__ __forceinline__ uint32_t rt_wave_mask(const RtK* __restrict__ rt, const CamK& c, int xb, int xe, int yi,
+                                                 int W, int H) {
+    const double s0 = ndc(xb, W), s1 = ndc(xe, W), u = ndc(yi, H);
+    double n0[3], n1[3], ax[3];
+    double m0 = 0.0, m1 = 0.0;
+    for (int k = 0; k < 3; ++k) {
+        n0[k] = (c.dir[k] + c.side[k] * s0) + c.up[k] * u;
+        n1[k] = (c.dir[k] + c.side[k] * s1) + c.up[k] * u;
+        m0 += n0[k] * n0[k];
+        m1 += n1[k] * n1[k];
+    }
+    m0 = 1.0 / sqrt(m0);
+    m1 = 1.0 / sqrt(m1);
+    double ma = 0.0;
+    for (int k = 0; k < 3; ++k) {
+        n0[k] *= m0;
+        n1[k] *= m1;
+        ax[k] = n0[k] + n1[k];
+        ma += ax[k] * ax[k];
+    }
+    ma = 1.0 / sqrt(ma);
+    double ct = 0.0;
+    for (int k = 0; k < 3; ++k) {
+        ax[k] *= ma;
+        ct += ax[k] * n0[k];
+    }
+    ct = fmin(ct, 1.0);
+    const double st = sqrt(1.0 - ct * ct);
+    const int l = threadIdx.x & 63;
+    double C[3] = {0.0, 0.0, 0.0}, R = 0.0;
+    bool cullable = false;
+    if (l < rt->n_pl) {
+        const PlaneK& p = rt->pl[l];
+        C[0] = p.cx;
+        C[1] = p.cy;
+        C[2] = p.cz;
+        R = p.radius;
+        cullable = true;
+    } else if (l >= 16 && l - 16 < rt->n_cy) {
+        const CylK& q = rt->cy[l - 16];
+        const double rmax = fmax(fabs(q.ra), fabs(q.rb));
+        for (int k = 0; k < 3; ++k) C[k] = (q.pa[k] + q.pb[k]) * 0.5;
+        R = sqrt(q.baba) * 0.5 + rmax;
+        cullable = fabs(q.rb - q.ra) >= 1e-3 * rmax;
+    }
+    const double Ri = R * 1.001 + 1e-7;
+    double w[3], L2 = 0.0, aw = 0.0;
+    for (int k = 0; k < 3; ++k) {
+        w[k] = C[k] - c.pos[k];
+        L2 += w[k] * w[k];
+        aw += ax[k] * w[k];
+    }
+    const double L = sqrt(L2);
+    const double sb = Ri / L;                      // sin(beta)
+    const double cb = sqrt(fmax(1.0 - sb * sb, 0.0));
+    const double thr = ct * cb - st * sb - 1e-7;   // cos(theta + beta), less the margin
+    const bool cull = cullable & (L > Ri) & (sb < 1.0) & (aw < thr * L);
+    return ~(uint32_t)__ballot(cull);  // lane i < 16: plane i; lane 16 + i: cylinder i
+}
+
+// rt_wave_mask culls whole primitives per wave: bits 0-15 planes, 16-31
+// cylinders.  A skipped primitive is one no ray of the wave can hit, so zb and
+// the hit are what the full loop would leave.
 __device__ __forceinline__ void trace_pixel(const RtK* __restrict__ rt, const double o[3], const double d[3],
-                                            double& zb_io, RtHit& hit) {
+                                            double& zb_io, RtHit& hit, uint32_t mask = ~0u) {
     double zb = zb_io;
     const int npl = rt->n_pl, ncy = rt->n_cy;
     for (int i = 0; i < npl; ++i) {
+        if (!((mask >> i) & 1u)) continue;  // wave-uniform
         double t;
         if (plane_hit(rt->pl[i], o, d, zb, t)) {
             hit.kind = 2;
@@ -555,6 +631,7 @@ __device__ __forceinline__ void trace_pixel(const RtK* __restrict__ rt, const do
         }
     }
     for (int i = 0; i < ncy; ++i) {
+        if (!((mask >> (16 + i)) & 1u)) continue;  // wave-uniform
         double n[3];
         const double t = icapped(rt->cy[i], o, d, n);
         if (t < 0.0) continue;  // behind the camera (and misses)
@@ -1344,7 +1421,7 @@ __device__ __forceinline__ void eye_tile(const EyePart& a, const ShadowPart& sh,
     const int yl = __builtin_amdgcn_readfirstlane((wide & 1) ? by : by * TILE_Y + wv);
     const int yi = a.row_begin + yl;
     const bool live = xi < a.W && yi < a.row_end;
-    unsigned long long n_tests = 0, n_hit = 0, n_lit = 0;
+    unsigned long long n_tests = 0, n_hit = 0, n_lit = 0, n_pl_tests = 0, n_cy_tests = 0;
     ShadowCounts sc;
     int hit_kind = 0, hit_id = -1;
     uint32_t n_evals = 0;
@@ -1352,6 +1429,10 @@ __device__ __forceinline__ void eye_tile(const EyePart& a, const ShadowPart& sh,
     uint32_t smask = union_may_cover(a, xb, xb + TILE_X - 1, yi, yi)
                          ? wave_sphere_mask(a.sph, a.n_spheres, xb, xb + TILE_X - 1, yi, yi)
                          : 0u;
+    // the wave's ray-traced primitives (PERSPECTIVE eye; all lanes active here)
+    uint32_t rmask = ~0u;
+    if (RT == 1 && rt && a.eye.type == RTM_CAMERA_PERSPECTIVE && !(wide & 4))
+        rmask = rt_wave_mask(rt, a.eye, min(xb, a.W - 1), min(xb + TILE_X - 1, a.W - 1), min(yi, a.H - 1), a.W, a.H);
     if (live) {
         const double x = a.nx[xi];
         const double y = a.ny[yi];
@@ -1381,7 +1462,13 @@ __device__ __forceinline__ void eye_tile(const EyePart& a, const ShadowPart& sh,
         if (RT) {
             cam_ray(a.eye, x, y, o, d);
             double zb = best;
-            if (rt) trace_pixel(rt, o, d, zb, hit);
+            if (rt) {
+                trace_pixel(rt, o, d, zb, hit, rmask);
+                if (COUNT) {
+                    n_pl_tests = __builtin_popcount(rmask & ((1u << rt->n_pl) - 1u));
+                    n_cy_tests = __builtin_popcount((rmask >> 16) & ((1u << rt->n_cy) - 1u));
+                }
+            }
             if (RT == 2) trace_sdfs(sdf, o, d, zb, hit, n_evals);
         }
         float4 c = make_float4(0.0f, 0.2f, 0.2f, 1.0f);  // (0.0, 0.2, 0.2) as f32 (main.rs:718-720)
@@ -1492,6 +1579,8 @@ __device__ __forceinline__ void eye_tile(const EyePart& a, const ShadowPart& sh,
         if (RT) {
             stat_add(&st->eye_circle_plane_pixels, hit_kind == 2);
             stat_add(&st->eye_capped_cylinder_pixels, hit_kind == 3);
+            stat_add(&st->eye_plane_tests, n_pl_tests);
+            stat_add(&st->eye_cylinder_tests, n_cy_tests);
             if (RT == 2) {
                 stat_add(&st->eye_sdf_pixels, hit_kind == 4);
                 stat_add(&st->sdf_distance_evals, n_evals);

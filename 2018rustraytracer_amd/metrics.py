@@ -29,6 +29,8 @@ off for bit parity).  Per-unit figures:
                  33 per circle plane      (calcRayPlane 15, hit point + radius test 18)
                  88 per capped cylinder   (iCappedCone: projections 22, cap test ~16,
                                            body quadratic 50)
+                 -- per (pixel, primitive) test run: stats eye_plane_tests /
+                 eye_cylinder_tests, after the PERSPECTIVE eye's per-wave cull
 
 HBM bytes the two-kernel design must move:
   shadow pass    8 B per texel            (f64 shadow-map store)
@@ -100,8 +102,12 @@ def frame_work(stats: dict, width: int, height: int, n_spheres: int, n_patches: 
     eye_ops = (px * EYE_PER_SPHERE * n_spheres + EYE_PER_COVER * stats["eye_sphere_tests"]
                + EYE_PER_HIT * stats["eye_hit_pixels"])
     if n_planes or n_cyls or n_sdfs:
-        eye_ops += px * ((RT_RAY_PERSP if perspective else RT_RAY_ORTHO) + RT_PER_PLANE * n_planes
-                         + RT_PER_CYL * n_cyls + SDF_PER_TRACE * n_sdfs)
+        # (pixel, primitive) tests actually run: the GPU's per-wave cull skips
+        # primitives no ray of a wave can reach (stats, ABI v4)
+        pl_tests = stats.get("eye_plane_tests", px * n_planes)
+        cy_tests = stats.get("eye_cylinder_tests", px * n_cyls)
+        eye_ops += (px * ((RT_RAY_PERSP if perspective else RT_RAY_ORTHO) + SDF_PER_TRACE * n_sdfs)
+                    + RT_PER_PLANE * pl_tests + RT_PER_CYL * cy_tests)
         eye_ops += SDF_PER_EVAL * stats.get("sdf_distance_evals", 0) + SDF_PER_HIT * stats.get("eye_sdf_pixels", 0)
     sh_bytes = 0 if fused else 8 * px
     eye_bytes = 16 * px + (0 if fused else 8 * stats["eye_hit_pixels"])

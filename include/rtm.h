@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define RTM_ABI_VERSION 3
+#define RTM_ABI_VERSION 4
 
 /* ---- limits: scene constants travel as kernel arguments (SGPR path) ---- */
 #define RTM_MAX_SPHERES 16
@@ -175,6 +175,11 @@ typedef struct rtm_stats {
     int64_t eye_capped_cylinder_pixels; /* ... a capped cylinder */
     int64_t eye_sdf_pixels;            /* ... an SDF implicit surface (row f-4) */
     int64_t sdf_distance_evals;        /* distanceFn0 calls of the eye's SDF traces (march steps + 4 normal taps per hit) */
+    /* (pixel, primitive) ray tests the eye pass ran: the oracle tests every
+     * primitive at every pixel; the GPU skips primitives its per-wave cull proves
+     * unreachable (ABI v4) */
+    int64_t eye_plane_tests;
+    int64_t eye_cylinder_tests;
 } rtm_stats;
 
 /* ---- library ---- */

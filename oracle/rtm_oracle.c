@@ -233,6 +233,7 @@ typedef struct {
     int64_t march_iterations, march_hits, march_in_range;
     int64_t eye_circle_plane_pixels, eye_capped_cylinder_pixels, eye_sdf_pixels;
     int64_t sdf_distance_evals;
+    int64_t eye_plane_tests, eye_cylinder_tests;
 } Counts; /* layout == rtm_stats */
 
 /* rasterizeSphere (main.rs:249-331).  Pixel loop over rows [y0,y1).  The
@@ -985,6 +986,8 @@ int rtmo_render(const rtm_scene* scene, const rtm_camera* eye, const rtm_camera*
             } else if (pass == 1) {
                 viewport_rasterize(&ve, scene, flags, y0, y1, &c.eye_sphere_tests);
                 viewport_process_raytracing_rays(&ve, scene, y0, y1, &c.sdf_distance_evals);
+                c.eye_plane_tests = (y1 - y0) * W * scene->n_circle_planes;  /* every pixel, every primitive */
+                c.eye_cylinder_tests = (y1 - y0) * W * scene->n_capped_cylinders;
             } else {
                 renderColorImage(scene, &ve, &vs, out_rgba, y0, y1, &c, NULL);
             }

@@ -95,7 +95,13 @@ def test_scene_r_bench_4k(rtm, oracle, scenes, gpu_ctx):
     got = rtm.render_frame(*args)
     want = _oracle(oracle, *args, want_stats=True)
     assert bits_equal(got, want["rgba"]), first_mismatch(got, want["rgba"])
-    assert gpu_ctx.stats(*args) == want["stats"]
+    st, ws = gpu_ctx.stats(*args), want["stats"]
+    cull = ("eye_plane_tests", "eye_cylinder_tests")
+    assert {k: v for k, v in st.items() if k not in cull} == {k: v for k, v in ws.items() if k not in cull}
+    # the per-wave cull (rt_wave_mask) skips most (pixel, primitive) tests; the oracle runs them all
+    assert ws["eye_plane_tests"] == 3840 * 2160 * 4 and ws["eye_cylinder_tests"] == 3840 * 2160 * 9
+    assert 0 < st["eye_plane_tests"] < ws["eye_plane_tests"]
+    assert 0 < st["eye_cylinder_tests"] < ws["eye_cylinder_tests"] // 2
 
 
 @pytest.mark.parametrize("flags", [0, 4])
@@ -247,6 +253,49 @@ def test_degenerate_primitives(rtm, oracle, scenes):
     for eye in (scenes.perspective_eye_camera(),
                 scenes.Camera(scenes.ORTHOGONAL, (0.0, 0.0, 0.0), (0.0, 0.0, 1.0), (0.0, 1.0, 0.0), (1.0, 0.0, 0.0))):
         _check(rtm, oracle, scene, eye, scenes.shadow_camera(), 257, 193, 0, scenes.RAYTRACING_FLAGS)
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_wave_cull_stress(rtm, oracle, scenes, seed):
+    """The per-wave primitive cull of the PERSPECTIVE eye pass (rt_wave_mask):
+    many small primitives scattered over the frustum so that most waves cull
+    most of them, primitives straddling the wave and frame edges, behind the
+    camera, enclosing it, near-cylinders (|rb - ra| tiny or 0: never culled)
+    and a frame width that leaves a partial last wave.  Bit-exact vs the
+    oracle, which has no cull."""
+    rng = np.random.default_rng(0x2018 + 300 + seed)
+    S, P, C = scenes.Shading, scenes.PrimitiveCirclePlane, scenes.PrimitiveCappedCylinder
+
+    def col():
+        return S(*(float(v) for v in rng.uniform(0.05, 1.0, 3)))
+
+    def front(zlo, zhi):
+        z = float(rng.uniform(zlo, zhi))
+        return (float(rng.uniform(-1.1, 1.1) * z), float(rng.uniform(-1.1, 1.1) * z), z)
+
+    planes, cyls = [], []
+    for i in range(16):
+        c = front(0.5, 12.0) if i else (0.0, 0.0, -2.0)  # plane 0 behind the camera
+        n = rng.normal(size=3)
+        n /= np.linalg.norm(n)
+        planes.append(P(i, col(), float(rng.uniform(0.01, 0.4)), c, tuple(float(v) for v in n)))
+    for i in range(16):
+        a = front(0.5, 12.0)
+        d = rng.normal(size=3) * rng.uniform(0.05, 1.5)
+        b = (a[0] + float(d[0]), a[1] + float(d[1]), a[2] + float(d[2]))
+        ra = float(rng.uniform(0.01, 0.3))
+        kind = i % 4
+        rb = ra if kind == 0 else ra * (1.0 + 1e-5) if kind == 1 else float(rng.uniform(0.01, 0.3))
+        if i == 15:  # encloses the camera origin
+            a, b, ra, rb = (0.0, 0.0, -1.0), (0.0, 0.0, 1.0), 0.5, 0.4
+        cyls.append(C(i, col(), a, b, ra, rb))
+    ids = rng.permutation(16)
+    for i, p in enumerate(planes):
+        p.id = int(ids[i])
+    scene = scenes.Scene([], [], planes, cyls)
+    w, h = (961, 541) if seed % 2 == 0 else (1283, 97)
+    _check(rtm, oracle, scene, scenes.perspective_eye_camera(), scenes.shadow_camera(), w, h, 0,
+           scenes.RAYTRACING_FLAGS)
 
 
 def test_raytrace_error_codes(rtm, scenes, gpu_ctx):
