@@ -1,0 +1,62 @@
+"""The compiled C caller of the ABI (examples/rtm_cli.c): includes only
+include/rtm.h, links only librtm.so, and renders testscene_closelyOrbitingSphere
+frames the way the reference's driver does (main.rs:1468-1633).  On the GPU its
+frames must be the oracle's bits and hash to the survey's known answers
+(SURVEY.md §8c-3), and its host-encoded PPM must equal the oracle's
+writeColorImage text."""
+import hashlib
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import ROOT, bits_equal, first_mismatch
+
+CLI = os.path.join(ROOT, "examples", "rtm_cli")
+
+
+def _sha16_rgb(rgba):
+    return hashlib.sha256(np.ascontiguousarray(rgba[..., :3]).tobytes()).hexdigest()[:16]
+
+
+def test_cli_built_and_linked_in_tree():
+    assert os.path.exists(CLI), "examples/rtm_cli not built: run __graft_entry__.build()"
+    out = subprocess.run(["ldd", CLI], capture_output=True, text=True, check=True).stdout
+    lib = [l for l in out.splitlines() if "librtm.so" in l]
+    assert lib and os.path.realpath(os.path.join(ROOT, "2018rustraytracer_amd", "librtm.so")) in \
+        os.path.realpath(lib[0].split("=>")[1].split("(")[0].strip())
+
+
+def test_cli_usage_without_gpu():
+    p = subprocess.run([CLI, "--bogus"], capture_output=True, text=True)
+    assert p.returncode == 2 and "usage" in p.stderr
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("frame,sha", [(0, "cf557d736f83a4f6"), (100, "cb7008f728da5208")])
+def test_cli_reference_frames(oracle, scenes, tmp_path, frame, sha):
+    raw, ppm = tmp_path / "f.raw", tmp_path / "f.ppm"
+    p = subprocess.run([CLI, "-w", "512", "-h", "512", "-k", "500", "-f", str(frame), "--raw", str(raw),
+                        "--ppm", str(ppm)], capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0, p.stderr
+    got = np.fromfile(raw, dtype=np.float32).reshape(512, 512, 4)
+    want = oracle.render(scenes.closely_orbiting_sphere(frame), scenes.eye_camera(), scenes.shadow_camera(),
+                         512, 512, 500, 0)["rgba"]
+    assert bits_equal(got, want), first_mismatch(got, want)
+    assert _sha16_rgb(got) == sha  # SURVEY.md §8c-3 known answer
+    assert ppm.read_bytes() == oracle.write_ppm(want)
+
+
+@pytest.mark.gpu
+def test_cli_bench_patch_frames(oracle, scenes, tmp_path):
+    """Scene A-bench (-b), a non-square size and several frames (the last one is kept)."""
+    raw = tmp_path / "f.raw"
+    w, h = 640, 360
+    p = subprocess.run([CLI, "-w", str(w), "-h", str(h), "-k", "64", "-f", "100", "-n", "3", "-b", "--raw", str(raw)],
+                       capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0, p.stderr
+    assert '"frames": 2' in p.stdout
+    got = np.fromfile(raw, dtype=np.float32).reshape(h, w, 4)
+    want = oracle.render(scenes.scene_a_bench(102), scenes.eye_camera(), scenes.shadow_camera(), w, h, 64, 0)["rgba"]
+    assert bits_equal(got, want), first_mismatch(got, want)
