@@ -6,7 +6,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 ROOT=$(pwd)
-TAG=${TAG:-r01_v11}
+TAG=${TAG:-r01_v12}
 OUT=$ROOT/gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
@@ -24,9 +24,11 @@ step() {
 [ "${SKIP_TESTS:-0}" = 1 ] || step pytest_gpu 900 python -m pytest tests -m gpu -q -p no:cacheprovider
 [ "${SKIP_TESTS:-0}" = 1 ] || step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 step bench3 600 python bench.py
+step bench2 300 python bench.py --config 2 --no-alt --no-cpu-baseline
 step bench4 300 python bench.py --config 4 --no-alt --no-cpu-baseline
 step bench5 300 python bench.py --config 5 --no-alt --no-cpu-baseline
 step bench6 300 python bench.py --config 6 --no-alt
+step bench7 300 python bench.py --config 7 --no-alt --no-cpu-baseline
 step bench8 300 python bench.py --config 8 --no-alt
 step prof3 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof3" -o run --output-format csv -- python3 "$ROOT/bench.py" --steps 200 --warmup 20 --no-cpu-baseline --no-alt
 step prof4 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof4" -o run --output-format csv -- python3 "$ROOT/bench.py" --config 4 --steps 100 --warmup 10 --no-cpu-baseline --no-alt
