@@ -83,8 +83,15 @@ def cpu_baseline(scene, eye, shadow, w, h, k, flags, threads, what):
     best = best_of(2, threads)
     all_cores = min(16, os.cpu_count() or 1)
     best_all = best_of(3, all_cores)
+    model = None  # log the host CPU model and hardware concurrency
+    try:
+        with open("/proc/cpuinfo") as f:
+            model = next((l.split(":", 1)[1].strip() for l in f if l.startswith("model name")), None)
+    except OSError:
+        pass
     return dict(value=round(w * h / best / 1e6, 3), unit="Mpixels/s", cores=threads, kind="port",
                 sample=f"full {w}x{h} frame, K={k}, {what}, best of 2, {threads} thread(s)",
+                cpu_model=model, hardware_concurrency=os.cpu_count(),
                 seconds_per_frame=round(best, 3),
                 all_cores={"value": round(w * h / best_all / 1e6, 3), "cores": all_cores,
                            "seconds_per_frame": round(best_all, 4),
