@@ -109,6 +109,43 @@ def _read_device_f64(ptr, n):
     return out
 
 
+@pytest.mark.parametrize("seed", range(10))
+def test_lean_shadow_path_fuzz(rtm, oracle, scenes, gpu_ctx, seed):
+    """The default shadow kernel (shadow_lean2_kernel: separable camera, shared
+    monotone z table, first-crossing search) under every table shape it takes:
+    increasing and decreasing z (dir.z = +-1), camera offsets in x/y/z, march
+    bounds around the register-fill (256) and LDS (2048) limits and past them,
+    patches whose surface depth lands exactly on a march step (the guess's
+    boundary case) or beyond K, partial tiles.  Shadow map and image bit for bit."""
+    import torch
+    rng = np.random.default_rng(0x2018 + 500 + seed)
+    dz = 1.0 if seed % 2 == 0 else -1.0
+    uy = 1.0 if seed % 3 else -1.0
+    sx = 1.0 if seed % 4 < 2 else -1.0
+    pos = (float(rng.uniform(-0.3, 0.3)), float(rng.uniform(-0.3, 0.3)), float(rng.choice([0.0, 0.25, -0.4])))
+    shadow = scenes.Camera(scenes.ORTHOGONAL, pos, (0.0, 0.0, dz), (0.0, uy, 0.0), (sx, 0.0, 0.0))
+    k = int([1, 63, 64, 65, 255, 256, 257, 1000, 2048, 2049][seed])
+    scene = _random_scene(scenes, rng, int(rng.integers(0, 6)), 0)
+    z0 = 0.0 if pos[2] == 0.0 else pos[2]
+    step = dz * 0.03
+    pats = []
+    for _ in range(int(rng.integers(1, 4))):
+        m = float(rng.integers(0, k + 3))  # a crossing on (or near) step m, maybe beyond K
+        a0 = z0 + m * step
+        pats.append(scenes.Bilinear(scenes.Linear(a0, a0 + float(rng.uniform(-0.5, 0.5))),
+                                    scenes.Linear(a0 + float(rng.uniform(-0.5, 0.5)), float(rng.uniform(-1, 1)))))
+    scene.patches = pats
+    w, h = int(rng.integers(65, 331)), int(rng.integers(17, 201))
+    out = torch.empty((h, w, 4), dtype=torch.float32, device="cuda")
+    torch.cuda.synchronize()
+    gpu_ctx.render_async(scene, scenes.eye_camera(), shadow, w, h, k, 0, out.data_ptr())
+    gpu_ctx.synchronize()
+    got = _read_device_f64(gpu_ctx.shadow_map_ptr(), h * w).reshape(h, w)
+    want = _oracle(oracle, scene, scenes.eye_camera(), shadow, w, h, k, want_shadow=True)
+    assert bits_equal(got, want["shadow"]), first_mismatch(got, want["shadow"])
+    assert bits_equal(out.cpu().numpy(), want["rgba"]), first_mismatch(out.cpu().numpy(), want["rgba"])
+
+
 def test_fused_shadow_identical(rtm, oracle, scenes):
     """RTM_FLAG_FUSED_SHADOW evaluates texels on demand: same image bits."""
     for scene, w, h, k in ((scenes.closely_orbiting_sphere(100), 512, 512, 500),
