@@ -972,113 +972,6 @@ __device__ __forceinline__ void shadow_tile_sep(const ShadowPart& a, double* __r
     }
 }
 
-// Lean separable shadow tile (default for the BASELINE scenes): the same
-// texels and bits as shadow_tile_sep<NR, MARCH_SEARCH> with the LDS table, with
-// the common path free of divergent control flow, so the wave issues no
-// exec-mask bookkeeping:
-//  * sphere coverage computes h = sqrt(1 - d*d) unconditionally and selects on
-//    d < 1 (the covered lanes get exactly the reference's h; the others'
-//    value, possibly NaN, is never used);
-//  * the first-crossing guess is clamped to [1, steps] (P(0) is false on
-//    every lane that marches, so the first true index is >= 1) and both table
-//    entries are read unconditionally from LDS;
-//  * lanes whose guess fails the verification, or whose D is not finite and
-//    nonzero, take the exact march_axis behind a wave ballot.
-// Needs 1 <= steps <= SEARCH_LDS_MAX_STEPS and a monotone z table (host).
-template <int NR>
-__device__ __forceinline__ void shadow_tile_lean(const ShadowPart& a, double* __restrict__ smap, int bx, int by,
-                                                 double2* __restrict__ T, int diag) {
-    const int lane = threadIdx.x & (TILE_X - 1);
-    const int xb = bx * TILE_X;
-    const int xi = xb + lane;
-    const int y0 = __builtin_amdgcn_readfirstlane(by * (TILE_Y * NR) + (threadIdx.x >> 6) * NR);
-    const bool colv = xi < a.W;
-    const int xs = colv ? xi : a.W - 1;
-    const int steps = a.steps;
-    // (the host sizes the LDS table for exactly this condition)
-    const bool march = !(a.flags & RTM_FLAG_NO_MARCH) && !(diag & 2) && a.n_patches > 0 && steps > 0;
-    if (march) {
-        for (int k = threadIdx.x; k <= steps; k += BLOCK)
-            T[k] = make_double2(a.tab.z[k], k < steps ? a.tab.t[k] : 0.0);
-        __syncthreads();
-    }
-    double zb[NR];
-#pragma unroll
-    for (int r = 0; r < NR; ++r) zb[r] = INFINITY;
-    // shadow viewport rasterize, face BACK (main.rs:1569, 243)
-    if (!(a.flags & RTM_FLAG_NO_SHADOW_RASTER) && !(diag & 1) &&
-        union_may_cover(a, xb, xb + TILE_X - 1, y0, y0 + NR - 1)) {
-        const double x = a.tab.nx[xs];
-        for (int i = 0; i < a.n_spheres; ++i) {
-            const RasterSphereK& sp = a.sph[i];
-            if (y0 + NR - 1 < sp.iy0 || y0 > sp.iy1 || xb + TILE_X - 1 < sp.ix0 || xb > sp.ix1) continue;
-            const double relx = x - sp.cx;
-            const double pa = (relx * sp.n) / sp.m;
-#pragma unroll
-            for (int r = 0; r < NR; ++r) {
-                const int y = y0 + r;
-                if (y >= a.H || y < sp.iy0 || y > sp.iy1) continue;  // wave-uniform
-                const double rely = ((cdouble*)a.tab.ny)[y] - sp.cy;
-                const double pb = (rely * sp.n) / sp.m;
-                const double d = sqrt(pa * pa + pb * pb);
-                const double h = sqrt(1.0 - d * d);
-                const double depth = sp.z + h * sp.r;
-                zb[r] = (d < 1.0 && depth < zb[r]) ? depth : zb[r];
-            }
-        }
-    }
-    if (march) {
-        const double oz = ((cdouble*)a.tab.z)[0];
-        const double sz = a.cam.dir[2] * 0.03;
-        const double inv_sz = 1.0 / sz;
-        const bool inc = a.tab.zmono > 0;
-        const double fsteps = (double)steps;
-        const bool colok = colv && a.tab.ok[xs] != 0;
-        for (int k = 0; k < a.n_patches; ++k) {
-            const double d0 = a.tab.d0[k * a.W + xs];
-            const double dd = a.tab.dd[k * a.W + xs];
-            unsigned slow = 0u;
-            double D[NR];
-#pragma unroll
-            for (int r = 0; r < NR; ++r) {
-                const int yr = y0 + r < a.H ? y0 + r : y0;  // wave-uniform: scalar loads
-                D[r] = d0 + dd * ((cdouble*)a.tab.py)[yr];
-                const bool inr = colok && y0 + r < a.H && ((cint*)a.tab.ok)[a.W + yr] != 0;
-                const bool p0 = (oz < D[r]) != inc;  // z_0 already past the surface: no hit
-                const bool fastD = fabs(D[r]) < INFINITY && D[r] != 0.0;
-                double g = fmin(fmax((D[r] - oz) * inv_sz, 1.0), fsteps);  // NaN -> 1
-                const int f = (int)ceil(g);
-                const double2 e = T[f];
-                const double zp = T[f - 1].x;
-                const bool ok = ((zp < D[r]) == inc) && (f == steps || ((e.x < D[r]) != inc));
-                const bool active = inr && !p0;
-                const bool hit = active && fastD && ok && f < steps;
-                zb[r] = (hit && e.y < zb[r]) ? e.y : zb[r];
-                slow |= (inr && (!fastD || (!p0 && !ok))) ? (1u << r) : 0u;
-            }
-            if (__any(slow != 0u)) {
-                // exact per-texel march for the lanes the fast path cannot decide
-#pragma unroll 1
-                for (int r = 0; r < NR; ++r) {
-                    if (!((slow >> r) & 1u)) continue;
-                    double Dr = D[0];
-#pragma unroll
-                    for (int q = 1; q < NR; ++q) Dr = r == q ? D[q] : Dr;
-                    MarchResult m = march_axis<false>(Dr, true, oz, sz, steps, a.tab);
-#pragma unroll
-                    for (int q = 0; q < NR; ++q)
-                        if (q == r && m.hit && m.t < zb[q]) zb[q] = m.t;
-                }
-            }
-        }
-    }
-    if (colv) {
-#pragma unroll
-        for (int r = 0; r < NR; ++r)
-            if (y0 + r < a.H) smap[(int64_t)(y0 + r) * a.W + xi] = zb[r];
-    }
-}
-
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ double readlane_f64(double v, int l) {
@@ -1099,9 +992,16 @@ __device__ unsigned long long g_phase[1 << 18];
         if ((threadIdx.x & 63) == 0 && wid_ * 8u + 8u <= (1u << 18)) g_phase[wid_ * 8u + (k)] = t_;        \
     }
 
-// shadow_tile_lean with CW columns per lane (a wave covers 64*CW columns, so a
-// row's texels leave as one 16-byte store per lane when CW == 2) and the table
-// direction as a template parameter.  Per texel the search is: D (exact, 2
+// The lean separable shadow tile (the default for every BASELINE scene): the
+// texels and bits of shadow_tile_sep<NR, MARCH_SEARCH>, with the common path
+// free of divergent control flow.  Sphere coverage computes h = sqrt(1 - d*d)
+// unconditionally and selects on d < 1; the first-crossing guess is clamped to
+// [1, steps] and both table entries are read from LDS unconditionally; lanes the
+// fast path cannot decide take the exact march_axis behind a wave ballot.
+// CW columns per lane (a wave covers 64*CW columns, so a row's texels leave as
+// one 16-byte store per lane when CW == 2), NR rows per wave, the table
+// direction as a template parameter.  Needs 1 <= steps <= SEARCH_LDS_MAX_STEPS
+// and a monotone z table (host-checked).  Per texel the search is: D (exact, 2
 // ops), "D finite and nonzero" (one class test), the index guess
 // fma(dd', py, d0') from per-column pre-scaled terms (a guess only: the
 // verification below decides), clamp/ceil/convert, two LDS reads, and with
@@ -1109,7 +1009,7 @@ __device__ unsigned long long g_phase[1 << 18];
 //   okA = !P(z_{f-1}), okB = P(z_f), entry = !P(z_0)   (monotone P)
 //   hit  = inr & fastD & okA & okB & f < steps      -> t = t_f
 //   slow = inr & (!fastD | (entry & !(okA & (f == steps | okB))))  -> exact march_axis
-template <int NR, int CW, bool INC, bool FILLED = false, int FILLN = 4>
+template <int NR, int CW, bool INC, int FILLN = 4>
 __device__ __forceinline__ void shadow_tile_lean2(const ShadowPart& a, double* __restrict__ smap, int bx, int by,
                                                   double2* __restrict__ T, int diag) {
     constexpr int TW = TILE_X * CW;
@@ -1131,7 +1031,7 @@ __device__ __forceinline__ void shadow_tile_lean2(const ShadowPart& a, double* _
     // raster below (which does not read it); written + barrier afterwards
     constexpr int FILL = FILLN;  // entries per thread held in registers (steps + 1 <= FILL * BLOCK)
     double2 fv[FILL];
-    const bool fill_regs = !FILLED && march && steps + 1 <= FILL * BLOCK;
+    const bool fill_regs = march && steps + 1 <= FILL * BLOCK;
     if (fill_regs) {
 #pragma unroll
         for (int u = 0; u < FILL; ++u) {
@@ -1218,7 +1118,7 @@ __device__ __forceinline__ void shadow_tile_lean2(const ShadowPart& a, double* _
         }
     }
     RTM_PHASE(1)
-    if (!FILLED && march) {
+    if (march) {
         if (fill_regs) {
 #pragma unroll
             for (int u = 0; u < FILL; ++u) {
@@ -1346,26 +1246,6 @@ __device__ __forceinline__ void shadow_tile_lean2(const ShadowPart& a, double* _
     }
 }
 
-// Persistent form of shadow_lean2_kernel: a grid of about one resident wave set
-// (CUs x workgroups per CU) walks the tiles round-robin, so the LDS table is
-// filled once per workgroup and a wave's stores for one tile drain while it
-// computes the next (one tile per wave otherwise runs the waves of a round in
-// phase: all compute, then all store).
-template <int NR, int CW, bool INC>
-__global__ __launch_bounds__(BLOCK) void shadow_persist_kernel(const FrameArgs a, double* __restrict__ smap, int diag,
-                                                               int tiles_x, int n_tiles) {
-    extern __shared__ double2 lds_zt[];
-    const ShadowPart& sh = a.sh;
-    const bool march = !(sh.flags & RTM_FLAG_NO_MARCH) && !(diag & 2) && sh.n_patches > 0 && sh.steps > 0;
-    if (march) {
-        for (int k = threadIdx.x; k <= sh.steps; k += BLOCK)
-            lds_zt[k] = make_double2(sh.tab.z[k], k < sh.steps ? sh.tab.t[k] : 0.0);
-        __syncthreads();
-    }
-    for (int t = blockIdx.x; t < n_tiles; t += gridDim.x)
-        shadow_tile_lean2<NR, CW, INC, true>(sh, smap, t % tiles_x, t / tiles_x, lds_zt, diag);
-}
-
 // Tile row of workgroup row b (of n) with the rows [h0, h1] that the spheres'
 // pixel-range union reaches dispatched first: their waves carry the raster work,
 // and started last they would be the kernel's tail.
@@ -1390,15 +1270,9 @@ __global__ __launch_bounds__(BLOCK) void shadow_lean2_kernel(const FrameArgs a, 
         const bool none = a.sh.cull_x0 > a.sh.cull_x1 || a.sh.cull_y0 > a.sh.cull_y1 || a.sh.cull_y1 < 0;
         by = none ? by : hot_rows_first(by, n, h0, h1);
     }
-    shadow_tile_lean2<NR, CW, INC, false, FILLN>(a.sh, smap, blockIdx.x, by, lds_zt, diag);
+    shadow_tile_lean2<NR, CW, INC, FILLN>(a.sh, smap, blockIdx.x, by, lds_zt, diag);
 }
 
-
-template <int NR>
-__global__ __launch_bounds__(BLOCK) void shadow_lean_kernel(const FrameArgs a, double* __restrict__ smap, int diag) {
-    extern __shared__ double2 lds_zt[];
-    shadow_tile_lean<NR>(a.sh, smap, blockIdx.x, blockIdx.y, lds_zt, diag);
-}
 
 // Eye tile: 64 x TILE_Y pixels: eye viewport rasterize (face FRONT, main.rs:1616)
 // [+ processRaytracingRays when RT, main.rs:1035] + renderColorImage
@@ -1895,7 +1769,6 @@ static bool use_sep(const ShadowPart& s) { return sep_rows() > 0 && s.tab.d0 && 
 // (47.1 vs 52.9 us for the sign bit at config 3, profiles/r01_ab_cmp.txt).
 // RTM_SEP_MODE=0/1/2 forces sign/compare/search for A/B runs (search only when
 // the table allows it) — identical results.
-constexpr int MARCH_LEAN = 3;   // shadow_lean_kernel
 constexpr int MARCH_LEAN2 = 4;  // shadow_lean2_kernel (the default when it applies)
 static int sep_mode(const ShadowPart& sh) {
     static int v = [] {
@@ -1905,25 +1778,11 @@ static int sep_mode(const ShadowPart& sh) {
     const bool march = !(sh.flags & RTM_FLAG_NO_MARCH) && sh.n_patches > 0 && sh.steps > 0;
     const bool lean_ok = sh.tab.zmono != 0 && sh.steps >= 1 && sh.steps <= SEARCH_LDS_MAX_STEPS;
     int want = v < 0 ? MARCH_LEAN2 : v;
-    if ((want == MARCH_LEAN || want == MARCH_LEAN2) && !(lean_ok || !march)) want = MARCH_SEARCH;
+    if (want == MARCH_LEAN2 && !(lean_ok || !march)) want = MARCH_SEARCH;
+    if (want != MARCH_LEAN2 && want != MARCH_CMP && want != MARCH_SIGN) want = MARCH_SEARCH;
     return (want == MARCH_SEARCH && sh.tab.zmono == 0) ? MARCH_CMP : want;
 }
 
-// Workgroups of the persistent shadow kernel: RTM_PERSIST=<workgroups per CU>
-// (0 = one tile per workgroup, the plain lean2 grid).  Default chosen by measurement.
-static int persist_blocks() {
-    static int v = [] {
-        const char* e = getenv("RTM_PERSIST");
-        const int per_cu = e ? atoi(e) : 0;
-        if (per_cu <= 0) return 0;
-        int dev = 0, cus = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
-            cus = 256;
-        return per_cu * cus;
-    }();
-    return v;
-}
 
 // Columns per lane of shadow_lean2_kernel (RTM_LEAN_COLS=1|2, default 2).
 static int lean_cols() {
@@ -1967,19 +1826,7 @@ static void launch_sep(const FrameArgs& a, double* smap, hipStream_t s) {
     const bool march = !(a.sh.flags & RTM_FLAG_NO_MARCH) && a.sh.n_patches > 0 && a.sh.steps > 0;
     const int lds = (mode == MARCH_SEARCH && lds_on && march && a.sh.steps <= SEARCH_LDS_MAX_STEPS) ? 1 : 0;
     const size_t smem = lds ? sizeof(double2) * (size_t)(a.sh.steps + 1) : 0;
-    if (mode == MARCH_LEAN2 && persist_blocks() > 0) {
-        const size_t lsm = march ? sizeof(double2) * (size_t)(a.sh.steps + 1) : 0;
-        const int tiles_x = (a.sh.W + 2 * TILE_X - 1) / (2 * TILE_X);
-        const int n_tiles = tiles_x * (int)g.y;
-        const int blocks = std::min(n_tiles, persist_blocks());
-        const bool inc = a.sh.tab.zmono >= 0;
-        if (inc)
-            hipLaunchKernelGGL((shadow_persist_kernel<NR, 2, true>), dim3((unsigned)blocks), dim3(BLOCK), lsm, s, a, smap,
-                               diag_mode(), tiles_x, n_tiles);
-        else
-            hipLaunchKernelGGL((shadow_persist_kernel<NR, 2, false>), dim3((unsigned)blocks), dim3(BLOCK), lsm, s, a,
-                               smap, diag_mode(), tiles_x, n_tiles);
-    } else if (mode == MARCH_LEAN2) {
+    if (mode == MARCH_LEAN2) {
         const size_t lsm = march ? sizeof(double2) * (size_t)(a.sh.steps + 1) : 0;
         const int cw = lean_cols();
         const int tw = TILE_X * cw;
@@ -2001,11 +1848,6 @@ static void launch_sep(const FrameArgs& a, double* smap, hipStream_t s) {
             else RTM_L2(1, false, 4);
         }
 #undef RTM_L2
-    } else if (mode == MARCH_LEAN) {
-        // LDS table iff the kernel marches: no NO_MARCH flag, patches, steps > 0 (diag 2 skips
-        // the march but the table size stays correct)
-        const size_t lsm = march ? sizeof(double2) * (size_t)(a.sh.steps + 1) : 0;
-        hipLaunchKernelGGL((shadow_lean_kernel<NR>), g, dim3(BLOCK), lsm, s, a, smap, diag_mode());
     } else if (mode == MARCH_SEARCH)
         hipLaunchKernelGGL((shadow_sep_kernel<NR, MARCH_SEARCH>), g, dim3(BLOCK), smem, s, a, smap, diag_mode(), lds);
     else if (mode == MARCH_CMP)
@@ -2122,7 +1964,7 @@ int launch_frame_pipe(const FrameArgs& a, double* smap_w, const double* smap_r, 
     float4* o = reinterpret_cast<float4*>(out);
     if (use_sep(a.sh)) {
         const int mode = sep_mode(a.sh);
-        if (mode == MARCH_LEAN2 || mode == MARCH_LEAN) {
+        if (mode == MARCH_LEAN2) {
             if (a.sh.tab.zmono >= 0) launch_pipe<2, 4, true>(a, smap_w, smap_r, o, s);
             else launch_pipe<2, 4, false>(a, smap_w, smap_r, o, s);
         } else {
