@@ -50,7 +50,13 @@ def parse():
 
 def _latest_traffic(cfg_id: int, kernel: str):
     """HBM bytes per launch from the newest committed PMC summary (tools/profile.sh)."""
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")))
+    import re
+
+    def key(f):  # newest round/version first: r01_v12 after r01_v9 (not lexicographic)
+        m = re.search(r"r(\d+)_v(\d+)", os.path.basename(f))
+        return (int(m.group(1)), int(m.group(2))) if m else (-1, -1)
+
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")), key=key)
     for f in reversed(files):
         try:
             d = json.load(open(f))
