@@ -1019,6 +1019,25 @@ int rtm_render_frames_async(rtm_ctx* ctx, int32_t n_frames, const rtm_scene* sce
     if (!ctx || !scenes || !out_rgba_dev || n_frames < 1) return fail(RTM_ERR_INVALID, "bad arguments");
     for (int32_t i = 0; i < n_frames; ++i)
         if (!out_rgba_dev[i]) return fail(RTM_ERR_INVALID, "out_rgba_dev[%d] is NULL", i);
+    static const bool pipeline_env = [] {
+        const char* e = getenv("RTM_PIPELINE");
+        return e && atoi(e) != 0;
+    }();
+    if (!pipeline_env) {
+        // two kernels per frame: build each frame's arguments just before its launches,
+        // so the GPU starts on frame 0 while the host prepares frame 1 (building all
+        // frames first left the GPU idle for the whole build)
+        DeviceGuard g(ctx->device);
+        for (int32_t i = 0; i < n_frames; ++i) {
+            FrameArgs fa;
+            FrameExtra ex1;
+            int rc = build_frame(fa, &scenes[i], eye, shadow, width, height, march_steps, flags);
+            if (rc) return rc;
+            build_extra(&scenes[i], eye, width, height, ex1);
+            if ((rc = enqueue_frame(ctx, fa, &ex1, out_rgba_dev[i], nullptr))) return rc;
+        }
+        return RTM_OK;
+    }
     std::vector<FrameArgs> f((size_t)n_frames);
     std::vector<FrameExtra> ex((size_t)n_frames);
     bool any_rt = false;

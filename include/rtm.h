@@ -250,7 +250,9 @@ int rtm_render_async(rtm_ctx* ctx, const rtm_scene* scene, const rtm_camera* eye
  * frame the sequence is software-pipelined instead: the shadow pass of frame i
  * and the eye pass of frame i-1 run in ONE launch (double-buffered shadow
  * maps) — correct, but measured slower on MI355X.  Each frame's
- * output is bit-identical to rtm_render. */
+ * output is bit-identical to rtm_render.  Frames are validated as they are
+ * enqueued: on an error return, the frames before the failing one may already
+ * be on the stream. */
 int rtm_render_frames_async(rtm_ctx* ctx, int32_t n_frames, const rtm_scene* scenes,
                             const rtm_camera* eye, const rtm_camera* shadow, int32_t width,
                             int32_t height, int32_t march_steps, int32_t flags,
