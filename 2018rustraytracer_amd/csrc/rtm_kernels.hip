@@ -1489,6 +1489,13 @@ __global__ __launch_bounds__(BLOCK) void eye_pass_kernel(const FrameArgs a, cons
     eye_tile<FUSED, COUNT, RT>(a.ey, a.sh, smap, out, blockIdx.x, blockIdx.y, st, tabs, wide);
 }
 
+// The SDF eye instantiation (row f-4) with a register cap: WPE waves per SIMD at least.
+template <int WPE>
+__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8))) void eye_sdf_kernel(
+    const FrameArgs a, const double* __restrict__ smap, float4* __restrict__ out, const DevTabs tabs, int wide) {
+    eye_tile<false, false, 2>(a.ey, a.sh, smap, out, blockIdx.x, blockIdx.y, nullptr, tabs, wide);
+}
+
 // launch_*_upload: one 8-byte word per thread from the kernarg copy.
 template <class T>
 __global__ void upload_kernel(const T k, T* __restrict__ dst) {
@@ -1885,6 +1892,16 @@ static int eye_wide() {
     return v;
 }
 
+// The SDF eye kernel at >= 5 waves per SIMD (default; RTM_SDF_WPE=0 for the
+// compiler's 99-VGPR, 4-wave allocation in A/B runs; 6 spills 44 VGPRs, 8 runs 1.6x slower).
+static bool sdf_wpe5() {
+    static bool v = [] {
+        const char* e = getenv("RTM_SDF_WPE");
+        return !(e && atoi(e) == 0);
+    }();
+    return v;
+}
+
 int launch_eye_pass(const FrameArgs& a, const double* smap, float* out, void* stream, StatsK* stats,
                     const DevTabs& tabs) {
     hipStream_t s = (hipStream_t)stream;
@@ -1903,6 +1920,8 @@ int launch_eye_pass(const FrameArgs& a, const double* smap, float* out, void* st
         if (fused && stats) RTM_EYE(true, true, 2);
         else if (fused) RTM_EYE(true, false, 2);
         else if (stats) RTM_EYE(false, true, 2);
+        else if (sdf_wpe5())  // 95 VGPRs, 5 waves/SIMD, no spill: eye 582 -> 565 us at config 8
+            hipLaunchKernelGGL(eye_sdf_kernel<5>, g, dim3(BLOCK), 0, s, a, smap, o, tabs, wide);
         else RTM_EYE(false, false, 2);
     } else if (tabs.rt || tabs.psp) {
         if (fused && stats) RTM_EYE(true, true, 1);
