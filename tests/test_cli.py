@@ -16,6 +16,14 @@ from conftest import ROOT, bits_equal, first_mismatch
 CLI = os.path.join(ROOT, "examples", "rtm_cli")
 
 
+@pytest.fixture(scope="module", autouse=True)
+def _cli_built():
+    """build() makes examples/rtm_cli; a tree with librtm.so but no CLI gets it here (gcc, seconds)."""
+    lib = os.path.join(ROOT, "2018rustraytracer_amd", "librtm.so")
+    if not os.path.exists(CLI) and os.path.exists(lib):
+        subprocess.run(["make", "-C", os.path.join(ROOT, "examples")], check=True, capture_output=True)
+
+
 def _sha16_rgb(rgba):
     return hashlib.sha256(np.ascontiguousarray(rgba[..., :3]).tobytes()).hexdigest()[:16]
 
