@@ -341,6 +341,28 @@ void build_extra(const rtm_scene* scene, const rtm_camera* eye, int32_t W, int32
         for (int i = 0; i < scene->n_spheres; ++i) (void)project_sphere_persp(*eye, scene->spheres[i], W, H, x.psp.s[i]);
 }
 
+// The largest double s >= +0 with sqrt(s) <= r (sqrt correctly rounded, monotone), so
+// that !(sqrt(s) > r) == !(s > T) for every s the radius test sees (s = q.q is +0,
+// positive, +inf or NaN): r NaN -> NaN (both tests always pass), r < 0 -> -1 (both
+// always fail for non-NaN s), r = +inf -> +inf; otherwise a search over the ordered
+// bit patterns of [+0, +inf).
+double sqrt_le_threshold(double r) {
+    if (r != r) return r;
+    if (r < 0.0) return -1.0;
+    if (std::sqrt(INFINITY) <= r) return INFINITY;
+    uint64_t lo = 0u, hi = 0x7FF0000000000000ull;  // sqrt(+0) <= r (r >= +-0), sqrt(+inf) > r
+    while (hi - lo > 1u) {
+        const uint64_t mid = lo + (hi - lo) / 2u;
+        double v;
+        std::memcpy(&v, &mid, sizeof v);
+        if (std::sqrt(v) <= r) lo = mid;
+        else hi = mid;
+    }
+    double t;
+    std::memcpy(&t, &lo, sizeof t);
+    return t;
+}
+
 // Ray-traced primitives of a (validated) scene, with iCappedCone's
 // ray-independent terms in the reference's operation order (main.rs:2906-2934).
 // Returns true when the scene has any.
@@ -358,6 +380,7 @@ bool build_rt(const rtm_scene* scene, RtK& k) {
         p.ny = q.n[1];
         p.nz = q.n[2];
         p.radius = q.radius;
+        p.r2max = sqrt_le_threshold(q.radius);
         p.cr = q.color[0];
         p.cg = q.color[1];
         p.cb = q.color[2];

@@ -127,6 +127,8 @@ struct PlaneK {            // PrimitiveCirclePlane (main.rs:370-380)
     double cx, cy, cz;     // pos (Plane.center)
     double nx, ny, nz;     // n
     double radius;
+    double r2max;          // largest s with sqrt(s) <= radius (host libm sqrt): the radius test
+                           // !(sqrt(s) > radius) is exactly !(s > r2max), no device sqrt
     double cr, cg, cb;     // shading
     int32_t id, pad;
 };
@@ -146,7 +148,7 @@ struct RtK {
     CylK cy[RTM_MAX_CAPPED_CYLINDERS];
     int32_t n_pl, n_cy;
 };
-static_assert(sizeof(PlaneK) == 88 && sizeof(CylK) == 152, "RtK layout");
+static_assert(sizeof(PlaneK) == 96 && sizeof(CylK) == 152, "RtK layout");
 static_assert(sizeof(RtK) + sizeof(void*) <= 4096, "RtK must fit the upload kernel's kernarg segment");
 
 // One sphere as seen by a PERSPECTIVE camera (row f-3; Viewport::rasterize,

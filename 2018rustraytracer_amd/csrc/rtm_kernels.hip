@@ -330,7 +330,9 @@ __device__ __forceinline__ bool plane_hit(const PlaneK& p, const double o[3], co
     const double qx = (o[0] + d[0] * t) - p.cx;
     const double qy = (o[1] + d[1] * t) - p.cy;
     const double qz = (o[2] + d[2] * t) - p.cz;
-    return !(sqrt(qx * qx + qy * qy + qz * qz) > p.radius);
+    // !(sqrt(s) > radius) == !(s > r2max): sqrt is monotone and r2max is the largest s
+    // whose (correctly rounded) root is <= radius, NaN and inf included (build_rt)
+    return !(qx * qx + qy * qy + qz * qz > p.r2max);
 }
 
 // iCappedCone (main.rs:2889-2959) in the reference's operation order; the
