@@ -12,7 +12,7 @@ _PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 # RTM_LIB: another build of the same library (A/B timing runs only, tools/ab_bench.py)
 LIB_PATH = os.environ.get("RTM_LIB") or os.path.join(_PKG_DIR, "librtm.so")
 
-RTM_ABI_VERSION = 4
+RTM_ABI_VERSION = 5
 RTM_MAX_SPHERES = 16
 RTM_MAX_PATCHES = 4
 RTM_MAX_CIRCLE_PLANES = 16
@@ -114,6 +114,8 @@ ABI_SYMBOLS = [
     ("rtm_ctx_last_kernel_ms", C.c_int, [_P, C.POINTER(C.c_float), C.POINTER(C.c_float)]),
     ("rtm_ctx_set_timing_capacity", C.c_int, [_P, _I32]),
     ("rtm_ctx_set_timing_stride", C.c_int, [_P, _I32]),
+    ("rtm_ctx_set_lanes", C.c_int, [_P, _I32]),
+    ("rtm_ctx_last_lanes", C.c_int, [_P, C.POINTER(_I32)]),
     ("rtm_ctx_kernel_ms_history", C.c_int, [_P, C.POINTER(C.c_float), C.POINTER(C.c_float), _I32,
                                             C.POINTER(_I32)]),
     ("rtm_render", C.c_int, [C.POINTER(rtm_scene), C.POINTER(rtm_camera), C.POINTER(rtm_camera),

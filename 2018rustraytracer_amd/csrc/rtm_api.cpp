@@ -583,9 +583,22 @@ struct TimingSlot {
     bool shadow = false;
 };
 
+// An extra stream of a context with its own per-frame buffers: the frame
+// sequence call spreads independent frames over lanes so one frame's kernels
+// fill the ramp and tail of another's (see frame_lanes).
+struct Lane {
+    hipStream_t stream = nullptr;
+    hipEvent_t done = nullptr;  // join: the context stream waits on it
+    DevBuf smap, rtk, pspk, sdfk;
+};
+
 struct rtm_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
+    std::vector<std::unique_ptr<Lane>> lanes;  // extra lanes 1..n (lane 0 is the context itself)
+    hipEvent_t fork = nullptr;                 // lanes wait on the context stream's earlier work
+    int32_t lanes_req = 0;                     // rtm_ctx_set_lanes (0 = auto)
+    int32_t lanes_last = 0;                    // lanes of the last frame-sequence call
     std::vector<TimingSlot> ring;  // per-render kernel events (capacity = ring.size())
     int64_t renders = 0;           // renders recorded into the ring
     int64_t calls = 0;             // renders enqueued (for the stride)
@@ -745,6 +758,7 @@ int ensure_tables(rtm_ctx* ctx, int32_t steps, int32_t W, int32_t H, const rtm_c
             }
         }
         HIP_TRY(hipStreamSynchronize(ctx->stream));  // earlier launches may still read the old tables
+        for (auto& l : ctx->lanes) HIP_TRY(hipStreamSynchronize(l->stream));
         int rc = ctx->tabs.ensure(h.size() * sizeof(double), ctx->device);
         if (rc) return rc;
         HIP_TRY(hipMemcpy(ctx->tabs.p, h.data(), h.size() * sizeof(double), hipMemcpyHostToDevice));
@@ -819,46 +833,49 @@ TimingSlot* next_slot(rtm_ctx* ctx) {
     return timed ? &ctx->ring[(size_t)(ctx->renders % (int64_t)ctx->ring.size())] : nullptr;
 }
 
-// The frame's ray-traced primitives into ctx->rtk (stream-ordered; the previous
-// frame's kernels have consumed the old contents by the time the upload runs).
-int upload_rt(rtm_ctx* ctx, const RtK& rt, const RtK** dev) {
-    int rc = ctx->rtk.ensure(sizeof(RtK), ctx->device);
+// The frame's ray-traced primitives into the lane's rtk (stream-ordered; the
+// lane's previous frame has consumed the old contents by the time the upload runs).
+int upload_rt(rtm_ctx* ctx, DevBuf& buf, hipStream_t s, const RtK& rt, const RtK** dev) {
+    int rc = buf.ensure(sizeof(RtK), ctx->device);
     if (rc) return rc;
-    if ((rc = launch_rt_upload(rt, (RtK*)ctx->rtk.p, ctx->stream))) return fail(rc, "rt upload launch failed");
-    *dev = (const RtK*)ctx->rtk.p;
+    if ((rc = launch_rt_upload(rt, (RtK*)buf.p, s))) return fail(rc, "rt upload launch failed");
+    *dev = (const RtK*)buf.p;
     return RTM_OK;
 }
 
-int upload_persp(rtm_ctx* ctx, const PerspK& k, const PerspK** dev) {
-    int rc = ctx->pspk.ensure(sizeof(PerspK), ctx->device);
+int upload_persp(rtm_ctx* ctx, DevBuf& buf, hipStream_t s, const PerspK& k, const PerspK** dev) {
+    int rc = buf.ensure(sizeof(PerspK), ctx->device);
     if (rc) return rc;
-    if ((rc = launch_persp_upload(k, (PerspK*)ctx->pspk.p, ctx->stream))) return fail(rc, "upload launch failed");
-    *dev = (const PerspK*)ctx->pspk.p;
+    if ((rc = launch_persp_upload(k, (PerspK*)buf.p, s))) return fail(rc, "upload launch failed");
+    *dev = (const PerspK*)buf.p;
     return RTM_OK;
 }
 
-int upload_sdf(rtm_ctx* ctx, const SdfTabK& k, const SdfTabK** dev) {
-    int rc = ctx->sdfk.ensure(sizeof(SdfTabK), ctx->device);
+int upload_sdf(rtm_ctx* ctx, DevBuf& buf, hipStream_t s, const SdfTabK& k, const SdfTabK** dev) {
+    int rc = buf.ensure(sizeof(SdfTabK), ctx->device);
     if (rc) return rc;
-    if ((rc = launch_sdf_upload(k, (SdfTabK*)ctx->sdfk.p, ctx->stream))) return fail(rc, "sdf upload launch failed");
-    *dev = (const SdfTabK*)ctx->sdfk.p;
+    if ((rc = launch_sdf_upload(k, (SdfTabK*)buf.p, s))) return fail(rc, "sdf upload launch failed");
+    *dev = (const SdfTabK*)buf.p;
     return RTM_OK;
 }
 
-int enqueue_frame(rtm_ctx* ctx, FrameArgs& a, const FrameExtra* x, float* out_dev, StatsK* stats) {
+// lane 0: the context's own stream and buffers; lane k > 0: ctx->lanes[k-1]
+int enqueue_frame(rtm_ctx* ctx, FrameArgs& a, const FrameExtra* x, float* out_dev, StatsK* stats, int lane = 0) {
     int rc;
     if ((rc = frame_tables(ctx, a))) return rc;
+    Lane* l = lane > 0 ? ctx->lanes[(size_t)lane - 1].get() : nullptr;
+    hipStream_t s = l ? l->stream : ctx->stream;
     DevTabs tabs{nullptr, nullptr, nullptr};
-    if (x && x->has_rt && (rc = upload_rt(ctx, x->rt, &tabs.rt))) return rc;
-    if (x && x->has_psp && (rc = upload_persp(ctx, x->psp, &tabs.psp))) return rc;
-    if (x && x->has_sdf && (rc = upload_sdf(ctx, x->sdf, &tabs.sdf))) return rc;
+    if (x && x->has_rt && (rc = upload_rt(ctx, l ? l->rtk : ctx->rtk, s, x->rt, &tabs.rt))) return rc;
+    if (x && x->has_psp && (rc = upload_persp(ctx, l ? l->pspk : ctx->pspk, s, x->psp, &tabs.psp))) return rc;
+    if (x && x->has_sdf && (rc = upload_sdf(ctx, l ? l->sdfk : ctx->sdfk, s, x->sdf, &tabs.sdf))) return rc;
     const bool fused = (a.ey.flags & RTM_FLAG_FUSED_SHADOW) != 0;
-    hipStream_t s = ctx->stream;
     double* smap = nullptr;
     TimingSlot* slot = next_slot(ctx);
     if (!fused) {
-        if ((rc = ctx->smap.ensure(sizeof(double) * (size_t)a.sh.W * (size_t)a.sh.H, ctx->device))) return rc;
-        smap = (double*)ctx->smap.p;
+        DevBuf& sb = l ? l->smap : ctx->smap;
+        if ((rc = sb.ensure(sizeof(double) * (size_t)a.sh.W * (size_t)a.sh.H, ctx->device))) return rc;
+        smap = (double*)sb.p;
         ctx->smap_w = a.sh.W;
         ctx->smap_h = a.sh.H;
         if (slot) HIP_TRY(hipEventRecord(slot->ev[0], s));
@@ -875,6 +892,50 @@ int enqueue_frame(rtm_ctx* ctx, FrameArgs& a, const FrameExtra* x, float* out_de
         HIP_TRY(hipEventRecord(slot->ev[3], s));
         slot->shadow = !fused;
         ctx->renders++;
+    }
+    return RTM_OK;
+}
+
+// How many lanes a frame sequence spreads over.  Frames are independent (own
+// scene, own shadow map, own output), so frame i can run beside frame i+1: at
+// 3840x2160 one frame's two kernels leave the chip part-empty in their ramp and
+// tail (the shadow pass is latency-bound), and 3 lanes take config 3 from ~40 to
+// ~34 us per frame; at 7680x4320 the passes are long and store-bound and
+// lanes only add cache pressure (2 lanes: 133 -> 157 us), hence the size
+// limit (tools/probes/two_ctx.py).  RTM_LANES=n overrides.
+// Frame i goes to lane (n-1-i) % L, so the last frame runs on lane 0 and the
+// context's shadow map holds its shadow pass, as on one lane.  Lanes stay at 1
+// when two frames of different lanes write overlapping output.
+int frame_lanes(int32_t req, int32_t n, int32_t W, int32_t H, float* const* out) {
+    static const int env = [] {
+        const char* e = getenv("RTM_LANES");
+        return e ? atoi(e) : 0;
+    }();
+    int L = req > 0 ? req : env > 0 ? env : ((int64_t)W * H <= 3840LL * 2160 ? 3 : 1);
+    if (L > 8) L = 8;
+    if (L > n) L = n;
+    if (L <= 1) return 1;
+    const uintptr_t bytes = (uintptr_t)W * (uintptr_t)H * 4u * sizeof(float);
+    std::vector<std::pair<uintptr_t, int>> r((size_t)n);
+    for (int32_t i = 0; i < n; ++i) r[(size_t)i] = {(uintptr_t)out[i], (n - 1 - i) % L};
+    std::sort(r.begin(), r.end());
+    // equal-length ranges: any two overlapping ranges are joined by a chain of
+    // overlapping sorted neighbours, so checking neighbours checks every pair
+    for (size_t i = 1; i < r.size(); ++i)
+        if (r[i].first < r[i - 1].first + bytes && r[i].second != r[i - 1].second) return 1;
+    return L;
+}
+
+int ensure_lanes(rtm_ctx* ctx, int L) {
+    if (!ctx->fork) HIP_TRY(hipEventCreateWithFlags(&ctx->fork, hipEventDisableTiming));
+    while ((int)ctx->lanes.size() < L - 1) {
+        std::unique_ptr<Lane> l(new Lane);
+        HIP_TRY(hipStreamCreateWithFlags(&l->stream, hipStreamNonBlocking));
+        if (hipEventCreateWithFlags(&l->done, hipEventDisableTiming) != hipSuccess) {
+            (void)hipStreamDestroy(l->stream);
+            return fail(RTM_ERR_HIP, "hipEventCreateWithFlags failed");
+        }
+        ctx->lanes.push_back(std::move(l));
     }
     return RTM_OK;
 }
@@ -941,6 +1002,13 @@ void rtm_ctx_destroy(rtm_ctx* ctx) {
     {
         DeviceGuard g(ctx->device);
         if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+        for (auto& l : ctx->lanes) {
+            (void)hipStreamSynchronize(l->stream);
+            if (l->done) (void)hipEventDestroy(l->done);
+            (void)hipStreamDestroy(l->stream);
+        }
+        ctx->lanes.clear();
+        if (ctx->fork) (void)hipEventDestroy(ctx->fork);
         for (auto& sl : ctx->ring)
             for (auto& e : sl.ev)
                 if (e) (void)hipEventDestroy(e);
@@ -980,6 +1048,18 @@ int rtm_ctx_set_timing_stride(rtm_ctx* ctx, int32_t stride) {
     if (!ctx || stride < 1) return fail(RTM_ERR_INVALID, "ctx NULL or stride %d < 1", stride);
     ctx->stride = stride;
     ctx->calls = 0;
+    return RTM_OK;
+}
+
+int rtm_ctx_set_lanes(rtm_ctx* ctx, int32_t lanes) {
+    if (!ctx || lanes < 0 || lanes > 8) return fail(RTM_ERR_INVALID, "ctx NULL or lanes %d outside [0,8]", lanes);
+    ctx->lanes_req = lanes;
+    return RTM_OK;
+}
+
+int rtm_ctx_last_lanes(rtm_ctx* ctx, int32_t* lanes) {
+    if (!ctx || !lanes) return fail(RTM_ERR_INVALID, "bad arguments");
+    *lanes = ctx->lanes_last;
     return RTM_OK;
 }
 
@@ -1051,16 +1131,31 @@ int rtm_render_frames_async(rtm_ctx* ctx, int32_t n_frames, const rtm_scene* sce
         // so the GPU starts on frame 0 while the host prepares frame 1 (building all
         // frames first left the GPU idle for the whole build)
         DeviceGuard g(ctx->device);
-        for (int32_t i = 0; i < n_frames; ++i) {
+        const int L = frame_lanes(ctx->lanes_req, n_frames, width, height, out_rgba_dev);
+        ctx->lanes_last = L;
+        int rc = RTM_OK;
+        if (L > 1) {  // fork: the lanes start after the context stream's earlier work
+            if ((rc = ensure_lanes(ctx, L))) return rc;
+            HIP_TRY(hipEventRecord(ctx->fork, ctx->stream));
+            for (int k = 1; k < L; ++k) HIP_TRY(hipStreamWaitEvent(ctx->lanes[(size_t)k - 1]->stream, ctx->fork, 0));
+        }
+        for (int32_t i = 0; i < n_frames && !rc; ++i) {
             FrameArgs fa;
             FrameExtra ex1;
-            int rc = build_frame(fa, &scenes[i], eye, shadow, width, height, march_steps, flags);
-            if (rc) return rc;
+            rc = build_frame(fa, &scenes[i], eye, shadow, width, height, march_steps, flags);
+            if (rc) break;
             build_extra(&scenes[i], eye, width, height, ex1);
-            if ((rc = enqueue_frame(ctx, fa, &ex1, out_rgba_dev[i], nullptr))) return rc;
+            rc = enqueue_frame(ctx, fa, &ex1, out_rgba_dev[i], nullptr, (n_frames - 1 - i) % L);
         }
-        return RTM_OK;
+        // join (also after an error, so the context stream still covers what was enqueued)
+        for (int k = 1; k < L; ++k) {
+            Lane& l = *ctx->lanes[(size_t)k - 1];
+            HIP_TRY(hipEventRecord(l.done, l.stream));
+            HIP_TRY(hipStreamWaitEvent(ctx->stream, l.done, 0));
+        }
+        return rc;
     }
+    ctx->lanes_last = 1;
     std::vector<FrameArgs> f((size_t)n_frames);
     std::vector<FrameExtra> ex((size_t)n_frames);
     bool any_rt = false;
@@ -1395,8 +1490,8 @@ int rtm_viewport_process_raytracing_rays(rtm_viewport* vp, const rtm_scene* scen
     a.cam = cam_k(vp->cam);
     a.W = vp->W;
     a.H = vp->H;
-    if (has_rt && (rc = upload_rt(ctx, k, &a.rt))) return rc;
-    if (has_sdf && (rc = upload_sdf(ctx, sk, &a.sdf))) return rc;
+    if (has_rt && (rc = upload_rt(ctx, ctx->rtk, ctx->stream, k, &a.rt))) return rc;
+    if (has_sdf && (rc = upload_sdf(ctx, ctx->sdfk, ctx->stream, sk, &a.sdf))) return rc;
     if ((rc = launch_vp_trace(a, (double*)vp->zbuf.p, (double*)vp->gh.p, (int32_t*)vp->gid.p, (double*)vp->gn.p,
                               ctx->stream)))
         return fail(rc, "trace launch failed");
@@ -1463,11 +1558,11 @@ int rtm_render_color_image(const rtm_scene* scene, const rtm_viewport* vp, const
     RtK k;
     SdfTabK sk;
     if (build_rt(scene, k)) {  // shading lookups circlePlanePrimitives[id] / cappedCylinderPrimitives[id]
-        if ((rc = upload_rt(ctx, k, &a.rt))) return rc;
+        if ((rc = upload_rt(ctx, ctx->rtk, ctx->stream, k, &a.rt))) return rc;
         a.gn = (const double*)vp->gn.p;
     }
     if (build_sdf(scene, sk)) {  // ... and the SDF colours (row f-4)
-        if ((rc = upload_sdf(ctx, sk, &a.sdf))) return rc;
+        if ((rc = upload_sdf(ctx, ctx->sdfk, ctx->stream, sk, &a.sdf))) return rc;
         a.gn = (const double*)vp->gn.p;
     }
     if ((rc = launch_vp_shade(a, (const double*)shadow_vp->zbuf.p, (const double*)vp->gh.p, (const double*)vp->gz.p,

@@ -65,6 +65,17 @@ class Context:
         lib = _lib()
         abi.check(lib, lib.rtm_ctx_set_timing_stride(self._h, n), "rtm_ctx_set_timing_stride")
 
+    def set_lanes(self, n: int):
+        """Lanes of render_frames_async (0 = auto, 1 = one frame after another)."""
+        lib = _lib()
+        abi.check(lib, lib.rtm_ctx_set_lanes(self._h, n), "rtm_ctx_set_lanes")
+
+    def last_lanes(self) -> int:
+        n = C.c_int32()
+        lib = _lib()
+        abi.check(lib, lib.rtm_ctx_last_lanes(self._h, C.byref(n)), "rtm_ctx_last_lanes")
+        return int(n.value)
+
     def kernel_ms_history(self, n: int):
         """Per-render (shadow_pass_ms, eye_pass_ms) from HIP events, oldest first."""
         sm = (C.c_float * max(n, 1))()

@@ -35,8 +35,10 @@ METRIC_F4 = "Mpixels/s, sphere-traced GL-preview SDFs (row f-4)"
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)
-    ap.add_argument("--warmup", type=int, default=20)
+    # 2000 frames x ~35 us: the timed region is ~70 ms; 500 warmup frames bring the
+    # clocks up (200/20 measured 188 Gpix/s where 2000/500 measured 203, same kernels)
+    ap.add_argument("--steps", type=int, default=2000)
+    ap.add_argument("--warmup", type=int, default=500)
     ap.add_argument("--config", type=int, default=3, help="scenes.CONFIGS id: 1-5 BASELINE, 6-7 row f-1, 8 row f-4")
     ap.add_argument("--mode", choices=["frames", "tile-gather"], default="frames")
     ap.add_argument("--fused", action="store_true", help="evaluate shadow texels on demand (same image)")
@@ -45,6 +47,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=1)
     ap.add_argument("--no-alt", action="store_true", help="skip the secondary fused-shadow measurement")
+    ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
+                    help="nccl (= RCCL, the multi-GPU run); gloo only to rehearse the N>1 frames path "
+                         "with several ranks on one GPU (timing tensors on the CPU)")
     return ap.parse_args()
 
 
@@ -114,9 +119,16 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one rank per GPU; a rehearsal with more ranks than GPUs (gloo) shares them round-robin
+    local = local % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if a.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            assert a.mode == "frames", "gloo rehearsal covers the frames mode only"
+            dist.init_process_group("gloo")
+    tdev = f"cuda:{local}" if a.dist_backend == "nccl" else "cpu"  # where the timing reductions run
 
     rtm = importlib.import_module("2018rustraytracer_amd")
     sc = importlib.import_module("2018rustraytracer_amd.scenes")
@@ -146,7 +158,11 @@ def main():
         # inputs prepared before the timed region: one scene per frame this rank renders
         scenes = [scene_for(i * world + rank) for i in range(total)]
         c_scenes = [s.to_c() for s in scenes]
-        out = torch.empty((H, W, 4), dtype=torch.float32, device=f"cuda:{local}")
+        # a ring of output frames (a renderer's swap chain): consecutive frames write
+        # different buffers, so the library may run them side by side (rtm_api.cpp
+        # frame_lanes); 12 covers any lane count 1-4 without two lanes sharing one
+        ring = [torch.empty((H, W, 4), dtype=torch.float32, device=f"cuda:{local}") for _ in range(12)]
+        out = ring[0]
         rows = (0, H)
     else:
         band = shard.band_rows(H, world)
@@ -191,7 +207,7 @@ def main():
         # frames (two kernels per frame; with RTM_PIPELINE=1 the software-pipelined launch)
         warm = ctx.prepare_frames(scenes[:a.warmup])
         timed = ctx.prepare_frames(scenes[a.warmup:])
-        outp = [out.data_ptr()] * max(a.warmup, a.steps)
+        outp = [ring[i % len(ring)].data_ptr() for i in range(max(a.warmup, a.steps))]
 
     if sequence:
         if a.warmup:
@@ -213,13 +229,43 @@ def main():
     barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
+        t = torch.tensor([elapsed], dtype=torch.float64, device=tdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
     # per-kernel HIP-event durations over the timed region (ctx stream)
     n_launches = a.steps + 1 if pipelined else a.steps
     sh_ms, eye_ms = ctx.kernel_ms_history((n_launches + timing_stride - 1) // timing_stride)
+
+    # With several lanes (rtm_ctx_set_lanes: independent frames on side-by-side
+    # streams) the kernels of the timed region overlap, and each event duration is
+    # a kernel's time BESIDE other frames' kernels.  The kernel roofline is taken
+    # from a one-lane pass over the same frames right after it (each kernel alone on
+    # the chip); the headline value stays the timed region's.
+    lanes = ctx.last_lanes() if sequence else 1
+    in_lanes, one_lane = None, None
+    if lanes > 1:
+        avg = lambda v: sum(v) / max(len(v), 1)
+        in_lanes = {"lanes": lanes, "shadow_pass_ms": round(avg(sh_ms), 5), "eye_pass_ms": round(avg(eye_ms), 5),
+                    "note": "HIP-event kernel durations in the timed region, kernels of other lanes alongside"}
+        n1 = min(a.steps, 400)
+        ctx.set_lanes(1)
+        ctx.render_frames_async([0] * min(a.warmup, 50), eye, shadow, W, H, K, flags, outp[:min(a.warmup, 50)],
+                                ctx.prepare_frames(scenes[:min(a.warmup, 50)]))
+        ctx.set_timing_capacity(max(1, n1 // timing_stride))
+        one = ctx.prepare_frames(scenes[a.warmup:a.warmup + n1])
+        barrier()
+        ctx.set_timing_stride(timing_stride)
+        t1 = time.perf_counter()
+        ctx.render_frames_async([0] * n1, eye, shadow, W, H, K, flags, outp[:n1], one)
+        barrier()
+        el1 = time.perf_counter() - t1
+        sh_ms, eye_ms = ctx.kernel_ms_history((n1 + timing_stride - 1) // timing_stride)
+        ctx.set_lanes(0)
+        one_lane = {"value": round(W * H * n1 / el1 / 1e6, 2), "unit": "Mpixels/s", "frames": n1,
+                    "ms_per_step": round(el1 / n1 * 1e3, 5),
+                    "note": "same frames, one lane (one frame after another): the per-kernel durations "
+                            "of `kernels` and `roofline` come from this pass"}
 
     # Secondary measurement, same run and frames (not the headline value): the
     # fused-shadow frame (RTM_FLAG_FUSED_SHADOW), which evaluates only the shadow
@@ -237,7 +283,7 @@ def main():
         barrier()
         el_f = time.perf_counter() - t1
         if world > 1:
-            t = torch.tensor([el_f], dtype=torch.float64, device=f"cuda:{local}")
+            t = torch.tensor([el_f], dtype=torch.float64, device=tdev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             el_f = float(t.item())
         alt_fused = {"value": round(W * H * a.steps * world / el_f / 1e6, 2), "unit": "Mpixels/s",
@@ -274,6 +320,13 @@ def main():
             for kk in work.values():
                 kk["ops"] = int(kk["ops"] * band_h / H)
                 kk["bytes"] = int(kk["bytes"] * band_h / H)
+        # the whole frame (both passes' algorithmic bytes) over the headline time per frame
+        passes = [work[k] for k in ("shadow_pass", "eye_pass") if k in work]
+        work["frame"] = {"ops": sum(w["ops"] for w in passes), "bytes": sum(w["bytes"] for w in passes)}
+        roof_frame = dict(metrics.roofline("frame", work, elapsed / a.steps * 1e3))  # per GPU
+        roof_frame.pop("traffic", None)
+        roof_frame["note"] = ("both passes' algorithmic bytes per frame / wall time per frame of the timed region"
+                              + (f" ({lanes} lanes)" if lanes > 1 else ""))
         if pipelined:
             dom, dom_ms = "frame_pipe", pipe_ms
             roof = metrics.roofline(dom, work, dom_ms, _latest_traffic(a.config, dom))
@@ -315,6 +368,10 @@ def main():
                          "frame_kernel_ms": round(avg_sh + avg_eye, 5)}),
             "roofline": roof,
             "roofline_other_kernel": roof_other,
+            "roofline_frame": roof_frame,
+            "lanes": lanes,
+            "kernels_in_lanes": in_lanes,
+            "one_lane": one_lane,
             "alt_fused_shadow": alt_fused,
             "parity": ("bit-exact vs CPU oracle (tests/test_gpu_parity.py)" if a.config <= 5
                        else "bit-exact vs CPU oracle (tests/test_raytrace.py)"),

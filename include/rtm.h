@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define RTM_ABI_VERSION 4
+#define RTM_ABI_VERSION 5
 
 /* ---- limits: scene constants travel as kernel arguments (SGPR path) ---- */
 #define RTM_MAX_SPHERES 16
@@ -211,6 +211,16 @@ int rtm_ctx_set_timing_capacity(rtm_ctx* ctx, int32_t capacity);
 int rtm_ctx_set_timing_stride(rtm_ctx* ctx, int32_t stride);
 int rtm_ctx_kernel_ms_history(rtm_ctx* ctx, float* shadow_pass_ms, float* eye_pass_ms, int32_t max,
                               int32_t* count);
+/* Lanes of rtm_render_frames_async: independent frames spread over `lanes`
+ * streams of the context (own shadow map each), so one frame's kernels run
+ * beside another's; the call still completes in ctx's stream order.  0 = auto
+ * (RTM_LANES from the environment, else 3 up to 3840x2160 frames and 1 above);
+ * 1 = strictly one frame after another; at most 8.  With several lanes the
+ * kernel durations of rtm_ctx_kernel_ms_history overlap (each is the kernel's
+ * time beside the other lanes).  rtm_ctx_last_lanes: lanes the last
+ * rtm_render_frames_async call used. */
+int rtm_ctx_set_lanes(rtm_ctx* ctx, int32_t lanes);
+int rtm_ctx_last_lanes(rtm_ctx* ctx, int32_t* lanes);
 
 /* ---- whole frame, host output (blocking) ----
  * Equivalent of: shadow viewport (ORTHO, face BACK, zBuffer=+INF) rasterize +
@@ -246,7 +256,9 @@ int rtm_render_async(rtm_ctx* ctx, const rtm_scene* scene, const rtm_camera* eye
 /* A sequence of frames (e.g. the animation of testscene_closelyOrbitingSphere,
  * main.rs:1469), asynchronous on ctx's stream: frame i is scenes[i] rendered
  * into out_rgba_dev[i] (full frames; pointers may repeat), two kernels per
- * frame.  With RTM_PIPELINE=1 in the environment and equal patches in every
+ * frame, spread over the context's lanes (rtm_ctx_set_lanes) when no two frames
+ * of different lanes share output memory; the context's shadow map ends up
+ * holding the last frame's shadow pass either way.  With RTM_PIPELINE=1 in the environment and equal patches in every
  * frame the sequence is software-pipelined instead: the shadow pass of frame i
  * and the eye pass of frame i-1 run in ONE launch (double-buffered shadow
  * maps) — correct, but measured slower on MI355X.  Each frame's

@@ -350,6 +350,84 @@ def test_pipelined_frames_differing_patches_fallback(rtm, scenes, gpu_ctx):
     _frames_vs_single(rtm, scenes, gpu_ctx, frames, scenes.eye_camera(), scenes.shadow_camera(), 640, 360, 64)
 
 
+@pytest.mark.parametrize("lanes", [1, 2, 3, 4])
+def test_frame_lanes_in_subprocess(rtm, scenes, lanes):
+    """RTM_LANES=n (read once per process): the frame sequence spread over n
+    streams, each with its own shadow map, == frame-by-frame rtm_render; the
+    context's shadow map then holds the LAST frame's shadow pass; a sequence whose
+    frames share one output falls back to one lane (the last frame's image wins)."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = r'''
+import ctypes, importlib, sys
+import numpy as np, torch
+sys.path.insert(0, %r)
+rtm = importlib.import_module("2018rustraytracer_amd")
+sc = importlib.import_module("2018rustraytracer_amd.scenes")
+eye, sh = sc.eye_camera(), sc.shadow_camera()
+ctx = rtm.Context(0)
+w, h, k = 960, 540, 64
+frames = [sc.scene_a_bench(100 + 5 * i) for i in range(7)] + [sc.scene_b()]
+u32 = lambda a: a.view(np.uint32)
+outs = [torch.empty((h, w, 4), dtype=torch.float32, device="cuda") for _ in frames]
+torch.cuda.synchronize()
+ctx.render_frames_async(frames, eye, sh, w, h, k, 0, [o.data_ptr() for o in outs])
+ctx.synchronize()
+last_map = torch.empty((h, w), dtype=torch.float64, device="cuda")
+hip = ctypes.CDLL("libamdhip64.so")
+hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+assert hip.hipMemcpy(last_map.data_ptr(), ctx.shadow_map_ptr(), h * w * 8, 3) == 0
+for s, o in zip(frames, outs):
+    assert np.array_equal(u32(o.cpu().numpy()), u32(rtm.render_frame(s, eye, sh, w, h, k, 0)))
+one = rtm.Context(0)
+one.render_async(frames[-1], eye, sh, w, h, k, 0, outs[0].data_ptr())
+one.synchronize()
+want_map = torch.empty_like(last_map)
+assert hip.hipMemcpy(want_map.data_ptr(), one.shadow_map_ptr(), h * w * 8, 3) == 0
+assert torch.equal(last_map.view(torch.int64), want_map.view(torch.int64))
+shared = torch.empty((h, w, 4), dtype=torch.float32, device="cuda")
+torch.cuda.synchronize()
+ctx.render_frames_async(frames, eye, sh, w, h, k, 0, [shared.data_ptr()] * len(frames))
+ctx.synchronize()
+assert np.array_equal(u32(shared.cpu().numpy()), u32(rtm.render_frame(frames[-1], eye, sh, w, h, k, 0)))
+print("lanes ok")
+''' % root
+    env = dict(os.environ, RTM_LANES=str(lanes))
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0 and "lanes ok" in r.stdout, r.stdout + r.stderr
+
+
+def test_set_lanes_api(rtm, scenes, gpu_ctx):
+    """rtm_ctx_set_lanes / rtm_ctx_last_lanes: range check, the requested count, the
+    fallback to one lane for shared outputs, and frame-by-frame parity at 2 lanes."""
+    import torch
+    abi = rtm.abi
+    for bad in (-1, 9):
+        with pytest.raises(abi.RtmError) as e:
+            gpu_ctx.set_lanes(bad)
+        assert e.value.code == abi.RTM_ERR_INVALID
+    w, h, k = 320, 200, 48
+    frames = [scenes.scene_a_bench(100 + i) for i in range(3)]
+    outs = [torch.empty((h, w, 4), dtype=torch.float32, device="cuda") for _ in frames]
+    try:
+        gpu_ctx.set_lanes(2)
+        _frames_vs_single(rtm, scenes, gpu_ctx, frames, scenes.eye_camera(), scenes.shadow_camera(), w, h, k)
+        assert gpu_ctx.last_lanes() == 2
+        torch.cuda.synchronize()
+        gpu_ctx.render_frames_async(frames, scenes.eye_camera(), scenes.shadow_camera(), w, h, k, 0,
+                                    [outs[0].data_ptr()] * 3)
+        gpu_ctx.synchronize()
+        assert gpu_ctx.last_lanes() == 1
+        gpu_ctx.set_lanes(8)  # more lanes than frames: one frame per lane
+        gpu_ctx.render_frames_async(frames, scenes.eye_camera(), scenes.shadow_camera(), w, h, k, 0,
+                                    [o.data_ptr() for o in outs])
+        gpu_ctx.synchronize()
+        assert gpu_ctx.last_lanes() == 3
+    finally:
+        gpu_ctx.set_lanes(0)
+
+
 def test_pipelined_frames_scene_b_8k(rtm, oracle, scenes, gpu_ctx):
     """BASELINE config 5 geometry through the pipelined path, against the oracle."""
     import torch

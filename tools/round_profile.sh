@@ -6,7 +6,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 ROOT=$(pwd)
-TAG=${TAG:-r01_v13}
+TAG=${TAG:-r01_v14}
 OUT=$ROOT/gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
@@ -31,6 +31,7 @@ step bench6 300 python bench.py --config 6 --no-alt
 step bench7 300 python bench.py --config 7 --no-alt --no-cpu-baseline
 step bench8 300 python bench.py --config 8 --no-alt
 step prof3 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof3" -o run --output-format csv -- python3 "$ROOT/bench.py" --steps 200 --warmup 20 --no-cpu-baseline --no-alt
+RTM_LANES=1 step prof3_one_lane 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof3_one_lane" -o run --output-format csv -- python3 "$ROOT/bench.py" --steps 200 --warmup 20 --no-cpu-baseline --no-alt
 step prof4 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof4" -o run --output-format csv -- python3 "$ROOT/bench.py" --config 4 --steps 100 --warmup 10 --no-cpu-baseline --no-alt
 step prof6 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof6" -o run --output-format csv -- python3 "$ROOT/bench.py" --config 6 --steps 200 --warmup 20 --no-cpu-baseline --no-alt
 step prof8 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof8" -o run --output-format csv -- python3 "$ROOT/bench.py" --config 8 --steps 100 --warmup 10 --no-cpu-baseline --no-alt
