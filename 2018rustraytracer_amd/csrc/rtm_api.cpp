@@ -902,7 +902,9 @@ int enqueue_frame(rtm_ctx* ctx, FrameArgs& a, const FrameExtra* x, float* out_de
 // tail (the shadow pass is latency-bound), and 3 lanes take config 3 from ~40 to
 // ~34 us per frame; at 7680x4320 the passes are long and store-bound and
 // lanes only add cache pressure (2 lanes: 133 -> 157 us), hence the size
-// limit (tools/probes/two_ctx.py).  RTM_LANES=n overrides.
+// limit; below 1 Mpixel the host's launch rate is the limit and switching
+// streams costs more than the overlap gains (512x512: 19.2 -> 14.2 Gpix/s with
+// 3 lanes) (tools/probes/two_ctx.py).  RTM_LANES=n overrides.
 // Frame i goes to lane (n-1-i) % L, so the last frame runs on lane 0 and the
 // context's shadow map holds its shadow pass, as on one lane.  Lanes stay at 1
 // when two frames of different lanes write overlapping output.
@@ -911,7 +913,8 @@ int frame_lanes(int32_t req, int32_t n, int32_t W, int32_t H, float* const* out)
         const char* e = getenv("RTM_LANES");
         return e ? atoi(e) : 0;
     }();
-    int L = req > 0 ? req : env > 0 ? env : ((int64_t)W * H <= 3840LL * 2160 ? 3 : 1);
+    const int64_t px = (int64_t)W * H;
+    int L = req > 0 ? req : env > 0 ? env : (px >= (1LL << 20) && px <= 3840LL * 2160 ? 3 : 1);
     if (L > 8) L = 8;
     if (L > n) L = n;
     if (L <= 1) return 1;
