@@ -12,5 +12,5 @@ from .abi import RtmError, load_library  # noqa: F401
 from .scenes import (Bilinear, Camera, EnumFace, Linear, PrimitiveCappedCylinder, PrimitiveCirclePlane,  # noqa: F401
                      PrimitiveSdf, PrimitiveSphere, Scene, Shading, eye_camera, perspective_eye_camera,
                      shadow_camera)
-from .renderer import (Context, Viewport, device_count, encode_thresholds, renderColorImage,  # noqa: F401
-                       render_frame, render_frame_multi, writeColorImage)
+from .renderer import (Context, Group, HostRegistration, Viewport, device_count, encode_thresholds,  # noqa: F401
+                       renderColorImage, render_frame, render_frame_ex, render_frame_multi, writeColorImage)

@@ -12,7 +12,7 @@ _PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 # RTM_LIB: another build of the same library (A/B timing runs only, tools/ab_bench.py)
 LIB_PATH = os.environ.get("RTM_LIB") or os.path.join(_PKG_DIR, "librtm.so")
 
-RTM_ABI_VERSION = 5
+RTM_ABI_VERSION = 6
 RTM_MAX_SPHERES = 16
 RTM_MAX_PATCHES = 4
 RTM_MAX_CIRCLE_PLANES = 16
@@ -26,6 +26,7 @@ RTM_ERR_UNSUPPORTED = -2
 RTM_ERR_HIP = -3
 RTM_ERR_NO_DEVICE = -4
 RTM_ERR_OOM = -5
+RTM_ERR_COMM = -6
 
 RTM_CAMERA_ORTHOGONAL = 0
 RTM_CAMERA_PERSPECTIVE = 1
@@ -35,6 +36,12 @@ RTM_FACE_BACK = 1
 RTM_FLAG_NO_MARCH = 0x1
 RTM_FLAG_NO_SHADOW_RASTER = 0x2
 RTM_FLAG_FUSED_SHADOW = 0x4
+
+# frame output formats (ABI v6): RGBA f32 / writeColorImage bytes + alpha 255 / packed RGB8
+RTM_FORMAT_RGBA32F = 0
+RTM_FORMAT_RGBA8 = 1
+RTM_FORMAT_RGB8 = 2
+FORMAT_BYTES = {RTM_FORMAT_RGBA32F: 16, RTM_FORMAT_RGBA8: 4, RTM_FORMAT_RGB8: 3}
 
 
 class rtm_sphere(C.Structure):
@@ -134,6 +141,25 @@ ABI_SYMBOLS = [
     ("rtm_ppm_max_bytes", C.c_int64, [_I32, _I32]),
     ("rtm_write_ppm", C.c_int, [_P, _P, _I32, _I32, C.c_char_p, C.c_int64, C.POINTER(C.c_int64)]),
     ("rtm_encode_thresholds", C.c_int, [C.POINTER(C.c_float)]),
+    ("rtm_render_ex", C.c_int, [C.POINTER(rtm_scene), C.POINTER(rtm_camera), C.POINTER(rtm_camera),
+                                _I32, _I32, _I32, _I32, _I32, _P]),
+    ("rtm_render_multi_ex", C.c_int, [C.POINTER(rtm_scene), C.POINTER(rtm_camera), C.POINTER(rtm_camera),
+                                      _I32, _I32, _I32, _I32, _I32, _P, _I32]),
+    ("rtm_format_bytes", C.c_int32, [_I32]),
+    ("rtm_host_register", C.c_int, [_P, C.c_int64]),
+    ("rtm_host_unregister", C.c_int, [_P]),
+    ("rtm_render_rows_async", C.c_int, [_P, C.POINTER(rtm_scene), C.POINTER(rtm_camera),
+                                        C.POINTER(rtm_camera), _I32, _I32, _I32, _I32, _I32, _I32, _I32, _P]),
+    ("rtm_group_unique_id", C.c_int, [C.POINTER(C.c_uint8)]),
+    ("rtm_group_create", C.c_int, [_I32, C.POINTER(_I32), C.POINTER(_P)]),
+    ("rtm_group_create_rank", C.c_int, [_I32, _I32, _I32, C.POINTER(C.c_uint8), C.POINTER(_P)]),
+    ("rtm_group_destroy", None, [_P]),
+    ("rtm_group_info", C.c_int, [_P, C.POINTER(_I32), C.POINTER(_I32), C.POINTER(_I32)]),
+    ("rtm_group_ctx", _P, [_P, _I32]),
+    ("rtm_group_render_async", C.c_int, [_P, C.POINTER(rtm_scene), C.POINTER(rtm_camera),
+                                         C.POINTER(rtm_camera), _I32, _I32, _I32, _I32, _I32, _I32, _P]),
+    ("rtm_group_synchronize", C.c_int, [_P, _I32]),
+    ("rtm_group_set_root_staging", C.c_int, [_P, _I32]),
     ("rtm_viewport_create", C.c_int, [_P, _I32, _I32, _I32, C.POINTER(rtm_camera), C.POINTER(_P)]),
     ("rtm_viewport_destroy", None, [_P]),
     ("rtm_viewport_rasterize", C.c_int, [_P, C.POINTER(rtm_scene)]),

@@ -14,9 +14,11 @@
 #include <cstring>
 #include <memory>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "rtm_encode.h"
+#include "rtm_internal.h"
 #include "rtm_kernels.h"
 
 #pragma clang fp contract(off)
@@ -833,6 +835,41 @@ TimingSlot* next_slot(rtm_ctx* ctx) {
     return timed ? &ctx->ring[(size_t)(ctx->renders % (int64_t)ctx->ring.size())] : nullptr;
 }
 
+int enc_tab_dev(rtm_ctx* ctx, const void** out);
+
+int32_t format_bytes(int32_t fmt) {
+    return fmt == RTM_FORMAT_RGBA32F ? 16 : fmt == RTM_FORMAT_RGBA8 ? 4 : fmt == RTM_FORMAT_RGB8 ? 3 : 0;
+}
+
+int validate_format(int32_t fmt, const void* out) {
+    if (!format_bytes(fmt)) return fail(RTM_ERR_INVALID, "unknown output format %d", fmt);
+    if (fmt == RTM_FORMAT_RGBA32F && ((uintptr_t)out & 15))
+        return fail(RTM_ERR_INVALID, "RGBA32F output must be 16-byte aligned");
+    return RTM_OK;
+}
+
+// The background pixel (0.0, 0.2, 0.2) (main.rs:718-720) through writeColorImage's
+// encode (main.rs:674-684), R | G<<8 | B<<16: the eye epilogue stores it without a lookup.
+uint32_t background_bytes() {
+    static const uint32_t v = (uint32_t)enc_byte(0.0f) | ((uint32_t)enc_byte(0.2f) << 8) |
+                              ((uint32_t)enc_byte(0.2f) << 16);
+    return v;
+}
+
+// The eye pass's output format: the encode table and background for RGBA8/RGB8,
+// and whether RGB8 rows start 4-byte aligned (W % 4 == 0, aligned base: dword stores).
+int format_tabs(rtm_ctx* ctx, int32_t fmt, int32_t W, const void* out, DevTabs& t) {
+    t.fmt = fmt;
+    t.enc = nullptr;
+    t.bg = 0u;
+    if (fmt == RTM_FORMAT_RGBA32F) return RTM_OK;
+    int rc = enc_tab_dev(ctx, &t.enc);
+    if (rc) return rc;
+    t.bg = background_bytes();
+    if (fmt == RTM_FORMAT_RGB8 && W % 4 == 0 && ((uintptr_t)out & 3) == 0) t.fmt |= FMT_RGB8_DWORDS;
+    return RTM_OK;
+}
+
 // The frame's ray-traced primitives into the lane's rtk (stream-ordered; the
 // lane's previous frame has consumed the old contents by the time the upload runs).
 int upload_rt(rtm_ctx* ctx, DevBuf& buf, hipStream_t s, const RtK& rt, const RtK** dev) {
@@ -860,12 +897,14 @@ int upload_sdf(rtm_ctx* ctx, DevBuf& buf, hipStream_t s, const SdfTabK& k, const
 }
 
 // lane 0: the context's own stream and buffers; lane k > 0: ctx->lanes[k-1]
-int enqueue_frame(rtm_ctx* ctx, FrameArgs& a, const FrameExtra* x, float* out_dev, StatsK* stats, int lane = 0) {
+int enqueue_frame(rtm_ctx* ctx, FrameArgs& a, const FrameExtra* x, void* out_dev, StatsK* stats, int lane = 0,
+                  int32_t fmt = RTM_FORMAT_RGBA32F) {
     int rc;
     if ((rc = frame_tables(ctx, a))) return rc;
     Lane* l = lane > 0 ? ctx->lanes[(size_t)lane - 1].get() : nullptr;
     hipStream_t s = l ? l->stream : ctx->stream;
-    DevTabs tabs{nullptr, nullptr, nullptr};
+    DevTabs tabs{};
+    if ((rc = format_tabs(ctx, fmt, a.ey.W, out_dev, tabs))) return rc;
     if (x && x->has_rt && (rc = upload_rt(ctx, l ? l->rtk : ctx->rtk, s, x->rt, &tabs.rt))) return rc;
     if (x && x->has_psp && (rc = upload_persp(ctx, l ? l->pspk : ctx->pspk, s, x->psp, &tabs.psp))) return rc;
     if (x && x->has_sdf && (rc = upload_sdf(ctx, l ? l->sdfk : ctx->sdfk, s, x->sdf, &tabs.sdf))) return rc;
@@ -1099,19 +1138,8 @@ int rtm_ctx_last_kernel_ms(rtm_ctx* ctx, float* shadow_ms, float* eye_ms) {
 int rtm_render_async(rtm_ctx* ctx, const rtm_scene* scene, const rtm_camera* eye, const rtm_camera* shadow,
                      int32_t width, int32_t height, int32_t march_steps, int32_t flags, int32_t row_begin,
                      int32_t row_end, float* out_rgba_dev) {
-    if (!ctx) return fail(RTM_ERR_INVALID, "ctx is NULL");
-    if (!out_rgba_dev) return fail(RTM_ERR_INVALID, "out_rgba_dev is NULL");
-    FrameArgs a;
-    int rc = build_frame(a, scene, eye, shadow, width, height, march_steps, flags);
-    if (rc) return rc;
-    if (row_begin < 0 || row_end > height || row_begin >= row_end)
-        return fail(RTM_ERR_INVALID, "row range [%d,%d) outside [0,%d)", row_begin, row_end, height);
-    a.ey.row_begin = row_begin;
-    a.ey.row_end = row_end;
-    FrameExtra x;
-    build_extra(scene, eye, width, height, x);
-    DeviceGuard g(ctx->device);
-    return enqueue_frame(ctx, a, &x, out_rgba_dev, nullptr);
+    return rtm_render_rows_async(ctx, scene, eye, shadow, width, height, march_steps, flags, RTM_FORMAT_RGBA32F,
+                                 row_begin, row_end, out_rgba_dev);
 }
 
 const double* rtm_ctx_shadow_map(rtm_ctx* ctx) {
@@ -1134,14 +1162,14 @@ int rtm_render_frames_async(rtm_ctx* ctx, int32_t n_frames, const rtm_scene* sce
         // so the GPU starts on frame 0 while the host prepares frame 1 (building all
         // frames first left the GPU idle for the whole build)
         DeviceGuard g(ctx->device);
-        const int L = frame_lanes(ctx->lanes_req, n_frames, width, height, out_rgba_dev);
-        ctx->lanes_last = L;
+        int L = frame_lanes(ctx->lanes_req, n_frames, width, height, out_rgba_dev);
         int rc = RTM_OK;
         if (L > 1) {  // fork: the lanes start after the context stream's earlier work
             if ((rc = ensure_lanes(ctx, L))) return rc;
             HIP_TRY(hipEventRecord(ctx->fork, ctx->stream));
             for (int k = 1; k < L; ++k) HIP_TRY(hipStreamWaitEvent(ctx->lanes[(size_t)k - 1]->stream, ctx->fork, 0));
         }
+        ctx->lanes_last = L;
         for (int32_t i = 0; i < n_frames && !rc; ++i) {
             FrameArgs fa;
             FrameExtra ex1;
@@ -1150,13 +1178,21 @@ int rtm_render_frames_async(rtm_ctx* ctx, int32_t n_frames, const rtm_scene* sce
             build_extra(&scenes[i], eye, width, height, ex1);
             rc = enqueue_frame(ctx, fa, &ex1, out_rgba_dev[i], nullptr, (n_frames - 1 - i) % L);
         }
-        // join (also after an error, so the context stream still covers what was enqueued)
+        // join every lane (also after an error, so the context stream still covers what
+        // was enqueued); the first error, of the frames or of a join, is returned
+        const std::string frame_err = rc ? g_last_error : std::string();
+        int join_rc = RTM_OK;
         for (int k = 1; k < L; ++k) {
             Lane& l = *ctx->lanes[(size_t)k - 1];
-            HIP_TRY(hipEventRecord(l.done, l.stream));
-            HIP_TRY(hipStreamWaitEvent(ctx->stream, l.done, 0));
+            hipError_t e = hipEventRecord(l.done, l.stream);
+            if (e == hipSuccess) e = hipStreamWaitEvent(ctx->stream, l.done, 0);
+            if (e != hipSuccess && !join_rc) join_rc = fail(RTM_ERR_HIP, "lane %d join: %s", k, hipGetErrorString(e));
         }
-        return rc;
+        if (rc) {
+            g_last_error = frame_err;
+            return rc;
+        }
+        return join_rc;
     }
     ctx->lanes_last = 1;
     std::vector<FrameArgs> f((size_t)n_frames);
@@ -1247,9 +1283,44 @@ int rtm_render_frames_async(rtm_ctx* ctx, int32_t n_frames, const rtm_scene* sce
     return RTM_OK;
 }
 
-int rtm_render(const rtm_scene* scene, const rtm_camera* eye, const rtm_camera* shadow, int32_t width,
-               int32_t height, int32_t march_steps, int32_t flags, float* out_rgba) {
-    if (!out_rgba) return fail(RTM_ERR_INVALID, "out_rgba is NULL");
+int32_t rtm_format_bytes(int32_t format) { return format_bytes(format); }
+
+int rtm_host_register(void* ptr, int64_t bytes) {
+    if (!ptr || bytes <= 0) return fail(RTM_ERR_INVALID, "bad host buffer");
+    if (rtm_device_count() <= 0) return fail(RTM_ERR_NO_DEVICE, "no HIP device visible");
+    HIP_TRY(hipHostRegister(ptr, (size_t)bytes, hipHostRegisterPortable));
+    return RTM_OK;
+}
+
+int rtm_host_unregister(void* ptr) {
+    if (!ptr) return fail(RTM_ERR_INVALID, "ptr is NULL");
+    HIP_TRY(hipHostUnregister(ptr));
+    return RTM_OK;
+}
+
+int rtm_render_rows_async(rtm_ctx* ctx, const rtm_scene* scene, const rtm_camera* eye, const rtm_camera* shadow,
+                          int32_t width, int32_t height, int32_t march_steps, int32_t flags, int32_t format,
+                          int32_t row_begin, int32_t row_end, void* out_dev) {
+    if (!ctx) return fail(RTM_ERR_INVALID, "ctx is NULL");
+    if (!out_dev) return fail(RTM_ERR_INVALID, "out_dev is NULL");
+    int rc = validate_format(format, out_dev);
+    if (rc) return rc;
+    FrameArgs a;
+    if ((rc = build_frame(a, scene, eye, shadow, width, height, march_steps, flags))) return rc;
+    if (row_begin < 0 || row_end > height || row_begin >= row_end)
+        return fail(RTM_ERR_INVALID, "row range [%d,%d) outside [0,%d)", row_begin, row_end, height);
+    a.ey.row_begin = row_begin;
+    a.ey.row_end = row_end;
+    FrameExtra x;
+    build_extra(scene, eye, width, height, x);
+    DeviceGuard g(ctx->device);
+    return enqueue_frame(ctx, a, &x, out_dev, nullptr, 0, format);
+}
+
+int rtm_render_ex(const rtm_scene* scene, const rtm_camera* eye, const rtm_camera* shadow, int32_t width,
+                  int32_t height, int32_t march_steps, int32_t flags, int32_t format, void* out_host) {
+    if (!out_host) return fail(RTM_ERR_INVALID, "out is NULL");
+    if (!format_bytes(format)) return fail(RTM_ERR_INVALID, "unknown output format %d", format);
     FrameArgs a;
     int rc = build_frame(a, scene, eye, shadow, width, height, march_steps, flags);
     if (rc) return rc;
@@ -1258,17 +1329,24 @@ int rtm_render(const rtm_scene* scene, const rtm_camera* eye, const rtm_camera* 
     FrameExtra x;
     build_extra(scene, eye, width, height, x);
     DeviceGuard g(ctx->device);
-    const size_t bytes = sizeof(float) * 4 * (size_t)width * (size_t)height;
+    const size_t bytes = (size_t)format_bytes(format) * (size_t)width * (size_t)height;
     if ((rc = ctx->out.ensure(bytes, ctx->device))) return rc;
-    if ((rc = enqueue_frame(ctx, a, &x, (float*)ctx->out.p, nullptr))) return rc;
-    HIP_TRY(hipMemcpyAsync(out_rgba, ctx->out.p, bytes, hipMemcpyDeviceToHost, ctx->stream));
+    if ((rc = enqueue_frame(ctx, a, &x, ctx->out.p, nullptr, 0, format))) return rc;
+    HIP_TRY(hipMemcpyAsync(out_host, ctx->out.p, bytes, hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(hipStreamSynchronize(ctx->stream));
     return RTM_OK;
 }
 
-int rtm_render_multi(const rtm_scene* scene, const rtm_camera* eye, const rtm_camera* shadow, int32_t width,
-                     int32_t height, int32_t march_steps, int32_t flags, float* out_rgba, int32_t n_gpus) {
-    if (!out_rgba) return fail(RTM_ERR_INVALID, "out_rgba is NULL");
+int rtm_render(const rtm_scene* scene, const rtm_camera* eye, const rtm_camera* shadow, int32_t width,
+               int32_t height, int32_t march_steps, int32_t flags, float* out_rgba) {
+    return rtm_render_ex(scene, eye, shadow, width, height, march_steps, flags, RTM_FORMAT_RGBA32F, out_rgba);
+}
+
+int rtm_render_multi_ex(const rtm_scene* scene, const rtm_camera* eye, const rtm_camera* shadow, int32_t width,
+                        int32_t height, int32_t march_steps, int32_t flags, int32_t format, void* out_host,
+                        int32_t n_gpus) {
+    if (!out_host) return fail(RTM_ERR_INVALID, "out is NULL");
+    if (!format_bytes(format)) return fail(RTM_ERR_INVALID, "unknown output format %d", format);
     const int n_dev = rtm_device_count();
     if (n_dev <= 0) return fail(RTM_ERR_NO_DEVICE, "no HIP device visible");
     if (n_gpus < 1 || n_gpus > n_dev) return fail(RTM_ERR_INVALID, "n_gpus=%d outside [1,%d]", n_gpus, n_dev);
@@ -1283,6 +1361,7 @@ int rtm_render_multi(const rtm_scene* scene, const rtm_camera* eye, const rtm_ca
     FrameExtra x;
     build_extra(scene, eye, width, height, x);
     const int32_t band = (height + n_gpus - 1) / n_gpus;
+    const size_t bpp = (size_t)format_bytes(format);
     std::vector<rtm_ctx*> ctxs((size_t)n_gpus, nullptr);
     for (int d = 0; d < n_gpus; ++d) {
         const int32_t r0 = std::min(height, d * band), r1 = std::min(height, (d + 1) * band);
@@ -1294,25 +1373,48 @@ int rtm_render_multi(const rtm_scene* scene, const rtm_camera* eye, const rtm_ca
         FrameArgs ad = a;
         ad.ey.row_begin = r0;
         ad.ey.row_end = r1;
-        const size_t bytes = sizeof(float) * 4 * (size_t)width * (size_t)(r1 - r0);
+        const size_t bytes = bpp * (size_t)width * (size_t)(r1 - r0);
         if ((rc = ctx->out.ensure(bytes, ctx->device))) return rc;
-        if ((rc = enqueue_frame(ctx, ad, &x, (float*)ctx->out.p, nullptr))) return rc;
+        if ((rc = enqueue_frame(ctx, ad, &x, ctx->out.p, nullptr, 0, format))) return rc;
     }
-    for (int d = 0; d < n_gpus; ++d) {  // the bands' D2H copies, then wait for all devices
+    // The bands' D2H copies, one host thread per device: a pageable copy blocks its
+    // calling thread, so issuing them from one thread would serialise the devices'
+    // PCIe links; into a registered buffer the copies are DMA and return at once.
+    std::vector<int> rcs((size_t)n_gpus, RTM_OK);
+    std::vector<std::string> errs((size_t)n_gpus);
+    auto copy_band = [&](int d) {
         rtm_ctx* ctx = ctxs[(size_t)d];
-        if (!ctx) continue;
         const int32_t r0 = std::min(height, d * band), r1 = std::min(height, (d + 1) * band);
         DeviceGuard g(ctx->device);
-        HIP_TRY(hipMemcpyAsync(out_rgba + (size_t)r0 * (size_t)width * 4, ctx->out.p,
-                               sizeof(float) * 4 * (size_t)width * (size_t)(r1 - r0), hipMemcpyDeviceToHost,
-                               ctx->stream));
+        hipError_t e = hipMemcpyAsync((char*)out_host + bpp * (size_t)r0 * (size_t)width, ctx->out.p,
+                                      bpp * (size_t)width * (size_t)(r1 - r0), hipMemcpyDeviceToHost, ctx->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+        if (e != hipSuccess) {
+            rcs[(size_t)d] = RTM_ERR_HIP;
+            errs[(size_t)d] = std::string("band copy from device ") + std::to_string(ctx->device) + ": " +
+                              hipGetErrorString(e);
+        }
+    };
+    int n_live = 0;
+    for (rtm_ctx* c : ctxs) n_live += c != nullptr;
+    if (n_live <= 1) {
+        for (int d = 0; d < n_gpus; ++d)
+            if (ctxs[(size_t)d]) copy_band(d);
+    } else {
+        std::vector<std::thread> th;
+        for (int d = 0; d < n_gpus; ++d)
+            if (ctxs[(size_t)d]) th.emplace_back(copy_band, d);
+        for (auto& t : th) t.join();
     }
-    for (rtm_ctx* ctx : ctxs) {
-        if (!ctx) continue;
-        DeviceGuard g(ctx->device);
-        HIP_TRY(hipStreamSynchronize(ctx->stream));
-    }
+    for (int d = 0; d < n_gpus; ++d)
+        if (rcs[(size_t)d]) return fail(rcs[(size_t)d], "%s", errs[(size_t)d].c_str());
     return RTM_OK;
+}
+
+int rtm_render_multi(const rtm_scene* scene, const rtm_camera* eye, const rtm_camera* shadow, int32_t width,
+                     int32_t height, int32_t march_steps, int32_t flags, float* out_rgba, int32_t n_gpus) {
+    return rtm_render_multi_ex(scene, eye, shadow, width, height, march_steps, flags, RTM_FORMAT_RGBA32F, out_rgba,
+                               n_gpus);
 }
 
 int rtm_render_stats(rtm_ctx* ctx, const rtm_scene* scene, const rtm_camera* eye, const rtm_camera* shadow,
@@ -1351,9 +1453,9 @@ int enc_tab_dev(rtm_ctx* ctx, const void** out) {
                                              t.max_crossings);
         int rc = ctx->enc_tab.ensure(ENC_DEV_BYTES, ctx->device);
         if (rc) return rc;
-        HIP_TRY(hipMemcpyAsync(ctx->enc_tab.p, t.t, 1024, hipMemcpyHostToDevice, ctx->stream));
-        HIP_TRY(hipMemcpyAsync((char*)ctx->enc_tab.p + 1024, t.bucket, ENC_BUCKETS, hipMemcpyHostToDevice,
-                               ctx->stream));
+        // synchronous: the eye epilogue may read it from any of the context's streams
+        HIP_TRY(hipMemcpy(ctx->enc_tab.p, t.t, 1024, hipMemcpyHostToDevice));
+        HIP_TRY(hipMemcpy((char*)ctx->enc_tab.p + 1024, t.bucket, ENC_BUCKETS, hipMemcpyHostToDevice));
         ctx->enc_tab_ready = true;
     }
     *out = ctx->enc_tab.p;
@@ -1586,3 +1688,24 @@ int rtm_viewport_read_zbuffer(const rtm_viewport* vp, double* out) {
 }
 
 }  // extern "C"
+
+// ---- internal interface for rtm_group.cpp (rtm_internal.h) ----
+namespace rtm {
+namespace internal {
+
+int check_frame(const rtm_scene* scene, const rtm_camera* eye, const rtm_camera* shadow, int32_t width,
+                int32_t height, int32_t march_steps, int32_t flags) {
+    FrameArgs a;
+    return build_frame(a, scene, eye, shadow, width, height, march_steps, flags);
+}
+
+int32_t bytes_per_pixel(int32_t format) { return format_bytes(format); }
+
+int set_error(int code, const char* msg) { return fail(code, "%s", msg); }
+
+int ctx_device(const rtm_ctx* ctx) { return ctx->device; }
+
+hipStream_t ctx_stream(const rtm_ctx* ctx) { return ctx->stream; }
+
+}  // namespace internal
+}  // namespace rtm

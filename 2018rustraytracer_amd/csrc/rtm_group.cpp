@@ -1,0 +1,462 @@
+// rtm_group.cpp — the north star's multi-GPU frame (BASELINE.json north_star,
+// SURVEY.md §8e): the image tile-partitioned into row bands over N devices and
+// assembled in the root's device buffer by ONE RCCL gather over xGMI.
+//
+// The reference renders one Map2d<Color32> frame on one CPU thread
+// (renderColorImage, main.rs:709-716, 896-898); nothing in it is distributed.
+// Every pixel is independent, so a band needs no other band's data except
+// shadow texels, which each band evaluates itself (RTM_FLAG_FUSED_SHADOW, the
+// same image bits).  The one exchange is the final gather.
+//
+// RCCL is loaded at run time (dlopen "librccl.so.1": the copy torch.distributed
+// already mapped when the process has one, so the process holds one RCCL), so
+// librtm.so itself does not depend on it: single-device callers never load it.
+#include <dlfcn.h>
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "rtm_internal.h"
+
+using rtm::internal::set_error;
+
+namespace {
+
+// ---- RCCL entry points (rccl.h) resolved from the shared library ----
+struct Rccl {
+    ncclResult_t (*GetUniqueId)(ncclUniqueId*) = nullptr;
+    ncclResult_t (*CommInitRank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
+    ncclResult_t (*CommInitAll)(ncclComm_t*, int, const int*) = nullptr;
+    ncclResult_t (*CommDestroy)(ncclComm_t) = nullptr;
+    ncclResult_t (*CommAbort)(ncclComm_t) = nullptr;
+    ncclResult_t (*CommGetAsyncError)(ncclComm_t, ncclResult_t*) = nullptr;
+    ncclResult_t (*Send)(const void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*Recv)(void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*GroupStart)() = nullptr;
+    ncclResult_t (*GroupEnd)() = nullptr;
+    const char* (*GetErrorString)(ncclResult_t) = nullptr;
+    std::string error;  // empty: loaded
+};
+
+const Rccl& rccl() {
+    static const Rccl r = [] {
+        Rccl x;
+        void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+        if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+        if (!h) {
+            const char* e = dlerror();
+            x.error = std::string("cannot load librccl.so.1: ") + (e ? e : "?");
+            return x;
+        }
+        bool ok = true;
+        auto sym = [&](const char* name) {
+            void* p = dlsym(h, name);
+            if (!p) {
+                ok = false;
+                x.error = std::string("librccl.so.1 lacks ") + name;
+            }
+            return p;
+        };
+        x.GetUniqueId = reinterpret_cast<decltype(x.GetUniqueId)>(sym("ncclGetUniqueId"));
+        x.CommInitRank = reinterpret_cast<decltype(x.CommInitRank)>(sym("ncclCommInitRank"));
+        x.CommInitAll = reinterpret_cast<decltype(x.CommInitAll)>(sym("ncclCommInitAll"));
+        x.CommDestroy = reinterpret_cast<decltype(x.CommDestroy)>(sym("ncclCommDestroy"));
+        x.CommAbort = reinterpret_cast<decltype(x.CommAbort)>(sym("ncclCommAbort"));
+        x.CommGetAsyncError = reinterpret_cast<decltype(x.CommGetAsyncError)>(sym("ncclCommGetAsyncError"));
+        x.Send = reinterpret_cast<decltype(x.Send)>(sym("ncclSend"));
+        x.Recv = reinterpret_cast<decltype(x.Recv)>(sym("ncclRecv"));
+        x.GroupStart = reinterpret_cast<decltype(x.GroupStart)>(sym("ncclGroupStart"));
+        x.GroupEnd = reinterpret_cast<decltype(x.GroupEnd)>(sym("ncclGroupEnd"));
+        x.GetErrorString = reinterpret_cast<decltype(x.GetErrorString)>(sym("ncclGetErrorString"));
+        if (!ok) x.GetErrorString = nullptr;
+        return x;
+    }();
+    return r;
+}
+
+int comm_fail(const char* what, ncclResult_t r) {
+    char buf[256];
+    const Rccl& R = rccl();
+    snprintf(buf, sizeof buf, "%s: %s", what, R.GetErrorString ? R.GetErrorString(r) : "RCCL error");
+    return set_error(RTM_ERR_COMM, buf);
+}
+
+int hip_fail(const char* what, hipError_t e) {
+    char buf[256];
+    snprintf(buf, sizeof buf, "%s: %s", what, hipGetErrorString(e));
+    return set_error(RTM_ERR_HIP, buf);
+}
+
+#define NCCL_TRY(expr)                                   \
+    do {                                                 \
+        ncclResult_t r_ = (expr);                        \
+        if (r_ != ncclSuccess) return comm_fail(#expr, r_); \
+    } while (0)
+#define GHIP_TRY(expr)                                  \
+    do {                                                \
+        hipError_t e_ = (expr);                         \
+        if (e_ != hipSuccess) return hip_fail(#expr, e_); \
+    } while (0)
+
+struct Guard {  // current device for a scope
+    int prev = 0;
+    explicit Guard(int dev) {
+        (void)hipGetDevice(&prev);
+        if (prev != dev) (void)hipSetDevice(dev);
+    }
+    ~Guard() { (void)hipSetDevice(prev); }
+};
+
+// Row band of rank r among n (N bands of ceil(H/N) rows; the last
+// ones may be short or empty when N does not divide H).  shard.py row_band mirrors it.
+inline void band_rows(int32_t H, int32_t n, int32_t r, int32_t* r0, int32_t* r1) {
+    const int32_t band = (H + n - 1) / n;
+    *r0 = std::min<int64_t>(H, (int64_t)r * band);
+    *r1 = std::min<int64_t>(H, (int64_t)(r + 1) * band);
+}
+
+}  // namespace
+
+// One local device of the group.
+struct Member {
+    rtm_ctx* ctx = nullptr;
+    int device = 0;
+    int rank = 0;
+    ncclComm_t comm = nullptr;
+    hipStream_t xfer = nullptr;      // the member's RCCL transfers
+    hipEvent_t start = nullptr;      // frame start on the render stream (the root's receives wait for it)
+    hipEvent_t ready[2] = {nullptr, nullptr};  // band rendered into stage[s]
+    hipEvent_t sent[2] = {nullptr, nullptr};   // stage[s] read by its send
+    hipEvent_t done = nullptr;       // the frame's transfers on this member are finished
+    void* stage[2] = {nullptr, nullptr};
+    size_t stage_bytes = 0;
+    int slot = 0;
+};
+
+struct rtm_group {
+    int32_t n_ranks = 0;
+    std::vector<Member> m;
+    bool aborted = false;
+    bool root_staging = false;
+};
+
+namespace {
+
+void release(rtm_group* g, bool destroy_comms) {
+    const Rccl& R = rccl();
+    for (Member& mb : g->m) {
+        Guard d(mb.device);
+        if (mb.xfer) (void)hipStreamSynchronize(mb.xfer);
+        if (mb.comm && destroy_comms && R.CommDestroy) (void)R.CommDestroy(mb.comm);
+        mb.comm = nullptr;
+        for (hipEvent_t* e : {&mb.start, &mb.ready[0], &mb.ready[1], &mb.sent[0], &mb.sent[1], &mb.done})
+            if (*e) {
+                (void)hipEventDestroy(*e);
+                *e = nullptr;
+            }
+        for (void*& p : mb.stage)
+            if (p) {
+                (void)hipFree(p);
+                p = nullptr;
+            }
+        if (mb.xfer) (void)hipStreamDestroy(mb.xfer);
+        mb.xfer = nullptr;
+        if (mb.ctx) rtm_ctx_destroy(mb.ctx);
+        mb.ctx = nullptr;
+    }
+}
+
+// Contexts, transfer streams and events of the members (comms set by the caller).
+int setup_members(rtm_group* g) {
+    for (Member& mb : g->m) {
+        int rc = rtm_ctx_create(mb.device, &mb.ctx);
+        if (rc) return rc;
+        Guard d(mb.device);
+        GHIP_TRY(hipStreamCreateWithFlags(&mb.xfer, hipStreamNonBlocking));
+        for (hipEvent_t* e : {&mb.start, &mb.ready[0], &mb.ready[1], &mb.sent[0], &mb.sent[1], &mb.done})
+            GHIP_TRY(hipEventCreateWithFlags(e, hipEventDisableTiming));
+    }
+    return RTM_OK;
+}
+
+int ensure_stage(Member& mb, size_t bytes) {
+    if (bytes <= mb.stage_bytes) return RTM_OK;
+    Guard d(mb.device);
+    // both staging buffers are idle once their last sends are done
+    GHIP_TRY(hipStreamSynchronize(mb.xfer));
+    for (void*& p : mb.stage) {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+    }
+    mb.stage_bytes = 0;
+    for (void*& p : mb.stage)
+        if (hipMalloc(&p, bytes) != hipSuccess) return set_error(RTM_ERR_OOM, "band staging allocation failed");
+    mb.stage_bytes = bytes;
+    return RTM_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int rtm_group_unique_id(uint8_t id[128]) {
+    if (!id) return set_error(RTM_ERR_INVALID, "id is NULL");
+    const Rccl& R = rccl();
+    if (!R.error.empty()) return set_error(RTM_ERR_COMM, R.error.c_str());
+    static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId size");
+    ncclUniqueId u;
+    NCCL_TRY(R.GetUniqueId(&u));
+    std::memcpy(id, &u, sizeof u);
+    return RTM_OK;
+}
+
+int rtm_group_create(int32_t n_devices, const int32_t* devices, rtm_group** out) {
+    if (!out) return set_error(RTM_ERR_INVALID, "out is NULL");
+    *out = nullptr;
+    const int nd = rtm_device_count();
+    if (nd <= 0) return set_error(RTM_ERR_NO_DEVICE, "no HIP device visible");
+    if (n_devices < 1 || n_devices > nd) return set_error(RTM_ERR_INVALID, "n_devices outside [1, device count]");
+    std::vector<int> dev((size_t)n_devices);
+    for (int i = 0; i < n_devices; ++i) {
+        dev[(size_t)i] = devices ? devices[i] : i;
+        if (dev[(size_t)i] < 0 || dev[(size_t)i] >= nd) return set_error(RTM_ERR_INVALID, "device id out of range");
+        for (int j = 0; j < i; ++j)
+            if (dev[(size_t)j] == dev[(size_t)i]) return set_error(RTM_ERR_INVALID, "a device appears twice");
+    }
+    const Rccl& R = rccl();
+    if (!R.error.empty()) return set_error(RTM_ERR_COMM, R.error.c_str());
+    std::unique_ptr<rtm_group> g(new rtm_group);
+    g->n_ranks = n_devices;
+    g->m.resize((size_t)n_devices);
+    for (int i = 0; i < n_devices; ++i) {
+        g->m[(size_t)i].device = dev[(size_t)i];
+        g->m[(size_t)i].rank = i;
+    }
+    int rc = setup_members(g.get());
+    if (rc) {
+        release(g.get(), false);
+        return rc;
+    }
+    std::vector<ncclComm_t> comms((size_t)n_devices, nullptr);
+    ncclResult_t r = R.CommInitAll(comms.data(), n_devices, dev.data());  // rccl.h:236
+    if (r != ncclSuccess) {
+        release(g.get(), false);
+        return comm_fail("ncclCommInitAll", r);
+    }
+    for (int i = 0; i < n_devices; ++i) g->m[(size_t)i].comm = comms[(size_t)i];
+    *out = g.release();
+    return RTM_OK;
+}
+
+int rtm_group_create_rank(int32_t device, int32_t n_ranks, int32_t rank, const uint8_t id[128], rtm_group** out) {
+    if (!out || !id) return set_error(RTM_ERR_INVALID, "out/id is NULL");
+    *out = nullptr;
+    const int nd = rtm_device_count();
+    if (nd <= 0) return set_error(RTM_ERR_NO_DEVICE, "no HIP device visible");
+    if (device < 0 || device >= nd) return set_error(RTM_ERR_INVALID, "device out of range");
+    if (n_ranks < 1 || rank < 0 || rank >= n_ranks) return set_error(RTM_ERR_INVALID, "rank outside [0, n_ranks)");
+    const Rccl& R = rccl();
+    if (!R.error.empty()) return set_error(RTM_ERR_COMM, R.error.c_str());
+    std::unique_ptr<rtm_group> g(new rtm_group);
+    g->n_ranks = n_ranks;
+    g->m.resize(1);
+    g->m[0].device = device;
+    g->m[0].rank = rank;
+    int rc = setup_members(g.get());
+    if (rc) {
+        release(g.get(), false);
+        return rc;
+    }
+    ncclUniqueId u;
+    std::memcpy(&u, id, sizeof u);
+    ncclComm_t c = nullptr;
+    ncclResult_t r;
+    {
+        Guard d(device);
+        r = R.CommInitRank(&c, n_ranks, u, rank);  // rccl.h:220
+    }
+    if (r != ncclSuccess) {
+        release(g.get(), false);
+        return comm_fail("ncclCommInitRank", r);
+    }
+    g->m[0].comm = c;
+    *out = g.release();
+    return RTM_OK;
+}
+
+void rtm_group_destroy(rtm_group* g) {
+    if (!g) return;
+    if (!g->aborted) (void)rtm_group_synchronize(g, 0);
+    release(g, !g->aborted);
+    delete g;
+}
+
+int rtm_group_info(rtm_group* g, int32_t* n_ranks, int32_t* n_local, int32_t* first_rank) {
+    if (!g) return set_error(RTM_ERR_INVALID, "group is NULL");
+    if (n_ranks) *n_ranks = g->n_ranks;
+    if (n_local) *n_local = (int32_t)g->m.size();
+    if (first_rank) *first_rank = g->m.empty() ? 0 : g->m[0].rank;
+    return RTM_OK;
+}
+
+rtm_ctx* rtm_group_ctx(rtm_group* g, int32_t local) {
+    if (!g || local < 0 || local >= (int32_t)g->m.size()) return nullptr;
+    return g->m[(size_t)local].ctx;
+}
+
+int rtm_group_set_root_staging(rtm_group* g, int32_t on) {
+    if (!g) return set_error(RTM_ERR_INVALID, "group is NULL");
+    g->root_staging = on != 0;
+    return RTM_OK;
+}
+
+int rtm_group_render_async(rtm_group* g, const rtm_scene* scene, const rtm_camera* eye, const rtm_camera* shadow,
+                           int32_t width, int32_t height, int32_t march_steps, int32_t flags, int32_t format,
+                           int32_t root, void* out_dev) {
+    if (!g) return set_error(RTM_ERR_INVALID, "group is NULL");
+    if (g->aborted) return set_error(RTM_ERR_COMM, "group was aborted");
+    const int32_t n = g->n_ranks;
+    if (root < 0 || root >= n) return set_error(RTM_ERR_INVALID, "root outside [0, n_ranks)");
+    const int32_t bpp = rtm::internal::bytes_per_pixel(format);
+    if (!bpp) return set_error(RTM_ERR_INVALID, "unknown output format");
+    // more than one band: each evaluates the shadow texels it reads (same image bits)
+    const int32_t f = flags | (n > 1 ? RTM_FLAG_FUSED_SHADOW : 0);
+    // Everything that can fail for the caller's inputs is checked before the first
+    // enqueue: a rank that stopped half-way would leave its peers' transfers unmatched.
+    int rc = rtm::internal::check_frame(scene, eye, shadow, width, height, march_steps, f);
+    if (rc) return rc;
+    const bool holds_root = std::any_of(g->m.begin(), g->m.end(), [&](const Member& mb) { return mb.rank == root; });
+    if (holds_root) {
+        if (!out_dev) return set_error(RTM_ERR_INVALID, "out_dev is NULL on the root");
+        if (format == RTM_FORMAT_RGBA32F && ((uintptr_t)out_dev & 15))
+            return set_error(RTM_ERR_INVALID, "RGBA32F output must be 16-byte aligned");
+    }
+    const size_t row_bytes = (size_t)bpp * (size_t)width;
+    int32_t b0 = 0, b1 = 0;
+    band_rows(height, n, 0, &b0, &b1);
+    for (Member& mb : g->m) {
+        const bool staged = mb.rank != root || g->root_staging;
+        if (staged && (rc = ensure_stage(mb, row_bytes * (size_t)(b1 - b0)))) return rc;
+    }
+    // 1. every local member renders its band: in place (the root) or into a staging buffer
+    for (Member& mb : g->m) {
+        int32_t r0, r1;
+        band_rows(height, n, mb.rank, &r0, &r1);
+        Guard d(mb.device);
+        hipStream_t rs = rtm::internal::ctx_stream(mb.ctx);
+        if (mb.rank == root) GHIP_TRY(hipEventRecord(mb.start, rs));
+        if (r0 >= r1) continue;
+        const bool staged = mb.rank != root || g->root_staging;
+        if (!staged) {
+            rc = rtm_render_rows_async(mb.ctx, scene, eye, shadow, width, height, march_steps, f, format, r0, r1,
+                                       (char*)out_dev + row_bytes * (size_t)r0);
+            if (rc) return rc;
+            continue;
+        }
+        const int s = mb.slot;
+        GHIP_TRY(hipStreamWaitEvent(rs, mb.sent[s], 0));  // stage[s]'s previous send has read it
+        rc = rtm_render_rows_async(mb.ctx, scene, eye, shadow, width, height, march_steps, f, format, r0, r1,
+                                   mb.stage[s]);
+        if (rc) return rc;
+        GHIP_TRY(hipEventRecord(mb.ready[s], rs));
+        GHIP_TRY(hipStreamWaitEvent(mb.xfer, mb.ready[s], 0));
+    }
+    // 2. ONE gather: the root receives every other band in place, the others send theirs
+    const Rccl& R = rccl();
+    for (Member& mb : g->m)
+        if (mb.rank == root) {
+            Guard d(mb.device);
+            GHIP_TRY(hipStreamWaitEvent(mb.xfer, mb.start, 0));  // no receive before the frame's start
+        }
+    NCCL_TRY(R.GroupStart());
+    for (Member& mb : g->m) {
+        if (mb.rank == root) {
+            for (int32_t p = 0; p < n; ++p) {
+                if (p == root && !g->root_staging) continue;
+                int32_t r0, r1;
+                band_rows(height, n, p, &r0, &r1);
+                if (r0 >= r1) continue;
+                ncclResult_t r = R.Recv((char*)out_dev + row_bytes * (size_t)r0, row_bytes * (size_t)(r1 - r0),
+                                        ncclUint8, p, mb.comm, mb.xfer);
+                if (r != ncclSuccess) {
+                    (void)R.GroupEnd();
+                    return comm_fail("ncclRecv", r);
+                }
+            }
+        }
+        int32_t r0, r1;
+        band_rows(height, n, mb.rank, &r0, &r1);
+        const bool staged = mb.rank != root || g->root_staging;
+        if (staged && r0 < r1) {
+            ncclResult_t r = R.Send(mb.stage[mb.slot], row_bytes * (size_t)(r1 - r0), ncclUint8, root, mb.comm, mb.xfer);
+            if (r != ncclSuccess) {
+                (void)R.GroupEnd();
+                return comm_fail("ncclSend", r);
+            }
+        }
+    }
+    NCCL_TRY(R.GroupEnd());
+    // 3. bookkeeping: staging slots and the root's completion in its render stream order
+    for (Member& mb : g->m) {
+        int32_t r0, r1;
+        band_rows(height, n, mb.rank, &r0, &r1);
+        Guard d(mb.device);
+        const bool staged = mb.rank != root || g->root_staging;
+        if (staged && r0 < r1) {
+            GHIP_TRY(hipEventRecord(mb.sent[mb.slot], mb.xfer));
+            mb.slot ^= 1;
+        }
+        if (mb.rank == root) {
+            GHIP_TRY(hipEventRecord(mb.done, mb.xfer));
+            GHIP_TRY(hipStreamWaitEvent(rtm::internal::ctx_stream(mb.ctx), mb.done, 0));
+        }
+    }
+    return RTM_OK;
+}
+
+int rtm_group_synchronize(rtm_group* g, int32_t timeout_ms) {
+    if (!g) return set_error(RTM_ERR_INVALID, "group is NULL");
+    if (g->aborted) return set_error(RTM_ERR_COMM, "group was aborted");
+    const Rccl& R = rccl();
+    const auto t0 = std::chrono::steady_clock::now();
+    for (;;) {
+        bool busy = false;
+        for (Member& mb : g->m) {
+            Guard d(mb.device);
+            for (hipStream_t s : {rtm::internal::ctx_stream(mb.ctx), mb.xfer}) {
+                const hipError_t e = hipStreamQuery(s);
+                if (e == hipErrorNotReady) busy = true;
+                else if (e != hipSuccess) return hip_fail("hipStreamQuery", e);
+            }
+            ncclResult_t ae = ncclSuccess;
+            if (mb.comm && R.CommGetAsyncError && R.CommGetAsyncError(mb.comm, &ae) == ncclSuccess &&
+                ae != ncclSuccess && ae != ncclInProgress) {
+                for (Member& m2 : g->m)
+                    if (m2.comm) (void)R.CommAbort(m2.comm);
+                for (Member& m2 : g->m) m2.comm = nullptr;
+                g->aborted = true;
+                return comm_fail("RCCL asynchronous error (communicators aborted)", ae);
+            }
+        }
+        if (!busy) return RTM_OK;
+        if (timeout_ms > 0 &&
+            std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(timeout_ms)) {
+            for (Member& mb : g->m)
+                if (mb.comm) (void)R.CommAbort(mb.comm);
+            for (Member& mb : g->m) mb.comm = nullptr;
+            g->aborted = true;
+            return set_error(RTM_ERR_COMM, "group work did not finish in time (communicators aborted)");
+        }
+        std::this_thread::sleep_for(std::chrono::microseconds(50));
+    }
+}
+
+}  // extern "C"

@@ -186,12 +186,20 @@ struct SdfTabK {
 };
 static_assert(sizeof(SdfTabK) + sizeof(void*) <= 4096, "SdfTabK must fit the upload kernel's kernarg segment");
 
-// The device tables a frame may carry beside FrameArgs (each nullptr when absent).
+// The device tables a frame may carry beside FrameArgs (each nullptr when absent),
+// and the eye pass's output format.
 struct DevTabs {
     const RtK* rt;        // circle planes + capped cylinders (f-1)
     const PerspK* psp;    // PERSPECTIVE eye sphere projections (f-3)
     const SdfTabK* sdf;   // SDF implicit surfaces (f-4)
+    // writeColorImage's encode (row f-2) as the eye pass's epilogue: the device
+    // EncodeTable (rtm_encode.h: t at +0, bucket at +1024) when fmt != RGBA32F
+    const void* enc;
+    int32_t fmt;          // RTM_FORMAT_* | FMT_RGB8_DWORDS (RGB8 rows start 4-byte aligned)
+    uint32_t bg;          // the encoded background pixel (0.0, 0.2, 0.2) (main.rs:718-720), R | G<<8 | B<<16
 };
+constexpr int32_t FMT_MASK = 0xff;
+constexpr int32_t FMT_RGB8_DWORDS = 0x100;
 
 // Reference-seam kernels (one per reference function).
 struct RasterArgs {
@@ -246,8 +254,9 @@ int launch_shadow_pass(const FrameArgs& a, double* smap, void* stream, StatsK* s
 // rt / psp != nullptr: the frame has ray-traced primitives / a PERSPECTIVE eye
 // with spheres (device RtK / PerspK, see launch_upload); either selects the
 // general eye kernel.
-int launch_eye_pass(const FrameArgs& a, const double* smap, float* out, void* stream, StatsK* stats,
-                    const DevTabs& tabs = DevTabs{nullptr, nullptr, nullptr});
+// out: (row_end-row_begin)*W pixels in tabs.fmt's format (RTM_FORMAT_RGBA32F: 16-byte aligned).
+int launch_eye_pass(const FrameArgs& a, const double* smap, void* out, void* stream, StatsK* stats,
+                    const DevTabs& tabs = DevTabs{});
 // Stream-ordered copy of a host struct into device memory (a kernel, so the
 // host copy is consumed at launch: no pinned staging, no host synchronisation).
 int launch_rt_upload(const RtK& k, RtK* dst, void* stream);

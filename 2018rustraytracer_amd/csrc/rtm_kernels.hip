@@ -34,6 +34,17 @@ constexpr int BLOCK = TILE_X * TILE_Y;
 using cdouble = const __attribute__((address_space(4))) double;  // scalar-loaded table
 using cint = const __attribute__((address_space(4))) int32_t;
 
+// writeColorImage's per-channel byte (main.rs:674-684) by threshold lookup, as
+// rtm_encode.hip's encode kernel computes it (the tables: rtm_encode.h): clamp as
+// f32::max(0.0).min(1.0) (NaN -> 0), bucket byte, then at most one threshold.
+__device__ __forceinline__ uint32_t enc_byte(float c, const float* __restrict__ T, const uint8_t* __restrict__ B) {
+    float v = c > 0.0f ? c : 0.0f;
+    v = v < 1.0f ? v : 1.0f;
+    uint32_t k = B[__float_as_uint(v) >> 16];
+    while (k < 255u && v >= T[k + 1]) ++k;
+    return k;
+}
+
 
 // main.rs:306-307 / 1903-1907: ((i as f64) / (res as f64)) * 2.0 - 1.0
 __device__ __forceinline__ double ndc(int i, int res) { return ((double)i / (double)res) * 2.0 - 1.0; }
@@ -1283,9 +1294,9 @@ __global__ __launch_bounds__(BLOCK) void shadow_lean2_kernel(const FrameArgs a, 
 // RT: 0 spheres only, 1 + ray-traced planes/cylinders and PERSPECTIVE spheres,
 // 2 + SDFs (its own instantiation: the sphere-trace loop's registers would
 // otherwise lower the occupancy of every ray-traced frame).
-template <bool FUSED, bool COUNT, int RT>
+template <bool FUSED, bool COUNT, int RT, int FMT = RTM_FORMAT_RGBA32F>
 __device__ __forceinline__ void eye_tile(const EyePart& a, const ShadowPart& sh, const double* __restrict__ smap,
-                                         float4* __restrict__ out, int bx, int by, StatsK* __restrict__ st,
+                                         void* __restrict__ out, int bx, int by, StatsK* __restrict__ st,
                                          const DevTabs tabs, int wide = 0) {
     const RtK* __restrict__ rt = tabs.rt;
     const PerspK* __restrict__ psp = tabs.psp;
@@ -1309,6 +1320,8 @@ __device__ __forceinline__ void eye_tile(const EyePart& a, const ShadowPart& sh,
     uint32_t rmask = ~0u;
     if (RT == 1 && rt && a.eye.type == RTM_CAMERA_PERSPECTIVE && !(wide & 4))
         rmask = rt_wave_mask(rt, a.eye, min(xb, a.W - 1), min(xb + TILE_X - 1, a.W - 1), min(yi, a.H - 1), a.W, a.H);
+    float4 c = make_float4(0.0f, 0.2f, 0.2f, 1.0f);  // (0.0, 0.2, 0.2) as f32 (main.rs:718-720)
+    bool shaded = false;
     if (live) {
         const double x = a.nx[xi];
         const double y = a.ny[yi];
@@ -1347,8 +1360,8 @@ __device__ __forceinline__ void eye_tile(const EyePart& a, const ShadowPart& sh,
             }
             if (RT == 2) trace_sdfs(sdf, o, d, zb, hit, n_evals);
         }
-        float4 c = make_float4(0.0f, 0.2f, 0.2f, 1.0f);  // (0.0, 0.2, 0.2) as f32 (main.rs:718-720)
         if (hit.kind) {
+            shaded = true;
             if (!RT) cam_ray(a.eye, x, y, o, d);
             // world position and normal per surface kind (main.rs:729-796)
             double wx, wy, wz, nx, ny, nz, cr, cg, cb;
@@ -1442,10 +1455,47 @@ __device__ __forceinline__ void eye_tile(const EyePart& a, const ShadowPart& sh,
                 hit_id = hit.id;
             }
         }
-        if (wide & 2)  // non-temporal: the frame's stores do not allocate in the caches
-            __builtin_nontemporal_store(f32x4{c.x, c.y, c.z, c.w}, reinterpret_cast<f32x4*>(&out[(int64_t)yl * a.W + xi]));
-        else
-            out[(int64_t)yl * a.W + xi] = c;
+    }
+    // the frame store (all lanes converged): RGBA f32, or writeColorImage's bytes
+    if (FMT == RTM_FORMAT_RGBA32F) {
+        float4* o = reinterpret_cast<float4*>(out);
+        if (live) {
+            if (wide & 2)  // non-temporal: the frame's stores do not allocate in the caches
+                __builtin_nontemporal_store(f32x4{c.x, c.y, c.z, c.w},
+                                            reinterpret_cast<f32x4*>(&o[(int64_t)yl * a.W + xi]));
+            else
+                o[(int64_t)yl * a.W + xi] = c;
+        }
+    } else {
+        uint32_t e = tabs.bg;  // background: one host-encoded constant
+        if (shaded) {
+            const float* T = reinterpret_cast<const float*>(tabs.enc);
+            const uint8_t* B = reinterpret_cast<const uint8_t*>(tabs.enc) + 1024;
+            e = enc_byte(c.x, T, B) | (enc_byte(c.y, T, B) << 8) | (enc_byte(c.z, T, B) << 16);
+        }
+        if (FMT == RTM_FORMAT_RGBA8) {  // alpha 1.0 -> 255; one dword per pixel, 256 B per wave
+            uint32_t* o = reinterpret_cast<uint32_t*>(out);
+            if (live) __builtin_nontemporal_store(e | 0xFF000000u, &o[(int64_t)yl * a.W + xi]);
+        } else {  // RGB8: the wave's 64 pixels are 192 contiguous bytes = 48 dwords
+            uint8_t* row = reinterpret_cast<uint8_t*>(out) + (int64_t)yl * a.W * 3;
+            if (tabs.fmt & FMT_RGB8_DWORDS) {
+                // dword j of the wave's segment: bytes 4j..4j+3 = the tail of pixel L (from
+                // byte o = 4j - 3L) and the head of pixel L + 1
+                const int j = threadIdx.x & (TILE_X - 1);
+                const int L = min((4 * j) / 3, TILE_X - 1);
+                const int o = min(4 * j - 3 * L, 2);  // (lanes j >= 48, clamped, store nothing)
+                const uint32_t p0 = (uint32_t)__shfl((int)e, L);
+                const uint32_t p1 = (uint32_t)__shfl((int)e, min(L + 1, TILE_X - 1));
+                const uint32_t w = (p0 >> (8 * o)) | (p1 << (8 * (3 - o)));
+                const int nv = min(TILE_X, a.W - xb);  // W % 4 == 0 (host-checked): 3*nv/4 whole dwords
+                if (yi < a.row_end && j < (3 * nv) >> 2)
+                    __builtin_nontemporal_store(w, reinterpret_cast<uint32_t*>(row + 3 * (int64_t)xb) + j);
+            } else if (live) {
+                row[3 * (int64_t)xi + 0] = (uint8_t)e;
+                row[3 * (int64_t)xi + 1] = (uint8_t)(e >> 8);
+                row[3 * (int64_t)xi + 2] = (uint8_t)(e >> 16);
+            }
+        }
     }
     if (COUNT) {
         stat_add(&st->eye_sphere_tests, n_tests);
@@ -1484,18 +1534,18 @@ __global__ __launch_bounds__(BLOCK) void shadow_sep_kernel(const FrameArgs a, do
     shadow_tile_sep<NR, MODE>(a.sh, smap, blockIdx.x, blockIdx.y, diag, lds ? lds_zt : nullptr);
 }
 
-template <bool FUSED, bool COUNT, int RT>
+template <bool FUSED, bool COUNT, int RT, int FMT>
 __global__ __launch_bounds__(BLOCK) void eye_pass_kernel(const FrameArgs a, const double* __restrict__ smap,
-                                                         float4* __restrict__ out, StatsK* __restrict__ st,
+                                                         void* __restrict__ out, StatsK* __restrict__ st,
                                                          const DevTabs tabs, int wide) {
-    eye_tile<FUSED, COUNT, RT>(a.ey, a.sh, smap, out, blockIdx.x, blockIdx.y, st, tabs, wide);
+    eye_tile<FUSED, COUNT, RT, FMT>(a.ey, a.sh, smap, out, blockIdx.x, blockIdx.y, st, tabs, wide);
 }
 
 // The SDF eye instantiation (row f-4) with a register cap: WPE waves per SIMD at least.
-template <int WPE>
+template <int WPE, int FMT>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8))) void eye_sdf_kernel(
-    const FrameArgs a, const double* __restrict__ smap, float4* __restrict__ out, const DevTabs tabs, int wide) {
-    eye_tile<false, false, 2>(a.ey, a.sh, smap, out, blockIdx.x, blockIdx.y, nullptr, tabs, wide);
+    const FrameArgs a, const double* __restrict__ smap, void* __restrict__ out, const DevTabs tabs, int wide) {
+    eye_tile<false, false, 2, FMT>(a.ey, a.sh, smap, out, blockIdx.x, blockIdx.y, nullptr, tabs, wide);
 }
 
 // launch_*_upload: one 8-byte word per thread from the kernarg copy.
@@ -1904,39 +1954,60 @@ static bool sdf_wpe5() {
     return v;
 }
 
-int launch_eye_pass(const FrameArgs& a, const double* smap, float* out, void* stream, StatsK* stats,
+template <int FMT>
+static void launch_eye_fmt(const FrameArgs& a, const double* smap, void* o, hipStream_t s, dim3 g, bool fused,
+                           const DevTabs& tabs, int wide) {
+#define RTM_EYE(F, R) \
+    hipLaunchKernelGGL((eye_pass_kernel<F, false, R, FMT>), g, dim3(BLOCK), 0, s, a, smap, o, nullptr, tabs, wide)
+    if (tabs.sdf) {
+        if (fused) RTM_EYE(true, 2);
+        else if (sdf_wpe5())  // 95 VGPRs, 5 waves/SIMD, no spill: eye 582 -> 565 us at config 8
+            hipLaunchKernelGGL((eye_sdf_kernel<5, FMT>), g, dim3(BLOCK), 0, s, a, smap, o, tabs, wide);
+        else RTM_EYE(false, 2);
+    } else if (tabs.rt || tabs.psp) {
+        if (fused) RTM_EYE(true, 1);
+        else RTM_EYE(false, 1);
+    } else {
+        if (fused) RTM_EYE(true, 0);
+        else RTM_EYE(false, 0);
+    }
+#undef RTM_EYE
+}
+
+int launch_eye_pass(const FrameArgs& a, const double* smap, void* out, void* stream, StatsK* stats,
                     const DevTabs& tabs) {
     hipStream_t s = (hipStream_t)stream;
     const int rows = a.ey.row_end - a.ey.row_begin;
     const int wide = eye_wide();
     dim3 g = (wide & 1) ? dim3((unsigned)((a.ey.W + BLOCK - 1) / BLOCK), (unsigned)rows) : grid_for(a.ey.W, rows);
-    float4* o = reinterpret_cast<float4*>(out);
     const bool fused = (a.ey.flags & RTM_FLAG_FUSED_SHADOW) != 0;
-    if (diag_eye()) {
-        hipLaunchKernelGGL(eye_store_only_kernel, g, dim3(BLOCK), 0, s, a, o, wide);
+    const int fmt = tabs.fmt & FMT_MASK;
+    if (diag_eye() && fmt == RTM_FORMAT_RGBA32F) {
+        hipLaunchKernelGGL(eye_store_only_kernel, g, dim3(BLOCK), 0, s, a, reinterpret_cast<float4*>(out), wide);
         return launched();
     }
-#define RTM_EYE(F, C, R) \
-    hipLaunchKernelGGL((eye_pass_kernel<F, C, R>), g, dim3(BLOCK), 0, s, a, smap, o, stats, tabs, wide)
-    if (tabs.sdf) {
-        if (fused && stats) RTM_EYE(true, true, 2);
-        else if (fused) RTM_EYE(true, false, 2);
-        else if (stats) RTM_EYE(false, true, 2);
-        else if (sdf_wpe5())  // 95 VGPRs, 5 waves/SIMD, no spill: eye 582 -> 565 us at config 8
-            hipLaunchKernelGGL(eye_sdf_kernel<5>, g, dim3(BLOCK), 0, s, a, smap, o, tabs, wide);
-        else RTM_EYE(false, false, 2);
-    } else if (tabs.rt || tabs.psp) {
-        if (fused && stats) RTM_EYE(true, true, 1);
-        else if (fused) RTM_EYE(true, false, 1);
-        else if (stats) RTM_EYE(false, true, 1);
-        else RTM_EYE(false, false, 1);
-    } else {
-        if (fused && stats) RTM_EYE(true, true, 0);
-        else if (fused) RTM_EYE(true, false, 0);
-        else if (stats) RTM_EYE(false, true, 0);
-        else RTM_EYE(false, false, 0);
-    }
+    if (stats) {  // counting kernels: RGBA f32 output only
+        if (fmt != RTM_FORMAT_RGBA32F) return RTM_ERR_INVALID;
+#define RTM_EYE(F, R) \
+    hipLaunchKernelGGL((eye_pass_kernel<F, true, R, RTM_FORMAT_RGBA32F>), g, dim3(BLOCK), 0, s, a, smap, out, stats, \
+                       tabs, wide)
+        const int rt = tabs.sdf ? 2 : (tabs.rt || tabs.psp) ? 1 : 0;
+        if (rt == 2) {
+            if (fused) RTM_EYE(true, 2);
+            else RTM_EYE(false, 2);
+        } else if (rt == 1) {
+            if (fused) RTM_EYE(true, 1);
+            else RTM_EYE(false, 1);
+        } else {
+            if (fused) RTM_EYE(true, 0);
+            else RTM_EYE(false, 0);
+        }
 #undef RTM_EYE
+        return launched();
+    }
+    if (fmt == RTM_FORMAT_RGBA8) launch_eye_fmt<RTM_FORMAT_RGBA8>(a, smap, out, s, g, fused, tabs, wide);
+    else if (fmt == RTM_FORMAT_RGB8) launch_eye_fmt<RTM_FORMAT_RGB8>(a, smap, out, s, g, fused, tabs, wide);
+    else launch_eye_fmt<RTM_FORMAT_RGBA32F>(a, smap, out, s, g, fused, tabs, wide);
     return launched();
 }
 

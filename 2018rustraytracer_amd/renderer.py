@@ -97,6 +97,18 @@ class Context:
                                             steps, flags, row_begin, row_end, C.c_void_p(out_ptr)),
                   "rtm_render_async")
 
+    def render_rows_async(self, scene: Scene, eye: Camera, shadow: Camera, width: int, height: int, steps: int,
+                          flags: int, fmt: int, out_ptr: int, row_begin: int = 0, row_end: int | None = None):
+        """rtm_render_rows_async: rows [row_begin, row_end) in output format `fmt`
+        (abi.RTM_FORMAT_*) into the device buffer at out_ptr."""
+        row_end = height if row_end is None else row_end
+        sc, keep = scene.to_c()
+        e, s = eye.to_c(), shadow.to_c()
+        lib = _lib()
+        abi.check(lib, lib.rtm_render_rows_async(self._h, C.byref(sc), C.byref(e), C.byref(s), width, height, steps,
+                                                 flags, fmt, row_begin, row_end, C.c_void_p(out_ptr)),
+                  "rtm_render_rows_async")
+
     def prepare_frames(self, scenes):
         """ctypes array of rtm_scene for render_frames_async (+ keepalive)."""
         arr = (abi.rtm_scene * len(scenes))()
@@ -184,6 +196,121 @@ def render_frame_multi(scene: Scene, eye: Camera, shadow: Camera, width: int, he
     abi.check(lib, lib.rtm_render_multi(C.byref(sc), C.byref(e), C.byref(s), width, height, steps, flags,
                                         out.ctypes.data_as(C.POINTER(C.c_float)), n_gpus), "rtm_render_multi")
     return out
+
+
+def _host_frame(height: int, width: int, fmt: int) -> np.ndarray:
+    if fmt == abi.RTM_FORMAT_RGBA32F:
+        return np.empty((height, width, 4), np.float32)
+    return np.empty((height, width, abi.FORMAT_BYTES[fmt]), np.uint8)
+
+
+def render_frame_ex(scene: Scene, eye: Camera, shadow: Camera, width: int, height: int, steps: int,
+                    flags: int = 0, fmt: int = abi.RTM_FORMAT_RGBA32F, n_gpus: int = 0, out=None) -> np.ndarray:
+    """rtm_render_ex (n_gpus == 0) or rtm_render_multi_ex: the frame in output format
+    `fmt` into host memory: (H, W, 4) f32, (H, W, 4) u8 (RGBA8) or (H, W, 3) u8 (RGB8)."""
+    out = _host_frame(height, width, fmt) if out is None else out
+    sc, keep = scene.to_c()
+    e, s = eye.to_c(), shadow.to_c()
+    lib = _lib()
+    if n_gpus:
+        abi.check(lib, lib.rtm_render_multi_ex(C.byref(sc), C.byref(e), C.byref(s), width, height, steps, flags, fmt,
+                                               C.c_void_p(out.ctypes.data), n_gpus), "rtm_render_multi_ex")
+    else:
+        abi.check(lib, lib.rtm_render_ex(C.byref(sc), C.byref(e), C.byref(s), width, height, steps, flags, fmt,
+                                         C.c_void_p(out.ctypes.data)), "rtm_render_ex")
+    return out
+
+
+class HostRegistration:
+    """rtm_host_register / rtm_host_unregister of a numpy array (context manager)."""
+
+    def __init__(self, arr: np.ndarray):
+        self.arr = arr
+        lib = _lib()
+        abi.check(lib, lib.rtm_host_register(C.c_void_p(arr.ctypes.data), arr.nbytes), "rtm_host_register")
+
+    def close(self):
+        if self.arr is not None:
+            lib = _lib()
+            abi.check(lib, lib.rtm_host_unregister(C.c_void_p(self.arr.ctypes.data)), "rtm_host_unregister")
+            self.arr = None
+
+    def __enter__(self):
+        return self.arr
+
+    def __exit__(self, *exc):
+        self.close()
+
+
+class Group:
+    """rtm_group: N ranks, one device each, one RCCL communicator; frames are
+    tile-partitioned into row bands and gathered into the root's device buffer
+    (SURVEY.md §8e).  Group(n_devices=N) drives devices 0..N-1 from this process
+    (ncclCommInitAll); Group(device=d, n_ranks=N, rank=r, uid=bytes) joins one
+    process per GPU (ncclCommInitRank, uid from Group.unique_id() on rank 0)."""
+
+    def __init__(self, n_devices: int | None = None, devices=None, *, device: int | None = None,
+                 n_ranks: int | None = None, rank: int | None = None, uid: bytes | None = None):
+        self._h = C.c_void_p()
+        lib = _lib()
+        if device is not None:
+            u = (C.c_uint8 * 128).from_buffer_copy(uid)
+            abi.check(lib, lib.rtm_group_create_rank(device, n_ranks, rank, u, C.byref(self._h)),
+                      "rtm_group_create_rank")
+        else:
+            n = n_devices if n_devices is not None else len(devices)
+            devs = (C.c_int32 * n)(*devices) if devices is not None else None
+            abi.check(lib, lib.rtm_group_create(n, devs, C.byref(self._h)), "rtm_group_create")
+
+    @property
+    def handle(self):
+        return self._h
+
+    @staticmethod
+    def unique_id() -> bytes:
+        u = (C.c_uint8 * 128)()
+        lib = _lib()
+        abi.check(lib, lib.rtm_group_unique_id(u), "rtm_group_unique_id")
+        return bytes(u)
+
+    def info(self):
+        n, loc, first = C.c_int32(), C.c_int32(), C.c_int32()
+        lib = _lib()
+        abi.check(lib, lib.rtm_group_info(self._h, C.byref(n), C.byref(loc), C.byref(first)), "rtm_group_info")
+        return int(n.value), int(loc.value), int(first.value)
+
+    def ctx_stream(self, local: int = 0) -> int:
+        lib = _lib()
+        c = lib.rtm_group_ctx(self._h, local)
+        return lib.rtm_ctx_stream(c) or 0
+
+    def set_root_staging(self, on: bool):
+        lib = _lib()
+        abi.check(lib, lib.rtm_group_set_root_staging(self._h, 1 if on else 0), "rtm_group_set_root_staging")
+
+    def render_async(self, scene: Scene, eye: Camera, shadow: Camera, width: int, height: int, steps: int,
+                     flags: int, fmt: int, root: int, out_ptr: int, prepared=None):
+        sc, keep = prepared if prepared is not None else scene.to_c()
+        e, s = eye.to_c(), shadow.to_c()
+        lib = _lib()
+        abi.check(lib, lib.rtm_group_render_async(self._h, C.byref(sc), C.byref(e), C.byref(s), width, height,
+                                                  steps, flags, fmt, root, C.c_void_p(out_ptr)),
+                  "rtm_group_render_async")
+
+    def synchronize(self, timeout_ms: int = 0):
+        lib = _lib()
+        abi.check(lib, lib.rtm_group_synchronize(self._h, timeout_ms), "rtm_group_synchronize")
+
+    def close(self):
+        if self._h:
+            _lib().rtm_group_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def encode_thresholds() -> np.ndarray:

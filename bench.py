@@ -10,8 +10,18 @@ Modes (--mode):
                r, r+N, ... of the orbiting-sphere sequence; each frame is
                independent, no data-path collective ("scaling": "weak").
   tile-gather  one frame per step, rows split into N bands, each rank renders
-               its band, then ONE RCCL gather assembles the RGBA f32 frame on
-               rank 0 ("scaling": "strong").
+               its band, then ONE RCCL gather (librtm's rtm_group, RCCL over
+               xGMI) assembles the frame in rank 0's device memory
+               ("scaling": "strong").  --format picks what is gathered: the
+               RGBA f32 frame (16 B/px) or writeColorImage's bytes (RGBA8,
+               4 B/px, encoded in the eye pass's epilogue).
+
+Whatever the mode, the line also carries `tile_gather`: the strong-scaling
+tile-partitioned frame (the north star's assembled framebuffer) measured in the
+same run for RGBA f32 and RGBA8, so every N of a scaling sweep reports both the
+weak (frames) and the strong (tile-gather) figure.  With --dist-backend gloo
+(several ranks rehearsing on one GPU) the bands are gathered on the CPU by gloo
+instead of RCCL.
 """
 from __future__ import annotations
 
@@ -48,9 +58,138 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=1)
     ap.add_argument("--no-alt", action="store_true", help="skip the secondary fused-shadow measurement")
     ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
-                    help="nccl (= RCCL, the multi-GPU run); gloo only to rehearse the N>1 frames path "
-                         "with several ranks on one GPU (timing tensors on the CPU)")
+                    help="nccl (= RCCL, the multi-GPU run); gloo only to rehearse the N>1 paths "
+                         "with several ranks on one GPU (timing tensors and tile-gather bands on the CPU)")
+    ap.add_argument("--format", choices=["rgba32f", "rgba8"], default="rgba32f",
+                    help="tile-gather mode: what is rendered and gathered")
+    ap.add_argument("--tile-gather-steps", type=int, default=200,
+                    help="frames of the secondary tile-gather measurement (0 = skip it)")
+    # The clocks ramp for tens of ms after an idle GPU: a time-based pre-roll before the
+    # counted warmup makes a short --steps/--warmup run read the steady state.
+    ap.add_argument("--preroll-ms", type=float, default=300.0)
+    ap.add_argument("--no-host-output", action="store_true",
+                    help="skip the secondary host-output (PCIe-inclusive drop-in) measurement")
     return ap.parse_args()
+
+
+FORMATS = {"rgba32f": 0, "rgba8": 1}
+
+
+def tile_gather(rtm, lib, ctx, group, world, rank, dist, tdev, c_scenes, eye, shadow, W, H, K, flags, fmt, steps,
+                warmup, timeout_ms=120000):
+    """The tile-partitioned frame: N row bands, one gather into rank
+    0.  RCCL (librtm rtm_group) with the nccl backend; with gloo the bands go to the
+    CPU and gloo gathers them (the rehearsal of this path on one GPU)."""
+    import ctypes as C
+    import torch
+
+    shard = importlib.import_module("2018rustraytracer_amd.shard")
+    bpp = rtm.abi.FORMAT_BYTES[fmt]
+    dev = torch.device("cuda", torch.cuda.current_device())
+    r0, r1 = shard.row_band(H, world, rank)
+    e_c, s_c = eye.to_c(), shadow.to_c()
+    if group is not None:
+        outs = ([torch.empty(W * H * bpp, dtype=torch.uint8, device=dev) for _ in range(2)] if rank == 0
+                else [None, None])
+
+        def step(i):
+            sc_c = c_scenes[i % len(c_scenes)][0]
+            ptr = outs[i % 2].data_ptr() if rank == 0 else 0
+            rc = lib.rtm_group_render_async(group.handle, C.byref(sc_c), C.byref(e_c), C.byref(s_c), W, H, K, flags,
+                                            fmt, 0, C.c_void_p(ptr))
+            rtm.abi.check(lib, rc, "rtm_group_render_async")
+
+        def drain():
+            group.synchronize(timeout_ms)
+    else:
+        band = shard.band_rows(H, world)
+        dbuf = torch.empty(max(r1 - r0, 1) * W * bpp, dtype=torch.uint8, device=dev)
+        hbuf = torch.zeros(band * W * bpp, dtype=torch.uint8)
+        fl = flags | (rtm.abi.RTM_FLAG_FUSED_SHADOW if world > 1 else 0)
+
+        def step(i):
+            sc_c = c_scenes[i % len(c_scenes)][0]
+            if r1 > r0:
+                rc = lib.rtm_render_rows_async(ctx.handle, C.byref(sc_c), C.byref(e_c), C.byref(s_c), W, H, K, fl,
+                                               fmt, r0, r1, C.c_void_p(dbuf.data_ptr()))
+                rtm.abi.check(lib, rc, "rtm_render_rows_async")
+                ctx.synchronize()
+                hbuf[: (r1 - r0) * W * bpp].copy_(dbuf[: (r1 - r0) * W * bpp])
+            if world > 1:
+                shard.gather_bands(hbuf.view(band, W * bpp), rank, world, H, dist)
+
+        def drain():
+            ctx.synchronize()
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    for i in range(warmup):
+        step(i)
+    drain()
+    barrier()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        step(warmup + i)
+    drain()
+    barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=tdev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    r00, r01 = shard.row_band(H, world, 0)
+    return {"value": round(W * H * steps / el / 1e6, 2), "unit": "Mpixels/s", "frames": steps,
+            "ms_per_step": round(el / steps * 1e3, 5), "scaling": "strong",
+            "format": {0: "RGBA32F", 1: "RGBA8", 2: "RGB8"}[fmt], "bytes_per_pixel": bpp,
+            "root_ingress_bytes_per_frame": int(W * (H - (r01 - r00)) * bpp),
+            "gather": ("RCCL: ncclSend/ncclRecv in one group into rank 0's device buffer (librtm rtm_group)"
+                       if group is not None else "gloo gather of CPU-staged bands (rehearsal, not RCCL)"),
+            "shadow": ("fused: each band evaluates the shadow texels it reads" if world > 1 or flags & 4
+                       else "two-pass (one band: the whole shadow map)")}
+
+
+def make_group(rtm, world, rank, local, dist, backend):
+    """librtm's RCCL group: ncclCommInitAll at N = 1, one rank per process otherwise
+    (the 128-byte id from rank 0, handed over by torch.distributed)."""
+    import torch
+    if backend != "nccl":
+        return None
+    if world == 1:
+        return rtm.Group(n_devices=1, devices=[local])
+    uid = torch.zeros(128, dtype=torch.uint8, device=f"cuda:{local}")
+    if rank == 0:
+        uid.copy_(torch.frombuffer(bytearray(rtm.Group.unique_id()), dtype=torch.uint8))
+    dist.broadcast(uid, src=0)
+    return rtm.Group(device=local, n_ranks=world, rank=rank, uid=bytes(uid.cpu().numpy().tobytes()))
+
+
+def host_output(rtm, scene, eye, shadow, W, H, K, flags, frames=8):
+    """The drop-in's host-output rate (PCIe included; never `value`): rtm_render_ex
+    into pageable and registered host memory, RGBA f32 and writeColorImage's RGB8."""
+    import numpy as np
+    res = {}
+    for fmt, name in ((0, "rgba32f"), (2, "rgb8")):
+        for reg in (False, True):
+            buf = np.empty((H, W, 4), np.float32) if fmt == 0 else np.empty((H, W, 3), np.uint8)
+            r = rtm.HostRegistration(buf) if reg else None
+            try:
+                rtm.render_frame_ex(scene, eye, shadow, W, H, K, flags, fmt, out=buf)
+                t0 = time.perf_counter()
+                for _ in range(frames):
+                    rtm.render_frame_ex(scene, eye, shadow, W, H, K, flags, fmt, out=buf)
+                el = (time.perf_counter() - t0) / frames
+            finally:
+                if r is not None:
+                    r.close()
+            res[f"{name}_{'registered' if reg else 'pageable'}"] = {
+                "value": round(W * H / el / 1e6, 2), "unit": "Mpixels/s", "ms_per_frame": round(el * 1e3, 4),
+                "bytes_per_frame": int(buf.nbytes), "GB_per_s": round(buf.nbytes / el / 1e9, 2)}
+    res["note"] = ("rtm_render_ex: blocking, the frame copied to host memory by every call, one frame at a time "
+                   f"({frames} frames); registered = a buffer pinned once with rtm_host_register (direct DMA)")
+    return res
 
 
 def _latest_traffic(cfg_id: int, kernel: str):
@@ -126,7 +265,6 @@ def main():
         if a.dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
-            assert a.mode == "frames", "gloo rehearsal covers the frames mode only"
             dist.init_process_group("gloo")
     tdev = f"cuda:{local}" if a.dist_backend == "nccl" else "cpu"  # where the timing reductions run
 
@@ -136,11 +274,13 @@ def main():
     metrics = importlib.import_module("2018rustraytracer_amd.metrics")
     cfg = sc.CONFIGS[a.config]
     W, H, K = cfg["width"], cfg["height"], cfg["steps"]
+    tile_mode = a.mode == "tile-gather"
     # tile-gather: each band evaluates only the shadow texels it reads (no cross-rank shadow map)
-    fused = a.fused or a.mode == "tile-gather"
+    fused = a.fused or tile_mode
     flags = cfg["flags"] | (rtm.abi.RTM_FLAG_FUSED_SHADOW if fused else 0)
-    eye, shadow = cfg.get("eye", sc.eye_camera)(), sc.shadow_camera()
+    eye, shadow = cfg.get("eye", sc.eye_camera)(), cfg.get("shadow", sc.shadow_camera)()
     ctx = rtm.Context(local)
+    lib = rtm.load_library()
     # kernel durations: HIP events on every TIMING_STRIDE-th frame of the timed region
     # (an event is a barrier packet; timing every frame would cost ~15% throughput)
     timing_stride = 10
@@ -153,89 +293,111 @@ def main():
             return sc.closely_orbiting_sphere(100 + frame_index)
         return sc.scene_a_bench(100 + frame_index)
 
-    total = a.warmup + a.steps
-    if a.mode == "frames":
-        # inputs prepared before the timed region: one scene per frame this rank renders
-        scenes = [scene_for(i * world + rank) for i in range(total)]
-        c_scenes = [s.to_c() for s in scenes]
-        # a ring of output frames (a renderer's swap chain): consecutive frames write
-        # different buffers, so the library may run them side by side (rtm_api.cpp
-        # frame_lanes); 12 covers any lane count 1-4 without two lanes sharing one
-        ring = [torch.empty((H, W, 4), dtype=torch.float32, device=f"cuda:{local}") for _ in range(12)]
-        out = ring[0]
-        rows = (0, H)
-    else:
-        band = shard.band_rows(H, world)
-        rows = shard.row_band(H, world, rank)
-        scenes = [scene_for(i) for i in range(total)]
-        c_scenes = [s.to_c() for s in scenes]
-        bufs = [torch.zeros((band, W, 4), dtype=torch.float32, device=f"cuda:{local}") for _ in range(2)]
-        ext = torch.cuda.ExternalStream(ctx.stream, device=torch.device("cuda", local))
-
-    lib = rtm.load_library()
-    import ctypes as C
-    e_c, s_c = eye.to_c(), shadow.to_c()
-    pending = [None, None]
-
-    def step(i: int):
-        sc_c = c_scenes[i][0]
-        if a.mode == "frames":
-            rc = lib.rtm_render_async(ctx.handle, C.byref(sc_c), C.byref(e_c), C.byref(s_c), W, H, K, flags,
-                                      0, H, C.c_void_p(out.data_ptr()))
-            rtm.abi.check(lib, rc, "rtm_render_async")
-            return
-        b = i % 2
-        with torch.cuda.stream(ext):
-            if pending[b] is not None:
-                pending[b].wait()  # the ctx stream waits until the gather reading bufs[b] is done
-            if rows[1] > rows[0]:
-                rc = lib.rtm_render_async(ctx.handle, C.byref(sc_c), C.byref(e_c), C.byref(s_c), W, H, K,
-                                          flags, rows[0], rows[1], C.c_void_p(bufs[b].data_ptr()))
-                rtm.abi.check(lib, rc, "rtm_render_async")
-            if world > 1:
-                pending[b], _ = shard.gather_bands(bufs[b], rank, world, H, dist, async_op=True)
-
     def barrier():
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
 
-    sequence = a.mode == "frames" and not a.per_frame_calls and not fused
+    def max_over_ranks(v: float) -> float:
+        if world == 1:
+            return v
+        t = torch.tensor([v], dtype=torch.float64, device=tdev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    total = a.warmup + a.steps
+    # inputs prepared before the timed region: one scene per frame this rank renders
+    # (frames mode: frames rank, rank+N, ...; tile-gather: every rank renders a band of every frame)
+    scenes = [scene_for(i if tile_mode else i * world + rank) for i in range(total)]
+    c_scenes = [s.to_c() for s in scenes]
+    group = make_group(rtm, world, rank, local, dist, a.dist_backend) if (tile_mode or a.tile_gather_steps) else None
+
+    # a ring of output frames (a renderer's swap chain): consecutive frames write
+    # different buffers, so the library may run them side by side (rtm_api.cpp
+    # frame_lanes puts frame i on lane (n-1-i) % L: the ring must be a multiple of L)
+    lanes_env = int(os.environ.get("RTM_LANES", "0") or 0)
+    n_ring = 12 if lanes_env in (0, 1, 2, 3, 4, 6) else lanes_env * ((12 + lanes_env - 1) // lanes_env)
+    ring = ([torch.empty((H, W, 4), dtype=torch.float32, device=f"cuda:{local}") for _ in range(n_ring)]
+            if not tile_mode else [])
+    sequence = not tile_mode and not a.per_frame_calls and not fused
     pipelined = sequence and os.environ.get("RTM_PIPELINE", "0") not in ("", "0")
+
+    import ctypes as C
+    e_c, s_c = eye.to_c(), shadow.to_c()
+
+    def frames_step(i: int):  # --per-frame-calls / --fused: one rtm_render_async per frame
+        rc = lib.rtm_render_async(ctx.handle, C.byref(c_scenes[i][0]), C.byref(e_c), C.byref(s_c), W, H, K, flags,
+                                  0, H, C.c_void_p(ring[i % n_ring].data_ptr()))
+        rtm.abi.check(lib, rc, "rtm_render_async")
+
     if sequence:
         # the whole timed region is ONE rtm_render_frames_async call over the animation
         # frames (two kernels per frame; with RTM_PIPELINE=1 the software-pipelined launch)
         warm = ctx.prepare_frames(scenes[:a.warmup])
         timed = ctx.prepare_frames(scenes[a.warmup:])
-        outp = [ring[i % len(ring)].data_ptr() for i in range(max(a.warmup, a.steps))]
+        outp = [ring[i % n_ring].data_ptr() for i in range(max(a.warmup, a.steps, 1))]
 
-    if sequence:
-        if a.warmup:
-            ctx.render_frames_async([0] * a.warmup, eye, shadow, W, H, K, flags, outp[:a.warmup], warm)
+    # clock ramp: frames for at least --preroll-ms of wall time before the counted warmup
+    preroll_frames, t_pre = 0, time.perf_counter()
+    while (time.perf_counter() - t_pre) * 1e3 < a.preroll_ms and not tile_mode:
+        n_pre = min(20, total)
+        if sequence:
+            ctx.render_frames_async([0] * n_pre, eye, shadow, W, H, K, flags, outp[:n_pre],
+                                    ctx.prepare_frames(scenes[:n_pre]))
+        else:
+            for i in range(n_pre):
+                frames_step(i)
+        ctx.synchronize()
+        preroll_frames += n_pre
+    preroll = {"ms": round((time.perf_counter() - t_pre) * 1e3, 1), "frames": preroll_frames,
+               "note": "untimed frames before the counted warmup, so the clocks have ramped (time-based)"}
+
+    tg_primary = None
+    if tile_mode:
+        fmt = FORMATS[a.format]
+        t_pre = time.perf_counter()
+        while (time.perf_counter() - t_pre) * 1e3 < a.preroll_ms:  # clock ramp
+            tile_gather(rtm, lib, ctx, group, world, rank, dist, tdev, c_scenes, eye, shadow, W, H, K, flags, fmt,
+                        50, 0)
+            preroll_frames += 50
+        preroll["ms"], preroll["frames"] = round((time.perf_counter() - t_pre) * 1e3, 1), preroll_frames
+        tg_primary = tile_gather(rtm, lib, ctx, group, world, rank, dist, tdev, c_scenes, eye, shadow, W, H, K,
+                                 flags, fmt, a.steps, a.warmup)
+        elapsed = tg_primary["ms_per_step"] * a.steps / 1e3
     else:
-        for i in range(a.warmup):
-            step(i)
-    barrier()
-    ctx.set_timing_stride(timing_stride)  # restarts the stride count: launch 0 of the timed region is timed
-    t0 = time.perf_counter()
-    if sequence:
-        ctx.render_frames_async([0] * a.steps, eye, shadow, W, H, K, flags, outp[:a.steps], timed)
-    else:
-        for i in range(a.warmup, total):
-            step(i)
-    for p in pending:
-        if p is not None:
-            p.wait()
-    barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=tdev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        if sequence:
+            if a.warmup:
+                ctx.render_frames_async([0] * a.warmup, eye, shadow, W, H, K, flags, outp[:a.warmup], warm)
+        else:
+            for i in range(a.warmup):
+                frames_step(i)
+        barrier()
+        ctx.set_timing_stride(timing_stride)  # restarts the stride count: launch 0 of the timed region is timed
+        t0 = time.perf_counter()
+        if sequence:
+            ctx.render_frames_async([0] * a.steps, eye, shadow, W, H, K, flags, outp[:a.steps], timed)
+        else:
+            for i in range(a.warmup, total):
+                frames_step(i)
+        barrier()
+        elapsed = max_over_ranks(time.perf_counter() - t0)
 
     # per-kernel HIP-event durations over the timed region (ctx stream)
     n_launches = a.steps + 1 if pipelined else a.steps
     sh_ms, eye_ms = ctx.kernel_ms_history((n_launches + timing_stride - 1) // timing_stride)
+    if tile_mode:  # the group's own contexts ran the bands: one timed pass of rank 0's band on ctx
+        ctx.set_timing_capacity(1)
+        r0, r1 = shard.row_band(H, world, rank)
+        if r1 > r0:
+            tmp = torch.empty(((r1 - r0) * W * rtm.abi.FORMAT_BYTES[FORMATS[a.format]] + 15) // 16 * 4,
+                              dtype=torch.float32, device=f"cuda:{local}")
+            for _ in range(3):
+                ctx.render_rows_async(scenes[0], eye, shadow, W, H, K, flags | (0 if world == 1 else 4),
+                                      FORMATS[a.format], tmp.data_ptr(), r0, r1)
+            ctx.synchronize()
+            sh_ms, eye_ms = ctx.kernel_ms_history(1)
+        else:
+            sh_ms, eye_ms = [0.0], [0.0]
 
     # With several lanes (rtm_ctx_set_lanes: independent frames on side-by-side
     # streams) the kernels of the timed region overlap, and each event duration is
@@ -274,24 +436,40 @@ def main():
     alt_fused = None
     if sequence and not pipelined and not a.no_alt:
         fflags = flags | rtm.abi.RTM_FLAG_FUSED_SHADOW
-        ctx.set_timing_capacity(1)
+        ctx.set_timing_capacity(max(1, a.steps // timing_stride))
         ctx.render_frames_async([0] * min(a.warmup, 5), eye, shadow, W, H, K, fflags, outp[:min(a.warmup, 5)],
                                 ctx.prepare_frames(scenes[:min(a.warmup, 5)]))
         barrier()
+        ctx.set_timing_stride(timing_stride)
         t1 = time.perf_counter()
         ctx.render_frames_async([0] * a.steps, eye, shadow, W, H, K, fflags, outp[:a.steps], timed)
         barrier()
-        el_f = time.perf_counter() - t1
-        if world > 1:
-            t = torch.tensor([el_f], dtype=torch.float64, device=tdev)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            el_f = float(t.item())
+        el_f = max_over_ranks(time.perf_counter() - t1)
+        _, f_eye = ctx.kernel_ms_history((a.steps + timing_stride - 1) // timing_stride)
         alt_fused = {"value": round(W * H * a.steps * world / el_f / 1e6, 2), "unit": "Mpixels/s",
                      "ms_per_step": round(el_f / a.steps * 1e3, 5),
+                     "fused_eye_pass_ms_in_lanes": round(sum(f_eye) / max(len(f_eye), 1), 5),
+                     "lanes": ctx.last_lanes(),
                      "note": "RTM_FLAG_FUSED_SHADOW (shadow texels evaluated on demand in the eye pass, "
                              "bit-identical image); secondary measurement, not the headline value"}
-    if rows[1] <= rows[0]:
-        sh_ms, eye_ms = [0.0], [0.0]
+
+    # Secondary: the tile-partitioned, gathered frame (strong scaling) in RGBA f32 and RGBA8
+    tile = None
+    if not tile_mode and a.tile_gather_steps > 0:
+        tile = {}
+        tg_scenes = [scene_for(i) for i in range(min(total, 64))]
+        tg_c = [s.to_c() for s in tg_scenes]
+        tflags = cfg["flags"]
+        for name, fmt in FORMATS.items():
+            try:
+                tile[name] = tile_gather(rtm, lib, ctx, group, world, rank, dist, tdev, tg_c, eye, shadow, W, H, K,
+                                         tflags, fmt, a.tile_gather_steps, min(20, a.tile_gather_steps))
+            except Exception as ex:  # a failed secondary measurement must not lose the headline line
+                tile[name] = {"error": str(ex)[:300]}
+                break
+    if group is not None:
+        group.close()
+
     pipe_ms = None
     if pipelined:
         # sampled launches j = 0, stride, 2*stride, ...: j = 0 is the prologue shadow pass,
@@ -303,10 +481,15 @@ def main():
         avg_sh = sum(sh_ms) / max(len(sh_ms), 1)
         avg_eye = sum(eye_ms) / max(len(eye_ms), 1)
 
+    host = None
+    if rank == 0 and world == 1 and not a.no_host_output and a.config == 3:
+        host = host_output(rtm, scenes[0], eye, shadow, W, H, K, cfg["flags"])
+
     if rank == 0:
-        pixels = W * H * a.steps * (world if a.mode == "frames" else 1)
+        rows = shard.row_band(H, world, rank) if tile_mode else (0, H)
+        pixels = W * H * a.steps * (1 if tile_mode else world)
         value = pixels / elapsed / 1e6
-        s0 = scenes[a.warmup]
+        s0 = scenes[a.warmup] if a.warmup < len(scenes) else scenes[0]
         band_h = rows[1] - rows[0]
         st = ctx.stats(s0, eye, shadow, W, H, K, flags)
         sep = metrics.shared_z_separable(shadow)
@@ -340,7 +523,7 @@ def main():
             roof_other = (metrics.roofline(other, work, other_ms, _latest_traffic(a.config, other))
                           if other_ms > 0 else None)
         res = {
-            "metric": METRIC if a.config <= 5 else METRIC_F1 if a.config <= 7 else METRIC_F4,
+            "metric": cfg.get("metric", METRIC if a.config <= 5 else METRIC_F1 if a.config <= 7 else METRIC_F4),
             "value": round(value, 2),
             "unit": "Mpixels/s",
             "n_gpus": world,
@@ -348,18 +531,19 @@ def main():
             "warmup": a.warmup,
             "ms_per_step": round(elapsed / a.steps * 1e3, 5),
             "higher_is_better": True,
-            "scaling": "weak" if a.mode == "frames" else "strong",
+            "scaling": "strong" if tile_mode else "weak",
             "vs_baseline": None,
             "dtype": "f64",
             "data": ("synthetic: Scene A-bench (SURVEY.md §8d-2) animation frames 100+i, f64 scene built on host"
                      if a.config in (2, 3, 4) else "synthetic: SURVEY.md §8d-2 scene" if a.config <= 5
                      else "synthetic: row f-1 scene (scenes.py), f64 scene built on host" if a.config <= 7
-                     else "synthetic: row f-4 Scene S-bench (scenes.py), f64 scene built on host"),
+                     else "synthetic: row f-4 Scene S-bench (scenes.py), f64 scene built on host" if a.config == 8
+                     else "synthetic: " + cfg["desc"]),
             "config": {"workload": cfg["desc"], "config_id": a.config, "width": W, "height": H,
                        "march_steps": K, "mode": a.mode, "shadow": "fused" if fused else "two-pass",
                        "pipelined": pipelined,
-                       "parallelism": (f"frame-parallel x{world}" if a.mode == "frames"
-                                       else f"row-bands x{world} + rccl gather"),
+                       "parallelism": (f"frame-parallel x{world}" if not tile_mode
+                                       else f"row-bands x{world} + one gather ({a.format})"),
                        "rows_rank0": band_h},
             "kernels": ({"frame_pipe_ms": round(pipe_ms, 5), "prologue_shadow_pass_ms": round(avg_sh, 5),
                          "note": "launch j = shadow pass of frame j + eye pass of frame j-1"}
@@ -372,9 +556,13 @@ def main():
             "lanes": lanes,
             "kernels_in_lanes": in_lanes,
             "one_lane": one_lane,
+            "preroll": preroll,
             "alt_fused_shadow": alt_fused,
+            "tile_gather": tg_primary if tile_mode else tile,
+            "host_output": host,
             "parity": ("bit-exact vs CPU oracle (tests/test_gpu_parity.py)" if a.config <= 5
-                       else "bit-exact vs CPU oracle (tests/test_raytrace.py)"),
+                       else "bit-exact vs CPU oracle (tests/test_raytrace.py)" if a.config <= 8
+                       else "bit-exact vs CPU oracle (tests/test_general_march.py)"),
         }
         if world == 1 and not a.no_cpu_baseline:
             what = ("Scene A-bench frame 100" if a.config in (2, 3, 4) else cfg["desc"].split(", ", 1)[1])

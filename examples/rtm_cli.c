@@ -7,13 +7,25 @@
  * image, so this program is the compiled, linked proof that the boundary is a
  * plain C ABI: it includes only rtm.h and links only librtm.so.
  *
- *   rtm_cli [-w W] [-h H] [-k STEPS] [-f FIRST_FRAME] [-n FRAMES] [-b]
- *           [--ppm PATH] [--raw PATH]
+ *   rtm_cli [-s SCENE] [-w W] [-h H] [-k STEPS] [-f FIRST_FRAME] [-n FRAMES] [-b]
+ *           [--ppm PATH] [--ppm-gpu PATH] [--raw PATH]
  *
+ *   -s SCENE    orbit   testscene_closelyOrbitingSphere (main.rs:1468-1633, default)
+ *               plane0  testscene_raytracingPlane0, main()'s default scene
+ *                       (main.rs:910-1046, 1652): one capped cylinder, PERSPECTIVE eye
+ *               plane0-disc  the same with the circle plane it has commented out
+ *                       (main.rs:916-929)
+ *               persp1  testscene_perspectiveSimple1 (main.rs:1059-1182)
+ *               persp2  testscene_perspectiveSimple2 (main.rs:1184-1316)
+ *               The non-orbit scenes have their shadow passes commented out in the
+ *               reference (main.rs:998-1003, 1115-1120): RTM_FLAG_NO_MARCH |
+ *               RTM_FLAG_NO_SHADOW_RASTER, and -k is ignored.
  *   -b          Scene A-bench's tilted patch instead of the
  *               reference's hard-coded one (main.rs:2024-2029)
  *   --ppm PATH  writeColorImage of the last frame (P3 text, main.rs:660-704),
  *               encoded on the host from rtm_encode_thresholds
+ *   --ppm-gpu PATH  the same file from the library's RGB8 output format
+ *               (rtm_render_ex, RTM_FORMAT_RGB8: the encode runs in the eye pass)
  *   --raw PATH  the last frame's RGBA f32 bytes (row-major y*W+x)
  *
  * Prints one line per run: frames, seconds, Mpixels/s of rtm_render (blocking,
@@ -93,6 +105,79 @@ static int write_ppm(const char* path, const float* rgba, int w, int h) {
     return fclose(f);
 }
 
+/* normalize (main.rs:105-108): v.scale(1.0 / |v|) */
+static void normalize3(double v[3]) {
+    const double m = sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
+    const double inv = 1.0 / m;
+    for (int k = 0; k < 3; k++) v[k] = v[k] * inv;
+}
+
+/* viewport0's PERSPECTIVE camera (main.rs:1016-1027; perspectiveSimple2 moves it to y = 1.5, main.rs:1283-1295) */
+static void persp_camera(rtm_camera* c, double py) {
+    memset(c, 0, sizeof *c);
+    c->type = RTM_CAMERA_PERSPECTIVE;
+    c->pos[1] = py;
+    c->dir[2] = 1.0;
+    c->up[1] = 1.0;
+    c->side[0] = 1.0;
+}
+
+/* the non-orbit scenes: testscene_raytracingPlane0 (main.rs:931-943 cylinder, 916-929 disc)
+ * and testscene_perspectiveSimple1/2 (main.rs:1069-1080, 1196-1221) */
+static int other_scene(const char* name, rtm_scene* sc, rtm_sphere sph[2], rtm_capped_cylinder* cyl,
+                       rtm_circle_plane* disc, rtm_camera* eye) {
+    memset(sc, 0, sizeof *sc);
+    persp_camera(eye, 0.0);
+    if (!strcmp(name, "plane0") || !strcmp(name, "plane0-disc")) {
+        memset(cyl, 0, sizeof *cyl);
+        cyl->pa[0] = 0.01, cyl->pa[1] = 10.01, cyl->pa[2] = 10.01;
+        cyl->pb[0] = 0.01, cyl->pb[1] = 0.01, cyl->pb[2] = 10.01;
+        cyl->ra = 0.3, cyl->rb = 0.2;
+        cyl->color[0] = 1.0, cyl->color[1] = 0.02, cyl->color[2] = 0.02;
+        sc->capped_cylinders = cyl;
+        sc->n_capped_cylinders = 1;
+        if (!strcmp(name, "plane0-disc")) {
+            memset(disc, 0, sizeof *disc);
+            disc->pos[0] = 0.01, disc->pos[1] = 0.01, disc->pos[2] = 2.0;
+            disc->n[0] = -1.0, disc->n[1] = 0.0, disc->n[2] = 1.0;
+            normalize3(disc->n);
+            disc->radius = 0.5;
+            disc->color[0] = 0.02, disc->color[1] = 0.02, disc->color[2] = 1.0;
+            sc->circle_planes = disc;
+            sc->n_circle_planes = 1;
+        }
+        return 0;
+    }
+    if (!strcmp(name, "persp1") || !strcmp(name, "persp2")) {
+        memset(sph, 0, 2 * sizeof *sph);
+        for (int i = 0; i < 2; i++) {
+            sph[i].id = i;
+            sph[i].pos[0] = 0.01, sph[i].pos[1] = 0.01, sph[i].pos[2] = i ? 6.0 : 4.0;
+            sph[i].r = 0.5;
+            sph[i].color[0] = 0.02, sph[i].color[1] = i ? 1.0 : 0.02, sph[i].color[2] = i ? 0.02 : 1.0;
+        }
+        sc->spheres = sph;
+        sc->n_spheres = strcmp(name, "persp1") ? 2 : 1;
+        if (!strcmp(name, "persp2")) persp_camera(eye, 1.5);
+        return 0;
+    }
+    return -1;
+}
+
+static int write_ppm_rgb8(const char* path, const uint8_t* rgb, int w, int h) {
+    FILE* f = fopen(path, "wb");
+    if (!f) return -1;
+    fprintf(f, "P3\n%d %d\n255\n", w, h);
+    for (int y = 0; y < h; y++) {
+        for (int x = 0; x < w; x++) {
+            const uint8_t* p = rgb + ((size_t)y * w + x) * 3;
+            fprintf(f, "%d %d %d  ", p[0], p[1], p[2]);
+        }
+        fputc('\n', f);
+    }
+    return fclose(f);
+}
+
 static double now(void) {
     struct timespec ts;
     clock_gettime(CLOCK_MONOTONIC, &ts);
@@ -101,7 +186,7 @@ static double now(void) {
 
 int main(int argc, char** argv) {
     int w = 512, h = 512, steps = 500, first = 0, frames = 1, bench_patch = 0;
-    const char *ppm = NULL, *raw = NULL;
+    const char *ppm = NULL, *ppm_gpu = NULL, *raw = NULL, *scene_name = "orbit";
     for (int i = 1; i < argc; i++) {
         const char* a = argv[i];
         const int more = i + 1 < argc;
@@ -111,10 +196,14 @@ int main(int argc, char** argv) {
         else if (!strcmp(a, "-f") && more) first = atoi(argv[++i]);
         else if (!strcmp(a, "-n") && more) frames = atoi(argv[++i]);
         else if (!strcmp(a, "-b")) bench_patch = 1;
+        else if (!strcmp(a, "-s") && more) scene_name = argv[++i];
+        else if (!strcmp(a, "--ppm-gpu") && more) ppm_gpu = argv[++i];
         else if (!strcmp(a, "--ppm") && more) ppm = argv[++i];
         else if (!strcmp(a, "--raw") && more) raw = argv[++i];
         else {
-            fprintf(stderr, "usage: %s [-w W] [-h H] [-k STEPS] [-f FIRST] [-n FRAMES] [-b] [--ppm P] [--raw P]\n",
+            fprintf(stderr,
+                    "usage: %s [-s orbit|plane0|plane0-disc|persp1|persp2] [-w W] [-h H] [-k STEPS] [-f FIRST] "
+                    "[-n FRAMES] [-b] [--ppm P] [--ppm-gpu P] [--raw P]\n",
                     argv[0]);
             return 2;
         }
@@ -132,20 +221,38 @@ int main(int argc, char** argv) {
     camera(&shadow, 0.0, 0.0, 0.0, 1.0, 0.0, 1.0, 0.0, 1.0, 0.0, 0.0);
     camera(&eye, -1.0, 1.0, 0.0, 0.0, 0.0, 1.0, 0.0, 0.0, 0.0, 1.0);
     const rtm_patch patch = bench_patch ? (rtm_patch){0.3, 2.1, 0.9, 2.7} : (rtm_patch){0.1, 0.1, 0.1, 0.1};
+    const int orbit = !strcmp(scene_name, "orbit");
+    rtm_scene other;
+    rtm_sphere osph[2];
+    rtm_capped_cylinder ocyl;
+    rtm_circle_plane odisc;
+    int flags = 0;
+    if (!orbit) {
+        if (other_scene(scene_name, &other, osph, &ocyl, &odisc, &eye)) {
+            fprintf(stderr, "unknown scene %s\n", scene_name);
+            return 2;
+        }
+        flags = RTM_FLAG_NO_MARCH | RTM_FLAG_NO_SHADOW_RASTER;
+        steps = 0;
+    }
     float* img = (float*)malloc((size_t)w * h * 4 * sizeof(float));
     if (!img) return 1;
     double t0 = 0.0;
+    rtm_scene sc;
+    rtm_sphere sph[3];
     for (int i = 0; i < frames; i++) {
-        rtm_sphere sph[3];
-        scene_a(first + i, sph);
-        rtm_scene sc;
-        memset(&sc, 0, sizeof sc);
-        sc.spheres = sph;
-        sc.n_spheres = 3;
-        sc.patches = &patch;
-        sc.n_patches = 1;
+        if (orbit) {
+            scene_a(first + i, sph);
+            memset(&sc, 0, sizeof sc);
+            sc.spheres = sph;
+            sc.n_spheres = 3;
+            sc.patches = &patch;
+            sc.n_patches = 1;
+        } else {
+            sc = other;
+        }
         if (i == 1 || frames == 1) t0 = now(); /* frame 0 pays the context/table set-up when frames > 1 */
-        const int rc = rtm_render(&sc, &eye, &shadow, w, h, steps, 0, img);
+        const int rc = rtm_render(&sc, &eye, &shadow, w, h, steps, flags, img);
         if (rc != RTM_OK) {
             fprintf(stderr, "rtm_render: %d (%s)\n", rc, rtm_last_error());
             free(img);
@@ -154,10 +261,24 @@ int main(int argc, char** argv) {
     }
     const double dt = now() - t0;
     const int timed = frames > 1 ? frames - 1 : 1;
-    printf("{\"frames\": %d, \"width\": %d, \"height\": %d, \"steps\": %d, \"seconds\": %.6f, "
-           "\"mpixels_per_s\": %.2f, \"path\": \"rtm_render (host output)\"}\n",
-           timed, w, h, steps, dt, (double)w * h * timed / dt / 1e6);
+    printf("{\"scene\": \"%s\", \"frames\": %d, \"width\": %d, \"height\": %d, \"steps\": %d, "
+           "\"seconds\": %.6f, \"mpixels_per_s\": %.2f, \"path\": \"rtm_render (host output)\"}\n",
+           scene_name, timed, w, h, steps, dt, (double)w * h * timed / dt / 1e6);
     int rc = 0;
+    if (ppm_gpu) {
+        uint8_t* rgb = (uint8_t*)malloc((size_t)w * h * 3);
+        if (!rgb) rc = 1;
+        else {
+            const int r = rtm_render_ex(&sc, &eye, &shadow, w, h, steps, flags, RTM_FORMAT_RGB8, rgb);
+            if (r != RTM_OK) {
+                fprintf(stderr, "rtm_render_ex: %d (%s)\n", r, rtm_last_error());
+                rc = 1;
+            } else {
+                rc |= write_ppm_rgb8(ppm_gpu, rgb, w, h) != 0;
+            }
+            free(rgb);
+        }
+    }
     if (raw) {
         FILE* f = fopen(raw, "wb");
         rc |= !f || fwrite(img, sizeof(float), (size_t)w * h * 4, f) != (size_t)w * h * 4;

@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define RTM_ABI_VERSION 5
+#define RTM_ABI_VERSION 6
 
 /* ---- limits: scene constants travel as kernel arguments (SGPR path) ---- */
 #define RTM_MAX_SPHERES 16
@@ -58,6 +58,7 @@ extern "C" {
 #define RTM_ERR_HIP -3         /* a HIP runtime call failed */
 #define RTM_ERR_NO_DEVICE -4   /* no usable gfx950 device */
 #define RTM_ERR_OOM -5         /* device allocation failed */
+#define RTM_ERR_COMM -6        /* RCCL unavailable, or a collective failed / timed out (the group is then aborted) */
 
 /* ---- enums (values mirror the reference's enum order) ---- */
 #define RTM_CAMERA_ORTHOGONAL 0 /* EnumCameraType::ORTHOGONAL main.rs:1882 */
@@ -71,6 +72,19 @@ extern "C" {
 #define RTM_FLAG_NO_SHADOW_RASTER 0x2 /* skip the shadow viewport's sphere rasterize (main.rs:1400) */
 #define RTM_FLAG_FUSED_SHADOW 0x4     /* evaluate each shadow texel on demand inside the eye pass
                                          instead of materialising the shadow map; same image bits */
+
+/* ---- frame output formats (ABI v6) ----
+ * RGBA32F: the reference's Map2d<Color32> (main.rs:709-716, 896-898) as RGBA f32,
+ *          alpha 1.0, 16 bytes per pixel (the default everywhere).
+ * RGBA8:   writeColorImage's bytes (main.rs:674-684: clamp, powf(1/2.2), *255 as
+ *          i64) per channel + alpha 255, 4 bytes per pixel, computed in the eye
+ *          pass's epilogue (no f32 frame is written).
+ * RGB8:    the same bytes packed R,G,B: exactly the PPM's pixel data, 3 bytes per
+ *          pixel.
+ * Every byte equals writeColorImage of the RGBA32F frame, bit for bit. */
+#define RTM_FORMAT_RGBA32F 0
+#define RTM_FORMAT_RGBA8 1
+#define RTM_FORMAT_RGB8 2
 
 /* PrimitiveSphere (main.rs:343-349) + Shading (main.rs:336-340). 64 bytes. */
 typedef struct rtm_sphere {
@@ -246,6 +260,26 @@ int rtm_render_multi(const rtm_scene* scene, const rtm_camera* eye, const rtm_ca
                      int32_t width, int32_t height, int32_t march_steps, int32_t flags,
                      float* out_rgba, int32_t n_gpus);
 
+/* ABI v6: rtm_render / rtm_render_multi with an output format (RTM_FORMAT_*):
+ * out_host receives width*height*rtm_format_bytes(format) bytes.  Host buffers
+ * registered with rtm_host_register are written by direct DMA from each device
+ * (rtm_render_multi_ex: the devices' copies run side by side on their own PCIe
+ * links); unregistered (pageable) buffers are copied through the runtime's
+ * staging, one host thread per device. */
+int rtm_render_ex(const rtm_scene* scene, const rtm_camera* eye, const rtm_camera* shadow, int32_t width,
+                  int32_t height, int32_t march_steps, int32_t flags, int32_t format, void* out_host);
+int rtm_render_multi_ex(const rtm_scene* scene, const rtm_camera* eye, const rtm_camera* shadow,
+                        int32_t width, int32_t height, int32_t march_steps, int32_t flags, int32_t format,
+                        void* out_host, int32_t n_gpus);
+/* bytes per pixel of a format (16, 4, 3), 0 for an unknown format */
+int32_t rtm_format_bytes(int32_t format);
+/* Page-lock a caller-owned host buffer for all devices (hipHostRegister,
+ * portable) so frame copies into it are direct DMA; undo with
+ * rtm_host_unregister before freeing it.  A Rust host registers its output
+ * Vec once and renders many frames into it. */
+int rtm_host_register(void* ptr, int64_t bytes);
+int rtm_host_unregister(void* ptr);
+
 /* ---- whole frame, device output (asynchronous on ctx's stream) ----
  * Renders eye rows [row_begin, row_end) into out_rgba_dev (device memory,
  * (row_end-row_begin)*width*4 floats, row-major, row 0 = row_begin).  The
@@ -254,6 +288,11 @@ int rtm_render_async(rtm_ctx* ctx, const rtm_scene* scene, const rtm_camera* eye
                      const rtm_camera* shadow, int32_t width, int32_t height,
                      int32_t march_steps, int32_t flags, int32_t row_begin, int32_t row_end,
                      float* out_rgba_dev);
+/* ABI v6: the same with an output format; out_dev holds (row_end-row_begin)*width
+ * pixels of rtm_format_bytes(format) bytes (RGBA32F: 16-byte aligned). */
+int rtm_render_rows_async(rtm_ctx* ctx, const rtm_scene* scene, const rtm_camera* eye,
+                          const rtm_camera* shadow, int32_t width, int32_t height, int32_t march_steps,
+                          int32_t flags, int32_t format, int32_t row_begin, int32_t row_end, void* out_dev);
 /* A sequence of frames (e.g. the animation of testscene_closelyOrbitingSphere,
  * main.rs:1469), asynchronous on ctx's stream: frame i is scenes[i] rendered
  * into out_rgba_dev[i] (full frames; pointers may repeat), two kernels per
@@ -279,6 +318,55 @@ const double* rtm_ctx_shadow_map(rtm_ctx* ctx);
 int rtm_render_stats(rtm_ctx* ctx, const rtm_scene* scene, const rtm_camera* eye,
                      const rtm_camera* shadow, int32_t width, int32_t height,
                      int32_t march_steps, int32_t flags, rtm_stats* out);
+
+/* ---- multi-GPU frame over RCCL (BASELINE north star) ----
+ * A group is N ranks, one device each, joined by one RCCL communicator.  A frame
+ * is tile-partitioned into N row bands of ceil(H/N) rows (rank r: rows
+ * [r*band, min(H,(r+1)*band))); every rank renders its band (each band evaluates
+ * the shadow texels it reads: RTM_FLAG_FUSED_SHADOW, same image bits), and ONE
+ * gather (ncclSend/ncclRecv in one ncclGroupStart/End, rccl.h:700-745: RCCL's own
+ * ncclGather is this same pattern, but needs equal counts and the last band may
+ * be short) assembles the frame in the root's device buffer.  The root renders
+ * its own band in place; the other ranks' bands go through double-buffered
+ * device staging on a communication stream, so frame i+1 renders while frame i
+ * is in flight.  RCCL is loaded at the first group call (librccl.so.1; the copy
+ * torch.distributed already loaded, if any); without it group calls fail with
+ * RTM_ERR_COMM and nothing else in the library needs it.
+ *
+ * Two ways to form a group:
+ *   rtm_group_create        one process drives devices[0..n-1] (NULL: 0..n-1):
+ *                           ncclCommInitAll (rccl.h:236);
+ *   rtm_group_create_rank   one process per GPU: rank r of n_ranks on `device`,
+ *                           with the 128-byte id rank 0 made by rtm_group_unique_id
+ *                           and handed to the others by the caller (e.g.
+ *                           torch.distributed.broadcast): ncclCommInitRank (rccl.h:220). */
+typedef struct rtm_group rtm_group;
+int rtm_group_unique_id(uint8_t id[128]);
+int rtm_group_create(int32_t n_devices, const int32_t* devices, rtm_group** out);
+int rtm_group_create_rank(int32_t device, int32_t n_ranks, int32_t rank, const uint8_t id[128],
+                          rtm_group** out);
+/* Waits for the group's work, then frees it (communicators destroyed). */
+void rtm_group_destroy(rtm_group* g);
+/* n_ranks in the group, members driven by this process, the first one's rank */
+int rtm_group_info(rtm_group* g, int32_t* n_ranks, int32_t* n_local, int32_t* first_rank);
+/* context of local member i (its device's stream; owned by the group) */
+rtm_ctx* rtm_group_ctx(rtm_group* g, int32_t local);
+/* One frame, tile-partitioned and gathered: out_dev is the root's device buffer of
+ * width*height pixels of rtm_format_bytes(format) bytes, on the root's device
+ * (ignored on a process that does not hold the root).  Asynchronous: the frame is
+ * complete in the root context's stream order.  RGBA8 / RGB8 gather 4 / 3 bytes
+ * per pixel instead of 16. */
+int rtm_group_render_async(rtm_group* g, const rtm_scene* scene, const rtm_camera* eye,
+                           const rtm_camera* shadow, int32_t width, int32_t height, int32_t march_steps,
+                           int32_t flags, int32_t format, int32_t root, void* out_dev);
+/* Wait for every local member's work (renders and transfers).  timeout_ms > 0:
+ * give up after that long, abort the communicators (ncclCommAbort) and return
+ * RTM_ERR_COMM; the group then fails every call but rtm_group_destroy.
+ * timeout_ms <= 0: wait indefinitely. */
+int rtm_group_synchronize(rtm_group* g, int32_t timeout_ms);
+/* Test hook: 1 = the root also stages its band and sends it to itself through
+ * RCCL (exercises the transfer path on a one-device group); 0 = in place (default). */
+int rtm_group_set_root_staging(rtm_group* g, int32_t on);
 
 /* ---- output encoding: writeColorImage (main.rs:660-704), BASELINE row f-2 ----
  * Per channel: c.max(0.0).min(1.0), f32::powf(v, 1.0/2.2), (v * 255.0) as i64,

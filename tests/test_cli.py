@@ -3,7 +3,10 @@ include/rtm.h, links only librtm.so, and renders testscene_closelyOrbitingSphere
 frames the way the reference's driver does (main.rs:1468-1633).  On the GPU its
 frames must be the oracle's bits and hash to the survey's known answers
 (SURVEY.md §8c-3), and its host-encoded PPM must equal the oracle's
-writeColorImage text."""
+writeColorImage text.  Its scene switch (-s) also drives main()'s default scene
+testscene_raytracingPlane0 (main.rs:910-1046, 1652) and
+testscene_perspectiveSimple1/2 (main.rs:1059-1316) through the same ABI, and
+--ppm-gpu writes the PPM from the library's RGB8 output format."""
 import hashlib
 import os
 import subprocess
@@ -16,12 +19,13 @@ from conftest import ROOT, bits_equal, first_mismatch
 CLI = os.path.join(ROOT, "examples", "rtm_cli")
 
 
-@pytest.fixture(scope="module", autouse=True)
-def _cli_built():
-    """build() makes examples/rtm_cli; a tree with librtm.so but no (or a stale) CLI gets it here (gcc, seconds)."""
-    lib = os.path.join(ROOT, "2018rustraytracer_amd", "librtm.so")
-    if os.path.exists(lib):  # make: rebuilds only when the CLI is missing or older than rtm.h / librtm.so
-        subprocess.run(["make", "-C", os.path.join(ROOT, "examples")], check=True, capture_output=True)
+def test_cli_abi_matches_library():
+    """build() relinks examples/rtm_cli on every call (make -B), and the CLI refuses to run
+    against a librtm.so of another ABI version: a stale caller fails loudly."""
+    assert os.path.exists(CLI), "examples/rtm_cli not built: run __graft_entry__.build()"
+    src = open(os.path.join(ROOT, "examples", "rtm_cli.c")).read()
+    assert "rtm_abi_version() != RTM_ABI_VERSION" in src
+    assert os.path.getmtime(CLI) >= os.path.getmtime(os.path.join(ROOT, "include", "rtm.h"))
 
 
 def _sha16_rgb(rgba):
@@ -68,3 +72,32 @@ def test_cli_bench_patch_frames(oracle, scenes, tmp_path):
     got = np.fromfile(raw, dtype=np.float32).reshape(h, w, 4)
     want = oracle.render(scenes.scene_a_bench(102), scenes.eye_camera(), scenes.shadow_camera(), w, h, 64, 0)["rgba"]
     assert bits_equal(got, want), first_mismatch(got, want)
+
+
+SCENES = {  # rtm_cli -s NAME -> (scenes factory, eye camera factory)
+    "plane0": ("raytracing_plane0", "perspective_eye_camera"),
+    "plane0-disc": ("raytracing_plane0_with_plane", "perspective_eye_camera"),
+    "persp1": ("perspective_simple1", "perspective_eye_camera"),
+    "persp2": ("perspective_simple2", "perspective_simple2_camera"),
+}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", list(SCENES))
+def test_cli_scene_switch(oracle, scenes, tmp_path, name):
+    """main()'s default scene and the perspective scenes through the compiled caller:
+    RGBA f32 frame == the oracle's, and both PPMs (host encode, GPU RGB8 format) ==
+    the oracle's writeColorImage text."""
+    raw, ppm, ppm_gpu = tmp_path / "f.raw", tmp_path / "f.ppm", tmp_path / "g.ppm"
+    p = subprocess.run([CLI, "-s", name, "-w", "512", "-h", "512", "--raw", str(raw), "--ppm", str(ppm),
+                        "--ppm-gpu", str(ppm_gpu)], capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0, p.stderr
+    fac, cam = SCENES[name]
+    scene = scenes.raytracing_plane0(True) if fac.endswith("_with_plane") else getattr(scenes, fac)()
+    want = oracle.render(scene, getattr(scenes, cam)(), scenes.shadow_camera(), 512, 512, 0,
+                         scenes.RAYTRACING_FLAGS)["rgba"]
+    got = np.fromfile(raw, dtype=np.float32).reshape(512, 512, 4)
+    assert bits_equal(got, want), first_mismatch(got, want)
+    text = oracle.write_ppm(want)
+    assert ppm.read_bytes() == text
+    assert ppm_gpu.read_bytes() == text

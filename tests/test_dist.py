@@ -83,3 +83,40 @@ def test_frames_for_rank_cover_each_frame_once():
         for world in (1, 2, 8):
             allf = sorted(f for r in range(world) for f in shard.frames_for_rank(n, r, world))
             assert allf == list(range(n))
+
+
+def _run_bench(args, world, timeout=300):
+    import subprocess
+    import sys
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+           "--master-addr", "127.0.0.1", f"--master-port={_free_port()}", os.path.join(ROOT, "bench.py")] + args
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, cwd=ROOT)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    import json
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    return json.loads(lines[0])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fmt", ["rgba32f", "rgba8"])
+def test_bench_tile_gather_gloo_rehearsal_world2(fmt):
+    """bench.py --mode tile-gather end to end with two ranks sharing the box's GPU
+    (gloo gathers the CPU-staged bands; the 8-GPU run uses RCCL): one JSON line,
+    strong scaling, both ranks' pixels counted once."""
+    res = _run_bench(["--gpus", "2", "--dist-backend", "gloo", "--mode", "tile-gather", "--format", fmt,
+                      "--config", "2", "--steps", "6", "--warmup", "2", "--preroll-ms", "0", "--no-cpu-baseline",
+                      "--no-alt"], 2)
+    assert res["n_gpus"] == 2 and res["scaling"] == "strong" and res["value"] > 0
+    assert res["tile_gather"]["format"] == fmt.upper() and "gloo" in res["tile_gather"]["gather"]
+    assert res["config"]["rows_rank0"] == 540
+
+
+@pytest.mark.gpu
+def test_bench_frames_gloo_rehearsal_world2_carries_tile_gather():
+    """The default (frames) mode with two ranks also reports the tile-gather figures."""
+    res = _run_bench(["--gpus", "2", "--dist-backend", "gloo", "--config", "2", "--steps", "20", "--warmup", "5",
+                      "--preroll-ms", "20", "--tile-gather-steps", "4", "--no-cpu-baseline", "--no-alt"], 2)
+    assert res["scaling"] == "weak" and res["n_gpus"] == 2
+    assert set(res["tile_gather"]) == {"rgba32f", "rgba8"}
+    assert all(v["value"] > 0 for v in res["tile_gather"].values())

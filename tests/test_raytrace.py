@@ -135,21 +135,37 @@ def test_mixed_row_bands(rtm, scenes, gpu_ctx):
     assert bits_equal(np.concatenate(parts, 0), full)
 
 
-def test_frames_async_with_raytraced_scenes(rtm, scenes, gpu_ctx):
-    """A frame sequence whose scenes differ in ray-traced primitives: each frame
-    uploads its own primitive table (stream-ordered) and matches rtm_render."""
+@pytest.mark.parametrize("lanes", [1, 2, 3])
+def test_frames_async_with_raytraced_scenes(rtm, scenes, gpu_ctx, lanes):
+    """A frame sequence whose scenes differ in ray-traced primitives, SDFs and
+    spheres, spread over 1-3 lanes: each lane uploads each frame's primitive,
+    SDF and (perspective eye) sphere tables into its own buffers, stream-ordered,
+    and every frame matches rtm_render bit for bit."""
     import torch
-    frames = [scenes.mixed_rt(f) for f in (0, 50, 100)] + [scenes.scene_a_bench(7), scenes.mixed_rt(9)]
-    frames[1].cappedCylinderPrimitives = frames[1].cappedCylinderPrimitives[:1]
     w, h, k = 640, 480, 64
-    outs = [torch.empty((h, w, 4), dtype=torch.float32, device="cuda") for _ in frames]
-    torch.cuda.synchronize()
-    gpu_ctx.render_frames_async(frames, scenes.eye_camera(), scenes.shadow_camera(), w, h, k, 0,
-                                [o.data_ptr() for o in outs])
-    gpu_ctx.synchronize()
-    for s, o in zip(frames, outs):
-        want = rtm.render_frame(s, scenes.eye_camera(), scenes.shadow_camera(), w, h, k)
-        assert bits_equal(o.cpu().numpy(), want)
+    cases = [
+        (scenes.eye_camera(), 0,
+         [scenes.mixed_rt(f) for f in (0, 50, 100)] + [scenes.scene_a_bench(7), scenes.mixed_rt(9),
+                                                        scenes.mixed_sdf(30), scenes.mixed_sdf(60)]),
+        (scenes.perspective_eye_camera(), scenes.RAYTRACING_FLAGS,
+         [scenes.perspective_simple1(), scenes.raytracing_plane0(True), scenes.perspective_simple2(),
+          scenes.scene_r_bench(), scenes.raytracing_plane0()]),
+    ]
+    cases[0][2][1].cappedCylinderPrimitives = cases[0][2][1].cappedCylinderPrimitives[:1]
+    try:
+        gpu_ctx.set_lanes(lanes)
+        for eye, flags, frames in cases:
+            outs = [torch.empty((h, w, 4), dtype=torch.float32, device="cuda") for _ in frames]
+            torch.cuda.synchronize()
+            gpu_ctx.render_frames_async(frames, eye, scenes.shadow_camera(), w, h, k, flags,
+                                        [o.data_ptr() for o in outs])
+            gpu_ctx.synchronize()
+            assert gpu_ctx.last_lanes() == lanes
+            for s, o in zip(frames, outs):
+                want = rtm.render_frame(s, eye, scenes.shadow_camera(), w, h, k, flags)
+                assert bits_equal(o.cpu().numpy(), want)
+    finally:
+        gpu_ctx.set_lanes(0)
 
 
 def test_staged_seams_match_oracle(rtm, oracle, scenes, gpu_ctx):
