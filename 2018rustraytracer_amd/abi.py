@@ -158,6 +158,10 @@ ABI_SYMBOLS = [
     ("rtm_group_ctx", _P, [_P, _I32]),
     ("rtm_group_render_async", C.c_int, [_P, C.POINTER(rtm_scene), C.POINTER(rtm_camera),
                                          C.POINTER(rtm_camera), _I32, _I32, _I32, _I32, _I32, _I32, _P]),
+    ("rtm_group_render_frames_async", C.c_int, [_P, _I32, C.POINTER(rtm_scene), C.POINTER(rtm_camera),
+                                                C.POINTER(rtm_camera), _I32, _I32, _I32, _I32, _I32, _I32,
+                                                C.POINTER(_P)]),
+    ("rtm_group_stream", _P, [_P]),
     ("rtm_group_synchronize", C.c_int, [_P, _I32]),
     ("rtm_group_set_root_staging", C.c_int, [_P, _I32]),
     ("rtm_viewport_create", C.c_int, [_P, _I32, _I32, _I32, C.POINTER(rtm_camera), C.POINTER(_P)]),

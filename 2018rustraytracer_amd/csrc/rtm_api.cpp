@@ -25,6 +25,23 @@
 
 using namespace rtm;
 
+namespace rtm {
+// What a frame needs beyond FrameArgs, in device memory: its ray-traced
+// primitives (row f-1) and the eye's PERSPECTIVE sphere projections (row f-3).
+struct FrameExtra {
+    RtK rt;
+    PerspK psp;
+    SdfTabK sdf;
+    bool has_rt = false, has_psp = false, has_sdf = false;
+};
+namespace internal {
+struct PreparedFrame {  // rtm_internal.h
+    FrameArgs a;
+    FrameExtra x;
+};
+}  // namespace internal
+}  // namespace rtm
+
 namespace {
 
 thread_local std::string g_last_error;
@@ -322,20 +339,12 @@ int validate_scene(const rtm_scene* scene) {
     return RTM_OK;
 }
 
-// What a frame needs beyond FrameArgs, in device memory: its ray-traced
-// primitives (row f-1) and the eye's PERSPECTIVE sphere projections (row f-3).
-struct FrameExtra {
-    RtK rt;
-    PerspK psp;
-    SdfTabK sdf;
-    bool has_rt = false, has_psp = false, has_sdf = false;
-};
 
-bool build_rt(const rtm_scene* scene, RtK& k);
+bool build_rt(const rtm_scene* scene, const rtm_camera* eye, RtK& k);
 bool build_sdf(const rtm_scene* scene, SdfTabK& k);
 
 void build_extra(const rtm_scene* scene, const rtm_camera* eye, int32_t W, int32_t H, FrameExtra& x) {
-    x.has_rt = build_rt(scene, x.rt);
+    x.has_rt = build_rt(scene, eye, x.rt);
     x.has_sdf = build_sdf(scene, x.sdf);
     std::memset(&x.psp, 0, sizeof x.psp);
     x.has_psp = eye->type != RTM_CAMERA_ORTHOGONAL && scene->n_spheres > 0;
@@ -367,11 +376,17 @@ double sqrt_le_threshold(double r) {
 
 // Ray-traced primitives of a (validated) scene, with iCappedCone's
 // ray-independent terms in the reference's operation order (main.rs:2906-2934).
-// Returns true when the scene has any.
-bool build_rt(const rtm_scene* scene, RtK& k) {
+// With a PERSPECTIVE `eye` every ray starts at eye->pos (main.rs:1922-1939), so
+// the origin-only terms of calcRayPlane and iCappedCone are constants too
+// (k.persp; the kernel's plane_hit_persp / icapped_persp): computed here with the
+// kernel's operations in its order, hence the same bits.  Returns true when the
+// scene has any primitive.
+bool build_rt(const rtm_scene* scene, const rtm_camera* eye, RtK& k) {
     std::memset(&k, 0, sizeof k);
     k.n_pl = scene->n_circle_planes;
     k.n_cy = scene->n_capped_cylinders;
+    k.persp = eye && eye->type == RTM_CAMERA_PERSPECTIVE;
+    const double* ro = eye ? eye->pos : nullptr;
     for (int i = 0; i < k.n_pl; ++i) {
         const rtm_circle_plane& q = scene->circle_planes[i];
         PlaneK& p = k.pl[i];
@@ -387,6 +402,8 @@ bool build_rt(const rtm_scene* scene, RtK& k) {
         p.cg = q.color[1];
         p.cb = q.color[2];
         p.id = (int32_t)q.id;
+        if (k.persp)  // calcRayPlane: dot(planeCenter - rayOrigin, planeN) (main.rs:2402)
+            p.num = (p.cx - ro[0]) * p.nx + (p.cy - ro[1]) * p.ny + (p.cz - ro[2]) * p.nz;
     }
     for (int i = 0; i < k.n_cy; ++i) {
         const rtm_capped_cylinder& q = scene->capped_cylinders[i];
@@ -406,6 +423,19 @@ bool build_rt(const rtm_scene* scene, RtK& k) {
         c.cg = q.color[1];
         c.cb = q.color[2];
         c.id = (int32_t)q.id;
+        if (k.persp) {  // iCappedCone's origin-only terms (main.rs:2907-2936), the kernel's order
+            for (int j = 0; j < 3; ++j) {
+                c.oa[j] = ro[j] - c.pa[j];
+                c.ob[j] = ro[j] - c.pb[j];
+            }
+            c.oaba = c.oa[0] * c.ba[0] + c.oa[1] * c.ba[1] + c.oa[2] * c.ba[2];
+            c.obba = c.ob[0] * c.ba[0] + c.ob[1] * c.ba[1] + c.ob[2] * c.ba[2];
+            for (int j = 0; j < 3; ++j) c.oc[j] = c.oa[j] * c.rb - c.ob[j] * c.ra;
+            c.ocba = c.oc[0] * c.ba[0] + c.oc[1] * c.ba[1] + c.oc[2] * c.ba[2];
+            const double ococ = c.oc[0] * c.oc[0] + c.oc[1] * c.oc[1] + c.oc[2] * c.oc[2];
+            c.bb = c.baba * c.baba;
+            c.k0 = c.bb * ococ - c.hy * c.ocba * c.ocba;
+        }
     }
     return k.n_pl + k.n_cy > 0;
 }
@@ -875,7 +905,7 @@ int format_tabs(rtm_ctx* ctx, int32_t fmt, int32_t W, const void* out, DevTabs& 
 int upload_rt(rtm_ctx* ctx, DevBuf& buf, hipStream_t s, const RtK& rt, const RtK** dev) {
     int rc = buf.ensure(sizeof(RtK), ctx->device);
     if (rc) return rc;
-    if ((rc = launch_rt_upload(rt, (RtK*)buf.p, s))) return fail(rc, "rt upload launch failed");
+    if ((rc = launch_upload(&rt, sizeof rt, buf.p, s))) return fail(rc, "rt upload launch failed");
     *dev = (const RtK*)buf.p;
     return RTM_OK;
 }
@@ -883,7 +913,7 @@ int upload_rt(rtm_ctx* ctx, DevBuf& buf, hipStream_t s, const RtK& rt, const RtK
 int upload_persp(rtm_ctx* ctx, DevBuf& buf, hipStream_t s, const PerspK& k, const PerspK** dev) {
     int rc = buf.ensure(sizeof(PerspK), ctx->device);
     if (rc) return rc;
-    if ((rc = launch_persp_upload(k, (PerspK*)buf.p, s))) return fail(rc, "upload launch failed");
+    if ((rc = launch_upload(&k, sizeof k, buf.p, s))) return fail(rc, "upload launch failed");
     *dev = (const PerspK*)buf.p;
     return RTM_OK;
 }
@@ -891,7 +921,7 @@ int upload_persp(rtm_ctx* ctx, DevBuf& buf, hipStream_t s, const PerspK& k, cons
 int upload_sdf(rtm_ctx* ctx, DevBuf& buf, hipStream_t s, const SdfTabK& k, const SdfTabK** dev) {
     int rc = buf.ensure(sizeof(SdfTabK), ctx->device);
     if (rc) return rc;
-    if ((rc = launch_sdf_upload(k, (SdfTabK*)buf.p, s))) return fail(rc, "sdf upload launch failed");
+    if ((rc = launch_upload(&k, sizeof k, buf.p, s))) return fail(rc, "sdf upload launch failed");
     *dev = (const SdfTabK*)buf.p;
     return RTM_OK;
 }
@@ -1585,7 +1615,7 @@ int rtm_viewport_process_raytracing_rays(rtm_viewport* vp, const rtm_scene* scen
     if ((rc = validate_scene(scene))) return rc;
     RtK k;
     SdfTabK sk;
-    const bool has_rt = build_rt(scene, k), has_sdf = build_sdf(scene, sk);
+    const bool has_rt = build_rt(scene, &vp->cam, k), has_sdf = build_sdf(scene, sk);
     if (!has_rt && !has_sdf) return RTM_OK;  // no circle planes, cylinders or SDFs: nothing to trace
     rtm_ctx* ctx = vp->ctx;
     DeviceGuard g(ctx->device);
@@ -1662,7 +1692,7 @@ int rtm_render_color_image(const rtm_scene* scene, const rtm_viewport* vp, const
     if ((rc = ctx->out.ensure(bytes, ctx->device))) return rc;
     RtK k;
     SdfTabK sk;
-    if (build_rt(scene, k)) {  // shading lookups circlePlanePrimitives[id] / cappedCylinderPrimitives[id]
+    if (build_rt(scene, nullptr, k)) {  // shading lookups circlePlanePrimitives[id] / cappedCylinderPrimitives[id]
         if ((rc = upload_rt(ctx, ctx->rtk, ctx->stream, k, &a.rt))) return rc;
         a.gn = (const double*)vp->gn.p;
     }
@@ -1697,6 +1727,32 @@ int check_frame(const rtm_scene* scene, const rtm_camera* eye, const rtm_camera*
                 int32_t height, int32_t march_steps, int32_t flags) {
     FrameArgs a;
     return build_frame(a, scene, eye, shadow, width, height, march_steps, flags);
+}
+
+PreparedFrame* new_prepared() { return new (std::nothrow) PreparedFrame; }
+
+void delete_prepared(PreparedFrame* f) { delete f; }
+
+int prepare_frame(PreparedFrame* f, const rtm_scene* scene, const rtm_camera* eye, const rtm_camera* shadow,
+                  int32_t width, int32_t height, int32_t march_steps, int32_t flags) {
+    int rc = build_frame(f->a, scene, eye, shadow, width, height, march_steps, flags);
+    if (rc) return rc;
+    build_extra(scene, eye, width, height, f->x);
+    return RTM_OK;
+}
+
+int enqueue_prepared(rtm_ctx* ctx, const PreparedFrame* f, int32_t format, int32_t row_begin, int32_t row_end,
+                     void* out_dev) {
+    if (!ctx || !f || !out_dev) return fail(RTM_ERR_INVALID, "bad arguments");
+    int rc = validate_format(format, out_dev);
+    if (rc) return rc;
+    if (row_begin < 0 || row_end > f->a.ey.H || row_begin >= row_end)
+        return fail(RTM_ERR_INVALID, "row range [%d,%d) outside [0,%d)", row_begin, row_end, f->a.ey.H);
+    FrameArgs a = f->a;
+    a.ey.row_begin = row_begin;
+    a.ey.row_end = row_end;
+    DeviceGuard g(ctx->device);
+    return enqueue_frame(ctx, a, &f->x, out_dev, nullptr, 0, format);
 }
 
 int32_t bytes_per_pixel(int32_t format) { return format_bytes(format); }

@@ -318,108 +318,162 @@ int rtm_group_set_root_staging(rtm_group* g, int32_t on) {
     return RTM_OK;
 }
 
-int rtm_group_render_async(rtm_group* g, const rtm_scene* scene, const rtm_camera* eye, const rtm_camera* shadow,
-                           int32_t width, int32_t height, int32_t march_steps, int32_t flags, int32_t format,
-                           int32_t root, void* out_dev) {
-    if (!g) return set_error(RTM_ERR_INVALID, "group is NULL");
-    if (g->aborted) return set_error(RTM_ERR_COMM, "group was aborted");
+namespace {
+
+// One frame of the group, its inputs already validated and prepared.  Per member:
+// the band renders on the member's context stream (the root's in place into
+// out_dev, the others' into staging slot s); the transfer stream waits for the
+// render and then carries the gather, so a context stream never waits for a
+// transfer and frame i+1 renders while frame i is in flight.  The frame is
+// complete in the root's transfer stream order (rtm_group_stream).
+int group_frame(rtm_group* g, const rtm::internal::PreparedFrame* pf, int32_t width, int32_t height, int32_t format,
+                int32_t root, void* out_dev) {
     const int32_t n = g->n_ranks;
-    if (root < 0 || root >= n) return set_error(RTM_ERR_INVALID, "root outside [0, n_ranks)");
-    const int32_t bpp = rtm::internal::bytes_per_pixel(format);
-    if (!bpp) return set_error(RTM_ERR_INVALID, "unknown output format");
-    // more than one band: each evaluates the shadow texels it reads (same image bits)
-    const int32_t f = flags | (n > 1 ? RTM_FLAG_FUSED_SHADOW : 0);
-    // Everything that can fail for the caller's inputs is checked before the first
-    // enqueue: a rank that stopped half-way would leave its peers' transfers unmatched.
-    int rc = rtm::internal::check_frame(scene, eye, shadow, width, height, march_steps, f);
-    if (rc) return rc;
-    const bool holds_root = std::any_of(g->m.begin(), g->m.end(), [&](const Member& mb) { return mb.rank == root; });
-    if (holds_root) {
-        if (!out_dev) return set_error(RTM_ERR_INVALID, "out_dev is NULL on the root");
-        if (format == RTM_FORMAT_RGBA32F && ((uintptr_t)out_dev & 15))
-            return set_error(RTM_ERR_INVALID, "RGBA32F output must be 16-byte aligned");
-    }
-    const size_t row_bytes = (size_t)bpp * (size_t)width;
-    int32_t b0 = 0, b1 = 0;
-    band_rows(height, n, 0, &b0, &b1);
-    for (Member& mb : g->m) {
-        const bool staged = mb.rank != root || g->root_staging;
-        if (staged && (rc = ensure_stage(mb, row_bytes * (size_t)(b1 - b0)))) return rc;
-    }
-    // 1. every local member renders its band: in place (the root) or into a staging buffer
+    const size_t row_bytes = (size_t)rtm::internal::bytes_per_pixel(format) * (size_t)width;
+    int rc;
+    // 1. every local member renders its band
     for (Member& mb : g->m) {
         int32_t r0, r1;
         band_rows(height, n, mb.rank, &r0, &r1);
         Guard d(mb.device);
         hipStream_t rs = rtm::internal::ctx_stream(mb.ctx);
-        if (mb.rank == root) GHIP_TRY(hipEventRecord(mb.start, rs));
-        if (r0 >= r1) continue;
         const bool staged = mb.rank != root || g->root_staging;
-        if (!staged) {
-            rc = rtm_render_rows_async(mb.ctx, scene, eye, shadow, width, height, march_steps, f, format, r0, r1,
-                                       (char*)out_dev + row_bytes * (size_t)r0);
+        if (r0 < r1 && !staged) {
+            rc = rtm::internal::enqueue_prepared(mb.ctx, pf, format, r0, r1, (char*)out_dev + row_bytes * (size_t)r0);
             if (rc) return rc;
-            continue;
+        } else if (r0 < r1) {
+            const int s = mb.slot;
+            GHIP_TRY(hipStreamWaitEvent(rs, mb.sent[s], 0));  // stage[s]'s previous send has read it
+            rc = rtm::internal::enqueue_prepared(mb.ctx, pf, format, r0, r1, mb.stage[s]);
+            if (rc) return rc;
+            GHIP_TRY(hipEventRecord(mb.ready[s], rs));
+            GHIP_TRY(hipStreamWaitEvent(mb.xfer, mb.ready[s], 0));
         }
-        const int s = mb.slot;
-        GHIP_TRY(hipStreamWaitEvent(rs, mb.sent[s], 0));  // stage[s]'s previous send has read it
-        rc = rtm_render_rows_async(mb.ctx, scene, eye, shadow, width, height, march_steps, f, format, r0, r1,
-                                   mb.stage[s]);
-        if (rc) return rc;
-        GHIP_TRY(hipEventRecord(mb.ready[s], rs));
-        GHIP_TRY(hipStreamWaitEvent(mb.xfer, mb.ready[s], 0));
+        if (mb.rank == root && !staged) {  // the root's own band, in the frame's completion order
+            GHIP_TRY(hipEventRecord(mb.start, rs));
+            GHIP_TRY(hipStreamWaitEvent(mb.xfer, mb.start, 0));
+        }
     }
-    // 2. ONE gather: the root receives every other band in place, the others send theirs
-    const Rccl& R = rccl();
-    for (Member& mb : g->m)
-        if (mb.rank == root) {
-            Guard d(mb.device);
-            GHIP_TRY(hipStreamWaitEvent(mb.xfer, mb.start, 0));  // no receive before the frame's start
-        }
-    NCCL_TRY(R.GroupStart());
-    for (Member& mb : g->m) {
-        if (mb.rank == root) {
-            for (int32_t p = 0; p < n; ++p) {
-                if (p == root && !g->root_staging) continue;
-                int32_t r0, r1;
-                band_rows(height, n, p, &r0, &r1);
-                if (r0 >= r1) continue;
-                ncclResult_t r = R.Recv((char*)out_dev + row_bytes * (size_t)r0, row_bytes * (size_t)(r1 - r0),
-                                        ncclUint8, p, mb.comm, mb.xfer);
+    // 2. ONE gather: the root receives every other band in place, the others send
+    //    theirs (nothing to move for a one-rank group rendering in place)
+    if (n > 1 || g->root_staging) {
+        const Rccl& R = rccl();
+        NCCL_TRY(R.GroupStart());
+        for (Member& mb : g->m) {
+            if (mb.rank == root) {
+                for (int32_t p = 0; p < n; ++p) {
+                    if (p == root && !g->root_staging) continue;
+                    int32_t r0, r1;
+                    band_rows(height, n, p, &r0, &r1);
+                    if (r0 >= r1) continue;
+                    ncclResult_t r = R.Recv((char*)out_dev + row_bytes * (size_t)r0, row_bytes * (size_t)(r1 - r0),
+                                            ncclUint8, p, mb.comm, mb.xfer);
+                    if (r != ncclSuccess) {
+                        (void)R.GroupEnd();
+                        return comm_fail("ncclRecv", r);
+                    }
+                }
+            }
+            int32_t r0, r1;
+            band_rows(height, n, mb.rank, &r0, &r1);
+            const bool staged = mb.rank != root || g->root_staging;
+            if (staged && r0 < r1) {
+                ncclResult_t r =
+                    R.Send(mb.stage[mb.slot], row_bytes * (size_t)(r1 - r0), ncclUint8, root, mb.comm, mb.xfer);
                 if (r != ncclSuccess) {
                     (void)R.GroupEnd();
-                    return comm_fail("ncclRecv", r);
+                    return comm_fail("ncclSend", r);
                 }
             }
         }
-        int32_t r0, r1;
-        band_rows(height, n, mb.rank, &r0, &r1);
-        const bool staged = mb.rank != root || g->root_staging;
-        if (staged && r0 < r1) {
-            ncclResult_t r = R.Send(mb.stage[mb.slot], row_bytes * (size_t)(r1 - r0), ncclUint8, root, mb.comm, mb.xfer);
-            if (r != ncclSuccess) {
-                (void)R.GroupEnd();
-                return comm_fail("ncclSend", r);
-            }
-        }
+        NCCL_TRY(R.GroupEnd());
     }
-    NCCL_TRY(R.GroupEnd());
-    // 3. bookkeeping: staging slots and the root's completion in its render stream order
+    // 3. staging slots: free again once their sends have read them
     for (Member& mb : g->m) {
         int32_t r0, r1;
         band_rows(height, n, mb.rank, &r0, &r1);
-        Guard d(mb.device);
         const bool staged = mb.rank != root || g->root_staging;
         if (staged && r0 < r1) {
+            Guard d(mb.device);
             GHIP_TRY(hipEventRecord(mb.sent[mb.slot], mb.xfer));
             mb.slot ^= 1;
         }
-        if (mb.rank == root) {
-            GHIP_TRY(hipEventRecord(mb.done, mb.xfer));
-            GHIP_TRY(hipStreamWaitEvent(rtm::internal::ctx_stream(mb.ctx), mb.done, 0));
-        }
     }
     return RTM_OK;
+}
+
+struct PreparedDeleter {
+    void operator()(rtm::internal::PreparedFrame* f) const { rtm::internal::delete_prepared(f); }
+};
+
+// Shared checks of the frame calls; allocates the staging buffers.
+int group_begin(rtm_group* g, int32_t width, int32_t height, int32_t format, int32_t root) {
+    if (!g) return set_error(RTM_ERR_INVALID, "group is NULL");
+    if (g->aborted) return set_error(RTM_ERR_COMM, "group was aborted");
+    if (root < 0 || root >= g->n_ranks) return set_error(RTM_ERR_INVALID, "root outside [0, n_ranks)");
+    const int32_t bpp = rtm::internal::bytes_per_pixel(format);
+    if (!bpp) return set_error(RTM_ERR_INVALID, "unknown output format");
+    if (width <= 0 || height <= 0 || width > RTM_MAX_DIM || height > RTM_MAX_DIM)
+        return set_error(RTM_ERR_INVALID, "image size outside [1, RTM_MAX_DIM]");
+    int32_t b0, b1;
+    band_rows(height, g->n_ranks, 0, &b0, &b1);
+    for (Member& mb : g->m) {
+        const bool staged = mb.rank != root || g->root_staging;
+        int rc;
+        if (staged && (rc = ensure_stage(mb, (size_t)bpp * (size_t)width * (size_t)(b1 - b0)))) return rc;
+    }
+    return RTM_OK;
+}
+
+int check_root_out(rtm_group* g, int32_t format, int32_t root, void* out) {
+    for (const Member& mb : g->m)
+        if (mb.rank == root) {
+            if (!out) return set_error(RTM_ERR_INVALID, "out_dev is NULL on the root");
+            if (format == RTM_FORMAT_RGBA32F && ((uintptr_t)out & 15))
+                return set_error(RTM_ERR_INVALID, "RGBA32F output must be 16-byte aligned");
+        }
+    return RTM_OK;
+}
+
+}  // namespace
+
+int rtm_group_render_async(rtm_group* g, const rtm_scene* scene, const rtm_camera* eye, const rtm_camera* shadow,
+                           int32_t width, int32_t height, int32_t march_steps, int32_t flags, int32_t format,
+                           int32_t root, void* out_dev) {
+    void* outs[1] = {out_dev};
+    return rtm_group_render_frames_async(g, 1, scene, eye, shadow, width, height, march_steps, flags, format, root,
+                                         outs);
+}
+
+int rtm_group_render_frames_async(rtm_group* g, int32_t n_frames, const rtm_scene* scenes, const rtm_camera* eye,
+                                  const rtm_camera* shadow, int32_t width, int32_t height, int32_t march_steps,
+                                  int32_t flags, int32_t format, int32_t root, void* const* out_dev) {
+    int rc = group_begin(g, width, height, format, root);
+    if (rc) return rc;
+    if (n_frames < 1 || !scenes || !out_dev) return set_error(RTM_ERR_INVALID, "bad frame list");
+    // more than one band: each evaluates the shadow texels it reads (same image bits)
+    const int32_t f = flags | (g->n_ranks > 1 ? RTM_FLAG_FUSED_SHADOW : 0);
+    std::unique_ptr<rtm::internal::PreparedFrame, PreparedDeleter> pf(rtm::internal::new_prepared());
+    if (!pf) return set_error(RTM_ERR_OOM, "host allocation failed");
+    // Everything that can fail for the caller's inputs is checked before the first
+    // enqueue: a rank that stopped half-way would leave its peers' transfers unmatched.
+    for (int32_t i = 0; i < n_frames; ++i) {
+        if ((rc = rtm::internal::check_frame(&scenes[i], eye, shadow, width, height, march_steps, f))) return rc;
+        if ((rc = check_root_out(g, format, root, out_dev[i]))) return rc;
+    }
+    for (int32_t i = 0; i < n_frames; ++i) {
+        if ((rc = rtm::internal::prepare_frame(pf.get(), &scenes[i], eye, shadow, width, height, march_steps, f)))
+            return rc;
+        if ((rc = group_frame(g, pf.get(), width, height, format, root, out_dev[i]))) return rc;
+    }
+    return RTM_OK;
+}
+
+void* rtm_group_stream(rtm_group* g) {
+    if (!g || g->m.empty()) return nullptr;
+    for (const Member& mb : g->m)
+        if (mb.rank == 0) return (void*)mb.xfer;
+    return (void*)g->m[0].xfer;
 }
 
 int rtm_group_synchronize(rtm_group* g, int32_t timeout_ms) {

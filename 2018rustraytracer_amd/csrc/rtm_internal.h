@@ -13,6 +13,16 @@ namespace internal {
 // Validate a frame's inputs as every render entry point does (rtm_last_error set on failure).
 int check_frame(const rtm_scene* scene, const rtm_camera* eye, const rtm_camera* shadow, int32_t width,
                 int32_t height, int32_t march_steps, int32_t flags);
+// A frame's inputs validated and precomputed once (FrameArgs + device tables),
+// then enqueued per row band on any context without repeating the host work.
+struct PreparedFrame;
+PreparedFrame* new_prepared();
+void delete_prepared(PreparedFrame* f);
+int prepare_frame(PreparedFrame* f, const rtm_scene* scene, const rtm_camera* eye, const rtm_camera* shadow,
+                  int32_t width, int32_t height, int32_t march_steps, int32_t flags);
+// rows [row_begin, row_end) in `format` into out_dev, on ctx's stream
+int enqueue_prepared(rtm_ctx* ctx, const PreparedFrame* f, int32_t format, int32_t row_begin, int32_t row_end,
+                     void* out_dev);
 // bytes per pixel of an RTM_FORMAT_* (0: unknown)
 int32_t bytes_per_pixel(int32_t format);
 // set rtm_last_error and return code

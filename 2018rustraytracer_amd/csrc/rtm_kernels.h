@@ -123,6 +123,11 @@ static_assert(sizeof(FrameArgs) <= 4096, "FrameArgs must fit the 4 KiB kernarg s
 // iCappedCone evaluated once on the host in the reference's operation order.
 // Lives in device memory (too large to share the 4 KiB kernarg segment with
 // FrameArgs); written per frame by a stream-ordered upload kernel.
+// With a PERSPECTIVE eye every ray starts at the camera position (main.rs:1922-1939),
+// so every term of calcRayPlane / iCappedCone that involves only the origin is a
+// per-(camera, primitive) constant: the host evaluates it once, in the reference's
+// operation order (RtK::persp), and the kernel keeps only the terms with the ray
+// direction -- the same bits, about half the per-pixel work.
 struct PlaneK {            // PrimitiveCirclePlane (main.rs:370-380)
     double cx, cy, cz;     // pos (Plane.center)
     double nx, ny, nz;     // n
@@ -130,6 +135,7 @@ struct PlaneK {            // PrimitiveCirclePlane (main.rs:370-380)
     double r2max;          // largest s with sqrt(s) <= radius (host libm sqrt): the radius test
                            // !(sqrt(s) > radius) is exactly !(s > r2max), no device sqrt
     double cr, cg, cb;     // shading
+    double num;            // persp: dot(pos - origin, n), calcRayPlane's numerator (main.rs:2402)
     int32_t id, pad;
 };
 struct CylK {              // PrimitiveCappedCylinder (main.rs:382-391)
@@ -141,15 +147,23 @@ struct CylK {              // PrimitiveCappedCylinder (main.rs:382-391)
     double hy;             // baba + rr*rr              (main.rs:2934)
     double isq;            // inversesqrt(baba) = 1.0/sqrt(baba) (main.rs:2919, 2963)
     double cr, cg, cb;
+    // persp: the origin-only terms of iCappedCone (main.rs:2907-2936)
+    double oa[3], ob[3];   // ro - pa, ro - pb
+    double oaba, obba;     // dot(oa, ba), dot(ob, ba)
+    double oc[3];          // oa*rb - ob*ra
+    double ocba;           // dot(oc, ba)
+    double bb;             // baba*baba
+    double k0;             // baba*baba*dot(oc, oc) - hy*ocba*ocba
     int32_t id, pad;
 };
 struct RtK {
     PlaneK pl[RTM_MAX_CIRCLE_PLANES];
     CylK cy[RTM_MAX_CAPPED_CYLINDERS];
     int32_t n_pl, n_cy;
+    int32_t persp, pad;    // the persp fields hold the eye camera's constants (PERSPECTIVE eye)
 };
-static_assert(sizeof(PlaneK) == 96 && sizeof(CylK) == 152, "RtK layout");
-static_assert(sizeof(RtK) + sizeof(void*) <= 4096, "RtK must fit the upload kernel's kernarg segment");
+static_assert(sizeof(PlaneK) == 104 && sizeof(CylK) == 264, "RtK layout");
+static_assert(sizeof(RtK) % 8 == 0, "RtK is uploaded in 8-byte words");
 
 // One sphere as seen by a PERSPECTIVE camera (row f-3; Viewport::rasterize,
 // main.rs:473-524 + projectSphere, main.rs:2796-2837): the ellipse centre and
@@ -164,7 +178,6 @@ struct PerspSphK {
 struct PerspK {
     PerspSphK s[RTM_MAX_SPHERES];
 };
-static_assert(sizeof(PerspK) + sizeof(void*) <= 4096, "PerspK must fit the upload kernel's kernarg segment");
 
 // The GL preview's SDF implicit surface (row f-4, entry.frag:416-442, 842-905),
 // with udTriangleSingle's point-independent terms precomputed on the host in
@@ -184,7 +197,8 @@ struct SdfTabK {
     SdfK s[RTM_MAX_SDFS];
     int32_t n, pad;
 };
-static_assert(sizeof(SdfTabK) + sizeof(void*) <= 4096, "SdfTabK must fit the upload kernel's kernarg segment");
+static_assert(sizeof(PerspK) % 8 == 0 && sizeof(SdfTabK) % 8 == 0, "device tables are uploaded in 8-byte words");
+
 
 // The device tables a frame may carry beside FrameArgs (each nullptr when absent),
 // and the eye pass's output format.
@@ -257,11 +271,10 @@ int launch_shadow_pass(const FrameArgs& a, double* smap, void* stream, StatsK* s
 // out: (row_end-row_begin)*W pixels in tabs.fmt's format (RTM_FORMAT_RGBA32F: 16-byte aligned).
 int launch_eye_pass(const FrameArgs& a, const double* smap, void* out, void* stream, StatsK* stats,
                     const DevTabs& tabs = DevTabs{});
-// Stream-ordered copy of a host struct into device memory (a kernel, so the
-// host copy is consumed at launch: no pinned staging, no host synchronisation).
-int launch_rt_upload(const RtK& k, RtK* dst, void* stream);
-int launch_persp_upload(const PerspK& k, PerspK* dst, void* stream);
-int launch_sdf_upload(const SdfTabK& k, SdfTabK* dst, void* stream);
+// Stream-ordered copy of host bytes into device memory by kernels whose
+// arguments carry the bytes (<= 3968 per launch), so the host copy is consumed
+// at launch: no pinned staging, no host synchronisation.  bytes % 8 == 0.
+int launch_upload(const void* src, size_t bytes, void* dst, void* stream);
 // Software-pipelined frame step: the shadow pass of a.sh into smap_w and the eye
 // pass of a.ey (the previous frame) from smap_r into out, in ONE launch whose
 // workgroups interleave the two roles (VALU-bound and HBM-store-bound tiles

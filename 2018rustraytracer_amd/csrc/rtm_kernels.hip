@@ -346,6 +346,64 @@ __device__ __forceinline__ bool plane_hit(const PlaneK& p, const double o[3], co
     return !(qx * qx + qy * qy + qz * qz > p.r2max);
 }
 
+// plane_hit for a ray from the PERSPECTIVE camera position o (RtK::persp): the
+// numerator dot(pos - o, n) is the host's constant, the rest as plane_hit.
+__device__ __forceinline__ bool plane_hit_persp(const PlaneK& p, const double o[3], const double d[3], double zb,
+                                                double& t) {
+    const double denom = p.nx * d[0] + p.ny * d[1] + p.nz * d[2];
+    if (!(fabs(denom) > 0.0001)) return false;
+    t = p.num / denom;
+    if (t < 0.0) return false;
+    if (t > zb) return false;
+    const double qx = (o[0] + d[0] * t) - p.cx;
+    const double qy = (o[1] + d[1] * t) - p.cy;
+    const double qz = (o[2] + d[2] * t) - p.cz;
+    return !(qx * qx + qy * qy + qz * qz > p.r2max);
+}
+
+// icapped for a ray from the PERSPECTIVE camera position (RtK::persp): oa, ob,
+// oaba, obba, oc, ocba, baba*baba and k0 are the host's constants (the same
+// operations in the same order), so the cap branches are uniform and only the
+// terms with rd remain per pixel.
+__device__ __forceinline__ double icapped_persp(const CylK& c, const double rd[3], double n[3]) {
+    const double rdba = rd[0] * c.ba[0] + rd[1] * c.ba[1] + rd[2] * c.ba[2];
+    if (c.oaba < 0.0) {
+        double w[3];
+        for (int k = 0; k < 3; ++k) w[k] = c.oa[k] * rdba - rd[k] * c.oaba;
+        if (w[0] * w[0] + w[1] * w[1] + w[2] * w[2] < c.ra * c.ra * rdba * rdba) {
+            const double sc = -c.isq;
+            for (int k = 0; k < 3; ++k) n[k] = c.ba[k] * sc;
+            return -c.oaba / rdba;
+        }
+    } else if (c.obba > 0.0) {
+        const double t = -c.obba / rdba;
+        double w[3];
+        for (int k = 0; k < 3; ++k) w[k] = c.ob[k] + rd[k] * t;
+        if (w[0] * w[0] + w[1] * w[1] + w[2] * w[2] < c.rb * c.rb) {
+            for (int k = 0; k < 3; ++k) n[k] = c.ba[k] * c.isq;
+            return t;
+        }
+    }
+    const double ocrd = c.oc[0] * rd[0] + c.oc[1] * rd[1] + c.oc[2] * rd[2];
+    const double k2 = c.bb - c.hy * rdba * rdba;
+    const double k1 = c.bb * ocrd - c.hy * rdba * c.ocba;
+    const double h = k1 * k1 - k2 * c.k0;
+    if (h < 0.0) return -1.0;
+    const double sg = c.rr >= 0.0 ? 1.0 : -1.0;
+    const double t = (-k1 - sg * sqrt(h)) / (k2 * c.rr);
+    const double y = c.oaba + rdba * t;
+    if (y > 0.0 && y < c.baba) {
+        const double rra = c.rr * c.ra, hyy = c.hy * y;
+        double v[3];
+        for (int k = 0; k < 3; ++k) v[k] = ((c.oa[k] + rd[k] * t) * c.baba - c.ba[k] * rra) * c.baba - c.ba[k] * hyy;
+        const double m = sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
+        const double inv = 1.0 / m;
+        for (int k = 0; k < 3; ++k) n[k] = v[k] * inv;
+        return t;
+    }
+    return -1.0;
+}
+
 // iCappedCone (main.rs:2889-2959) in the reference's operation order; the
 // ray-independent terms (ba, baba, rr, hy, inversesqrt(baba)) come from the
 // host.  Returns t (-1 on a miss) and the hit normal in n.
@@ -633,10 +691,11 @@ __device__ __forceinline__ void trace_pixel(const RtK* __restrict__ rt, const do
                                             double& zb_io, RtHit& hit, uint32_t mask = ~0u) {
     double zb = zb_io;
     const int npl = rt->n_pl, ncy = rt->n_cy;
+    const bool persp = rt->persp != 0;  // (uniform: the frame's eye camera)
     for (int i = 0; i < npl; ++i) {
         if (!((mask >> i) & 1u)) continue;  // wave-uniform
         double t;
-        if (plane_hit(rt->pl[i], o, d, zb, t)) {
+        if (persp ? plane_hit_persp(rt->pl[i], o, d, zb, t) : plane_hit(rt->pl[i], o, d, zb, t)) {
             hit.kind = 2;
             hit.id = rt->pl[i].id;
             hit.t = t;
@@ -646,7 +705,7 @@ __device__ __forceinline__ void trace_pixel(const RtK* __restrict__ rt, const do
     for (int i = 0; i < ncy; ++i) {
         if (!((mask >> (16 + i)) & 1u)) continue;  // wave-uniform
         double n[3];
-        const double t = icapped(rt->cy[i], o, d, n);
+        const double t = persp ? icapped_persp(rt->cy[i], d, n) : icapped(rt->cy[i], o, d, n);
         if (t < 0.0) continue;  // behind the camera (and misses)
         if (t > zb) continue;   // behind a known intersection
         hit.kind = 3;
@@ -1548,14 +1607,13 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
     eye_tile<false, false, 2, FMT>(a.ey, a.sh, smap, out, blockIdx.x, blockIdx.y, nullptr, tabs, wide);
 }
 
-// launch_*_upload: one 8-byte word per thread from the kernarg copy.
-template <class T>
-__global__ void upload_kernel(const T k, T* __restrict__ dst) {
-    constexpr int N = (int)(sizeof(T) / sizeof(uint64_t));
-    static_assert(sizeof(T) % sizeof(uint64_t) == 0, "upload size");
-    const uint64_t* src = reinterpret_cast<const uint64_t*>(&k);
-    uint64_t* d = reinterpret_cast<uint64_t*>(dst);
-    for (int i = threadIdx.x; i < N; i += blockDim.x) d[i] = src[i];
+// launch_upload: one 8-byte word per thread from the kernarg copy.
+constexpr int UPLOAD_WORDS = 496;  // 3968 bytes: the chunk plus its two arguments fit 4 KiB of kernarg
+struct UploadChunk {
+    uint64_t w[UPLOAD_WORDS];
+};
+__global__ void upload_kernel(const UploadChunk k, uint64_t* __restrict__ dst, int n) {
+    for (int i = threadIdx.x; i < n; i += blockDim.x) dst[i] = k.w[i];
 }
 
 // Timing diagnostic only (RTM_DIAG_EYE=1): the eye pass's stores without its work.
@@ -2011,14 +2069,18 @@ int launch_eye_pass(const FrameArgs& a, const double* smap, void* out, void* str
     return launched();
 }
 
-int launch_rt_upload(const RtK& k, RtK* dst, void* stream) {
-    hipLaunchKernelGGL(upload_kernel<RtK>, dim3(1), dim3(512), 0, (hipStream_t)stream, k, dst);
-    return launched();
-}
-
-int launch_persp_upload(const PerspK& k, PerspK* dst, void* stream) {
-    hipLaunchKernelGGL(upload_kernel<PerspK>, dim3(1), dim3(256), 0, (hipStream_t)stream, k, dst);
-    return launched();
+int launch_upload(const void* src, size_t bytes, void* dst, void* stream) {
+    if (bytes % 8) return RTM_ERR_INVALID;
+    const uint64_t* s8 = static_cast<const uint64_t*>(src);
+    uint64_t* d8 = static_cast<uint64_t*>(dst);
+    for (size_t w = 0, nw = bytes / 8; w < nw; w += UPLOAD_WORDS) {
+        UploadChunk c;
+        const int n = (int)std::min<size_t>(UPLOAD_WORDS, nw - w);
+        std::copy(s8 + w, s8 + w + n, c.w);
+        hipLaunchKernelGGL(upload_kernel, dim3(1), dim3(512), 0, (hipStream_t)stream, c, d8 + w, n);
+        if (launched()) return RTM_ERR_HIP;
+    }
+    return 0;
 }
 
 }  // namespace rtm
@@ -2032,10 +2094,6 @@ extern "C" int rtm_diag_shadow_phases(unsigned long long* out, int n) {
 
 namespace rtm {
 
-int launch_sdf_upload(const SdfTabK& k, SdfTabK* dst, void* stream) {
-    hipLaunchKernelGGL(upload_kernel<SdfTabK>, dim3(1), dim3(512), 0, (hipStream_t)stream, k, dst);
-    return launched();
-}
 
 template <int KIND, int NR, bool INC>
 static void launch_pipe(const FrameArgs& a, double* smap_w, const double* smap_r, float4* out, hipStream_t s) {

@@ -297,6 +297,23 @@ class Group:
                                                   steps, flags, fmt, root, C.c_void_p(out_ptr)),
                   "rtm_group_render_async")
 
+    def render_frames_async(self, scenes, eye: Camera, shadow: Camera, width: int, height: int, steps: int,
+                            flags: int, fmt: int, root: int, out_ptrs, prepared=None):
+        """rtm_group_render_frames_async: frame i into out_ptrs[i] (ignored off the root)."""
+        arr, keep = prepared if prepared is not None else Context.prepare_frames(None, scenes)
+        n = len(arr)
+        outs = (C.c_void_p * n)(*[C.c_void_p(p or 0) for p in out_ptrs])
+        e, s = eye.to_c(), shadow.to_c()
+        lib = _lib()
+        abi.check(lib, lib.rtm_group_render_frames_async(self._h, n, arr, C.byref(e), C.byref(s), width, height,
+                                                         steps, flags, fmt, root, outs),
+                  "rtm_group_render_frames_async")
+
+    @property
+    def stream(self) -> int:
+        """hipStream_t in whose order a gathered frame is complete on this process."""
+        return _lib().rtm_group_stream(self._h) or 0
+
     def synchronize(self, timeout_ms: int = 0):
         lib = _lib()
         abi.check(lib, lib.rtm_group_synchronize(self._h, timeout_ms), "rtm_group_synchronize")

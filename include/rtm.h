@@ -354,11 +354,21 @@ rtm_ctx* rtm_group_ctx(rtm_group* g, int32_t local);
 /* One frame, tile-partitioned and gathered: out_dev is the root's device buffer of
  * width*height pixels of rtm_format_bytes(format) bytes, on the root's device
  * (ignored on a process that does not hold the root).  Asynchronous: the frame is
- * complete in the root context's stream order.  RGBA8 / RGB8 gather 4 / 3 bytes
- * per pixel instead of 16. */
+ * complete in the order of the root's rtm_group_stream.  RGBA8 / RGB8 gather 4 / 3
+ * bytes per pixel instead of 16.  A frame's out_dev must not be reused before that
+ * frame is complete (the root's next band may already be rendering). */
 int rtm_group_render_async(rtm_group* g, const rtm_scene* scene, const rtm_camera* eye,
                            const rtm_camera* shadow, int32_t width, int32_t height, int32_t march_steps,
                            int32_t flags, int32_t format, int32_t root, void* out_dev);
+/* A sequence of frames, frame i into out_dev[i] (entries ignored off the root);
+ * every frame's inputs are validated before the first is enqueued. */
+int rtm_group_render_frames_async(rtm_group* g, int32_t n_frames, const rtm_scene* scenes,
+                                  const rtm_camera* eye, const rtm_camera* shadow, int32_t width, int32_t height,
+                                  int32_t march_steps, int32_t flags, int32_t format, int32_t root,
+                                  void* const* out_dev);
+/* hipStream_t (as void*) in whose order a frame gathered to rank 0 is complete on
+ * this process (the root's transfer stream; on other ranks, where their sends run) */
+void* rtm_group_stream(rtm_group* g);
 /* Wait for every local member's work (renders and transfers).  timeout_ms > 0:
  * give up after that long, abort the communicators (ncclCommAbort) and return
  * RTM_ERR_COMM; the group then fails every call but rtm_group_destroy.
