@@ -621,7 +621,7 @@ struct TimingSlot {
 struct Lane {
     hipStream_t stream = nullptr;
     hipEvent_t done = nullptr;  // join: the context stream waits on it
-    DevBuf smap, rtk, pspk, sdfk;
+    DevBuf smap, rtk, pspk, sdfk, rtmask;
 };
 
 struct rtm_ctx {
@@ -648,6 +648,7 @@ struct rtm_ctx {
     DevBuf rtk;                          // RtK of the frame being enqueued (row f-1)
     DevBuf pspk;                         // PerspK of the frame being enqueued (row f-3)
     DevBuf sdfk;                         // SdfTabK of the frame being enqueued (row f-4)
+    DevBuf rtmask;                       // per-wave primitive masks of a PERSPECTIVE eye pass (row f-1)
     std::vector<rtm_viewport*> viewports;  // live viewports (orphaned when the context goes first)
     bool enc_tab_ready = false;
     uint64_t tab_key = 0;
@@ -938,6 +939,18 @@ int enqueue_frame(rtm_ctx* ctx, FrameArgs& a, const FrameExtra* x, void* out_dev
     if (x && x->has_rt && (rc = upload_rt(ctx, l ? l->rtk : ctx->rtk, s, x->rt, &tabs.rt))) return rc;
     if (x && x->has_psp && (rc = upload_persp(ctx, l ? l->pspk : ctx->pspk, s, x->psp, &tabs.psp))) return rc;
     if (x && x->has_sdf && (rc = upload_sdf(ctx, l ? l->sdfk : ctx->sdfk, s, x->sdf, &tabs.sdf))) return rc;
+    if (x && x->has_rt && x->rt.persp && !stats) {
+        // RT 3 (the host's origin-only primitive constants); from 1 Mpixel on, the
+        // per-wave primitive masks come from a separate one-thread-per-wave kernel
+        // (config 6 eye pass 160 -> 90 us); below, its launch costs more than it saves
+        tabs.rt_persp = 1;
+    }
+    if (x && x->has_rt && x->rt.persp && !stats && (int64_t)a.ey.W * (a.ey.row_end - a.ey.row_begin) >= (1 << 20)) {
+        DevBuf& mb = l ? l->rtmask : ctx->rtmask;
+        const size_t words = (size_t)((a.ey.W + 63) / 64) * (size_t)(a.ey.row_end - a.ey.row_begin);
+        if ((rc = mb.ensure(words * sizeof(uint32_t), ctx->device))) return rc;
+        tabs.rtmask = (uint32_t*)mb.p;
+    }
     const bool fused = (a.ey.flags & RTM_FLAG_FUSED_SHADOW) != 0;
     double* smap = nullptr;
     TimingSlot* slot = next_slot(ctx);

@@ -211,6 +211,11 @@ struct DevTabs {
     const void* enc;
     int32_t fmt;          // RTM_FORMAT_* | FMT_RGB8_DWORDS (RGB8 rows start 4-byte aligned)
     uint32_t bg;          // the encoded background pixel (0.0, 0.2, 0.2) (main.rs:718-720), R | G<<8 | B<<16
+    // PERSPECTIVE eye with ray-traced primitives: rt holds the origin-only constants
+    // (rt_persp) and rtmask is scratch for the per-wave primitive masks,
+    // ceil(W/64) * rows words (launch_eye_pass fills it first; nullptr: in-kernel cull)
+    uint32_t* rtmask;
+    int32_t rt_persp, pad;
 };
 constexpr int32_t FMT_MASK = 0xff;
 constexpr int32_t FMT_RGB8_DWORDS = 0x100;

@@ -624,37 +624,48 @@ __device__ __forceinline__ void trace_sdfs(const SdfTabK* __restrict__ sdf, cons
 // margin 1e-7) dwarfs the f64 rounding of the exact tests.  Kept (never culled):
 // non-finite data (every comparison is false), origins inside a sphere, and
 // near-cylinders (|rb - ra| < 1e-3 max|r|: the cone formula's cancellation, main.rs:2924-2936).
-__device__ __forceinline__ uint32_t rt_wave_mask(const RtK* __restrict__ rt, const CamK& c, int xb, int xe, int yi,
-                                                 int W, int H) {
+struct RayCone {
+    double ax[3];  // unit axis
+    double ct, st; // cos / sin of the half-angle
+};
+
+__device__ __forceinline__ RayCone ray_cone(const CamK& c, int xb, int xe, int yi, int W, int H) {
     const double s0 = ndc(xb, W), s1 = ndc(xe, W), u = ndc(yi, H);
-    double n0[3], n1[3], ax[3];
+    double n0[3], n1[3];
+    RayCone k;
     double m0 = 0.0, m1 = 0.0;
-    for (int k = 0; k < 3; ++k) {
-        n0[k] = (c.dir[k] + c.side[k] * s0) + c.up[k] * u;
-        n1[k] = (c.dir[k] + c.side[k] * s1) + c.up[k] * u;
-        m0 += n0[k] * n0[k];
-        m1 += n1[k] * n1[k];
+    for (int j = 0; j < 3; ++j) {
+        n0[j] = (c.dir[j] + c.side[j] * s0) + c.up[j] * u;
+        n1[j] = (c.dir[j] + c.side[j] * s1) + c.up[j] * u;
+        m0 += n0[j] * n0[j];
+        m1 += n1[j] * n1[j];
     }
     m0 = 1.0 / sqrt(m0);
     m1 = 1.0 / sqrt(m1);
     double ma = 0.0;
-    for (int k = 0; k < 3; ++k) {
-        n0[k] *= m0;
-        n1[k] *= m1;
-        ax[k] = n0[k] + n1[k];
-        ma += ax[k] * ax[k];
+    for (int j = 0; j < 3; ++j) {
+        n0[j] *= m0;
+        n1[j] *= m1;
+        k.ax[j] = n0[j] + n1[j];
+        ma += k.ax[j] * k.ax[j];
     }
     ma = 1.0 / sqrt(ma);
     double ct = 0.0;
-    for (int k = 0; k < 3; ++k) {
-        ax[k] *= ma;
-        ct += ax[k] * n0[k];
+    for (int j = 0; j < 3; ++j) {
+        k.ax[j] *= ma;
+        ct += k.ax[j] * n0[j];
     }
-    ct = fmin(ct, 1.0);
-    const double st = sqrt(1.0 - ct * ct);
-    const int l = threadIdx.x & 63;
-    double C[3] = {0.0, 0.0, 0.0}, R = 0.0;
-    bool cullable = false;
+    k.ct = fmin(ct, 1.0);
+    k.st = sqrt(1.0 - k.ct * k.ct);
+    return k;
+}
+
+// Bounding sphere of primitive slot l (l < 16: circle plane l; 16 + i: cylinder i);
+// cullable false for an empty slot and for near-cylinders.
+__device__ __forceinline__ void rt_bound(const RtK* __restrict__ rt, int l, double C[3], double& R, bool& cullable) {
+    C[0] = C[1] = C[2] = 0.0;
+    R = 0.0;
+    cullable = false;
     if (l < rt->n_pl) {
         const PlaneK& p = rt->pl[l];
         C[0] = p.cx;
@@ -665,33 +676,49 @@ __device__ __forceinline__ uint32_t rt_wave_mask(const RtK* __restrict__ rt, con
     } else if (l >= 16 && l - 16 < rt->n_cy) {
         const CylK& q = rt->cy[l - 16];
         const double rmax = fmax(fabs(q.ra), fabs(q.rb));
-        for (int k = 0; k < 3; ++k) C[k] = (q.pa[k] + q.pb[k]) * 0.5;
+        for (int j = 0; j < 3; ++j) C[j] = (q.pa[j] + q.pb[j]) * 0.5;
         R = sqrt(q.baba) * 0.5 + rmax;
         cullable = fabs(q.rb - q.ra) >= 1e-3 * rmax;
     }
+}
+
+__device__ __forceinline__ bool cone_culls(const RayCone& k, const CamK& c, const double C[3], double R, bool cullable) {
     const double Ri = R * 1.001 + 1e-7;
     double w[3], L2 = 0.0, aw = 0.0;
-    for (int k = 0; k < 3; ++k) {
-        w[k] = C[k] - c.pos[k];
-        L2 += w[k] * w[k];
-        aw += ax[k] * w[k];
+    for (int j = 0; j < 3; ++j) {
+        w[j] = C[j] - c.pos[j];
+        L2 += w[j] * w[j];
+        aw += k.ax[j] * w[j];
     }
     const double L = sqrt(L2);
-    const double sb = Ri / L;                      // sin(beta)
+    const double sb = Ri / L;                          // sin(beta)
     const double cb = sqrt(fmax(1.0 - sb * sb, 0.0));
-    const double thr = ct * cb - st * sb - 1e-7;   // cos(theta + beta), less the margin
-    const bool cull = cullable & (L > Ri) & (sb < 1.0) & (aw < thr * L);
-    return ~(uint32_t)__ballot(cull);  // lane i < 16: plane i; lane 16 + i: cylinder i
+    const double thr = k.ct * cb - k.st * sb - 1e-7;   // cos(theta + beta), less the margin
+    return cullable & (L > Ri) & (sb < 1.0) & (aw < thr * L);
+}
+
+// Lane-parallel form inside a kernel (all lanes active): lane l tests slot l.
+__device__ __forceinline__ uint32_t rt_wave_mask(const RtK* __restrict__ rt, const CamK& c, int xb, int xe, int yi,
+                                                 int W, int H) {
+    const RayCone k = ray_cone(c, xb, xe, yi, W, H);
+    double C[3], R;
+    bool cullable;
+    rt_bound(rt, threadIdx.x & 63, C, R, cullable);
+    return ~(uint32_t)__ballot(cone_culls(k, c, C, R, cullable));  // lane i < 16: plane i; lane 16 + i: cylinder i
 }
 
 // rt_wave_mask culls whole primitives per wave: bits 0-15 planes, 16-31
 // cylinders.  A skipped primitive is one no ray of the wave can hit, so zb and
 // the hit are what the full loop would leave.
+// PERSP: the rays start at the PERSPECTIVE camera position and rt holds its
+// origin-only constants (RtK::persp; a compile-time choice, so the kernel carries
+// one path).
+template <bool PERSP>
 __device__ __forceinline__ void trace_pixel(const RtK* __restrict__ rt, const double o[3], const double d[3],
                                             double& zb_io, RtHit& hit, uint32_t mask = ~0u) {
     double zb = zb_io;
     const int npl = rt->n_pl, ncy = rt->n_cy;
-    const bool persp = rt->persp != 0;  // (uniform: the frame's eye camera)
+    constexpr bool persp = PERSP;
     for (int i = 0; i < npl; ++i) {
         if (!((mask >> i) & 1u)) continue;  // wave-uniform
         double t;
@@ -1357,6 +1384,10 @@ template <bool FUSED, bool COUNT, int RT, int FMT = RTM_FORMAT_RGBA32F>
 __device__ __forceinline__ void eye_tile(const EyePart& a, const ShadowPart& sh, const double* __restrict__ smap,
                                          void* __restrict__ out, int bx, int by, StatsK* __restrict__ st,
                                          const DevTabs tabs, int wide = 0) {
+    // RT 3: RT 1 under a PERSPECTIVE eye, with the host's origin-only primitive
+    // constants (RtK::persp) and the per-wave primitive masks of rt_cull_kernel
+    constexpr bool RTP = RT == 3;
+    constexpr int RTB = RTP ? 1 : RT;
     const RtK* __restrict__ rt = tabs.rt;
     const PerspK* __restrict__ psp = tabs.psp;
     const SdfTabK* __restrict__ sdf = tabs.sdf;
@@ -1377,7 +1408,10 @@ __device__ __forceinline__ void eye_tile(const EyePart& a, const ShadowPart& sh,
                          : 0u;
     // the wave's ray-traced primitives (PERSPECTIVE eye; all lanes active here)
     uint32_t rmask = ~0u;
-    if (RT == 1 && rt && a.eye.type == RTM_CAMERA_PERSPECTIVE && !(wide & 4))
+    if (RTP && tabs.rtmask)
+        rmask = ((const __attribute__((address_space(4))) uint32_t*)tabs.rtmask)[yl * ((a.W + TILE_X - 1) / TILE_X) +
+                                                                                 (xb / TILE_X)];
+    else if (RTB == 1 && rt && a.eye.type == RTM_CAMERA_PERSPECTIVE && !(wide & 4))
         rmask = rt_wave_mask(rt, a.eye, min(xb, a.W - 1), min(xb + TILE_X - 1, a.W - 1), min(yi, a.H - 1), a.W, a.H);
     float4 c = make_float4(0.0f, 0.2f, 0.2f, 1.0f);  // (0.0, 0.2, 0.2) as f32 (main.rs:718-720)
     bool shaded = false;
@@ -1392,7 +1426,7 @@ __device__ __forceinline__ void eye_tile(const EyePart& a, const ShadowPart& sh,
             smask &= smask - 1u;
             double h;
             // (RT variant only: a PERSPECTIVE eye with spheres, row f-3; psp is wave-uniform)
-            if ((RT && psp) ? cover_persp(psp->s[i], x, y, h) : cover(a.sph[i], x, y, h)) {
+            if ((RTB && psp) ? cover_persp(psp->s[i], x, y, h) : cover(a.sph[i], x, y, h)) {
                 if (COUNT) ++n_tests;
                 const double depth = a.sph[i].z - h * a.sph[i].r;  // EnumFace::FRONT (main.rs:239)
                 if (depth < best) {
@@ -1407,11 +1441,11 @@ __device__ __forceinline__ void eye_tile(const EyePart& a, const ShadowPart& sh,
         hit.kind = bid >= 0 ? 1 : 0;
         hit.id = bid;
         double o[3], d[3];
-        if (RT) {
+        if (RTB) {
             cam_ray(a.eye, x, y, o, d);
             double zb = best;
             if (rt) {
-                trace_pixel(rt, o, d, zb, hit, rmask);
+                trace_pixel<RTP>(rt, o, d, zb, hit, rmask);
                 if (COUNT) {
                     n_pl_tests = __builtin_popcount(rmask & ((1u << rt->n_pl) - 1u));
                     n_cy_tests = __builtin_popcount((rmask >> 16) & ((1u << rt->n_cy) - 1u));
@@ -1421,10 +1455,10 @@ __device__ __forceinline__ void eye_tile(const EyePart& a, const ShadowPart& sh,
         }
         if (hit.kind) {
             shaded = true;
-            if (!RT) cam_ray(a.eye, x, y, o, d);
+            if (!RTB) cam_ray(a.eye, x, y, o, d);
             // world position and normal per surface kind (main.rs:729-796)
             double wx, wy, wz, nx, ny, nz, cr, cg, cb;
-            if (!RT || hit.kind == 1) {
+            if (!RTB || hit.kind == 1) {
                 const ShadeSphereK& s = a.shade[bid];
                 const double depth = bz - bh * s.r;  // calcDepth (main.rs:160-162)
                 wx = o[0] + d[0] * depth;
@@ -1471,7 +1505,7 @@ __device__ __forceinline__ void eye_tile(const EyePart& a, const ShadowPart& sh,
             const double Rx = Lx - nx * k2, Ry = Ly - ny * k2, Rz = Lz - nz * k2;
             // retViewDirOfPixel (main.rs:1981-2013): -dir (ORTHOGONAL) or -normalize(ray) (PERSPECTIVE)
             double vx, vy, vz;
-            if (!RT || a.eye.type == RTM_CAMERA_ORTHOGONAL) {
+            if (!RTB || (!RTP && a.eye.type == RTM_CAMERA_ORTHOGONAL)) {
                 vx = a.eye.dir[0] * -1.0;
                 vy = a.eye.dir[1] * -1.0;
                 vz = a.eye.dir[2] * -1.0;
@@ -1561,7 +1595,7 @@ __device__ __forceinline__ void eye_tile(const EyePart& a, const ShadowPart& sh,
         stat_add(&st->eye_hit_pixels, n_hit);
         stat_add(&st->lit_pixels, n_lit);
         for (int i = 0; i < a.n_spheres; ++i) stat_add(&st->eye_hits[i], hit_kind == 1 && hit_id == i);
-        if (RT) {
+        if (RTB) {
             stat_add(&st->eye_circle_plane_pixels, hit_kind == 2);
             stat_add(&st->eye_capped_cylinder_pixels, hit_kind == 3);
             stat_add(&st->eye_plane_tests, n_pl_tests);
@@ -1614,6 +1648,29 @@ struct UploadChunk {
 };
 __global__ void upload_kernel(const UploadChunk k, uint64_t* __restrict__ dst, int n) {
     for (int i = threadIdx.x; i < n; i += blockDim.x) dst[i] = k.w[i];
+}
+
+// Per-wave primitive masks of an eye pass under a PERSPECTIVE eye (RT 3): the
+// cone cull of rt_wave_mask, one thread per wave of the eye pass (wave (bx, yl):
+// pixels bx*64 .. bx*64+63 of row row_begin + yl), so the cone set-up and the
+// bounding-sphere tests run once per wave instead of on every lane of it.  The
+// same operations, hence the same masks.
+__global__ __launch_bounds__(BLOCK) void rt_cull_kernel(const CamK c, const RtK* __restrict__ rt, int W, int H,
+                                                        int row_begin, int rows, uint32_t* __restrict__ masks) {
+    const int gx = (W + TILE_X - 1) / TILE_X;
+    const int t = blockIdx.x * BLOCK + threadIdx.x;
+    if (t >= gx * rows) return;
+    const int xb = (t % gx) * TILE_X, yi = row_begin + t / gx;
+    const RayCone k = ray_cone(c, min(xb, W - 1), min(xb + TILE_X - 1, W - 1), min(yi, H - 1), W, H);
+    uint32_t m = ~0u;
+    for (int l = 0; l < 32; ++l) {
+        if (l < 16 ? l >= rt->n_pl : l - 16 >= rt->n_cy) continue;
+        double C[3], R;
+        bool cullable;
+        rt_bound(rt, l, C, R, cullable);
+        if (cone_culls(k, c, C, R, cullable)) m &= ~(1u << l);
+    }
+    masks[t] = m;
 }
 
 // Timing diagnostic only (RTM_DIAG_EYE=1): the eye pass's stores without its work.
@@ -1728,7 +1785,10 @@ __global__ __launch_bounds__(BLOCK) void vp_trace_kernel(const TraceArgs a, doub
     hit.kind = 0;
     hit.id = 0;
     double zb = zbuf[idx];
-    if (a.rt) trace_pixel(a.rt, o, d, zb, hit);
+    if (a.rt) {
+        if (a.rt->persp) trace_pixel<true>(a.rt, o, d, zb, hit);
+        else trace_pixel<false>(a.rt, o, d, zb, hit);
+    }
     uint32_t evals = 0;
     if (a.sdf) trace_sdfs(a.sdf, o, d, zb, hit, evals);
     if (hit.kind) {
@@ -2022,6 +2082,9 @@ static void launch_eye_fmt(const FrameArgs& a, const double* smap, void* o, hipS
         else if (sdf_wpe5())  // 95 VGPRs, 5 waves/SIMD, no spill: eye 582 -> 565 us at config 8
             hipLaunchKernelGGL((eye_sdf_kernel<5, FMT>), g, dim3(BLOCK), 0, s, a, smap, o, tabs, wide);
         else RTM_EYE(false, 2);
+    } else if (tabs.rt && tabs.rt_persp) {
+        if (fused) RTM_EYE(true, 3);
+        else RTM_EYE(false, 3);
     } else if (tabs.rt || tabs.psp) {
         if (fused) RTM_EYE(true, 1);
         else RTM_EYE(false, 1);
@@ -2063,9 +2126,20 @@ int launch_eye_pass(const FrameArgs& a, const double* smap, void* out, void* str
 #undef RTM_EYE
         return launched();
     }
-    if (fmt == RTM_FORMAT_RGBA8) launch_eye_fmt<RTM_FORMAT_RGBA8>(a, smap, out, s, g, fused, tabs, wide);
-    else if (fmt == RTM_FORMAT_RGB8) launch_eye_fmt<RTM_FORMAT_RGB8>(a, smap, out, s, g, fused, tabs, wide);
-    else launch_eye_fmt<RTM_FORMAT_RGBA32F>(a, smap, out, s, g, fused, tabs, wide);
+    DevTabs t = tabs;
+    if (t.rt && t.rt_persp && !t.sdf) {
+        // the per-wave primitive masks (RT 3): one thread per wave of the eye pass
+        if (t.rtmask && !(wide & 4)) {
+            const int n = ((a.ey.W + TILE_X - 1) / TILE_X) * rows;
+            hipLaunchKernelGGL(rt_cull_kernel, dim3((unsigned)((n + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, s, a.ey.eye,
+                               t.rt, a.ey.W, a.ey.H, a.ey.row_begin, rows, t.rtmask);
+        } else {
+            t.rtmask = nullptr;
+        }
+    }
+    if (fmt == RTM_FORMAT_RGBA8) launch_eye_fmt<RTM_FORMAT_RGBA8>(a, smap, out, s, g, fused, t, wide);
+    else if (fmt == RTM_FORMAT_RGB8) launch_eye_fmt<RTM_FORMAT_RGB8>(a, smap, out, s, g, fused, t, wide);
+    else launch_eye_fmt<RTM_FORMAT_RGBA32F>(a, smap, out, s, g, fused, t, wide);
     return launched();
 }
 
