@@ -123,6 +123,8 @@ ABI_SYMBOLS = [
     ("rtm_ctx_set_timing_stride", C.c_int, [_P, _I32]),
     ("rtm_ctx_set_lanes", C.c_int, [_P, _I32]),
     ("rtm_ctx_last_lanes", C.c_int, [_P, C.POINTER(_I32)]),
+    ("rtm_ctx_set_batch", C.c_int, [_P, _I32]),
+    ("rtm_ctx_last_batch", C.c_int, [_P, C.POINTER(_I32)]),
     ("rtm_ctx_kernel_ms_history", C.c_int, [_P, C.POINTER(C.c_float), C.POINTER(C.c_float), _I32,
                                             C.POINTER(_I32)]),
     ("rtm_render", C.c_int, [C.POINTER(rtm_scene), C.POINTER(rtm_camera), C.POINTER(rtm_camera),

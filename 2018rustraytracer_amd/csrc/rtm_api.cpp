@@ -615,6 +615,38 @@ struct TimingSlot {
     bool shadow = false;
 };
 
+// Batched frame uploads of one lane: a ring of R slots, each a pinned host
+// staging area and a device copy of a batch's BatchFrame table (+ the frames'
+// ray-traced / perspective / SDF tables).  A slot's host side is refilled once
+// its previous upload has completed (copied[j]), its device side once the
+// kernels that read it have run (used[j]); the upload runs on its own stream, so
+// batch i+1's table crosses PCIe while batch i renders.
+struct BatchRing {
+    static constexpr int R = 4;
+    hipStream_t copy = nullptr;
+    void* host[R] = {};
+    size_t host_bytes[R] = {};
+    DevBuf dev[R];
+    hipEvent_t copied[R] = {}, used[R] = {};
+    int next = 0;
+    DevBuf smaps;  // the batch's shadow maps, B x W x H f64
+    int device = 0;
+    ~BatchRing() {
+        int cur = 0;
+        (void)hipGetDevice(&cur);
+        (void)hipSetDevice(device);
+        if (copy) (void)hipStreamSynchronize(copy);
+        for (int j = 0; j < R; ++j) {
+            if (used[j]) (void)hipEventSynchronize(used[j]);
+            if (host[j]) (void)hipHostFree(host[j]);
+            if (copied[j]) (void)hipEventDestroy(copied[j]);
+            if (used[j]) (void)hipEventDestroy(used[j]);
+        }
+        if (copy) (void)hipStreamDestroy(copy);
+        (void)hipSetDevice(cur);
+    }
+};
+
 // An extra stream of a context with its own per-frame buffers: the frame
 // sequence call spreads independent frames over lanes so one frame's kernels
 // fill the ramp and tail of another's (see frame_lanes).
@@ -622,6 +654,7 @@ struct Lane {
     hipStream_t stream = nullptr;
     hipEvent_t done = nullptr;  // join: the context stream waits on it
     DevBuf smap, rtk, pspk, sdfk, rtmask;
+    std::unique_ptr<BatchRing> batch;
 };
 
 struct rtm_ctx {
@@ -631,6 +664,9 @@ struct rtm_ctx {
     hipEvent_t fork = nullptr;                 // lanes wait on the context stream's earlier work
     int32_t lanes_req = 0;                     // rtm_ctx_set_lanes (0 = auto)
     int32_t lanes_last = 0;                    // lanes of the last frame-sequence call
+    int32_t batch_req = 0;                     // rtm_ctx_set_batch (0 = auto)
+    int32_t batch_last = 1;                    // frames per launch of the last frame-sequence call
+    std::unique_ptr<BatchRing> batch;          // lane 0's batch uploads
     std::vector<TimingSlot> ring;  // per-render kernel events (capacity = ring.size())
     int64_t renders = 0;           // renders recorded into the ring
     int64_t calls = 0;             // renders enqueued (for the stride)
@@ -990,19 +1026,20 @@ int enqueue_frame(rtm_ctx* ctx, FrameArgs& a, const FrameExtra* x, void* out_dev
 // Frame i goes to lane (n-1-i) % L, so the last frame runs on lane 0 and the
 // context's shadow map holds its shadow pass, as on one lane.  Lanes stay at 1
 // when two frames of different lanes write overlapping output.
-int frame_lanes(int32_t req, int32_t n, int32_t W, int32_t H, float* const* out) {
+int frame_lanes(int32_t req, int32_t n, int32_t W, int32_t H, float* const* out, int32_t B = 1) {
     static const int env = [] {
         const char* e = getenv("RTM_LANES");
         return e ? atoi(e) : 0;
     }();
     const int64_t px = (int64_t)W * H;
     int L = req > 0 ? req : env > 0 ? env : (px >= (1LL << 20) && px <= 3840LL * 2160 ? 3 : 1);
+    const int32_t nb = (n + B - 1) / B;  // batches of B frames; batch b runs on lane (nb-1-b) % L
     if (L > 8) L = 8;
-    if (L > n) L = n;
+    if (L > nb) L = nb;
     if (L <= 1) return 1;
     const uintptr_t bytes = (uintptr_t)W * (uintptr_t)H * 4u * sizeof(float);
     std::vector<std::pair<uintptr_t, int>> r((size_t)n);
-    for (int32_t i = 0; i < n; ++i) r[(size_t)i] = {(uintptr_t)out[i], (n - 1 - i) % L};
+    for (int32_t i = 0; i < n; ++i) r[(size_t)i] = {(uintptr_t)out[i], (nb - 1 - i / B) % L};
     std::sort(r.begin(), r.end());
     // equal-length ranges: any two overlapping ranges are joined by a chain of
     // overlapping sorted neighbours, so checking neighbours checks every pair
@@ -1022,6 +1059,133 @@ int ensure_lanes(rtm_ctx* ctx, int L) {
         }
         ctx->lanes.push_back(std::move(l));
     }
+    return RTM_OK;
+}
+
+// Frames per launch of a frame sequence: below 4 Mpixel a frame's two kernels
+// are short and the host's per-frame launches bound the rate (512x512: ~16
+// Gpix/s), so 4 Mpixel worth of frames (at most 16) share one launch per pass
+// (rtm_ctx_set_batch / RTM_BATCH override; 1 = one frame per launch).
+int frame_batch(int32_t req, int32_t W, int32_t H) {
+    static const int env = [] {
+        const char* e = getenv("RTM_BATCH");
+        return e ? atoi(e) : 0;
+    }();
+    const int64_t px = (int64_t)W * H;
+    int B = req > 0 ? req : env > 0 ? env : (int)std::max<int64_t>(1, std::min<int64_t>(16, (4LL << 20) / px));
+    return std::max(1, std::min(B, 64));
+}
+
+// Enqueue frames [0, n) of `fa` (same tables, flags and sizes) as ONE batched
+// launch per pass on `lane`; a frame's output is outs[k] (RGBA f32).
+int enqueue_batch(rtm_ctx* ctx, int lane, FrameArgs* fa, const FrameExtra* ex, float* const* outs, int n) {
+    int rc;
+    if ((rc = frame_tables(ctx, fa[0]))) return rc;
+    for (int k = 1; k < n; ++k) {
+        fa[k].sh.tab = fa[0].sh.tab;
+        fa[k].ey.nx = fa[0].ey.nx;
+        fa[k].ey.ny = fa[0].ey.ny;
+    }
+    Lane* l = lane > 0 ? ctx->lanes[(size_t)lane - 1].get() : nullptr;
+    hipStream_t s = l ? l->stream : ctx->stream;
+    std::unique_ptr<BatchRing>& brp = l ? l->batch : ctx->batch;
+    if (!brp) {
+        std::unique_ptr<BatchRing> b(new BatchRing);
+        b->device = ctx->device;
+        HIP_TRY(hipStreamCreateWithFlags(&b->copy, hipStreamNonBlocking));
+        for (int j = 0; j < BatchRing::R; ++j) {
+            HIP_TRY(hipEventCreateWithFlags(&b->copied[j], hipEventDisableTiming));
+            HIP_TRY(hipEventCreateWithFlags(&b->used[j], hipEventDisableTiming));
+        }
+        brp = std::move(b);
+    }
+    BatchRing& br = *brp;
+    const bool fused = (fa[0].ey.flags & RTM_FLAG_FUSED_SHADOW) != 0;
+    const size_t map_words = (size_t)fa[0].sh.W * (size_t)fa[0].sh.H;
+    if (!fused && (rc = br.smaps.ensure(sizeof(double) * map_words * (size_t)n, ctx->device))) return rc;
+    // layout of the upload: the BatchFrame table, then each frame's device tables
+    auto up = [](size_t v) { return (v + 255) & ~(size_t)255; };
+    size_t off = up(sizeof(BatchFrame) * (size_t)n);
+    std::vector<size_t> o_rt((size_t)n, 0), o_psp((size_t)n, 0), o_sdf((size_t)n, 0);
+    for (int k = 0; k < n; ++k) {
+        if (ex[k].has_rt) { o_rt[(size_t)k] = off; off = up(off + sizeof(RtK)); }
+        if (ex[k].has_psp) { o_psp[(size_t)k] = off; off = up(off + sizeof(PerspK)); }
+        if (ex[k].has_sdf) { o_sdf[(size_t)k] = off; off = up(off + sizeof(SdfTabK)); }
+    }
+    const size_t bytes = off;
+    const int j = br.next;
+    br.next = (br.next + 1) % BatchRing::R;
+    HIP_TRY(hipEventSynchronize(br.copied[j]));  // the slot's previous upload has left the host buffer
+    if (br.host_bytes[j] < bytes) {
+        if (br.host[j]) HIP_TRY(hipHostFree(br.host[j]));
+        br.host[j] = nullptr;
+        br.host_bytes[j] = 0;
+        HIP_TRY(hipHostMalloc(&br.host[j], bytes, hipHostMallocDefault));
+        br.host_bytes[j] = bytes;
+    }
+    if (br.dev[j].bytes < bytes) {
+        HIP_TRY(hipEventSynchronize(br.used[j]));  // no kernel still reads the old device slot
+        if ((rc = br.dev[j].ensure(bytes, ctx->device))) return rc;
+    }
+    char* hb = (char*)br.host[j];
+    char* db = (char*)br.dev[j].p;
+    DevTabs t0{};
+    for (int k = 0; k < n; ++k) {
+        BatchFrame& bf = *(BatchFrame*)(hb + sizeof(BatchFrame) * (size_t)k);
+        bf.a = fa[k];
+        bf.smap = fused ? nullptr : (double*)br.smaps.p + map_words * (size_t)k;
+        bf.out = outs[k];
+        if ((rc = format_tabs(ctx, RTM_FORMAT_RGBA32F, fa[k].ey.W, outs[k], bf.tabs))) return rc;
+        bf.tabs.rt = nullptr;
+        bf.tabs.psp = nullptr;
+        bf.tabs.sdf = nullptr;
+        bf.tabs.rtmask = nullptr;
+        bf.tabs.rt_persp = 0;
+        if (ex[k].has_rt) {
+            std::memcpy(hb + o_rt[(size_t)k], &ex[k].rt, sizeof(RtK));
+            bf.tabs.rt = (const RtK*)(db + o_rt[(size_t)k]);
+            bf.tabs.rt_persp = ex[k].rt.persp;
+            t0.rt = bf.tabs.rt;
+            t0.rt_persp = ex[k].rt.persp;
+        }
+        if (ex[k].has_psp) {
+            std::memcpy(hb + o_psp[(size_t)k], &ex[k].psp, sizeof(PerspK));
+            bf.tabs.psp = (const PerspK*)(db + o_psp[(size_t)k]);
+            t0.psp = bf.tabs.psp;
+        }
+        if (ex[k].has_sdf) {
+            std::memcpy(hb + o_sdf[(size_t)k], &ex[k].sdf, sizeof(SdfTabK));
+            bf.tabs.sdf = (const SdfTabK*)(db + o_sdf[(size_t)k]);
+            t0.sdf = bf.tabs.sdf;
+        }
+    }
+    // a frame without ray-traced primitives in a RT 3 batch: every frame shares the eye camera
+    t0.rt_persp = t0.rt ? t0.rt_persp : 0;
+    t0.fmt = RTM_FORMAT_RGBA32F;
+    HIP_TRY(hipStreamWaitEvent(br.copy, br.used[j], 0));  // the device slot is free
+    HIP_TRY(hipMemcpyAsync(db, hb, bytes, hipMemcpyHostToDevice, br.copy));
+    HIP_TRY(hipEventRecord(br.copied[j], br.copy));
+    HIP_TRY(hipStreamWaitEvent(s, br.copied[j], 0));
+    TimingSlot* slot = next_slot(ctx);
+    if (!fused) {
+        if (slot) HIP_TRY(hipEventRecord(slot->ev[0], s));
+        if ((rc = launch_shadow_batch((const BatchFrame*)db, n, fa[0], s))) return fail(rc, "batched shadow pass failed");
+        if (slot) HIP_TRY(hipEventRecord(slot->ev[1], s));
+        ctx->have_shadow_pass = true;
+        ctx->last_smap = (const double*)br.smaps.p + map_words * (size_t)(n - 1);
+        ctx->smap_w = fa[0].sh.W;
+        ctx->smap_h = fa[0].sh.H;
+    } else {
+        ctx->have_shadow_pass = false;
+    }
+    if (slot) HIP_TRY(hipEventRecord(slot->ev[2], s));
+    if ((rc = launch_eye_batch((const BatchFrame*)db, n, fa[0], t0, s))) return fail(rc, "batched eye pass failed");
+    if (slot) {
+        HIP_TRY(hipEventRecord(slot->ev[3], s));
+        slot->shadow = !fused;
+        ctx->renders++;
+    }
+    HIP_TRY(hipEventRecord(br.used[j], s));
     return RTM_OK;
 }
 
@@ -1089,10 +1253,12 @@ void rtm_ctx_destroy(rtm_ctx* ctx) {
         if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
         for (auto& l : ctx->lanes) {
             (void)hipStreamSynchronize(l->stream);
+            l->batch.reset();
             if (l->done) (void)hipEventDestroy(l->done);
             (void)hipStreamDestroy(l->stream);
         }
         ctx->lanes.clear();
+        ctx->batch.reset();
         if (ctx->fork) (void)hipEventDestroy(ctx->fork);
         for (auto& sl : ctx->ring)
             for (auto& e : sl.ev)
@@ -1139,6 +1305,18 @@ int rtm_ctx_set_timing_stride(rtm_ctx* ctx, int32_t stride) {
 int rtm_ctx_set_lanes(rtm_ctx* ctx, int32_t lanes) {
     if (!ctx || lanes < 0 || lanes > 8) return fail(RTM_ERR_INVALID, "ctx NULL or lanes %d outside [0,8]", lanes);
     ctx->lanes_req = lanes;
+    return RTM_OK;
+}
+
+int rtm_ctx_set_batch(rtm_ctx* ctx, int32_t frames) {
+    if (!ctx || frames < 0 || frames > 64) return fail(RTM_ERR_INVALID, "ctx NULL or batch %d outside [0,64]", frames);
+    ctx->batch_req = frames;
+    return RTM_OK;
+}
+
+int rtm_ctx_last_batch(rtm_ctx* ctx, int32_t* frames) {
+    if (!ctx || !frames) return fail(RTM_ERR_INVALID, "bad arguments");
+    *frames = ctx->batch_last;
     return RTM_OK;
 }
 
@@ -1205,7 +1383,8 @@ int rtm_render_frames_async(rtm_ctx* ctx, int32_t n_frames, const rtm_scene* sce
         // so the GPU starts on frame 0 while the host prepares frame 1 (building all
         // frames first left the GPU idle for the whole build)
         DeviceGuard g(ctx->device);
-        int L = frame_lanes(ctx->lanes_req, n_frames, width, height, out_rgba_dev);
+        int B = std::min<int32_t>(frame_batch(ctx->batch_req, width, height), n_frames);
+        int L = frame_lanes(ctx->lanes_req, n_frames, width, height, out_rgba_dev, B);
         int rc = RTM_OK;
         if (L > 1) {  // fork: the lanes start after the context stream's earlier work
             if ((rc = ensure_lanes(ctx, L))) return rc;
@@ -1213,13 +1392,38 @@ int rtm_render_frames_async(rtm_ctx* ctx, int32_t n_frames, const rtm_scene* sce
             for (int k = 1; k < L; ++k) HIP_TRY(hipStreamWaitEvent(ctx->lanes[(size_t)k - 1]->stream, ctx->fork, 0));
         }
         ctx->lanes_last = L;
-        for (int32_t i = 0; i < n_frames && !rc; ++i) {
-            FrameArgs fa;
-            FrameExtra ex1;
-            rc = build_frame(fa, &scenes[i], eye, shadow, width, height, march_steps, flags);
+        ctx->batch_last = B;
+        const int32_t nb = (n_frames + B - 1) / B;
+        std::vector<FrameArgs> fa((size_t)B);
+        std::vector<FrameExtra> fx((size_t)B);
+        for (int32_t b = 0; b < nb && !rc; ++b) {
+            const int32_t i0 = b * B, nf = std::min(B, n_frames - i0);
+            const int lane = (nb - 1 - b) % L;
+            for (int32_t k = 0; k < nf && !rc; ++k) {
+                rc = build_frame(fa[(size_t)k], &scenes[i0 + k], eye, shadow, width, height, march_steps, flags);
+                if (!rc) build_extra(&scenes[i0 + k], eye, width, height, fx[(size_t)k]);
+            }
             if (rc) break;
-            build_extra(&scenes[i], eye, width, height, ex1);
-            rc = enqueue_frame(ctx, fa, &ex1, out_rgba_dev[i], nullptr, (n_frames - 1 - i) % L);
+            // runs of frames with the same march tables (patches) share one launch per pass;
+            // the A/B-only shadow modes and single frames take the per-frame kernels
+            for (int32_t k = 0; k < nf && !rc;) {
+                int32_t e = k + 1;
+                while (e < nf && fa[(size_t)e].sh.n_patches == fa[(size_t)k].sh.n_patches &&
+                       std::memcmp(fa[(size_t)e].sh.patch, fa[(size_t)k].sh.patch,
+                                   sizeof(PatchK) * (size_t)fa[(size_t)k].sh.n_patches) == 0)
+                    ++e;
+                if (e - k >= 2 && shadow_batchable(fa[(size_t)k].sh)) {
+                    if (!(rc = frame_tables(ctx, fa[(size_t)k])) && shadow_batchable(fa[(size_t)k].sh))
+                        rc = enqueue_batch(ctx, lane, &fa[(size_t)k], &fx[(size_t)k], out_rgba_dev + i0 + k, e - k);
+                    else if (!rc)
+                        for (int32_t q = k; q < e && !rc; ++q)
+                            rc = enqueue_frame(ctx, fa[(size_t)q], &fx[(size_t)q], out_rgba_dev[i0 + q], nullptr, lane);
+                } else {
+                    for (int32_t q = k; q < e && !rc; ++q)
+                        rc = enqueue_frame(ctx, fa[(size_t)q], &fx[(size_t)q], out_rgba_dev[i0 + q], nullptr, lane);
+                }
+                k = e;
+            }
         }
         // join every lane (also after an error, so the context stream still covers what
         // was enqueued); the first error, of the frames or of a join, is returned

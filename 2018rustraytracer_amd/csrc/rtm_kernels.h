@@ -220,6 +220,17 @@ struct DevTabs {
 constexpr int32_t FMT_MASK = 0xff;
 constexpr int32_t FMT_RGB8_DWORDS = 0x100;
 
+// One frame of a batched launch (rtm_render_frames_async on small frames): every
+// workgroup of blockIdx.z == frame reads its constants from here (device memory,
+// scalar loads like a kernel argument), so one launch per pass covers a batch of
+// frames instead of one launch per frame.
+struct BatchFrame {
+    FrameArgs a;
+    double* smap;  // the frame's shadow map (W*H f64)
+    void* out;     // the frame's output (rows [row_begin, row_end) in tabs.fmt)
+    DevTabs tabs;  // its device tables (rt/psp/sdf inside the batch upload)
+};
+
 // Reference-seam kernels (one per reference function).
 struct RasterArgs {
     RasterSphereK sph[RTM_MAX_SPHERES];
@@ -276,6 +287,12 @@ int launch_shadow_pass(const FrameArgs& a, double* smap, void* stream, StatsK* s
 // out: (row_end-row_begin)*W pixels in tabs.fmt's format (RTM_FORMAT_RGBA32F: 16-byte aligned).
 int launch_eye_pass(const FrameArgs& a, const double* smap, void* out, void* stream, StatsK* stats,
                     const DevTabs& tabs = DevTabs{});
+// Batched passes over n frames (gridDim.z = n) whose BatchFrame table is at dev
+// (device memory); a0 / t0: the host copy of frame 0's arguments (every frame of
+// a batch shares the shapes, flags, tables and kernel variant).
+int launch_shadow_batch(const BatchFrame* dev, int n, const FrameArgs& a0, void* stream);
+int launch_eye_batch(const BatchFrame* dev, int n, const FrameArgs& a0, const DevTabs& t0, void* stream);
+bool shadow_batchable(const ShadowPart& sh);
 // Stream-ordered copy of host bytes into device memory by kernels whose
 // arguments carry the bytes (<= 3968 per launch), so the host copy is consumed
 // at launch: no pinned staging, no host synchronisation.  bytes % 8 == 0.

@@ -1356,20 +1356,38 @@ __device__ __forceinline__ int hot_rows_first(int b, int n, int h0, int h1) {
     return r < h0 ? r : r + nh;
 }
 
-template <int NR, int CW, bool INC, int FILLN = 4>
-__global__ __launch_bounds__(BLOCK) void shadow_lean2_kernel(const FrameArgs a, double* __restrict__ smap, int diag,
-                                                             int hot) {
-    extern __shared__ double2 lds_zt[];
+template <int NR, int CW, bool INC, int FILLN>
+__device__ __forceinline__ void shadow_lean2_block(const ShadowPart& sh, double* __restrict__ smap, int diag, int hot,
+                                                   double2* __restrict__ lds) {
     int by = blockIdx.y;
     if (hot) {
         constexpr int TR = TILE_Y * NR;
         const int n = (int)gridDim.y;
-        const int h0 = max(a.sh.cull_y0, 0) / TR;
-        const int h1 = min(min(a.sh.cull_y1, a.sh.H - 1) / TR, n - 1);
-        const bool none = a.sh.cull_x0 > a.sh.cull_x1 || a.sh.cull_y0 > a.sh.cull_y1 || a.sh.cull_y1 < 0;
+        const int h0 = max(sh.cull_y0, 0) / TR;
+        const int h1 = min(min(sh.cull_y1, sh.H - 1) / TR, n - 1);
+        const bool none = sh.cull_x0 > sh.cull_x1 || sh.cull_y0 > sh.cull_y1 || sh.cull_y1 < 0;
         by = none ? by : hot_rows_first(by, n, h0, h1);
     }
-    shadow_tile_lean2<NR, CW, INC, FILLN>(a.sh, smap, blockIdx.x, by, lds_zt, diag);
+    shadow_tile_lean2<NR, CW, INC, FILLN>(sh, smap, blockIdx.x, by, lds, diag);
+}
+
+template <int NR, int CW, bool INC, int FILLN = 4>
+__global__ __launch_bounds__(BLOCK) void shadow_lean2_kernel(const FrameArgs a, double* __restrict__ smap, int diag,
+                                                             int hot) {
+    extern __shared__ double2 lds_zt[];
+    shadow_lean2_block<NR, CW, INC, FILLN>(a.sh, smap, diag, hot, lds_zt);
+}
+
+// Batched forms: frame blockIdx.z of a BatchFrame table in device memory.  The
+// table is read through the constant address space, so its fields become scalar
+// loads exactly like kernel arguments.
+using CBatch = const __attribute__((address_space(4))) BatchFrame;
+
+template <int NR, int CW, bool INC, int FILLN>
+__global__ __launch_bounds__(BLOCK) void shadow_lean2_batch_kernel(CBatch* __restrict__ fr, int diag, int hot) {
+    extern __shared__ double2 lds_zt[];
+    CBatch* f = fr + blockIdx.z;
+    shadow_lean2_block<NR, CW, INC, FILLN>(*(const ShadowPart*)&f->a.sh, f->smap, diag, hot, lds_zt);
 }
 
 
@@ -1620,6 +1638,11 @@ __global__ __launch_bounds__(BLOCK) void shadow_pass_kernel(const FrameArgs a, d
     shadow_tile_generic<COUNT>(a.sh, smap, blockIdx.x, blockIdx.y, st);
 }
 
+__global__ __launch_bounds__(BLOCK) void shadow_pass_batch_kernel(CBatch* __restrict__ fr) {
+    CBatch* f = fr + blockIdx.z;
+    shadow_tile_generic<false>(*(const ShadowPart*)&f->a.sh, f->smap, blockIdx.x, blockIdx.y, nullptr);
+}
+
 template <int NR, int MODE>
 __global__ __launch_bounds__(BLOCK) void shadow_sep_kernel(const FrameArgs a, double* __restrict__ smap, int diag,
                                                            int lds) {
@@ -1639,6 +1662,23 @@ template <int WPE, int FMT>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8))) void eye_sdf_kernel(
     const FrameArgs a, const double* __restrict__ smap, void* __restrict__ out, const DevTabs tabs, int wide) {
     eye_tile<false, false, 2, FMT>(a.ey, a.sh, smap, out, blockIdx.x, blockIdx.y, nullptr, tabs, wide);
+}
+
+template <bool FUSED, int RT, int FMT>
+__global__ __launch_bounds__(BLOCK) void eye_batch_kernel(CBatch* __restrict__ fr, int wide) {
+    CBatch* f = fr + blockIdx.z;
+    const DevTabs tabs = *(const DevTabs*)&f->tabs;
+    eye_tile<FUSED, false, RT, FMT>(*(const EyePart*)&f->a.ey, *(const ShadowPart*)&f->a.sh, f->smap, f->out,
+                                    blockIdx.x, blockIdx.y, nullptr, tabs, wide);
+}
+
+template <int WPE, int FMT>
+__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8))) void eye_sdf_batch_kernel(
+    CBatch* __restrict__ fr, int wide) {
+    CBatch* f = fr + blockIdx.z;
+    const DevTabs tabs = *(const DevTabs*)&f->tabs;
+    eye_tile<false, false, 2, FMT>(*(const EyePart*)&f->a.ey, *(const ShadowPart*)&f->a.sh, f->smap, f->out,
+                                   blockIdx.x, blockIdx.y, nullptr, tabs, wide);
 }
 
 // launch_upload: one 8-byte word per thread from the kernarg copy.
@@ -2140,6 +2180,69 @@ int launch_eye_pass(const FrameArgs& a, const double* smap, void* out, void* str
     if (fmt == RTM_FORMAT_RGBA8) launch_eye_fmt<RTM_FORMAT_RGBA8>(a, smap, out, s, g, fused, t, wide);
     else if (fmt == RTM_FORMAT_RGB8) launch_eye_fmt<RTM_FORMAT_RGB8>(a, smap, out, s, g, fused, t, wide);
     else launch_eye_fmt<RTM_FORMAT_RGBA32F>(a, smap, out, s, g, fused, t, wide);
+    return launched();
+}
+
+int launch_shadow_batch(const BatchFrame* dev, int n, const FrameArgs& a0, void* stream) {
+    hipStream_t s = (hipStream_t)stream;
+    CBatch* fr = (CBatch*)dev;
+    const ShadowPart& sh = a0.sh;
+    if (use_sep(sh) && sep_mode(sh) == MARCH_LEAN2 && sep_rows() == 4 && lean_cols() == 2) {
+        const bool march = !(sh.flags & RTM_FLAG_NO_MARCH) && sh.n_patches > 0 && sh.steps > 0;
+        const size_t lsm = march ? sizeof(double2) * (size_t)(sh.steps + 1) : 0;
+        dim3 g((unsigned)((sh.W + 2 * TILE_X - 1) / (2 * TILE_X)), (unsigned)((sh.H + TILE_Y * 4 - 1) / (TILE_Y * 4)),
+               (unsigned)n);
+        const bool inc = sh.tab.zmono >= 0;
+        const bool fill1 = lean_fill1() && sh.steps + 1 <= BLOCK;
+        const int hot = lean_hot() ? 1 : 0;
+#define RTM_LB(I, F) hipLaunchKernelGGL((shadow_lean2_batch_kernel<4, 2, I, F>), g, dim3(BLOCK), lsm, s, fr, diag_mode(), hot)
+        if (fill1) {
+            if (inc) RTM_LB(true, 1);
+            else RTM_LB(false, 1);
+        } else {
+            if (inc) RTM_LB(true, 4);
+            else RTM_LB(false, 4);
+        }
+#undef RTM_LB
+        return launched();
+    }
+    if (use_sep(sh)) return RTM_ERR_UNSUPPORTED;  // A/B-only shadow modes: the caller renders frame by frame
+    dim3 g = grid_for(sh.W, sh.H);
+    g.z = (unsigned)n;
+    hipLaunchKernelGGL(shadow_pass_batch_kernel, g, dim3(BLOCK), 0, s, fr);
+    return launched();
+}
+
+// Can a batch take the batched shadow kernels (the lean tile or the generic one)?
+bool shadow_batchable(const ShadowPart& sh) {
+    return !use_sep(sh) || (sep_mode(sh) == MARCH_LEAN2 && sep_rows() == 4 && lean_cols() == 2);
+}
+
+int launch_eye_batch(const BatchFrame* dev, int n, const FrameArgs& a0, const DevTabs& t0, void* stream) {
+    hipStream_t s = (hipStream_t)stream;
+    CBatch* fr = (CBatch*)dev;
+    const int rows = a0.ey.row_end - a0.ey.row_begin;
+    const int wide = eye_wide();
+    dim3 g = (wide & 1) ? dim3((unsigned)((a0.ey.W + BLOCK - 1) / BLOCK), (unsigned)rows) : grid_for(a0.ey.W, rows);
+    g.z = (unsigned)n;
+    const bool fused = (a0.ey.flags & RTM_FLAG_FUSED_SHADOW) != 0;
+    const int fmt = t0.fmt & FMT_MASK;
+    const int rt = t0.sdf ? 2 : (t0.rt && t0.rt_persp) ? 3 : (t0.rt || t0.psp) ? 1 : 0;
+#define RTM_EB(F, R, M) hipLaunchKernelGGL((eye_batch_kernel<F, R, M>), g, dim3(BLOCK), 0, s, fr, wide)
+#define RTM_EBF(M)                                                                           \
+    do {                                                                                     \
+        if (rt == 2 && !fused && sdf_wpe5())                                                 \
+            hipLaunchKernelGGL((eye_sdf_batch_kernel<5, M>), g, dim3(BLOCK), 0, s, fr, wide); \
+        else if (rt == 2) { if (fused) RTM_EB(true, 2, M); else RTM_EB(false, 2, M); }      \
+        else if (rt == 3) { if (fused) RTM_EB(true, 3, M); else RTM_EB(false, 3, M); }      \
+        else if (rt == 1) { if (fused) RTM_EB(true, 1, M); else RTM_EB(false, 1, M); }      \
+        else { if (fused) RTM_EB(true, 0, M); else RTM_EB(false, 0, M); }                   \
+    } while (0)
+    if (fmt == RTM_FORMAT_RGBA8) RTM_EBF(RTM_FORMAT_RGBA8);
+    else if (fmt == RTM_FORMAT_RGB8) RTM_EBF(RTM_FORMAT_RGB8);
+    else RTM_EBF(RTM_FORMAT_RGBA32F);
+#undef RTM_EBF
+#undef RTM_EB
     return launched();
 }
 

@@ -70,6 +70,17 @@ class Context:
         lib = _lib()
         abi.check(lib, lib.rtm_ctx_set_lanes(self._h, n), "rtm_ctx_set_lanes")
 
+    def set_batch(self, n: int):
+        """Frames per launch of render_frames_async (0 = auto, 1 = one frame per launch)."""
+        lib = _lib()
+        abi.check(lib, lib.rtm_ctx_set_batch(self._h, n), "rtm_ctx_set_batch")
+
+    def last_batch(self) -> int:
+        n = C.c_int32()
+        lib = _lib()
+        abi.check(lib, lib.rtm_ctx_last_batch(self._h, C.byref(n)), "rtm_ctx_last_batch")
+        return int(n.value)
+
     def last_lanes(self) -> int:
         n = C.c_int32()
         lib = _lib()

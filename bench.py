@@ -407,6 +407,12 @@ def main():
         else:
             sh_ms, eye_ms = [0.0], [0.0]
 
+    # batched launches (rtm_ctx_set_batch: several frames per launch): the events
+    # time a launch, i.e. a batch of frames; the per-kernel figures are per frame
+    batch = ctx.last_batch() if sequence else 1
+    if batch > 1:
+        sh_ms, eye_ms = [v / batch for v in sh_ms], [v / batch for v in eye_ms]
+
     # With several lanes (rtm_ctx_set_lanes: independent frames on side-by-side
     # streams) the kernels of the timed region overlap, and each event duration is
     # a kernel's time BESIDE other frames' kernels.  The kernel roofline is taken
@@ -431,6 +437,8 @@ def main():
         barrier()
         el1 = time.perf_counter() - t1
         sh_ms, eye_ms = ctx.kernel_ms_history((n1 + timing_stride - 1) // timing_stride)
+        b1 = ctx.last_batch()
+        sh_ms, eye_ms = [v / b1 for v in sh_ms], [v / b1 for v in eye_ms]
         ctx.set_lanes(0)
         one_lane = {"value": round(W * H * n1 / el1 / 1e6, 2), "unit": "Mpixels/s", "frames": n1,
                     "ms_per_step": round(el1 / n1 * 1e3, 5),
@@ -564,6 +572,7 @@ def main():
             "roofline_other_kernel": roof_other,
             "roofline_frame": roof_frame,
             "lanes": lanes,
+            "frames_per_launch": batch,
             "kernels_in_lanes": in_lanes,
             "one_lane": one_lane,
             "preroll": preroll,

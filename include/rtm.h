@@ -236,6 +236,17 @@ int rtm_ctx_kernel_ms_history(rtm_ctx* ctx, float* shadow_pass_ms, float* eye_pa
  * rtm_render_frames_async call used. */
 int rtm_ctx_set_lanes(rtm_ctx* ctx, int32_t lanes);
 int rtm_ctx_last_lanes(rtm_ctx* ctx, int32_t* lanes);
+/* Frames per launch of rtm_render_frames_async (ABI v6): consecutive frames with
+ * the same patches share ONE launch per pass (the frame index is the grid's z
+ * dimension; each frame's constants come from a table uploaded per batch), so
+ * small frames stop paying a launch per pass per frame.  0 = auto (RTM_BATCH
+ * from the environment, else as many frames as make 4 Mpixel, at most 16: 16 at
+ * 512x512, 2 at 1920x1080, 1 from 4 Mpixel up); 1 = one frame per launch; at
+ * most 64.  Batches are spread over the lanes.  Kernel durations of
+ * rtm_ctx_kernel_ms_history are then per launch, i.e. per batch;
+ * rtm_ctx_last_batch: frames per launch of the last call. */
+int rtm_ctx_set_batch(rtm_ctx* ctx, int32_t frames);
+int rtm_ctx_last_batch(rtm_ctx* ctx, int32_t* frames);
 
 /* ---- whole frame, host output (blocking) ----
  * Equivalent of: shadow viewport (ORTHO, face BACK, zBuffer=+INF) rasterize +

@@ -534,3 +534,63 @@ def test_maximum_size_frames(rtm, oracle, scenes, gpu_ctx, case):
             assert bits_equal(band.cpu().numpy(), want), (r0, r1, f)
     del out
     torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("batch,lanes", [(0, 1), (4, 1), (3, 2), (16, 1), (1, 3)])
+def test_batched_frame_sequences(rtm, scenes, gpu_ctx, batch, lanes):
+    """rtm_ctx_set_batch: runs of frames with the same patches share one launch per
+    pass (frame index = grid z, constants from an uploaded table); a patch change
+    splits a run; batches spread over lanes.  Every frame == rtm_render bit for bit,
+    and the context's shadow map is the last frame's."""
+    import torch
+    w, h, k = 320, 200, 48
+    eye, sh = scenes.eye_camera(), scenes.shadow_camera()
+    frames = ([scenes.scene_a_bench(100 + 3 * i) for i in range(6)] + [scenes.closely_orbiting_sphere(7)] +
+              [scenes.scene_a_bench(1), scenes.scene_b(), scenes.scene_b(), scenes.mixed_rt(20), scenes.mixed_sdf(5)])
+    outs = [torch.empty((h, w, 4), dtype=torch.float32, device="cuda") for _ in frames]
+    try:
+        gpu_ctx.set_batch(batch)
+        gpu_ctx.set_lanes(lanes)
+        torch.cuda.synchronize()
+        gpu_ctx.render_frames_async(frames, eye, sh, w, h, k, 0, [o.data_ptr() for o in outs])
+        gpu_ctx.synchronize()
+        assert gpu_ctx.last_batch() == (16 if batch == 0 else batch) or batch == 0
+        for s, o in zip(frames, outs):
+            assert bits_equal(o.cpu().numpy(), rtm.render_frame(s, eye, sh, w, h, k)), "frame differs"
+        # the last frame's shadow map
+        one = rtm.Context(0)
+        ref = torch.empty((h, w, 4), dtype=torch.float32, device="cuda")
+        one.render_async(frames[-1], eye, sh, w, h, k, 0, ref.data_ptr())
+        one.synchronize()
+        import ctypes
+        hip = ctypes.CDLL("libamdhip64.so")
+        hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+        a = torch.empty((h, w), dtype=torch.float64, device="cuda")
+        b = torch.empty_like(a)
+        assert hip.hipMemcpy(a.data_ptr(), gpu_ctx.shadow_map_ptr(), h * w * 8, 3) == 0
+        assert hip.hipMemcpy(b.data_ptr(), one.shadow_map_ptr(), h * w * 8, 3) == 0
+        assert torch.equal(a.view(torch.int64), b.view(torch.int64))
+        one.close()
+        # perspective eye + ray-traced primitives, SDFs, fused shadow: the other kernel variants
+        for eye2, fl, fr in ((scenes.perspective_eye_camera(), scenes.RAYTRACING_FLAGS,
+                              [scenes.raytracing_plane0(True), scenes.perspective_simple2(), scenes.scene_r_bench(),
+                               scenes.raytracing_plane0(), scenes.perspective_simple1()]),
+                             (scenes.sdf_eye_camera(), scenes.RAYTRACING_FLAGS,
+                              [scenes.sdf_bench_scene(), scenes.sdf_preview_scene(), scenes.sdf_bench_scene()]),
+                             (eye, rtm.abi.RTM_FLAG_FUSED_SHADOW, [scenes.scene_a_bench(i) for i in range(5)])):
+            o2 = [torch.empty((h, w, 4), dtype=torch.float32, device="cuda") for _ in fr]
+            torch.cuda.synchronize()
+            gpu_ctx.render_frames_async(fr, eye2, sh, w, h, k, fl, [o.data_ptr() for o in o2])
+            gpu_ctx.synchronize()
+            for s, o in zip(fr, o2):
+                assert bits_equal(o.cpu().numpy(), rtm.render_frame(s, eye2, sh, w, h, k, fl)), "variant differs"
+    finally:
+        gpu_ctx.set_batch(0)
+        gpu_ctx.set_lanes(0)
+
+
+def test_set_batch_api(rtm, gpu_ctx):
+    for bad in (-1, 65):
+        with pytest.raises(rtm.abi.RtmError) as e:
+            gpu_ctx.set_batch(bad)
+        assert e.value.code == rtm.abi.RTM_ERR_INVALID
