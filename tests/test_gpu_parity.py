@@ -411,6 +411,7 @@ def test_set_lanes_api(rtm, scenes, gpu_ctx):
     frames = [scenes.scene_a_bench(100 + i) for i in range(3)]
     outs = [torch.empty((h, w, 4), dtype=torch.float32, device="cuda") for _ in frames]
     try:
+        gpu_ctx.set_batch(1)  # lanes spread batches; one frame per batch here
         gpu_ctx.set_lanes(2)
         _frames_vs_single(rtm, scenes, gpu_ctx, frames, scenes.eye_camera(), scenes.shadow_camera(), w, h, k)
         assert gpu_ctx.last_lanes() == 2
@@ -424,8 +425,14 @@ def test_set_lanes_api(rtm, scenes, gpu_ctx):
                                     [o.data_ptr() for o in outs])
         gpu_ctx.synchronize()
         assert gpu_ctx.last_lanes() == 3
+        gpu_ctx.set_batch(2)  # 3 frames in batches of 2: two batches, at most two lanes
+        gpu_ctx.render_frames_async(frames, scenes.eye_camera(), scenes.shadow_camera(), w, h, k, 0,
+                                    [o.data_ptr() for o in outs])
+        gpu_ctx.synchronize()
+        assert gpu_ctx.last_lanes() == 2 and gpu_ctx.last_batch() == 2
     finally:
         gpu_ctx.set_lanes(0)
+        gpu_ctx.set_batch(0)
 
 
 def test_pipelined_frames_scene_b_8k(rtm, oracle, scenes, gpu_ctx):

@@ -153,6 +153,7 @@ def test_frames_async_with_raytraced_scenes(rtm, scenes, gpu_ctx, lanes):
     ]
     cases[0][2][1].cappedCylinderPrimitives = cases[0][2][1].cappedCylinderPrimitives[:1]
     try:
+        gpu_ctx.set_batch(1)  # one frame per launch: the lanes carry single frames
         gpu_ctx.set_lanes(lanes)
         for eye, flags, frames in cases:
             outs = [torch.empty((h, w, 4), dtype=torch.float32, device="cuda") for _ in frames]
@@ -166,6 +167,7 @@ def test_frames_async_with_raytraced_scenes(rtm, scenes, gpu_ctx, lanes):
                 assert bits_equal(o.cpu().numpy(), want)
     finally:
         gpu_ctx.set_lanes(0)
+        gpu_ctx.set_batch(0)
 
 
 def test_staged_seams_match_oracle(rtm, oracle, scenes, gpu_ctx):
