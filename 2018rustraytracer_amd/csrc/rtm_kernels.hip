@@ -1469,7 +1469,7 @@ __device__ __forceinline__ void eye_tile(const EyePart& a, const ShadowPart& sh,
                     n_cy_tests = __builtin_popcount((rmask >> 16) & ((1u << rt->n_cy) - 1u));
                 }
             }
-            if (RT == 2) trace_sdfs(sdf, o, d, zb, hit, n_evals);
+            if (RT == 2 && sdf) trace_sdfs(sdf, o, d, zb, hit, n_evals);  // (a batch mixes frames with and without SDFs)
         }
         if (hit.kind) {
             shaded = true;
