@@ -1062,17 +1062,18 @@ int ensure_lanes(rtm_ctx* ctx, int L) {
     return RTM_OK;
 }
 
-// Frames per launch of a frame sequence: below 4 Mpixel a frame's two kernels
-// are short and the host's per-frame launches bound the rate (512x512: ~16
-// Gpix/s), so 4 Mpixel worth of frames (at most 16) share one launch per pass
-// (rtm_ctx_set_batch / RTM_BATCH override; 1 = one frame per launch).
+// Frames per launch of a frame sequence: below 8 Mpixel a frame's two kernels
+// are short and the host's per-frame launches bound the rate (512x512: 12 Gpix/s
+// one frame per launch, 43 at 16; 1920x1080 on 3 lanes: 123 at 1, 181 at 4,
+// tools/probes/batch_probe.py), so 8 Mpixel worth of frames (at most 16) share
+// one launch per pass (rtm_ctx_set_batch / RTM_BATCH override; 1 = one frame per launch).
 int frame_batch(int32_t req, int32_t W, int32_t H) {
     static const int env = [] {
         const char* e = getenv("RTM_BATCH");
         return e ? atoi(e) : 0;
     }();
     const int64_t px = (int64_t)W * H;
-    int B = req > 0 ? req : env > 0 ? env : (int)std::max<int64_t>(1, std::min<int64_t>(16, (4LL << 20) / px));
+    int B = req > 0 ? req : env > 0 ? env : (int)std::max<int64_t>(1, std::min<int64_t>(16, (8LL << 20) / px));
     return std::max(1, std::min(B, 64));
 }
 
@@ -1404,13 +1405,25 @@ int rtm_render_frames_async(rtm_ctx* ctx, int32_t n_frames, const rtm_scene* sce
                 if (!rc) build_extra(&scenes[i0 + k], eye, width, height, fx[(size_t)k]);
             }
             if (rc) break;
-            // runs of frames with the same march tables (patches) share one launch per pass;
-            // the A/B-only shadow modes and single frames take the per-frame kernels
+            // runs of frames with the same march tables (patches) and disjoint outputs share
+            // one launch per pass (frames of one launch run concurrently, so a repeated
+            // output pointer starts a new run: the later frame still lands last); the
+            // A/B-only shadow modes and single frames take the per-frame kernels
+            const uintptr_t frame_bytes = (uintptr_t)width * (uintptr_t)height * 4u * sizeof(float);
             for (int32_t k = 0; k < nf && !rc;) {
                 int32_t e = k + 1;
+                auto disjoint = [&](int32_t q) {
+                    const uintptr_t o = (uintptr_t)out_rgba_dev[i0 + q];
+                    for (int32_t p = k; p < q; ++p) {
+                        const uintptr_t op = (uintptr_t)out_rgba_dev[i0 + p];
+                        if (o < op + frame_bytes && op < o + frame_bytes) return false;
+                    }
+                    return true;
+                };
                 while (e < nf && fa[(size_t)e].sh.n_patches == fa[(size_t)k].sh.n_patches &&
                        std::memcmp(fa[(size_t)e].sh.patch, fa[(size_t)k].sh.patch,
-                                   sizeof(PatchK) * (size_t)fa[(size_t)k].sh.n_patches) == 0)
+                                   sizeof(PatchK) * (size_t)fa[(size_t)k].sh.n_patches) == 0 &&
+                       disjoint(e))
                     ++e;
                 if (e - k >= 2 && shadow_batchable(fa[(size_t)k].sh)) {
                     if (!(rc = frame_tables(ctx, fa[(size_t)k])) && shadow_batchable(fa[(size_t)k].sh))

@@ -323,8 +323,12 @@ def main():
     # a ring of output frames (a renderer's swap chain): consecutive frames write
     # different buffers, so the library may run them side by side (rtm_api.cpp
     # frame_lanes puts frame i on lane (n-1-i) % L: the ring must be a multiple of L)
+    # and batch (several frames per launch, rtm_ctx_set_batch: frames of one launch need
+    # distinct outputs): 48 frames below 8 Mpixel (batches of up to 16 on up to 3 lanes)
     lanes_env = int(os.environ.get("RTM_LANES", "0") or 0)
     n_ring = 12 if lanes_env in (0, 1, 2, 3, 4, 6) else lanes_env * ((12 + lanes_env - 1) // lanes_env)
+    if W * H < (8 << 20):
+        n_ring = max(n_ring, 48 if lanes_env in (0, 1, 2, 3, 4, 6, 8, 12, 16) else 16 * max(lanes_env, 1))
     ring = ([torch.empty((H, W, 4), dtype=torch.float32, device=f"cuda:{local}") for _ in range(n_ring)]
             if not tile_mode else [])
     sequence = not tile_mode and not a.per_frame_calls and not fused

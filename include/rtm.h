@@ -240,9 +240,10 @@ int rtm_ctx_last_lanes(rtm_ctx* ctx, int32_t* lanes);
  * the same patches share ONE launch per pass (the frame index is the grid's z
  * dimension; each frame's constants come from a table uploaded per batch), so
  * small frames stop paying a launch per pass per frame.  0 = auto (RTM_BATCH
- * from the environment, else as many frames as make 4 Mpixel, at most 16: 16 at
- * 512x512, 2 at 1920x1080, 1 from 4 Mpixel up); 1 = one frame per launch; at
- * most 64.  Batches are spread over the lanes.  Kernel durations of
+ * from the environment, else as many frames as make 8 Mpixel, at most 16: 16 at
+ * 512x512, 4 at 1920x1080, 1 at 3840x2160); 1 = one frame per launch; at most
+ * 64.  Frames with overlapping outputs never share a launch (a repeated output
+ * pointer still ends with the later frame).  Batches are spread over the lanes.  Kernel durations of
  * rtm_ctx_kernel_ms_history are then per launch, i.e. per batch;
  * rtm_ctx_last_batch: frames per launch of the last call. */
 int rtm_ctx_set_batch(rtm_ctx* ctx, int32_t frames);

@@ -596,6 +596,31 @@ def test_batched_frame_sequences(rtm, scenes, gpu_ctx, batch, lanes):
         gpu_ctx.set_lanes(0)
 
 
+def test_batch_with_repeated_outputs(rtm, scenes, gpu_ctx):
+    """Frames whose outputs repeat never share a launch: one shared output ends with
+    the last frame's image, and a ring of 3 outputs holds the last 3 frames."""
+    import torch
+    w, h, k = 256, 160, 40
+    eye, sh = scenes.eye_camera(), scenes.shadow_camera()
+    frames = [scenes.scene_a_bench(10 * i) for i in range(10)]
+    ring = [torch.zeros((h, w, 4), dtype=torch.float32, device="cuda") for _ in range(3)]
+    try:
+        for b in (0, 16, 4):
+            gpu_ctx.set_batch(b)
+            for n_out in (1, 3):
+                for r in ring:
+                    r.zero_()
+                torch.cuda.synchronize()
+                gpu_ctx.render_frames_async(frames, eye, sh, w, h, k, 0, [ring[i % n_out].data_ptr()
+                                                                         for i in range(len(frames))])
+                gpu_ctx.synchronize()
+                for j in range(n_out):
+                    last = max(i for i in range(len(frames)) if i % n_out == j)
+                    assert bits_equal(ring[j].cpu().numpy(), rtm.render_frame(frames[last], eye, sh, w, h, k))
+    finally:
+        gpu_ctx.set_batch(0)
+
+
 def test_set_batch_api(rtm, gpu_ctx):
     for bad in (-1, 65):
         with pytest.raises(rtm.abi.RtmError) as e:
