@@ -176,6 +176,22 @@ def eye_camera() -> Camera:
     return Camera(ORTHOGONAL, (-1.0, 0.0, 0.0), (1.0, 0.0, 0.0), (0.0, 1.0, 0.0), (0.0, 0.0, 1.0))
 
 
+def tilted_shadow_camera() -> Camera:
+    """An orthographic sun that does not shine along an axis (synthetic, bench
+    config 9): its shadow rays move in x and y as they march, so the march takes
+    the general per-step loop (in-range test and surface depth re-evaluated every
+    step, main.rs:2247-2274) instead of the axis-aligned first-crossing search.
+    dir = normalize(0.25, -0.15, 1), side = normalize(up0 x dir) with up0 = +y,
+    up = dir x side, all f64 on the host (Camera::project only needs an
+    ORTHOGONAL camera, main.rs:1949)."""
+    def cross(a, b):
+        return (a[1] * b[2] - a[2] * b[1], a[2] * b[0] - a[0] * b[2], a[0] * b[1] - a[1] * b[0])
+    d = normalize((0.25, -0.15, 1.0))
+    s = normalize(cross((0.0, 1.0, 0.0), d))
+    u = cross(d, s)
+    return Camera(ORTHOGONAL, (0.0, 0.0, 0.0), d, u, s)
+
+
 # ---- scenes ----
 def closely_orbiting_sphere(frame: int, patches=None) -> Scene:
     """testscene_closelyOrbitingSphere frame `frame` (main.rs:1468-1522).
@@ -326,6 +342,12 @@ CONFIGS = {
     8: dict(width=3840, height=2160, steps=0, scene=lambda: sdf_bench_scene(), flags=RAYTRACING_FLAGS,
             eye=lambda: sdf_eye_camera(),
             desc="3840x2160, Scene S-bench: 8 GL-preview SDFs + 1 circle plane, perspective (row f-4)"),
+    # the general march: Scene A-bench under a tilted orthographic sun, so every
+    # shadow ray moves in x/y and the march is the per-step loop (raymarchPatch as
+    # written) rather than the axis-aligned first-crossing search
+    9: dict(width=3840, height=2160, steps=64, scene=scene_a_bench, flags=0, shadow=lambda: tilted_shadow_camera(),
+            desc="3840x2160, 3 spheres + 1 implicit, 64 march steps, tilted orthographic sun (general march)",
+            metric="Mpixels/s at 3840x2160, 64 march steps, general (x/y-moving) shadow rays"),
 }
 
 

@@ -49,7 +49,8 @@ def parse():
     # clocks up (200/20 measured 188 Gpix/s where 2000/500 measured 203, same kernels)
     ap.add_argument("--steps", type=int, default=2000)
     ap.add_argument("--warmup", type=int, default=500)
-    ap.add_argument("--config", type=int, default=3, help="scenes.CONFIGS id: 1-5 BASELINE, 6-7 row f-1, 8 row f-4")
+    ap.add_argument("--config", type=int, default=3,
+                    help="scenes.CONFIGS id: 1-5 BASELINE, 6-7 row f-1, 8 row f-4, 9 general march (tilted sun)")
     ap.add_argument("--mode", choices=["frames", "tile-gather"], default="frames")
     ap.add_argument("--fused", action="store_true", help="evaluate shadow texels on demand (same image)")
     ap.add_argument("--per-frame-calls", action="store_true",
@@ -331,7 +332,7 @@ def main():
         n_ring = max(n_ring, 48 if lanes_env in (0, 1, 2, 3, 4, 6, 8, 12, 16) else 16 * max(lanes_env, 1))
     ring = ([torch.empty((H, W, 4), dtype=torch.float32, device=f"cuda:{local}") for _ in range(n_ring)]
             if not tile_mode else [])
-    sequence = not tile_mode and not a.per_frame_calls and not fused
+    sequence = not tile_mode and not a.per_frame_calls
     pipelined = sequence and os.environ.get("RTM_PIPELINE", "0") not in ("", "0")
 
     import ctypes as C
@@ -454,7 +455,7 @@ def main():
     # texels the eye pass looks up instead of materialising the whole shadow map.
     # Bit-identical image (tests/test_gpu_parity.py::test_fused_shadow_identical).
     alt_fused = None
-    if sequence and not pipelined and not a.no_alt:
+    if sequence and not pipelined and not a.no_alt and not fused:
         fflags = flags | rtm.abi.RTM_FLAG_FUSED_SHADOW
         ctx.set_timing_capacity(max(1, a.steps // timing_stride))
         ctx.render_frames_async([0] * min(a.warmup, 5), eye, shadow, W, H, K, fflags, outp[:min(a.warmup, 5)],

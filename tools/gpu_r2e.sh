@@ -2,7 +2,7 @@
 set -o pipefail
 mkdir -p gpurun_out/r2e
 export TMPDIR=/tmp
-timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_parity.py -k "batched or set_batch or lanes" -m gpu -p no:cacheprovider > gpurun_out/r2e/pytest_batch.log 2>&1 && timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests -m gpu -p no:cacheprovider > gpurun_out/r2e/pytest_gpu.log 2>&1
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_parity.py -k "batch or lanes" -m gpu -p no:cacheprovider > gpurun_out/r2e/pytest_batch.log 2>&1 && timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests -m gpu -p no:cacheprovider > gpurun_out/r2e/pytest_gpu.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -15 gpurun_out/r2e/pytest_gpu.log
 [ $rc -ne 0 ] && exit $rc
 for c in 7 2 3; do
