@@ -124,10 +124,12 @@ class Context:
         """ctypes array of rtm_scene for render_frames_async (+ keepalive)."""
         arr = (abi.rtm_scene * len(scenes))()
         keep = []
+        conv = {}  # a scene repeated in the sequence is converted once
         for i, s in enumerate(scenes):
-            c, k = s.to_c()
-            arr[i] = c
-            keep.append(k)
+            if id(s) not in conv:
+                conv[id(s)] = s.to_c()
+                keep.append(conv[id(s)][1])
+            arr[i] = conv[id(s)][0]
         return arr, keep
 
     def render_frames_async(self, scenes, eye: Camera, shadow: Camera, width: int, height: int, steps: int,

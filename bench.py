@@ -5,6 +5,12 @@ march, eye viewport rasterize + shade) at BASELINE config 3 — 3840x2160,
 
 One process per GPU (torch.distributed.run); prints ONE JSON line on rank 0.
 
+A step is one segment of the animation: --frames-per-step frames (auto: at least 8
+and at least 64 Mpixel worth, so 8 at 3840x2160) enqueued by one
+rtm_render_frames_async call into a ring of output frames.  `value` is pixels of all
+timed frames / the timed region's wall time; `ms_per_step` is per segment and
+`ms_per_frame` per frame.
+
 Modes (--mode):
   frames       (default) frame-parallel: rank r renders animation frames
                r, r+N, ... of the orbiting-sphere sequence; each frame is
@@ -45,10 +51,13 @@ METRIC_F4 = "Mpixels/s, sphere-traced GL-preview SDFs (row f-4)"
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    # 2000 frames x ~35 us: the timed region is ~70 ms; 500 warmup frames bring the
-    # clocks up (200/20 measured 188 Gpix/s where 2000/500 measured 203, same kernels)
-    ap.add_argument("--steps", type=int, default=2000)
-    ap.add_argument("--warmup", type=int, default=500)
+    # a step is one segment of the animation: --frames-per-step frames rendered by one
+    # rtm_render_frames_async call (the renderer's swap chain); 250 steps x 8 frames x
+    # ~35 us: the timed region is ~70 ms at config 3
+    ap.add_argument("--steps", type=int, default=250)
+    ap.add_argument("--warmup", type=int, default=60)
+    ap.add_argument("--frames-per-step", type=int, default=0,
+                    help="frames of one step (0 = auto: at least 8 and at least 64 Mpixel worth, at most 256)")
     ap.add_argument("--config", type=int, default=3,
                     help="scenes.CONFIGS id: 1-5 BASELINE, 6-7 row f-1, 8 row f-4, 9 general march (tilted sun)")
     ap.add_argument("--mode", choices=["frames", "tile-gather"], default="frames")
@@ -283,6 +292,10 @@ def main():
     metrics = importlib.import_module("2018rustraytracer_amd.metrics")
     cfg = sc.CONFIGS[a.config]
     W, H, K = cfg["width"], cfg["height"], cfg["steps"]
+    # frames per step: a step renders F frames of the sequence (at least 8, and at least
+    # 64 Mpixel, so a short --steps run still times milliseconds of work, not a few frames)
+    F = a.frames_per_step or min(256, max(8, -(-(1 << 26) // (W * H))))
+    nW, nS = a.warmup * F, a.steps * F  # warmup / timed frames
     tile_mode = a.mode == "tile-gather"
     # tile-gather: each band evaluates only the shadow texels it reads (no cross-rank shadow map)
     fused = a.fused or tile_mode
@@ -293,7 +306,7 @@ def main():
     # kernel durations: HIP events on every TIMING_STRIDE-th frame of the timed region
     # (an event is a barrier packet; timing every frame would cost ~15% throughput)
     timing_stride = 10
-    ctx.set_timing_capacity(max(1, a.steps // timing_stride))
+    ctx.set_timing_capacity(max(1, nS // timing_stride))
 
     def scene_for(frame_index: int):
         if a.config >= 5:
@@ -314,11 +327,15 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
-    total = a.warmup + a.steps
+    total = nW + nS
     # inputs prepared before the timed region: one scene per frame this rank renders
-    # (frames mode: frames rank, rank+N, ...; tile-gather: every rank renders a band of every frame)
-    scenes = [scene_for(i if tile_mode else i * world + rank) for i in range(total)]
-    c_scenes = [s.to_c() for s in scenes]
+    # (frames mode: frames rank, rank+N, ...; tile-gather: every rank renders a band of every
+    # frame), the animation cycling through its first 600 frames (the reference animates 300)
+    n_distinct = min(total, 600)
+    distinct = [scene_for(i if tile_mode else i * world + rank) for i in range(n_distinct)]
+    scenes = [distinct[i % n_distinct] for i in range(total)]
+    c_distinct = [s.to_c() for s in distinct]
+    c_scenes = [c_distinct[i % n_distinct] for i in range(total)]
     group = make_group(rtm, world, rank, local, dist, a.dist_backend) if (tile_mode or a.tile_gather_steps) else None
 
     # a ring of output frames (a renderer's swap chain): consecutive frames write
@@ -346,9 +363,9 @@ def main():
     if sequence:
         # the whole timed region is ONE rtm_render_frames_async call over the animation
         # frames (two kernels per frame; with RTM_PIPELINE=1 the software-pipelined launch)
-        warm = ctx.prepare_frames(scenes[:a.warmup])
-        timed = ctx.prepare_frames(scenes[a.warmup:])
-        outp = [ring[i % n_ring].data_ptr() for i in range(max(a.warmup, a.steps, 1))]
+        warm = ctx.prepare_frames(scenes[:nW])
+        timed = ctx.prepare_frames(scenes[nW:])
+        outp = [ring[i % n_ring].data_ptr() for i in range(max(nW, nS, 1))]
 
     # clock ramp: frames for at least --preroll-ms of wall time before the counted warmup
     preroll_frames, t_pre = 0, time.perf_counter()
@@ -375,28 +392,28 @@ def main():
             preroll_frames += 50
         preroll["ms"], preroll["frames"] = round((time.perf_counter() - t_pre) * 1e3, 1), preroll_frames
         tg_primary = tile_gather(rtm, lib, ctx, group, world, rank, dist, tdev, c_scenes, eye, shadow, W, H, K,
-                                 flags, fmt, a.steps, a.warmup)
-        elapsed = tg_primary["ms_per_step"] * a.steps / 1e3
+                                 flags, fmt, nS, nW)
+        elapsed = tg_primary["ms_per_step"] * nS / 1e3
     else:
         if sequence:
-            if a.warmup:
-                ctx.render_frames_async([0] * a.warmup, eye, shadow, W, H, K, flags, outp[:a.warmup], warm)
+            if nW:
+                ctx.render_frames_async([0] * nW, eye, shadow, W, H, K, flags, outp[:nW], warm)
         else:
-            for i in range(a.warmup):
+            for i in range(nW):
                 frames_step(i)
         barrier()
         ctx.set_timing_stride(timing_stride)  # restarts the stride count: launch 0 of the timed region is timed
         t0 = time.perf_counter()
         if sequence:
-            ctx.render_frames_async([0] * a.steps, eye, shadow, W, H, K, flags, outp[:a.steps], timed)
+            ctx.render_frames_async([0] * nS, eye, shadow, W, H, K, flags, outp[:nS], timed)
         else:
-            for i in range(a.warmup, total):
+            for i in range(nW, total):
                 frames_step(i)
         barrier()
         elapsed = max_over_ranks(time.perf_counter() - t0)
 
     # per-kernel HIP-event durations over the timed region (ctx stream)
-    n_launches = a.steps + 1 if pipelined else a.steps
+    n_launches = nS + 1 if pipelined else nS
     sh_ms, eye_ms = ctx.kernel_ms_history((n_launches + timing_stride - 1) // timing_stride)
     if tile_mode:  # the group's own contexts ran the bands: one timed pass of rank 0's band on ctx
         ctx.set_timing_capacity(1)
@@ -429,12 +446,12 @@ def main():
         avg = lambda v: sum(v) / max(len(v), 1)
         in_lanes = {"lanes": lanes, "shadow_pass_ms": round(avg(sh_ms), 5), "eye_pass_ms": round(avg(eye_ms), 5),
                     "note": "HIP-event kernel durations in the timed region, kernels of other lanes alongside"}
-        n1 = min(a.steps, 400)
+        n1 = min(nS, 400)
         ctx.set_lanes(1)
-        ctx.render_frames_async([0] * min(a.warmup, 50), eye, shadow, W, H, K, flags, outp[:min(a.warmup, 50)],
-                                ctx.prepare_frames(scenes[:min(a.warmup, 50)]))
+        ctx.render_frames_async([0] * min(nW, 50), eye, shadow, W, H, K, flags, outp[:min(nW, 50)],
+                                ctx.prepare_frames(scenes[:min(nW, 50)]))
         ctx.set_timing_capacity(max(1, n1 // timing_stride))
-        one = ctx.prepare_frames(scenes[a.warmup:a.warmup + n1])
+        one = ctx.prepare_frames(scenes[nW:nW + n1])
         barrier()
         ctx.set_timing_stride(timing_stride)
         t1 = time.perf_counter()
@@ -457,18 +474,18 @@ def main():
     alt_fused = None
     if sequence and not pipelined and not a.no_alt and not fused:
         fflags = flags | rtm.abi.RTM_FLAG_FUSED_SHADOW
-        ctx.set_timing_capacity(max(1, a.steps // timing_stride))
-        ctx.render_frames_async([0] * min(a.warmup, 5), eye, shadow, W, H, K, fflags, outp[:min(a.warmup, 5)],
-                                ctx.prepare_frames(scenes[:min(a.warmup, 5)]))
+        ctx.set_timing_capacity(max(1, nS // timing_stride))
+        ctx.render_frames_async([0] * min(nW, 5), eye, shadow, W, H, K, fflags, outp[:min(nW, 5)],
+                                ctx.prepare_frames(scenes[:min(nW, 5)]))
         barrier()
         ctx.set_timing_stride(timing_stride)
         t1 = time.perf_counter()
-        ctx.render_frames_async([0] * a.steps, eye, shadow, W, H, K, fflags, outp[:a.steps], timed)
+        ctx.render_frames_async([0] * nS, eye, shadow, W, H, K, fflags, outp[:nS], timed)
         barrier()
         el_f = max_over_ranks(time.perf_counter() - t1)
-        _, f_eye = ctx.kernel_ms_history((a.steps + timing_stride - 1) // timing_stride)
-        alt_fused = {"value": round(W * H * a.steps * world / el_f / 1e6, 2), "unit": "Mpixels/s",
-                     "ms_per_step": round(el_f / a.steps * 1e3, 5),
+        _, f_eye = ctx.kernel_ms_history((nS + timing_stride - 1) // timing_stride)
+        alt_fused = {"value": round(W * H * nS * world / el_f / 1e6, 2), "unit": "Mpixels/s",
+                     "ms_per_step": round(el_f / a.steps * 1e3, 5), "ms_per_frame": round(el_f / nS * 1e3, 5),
                      "fused_eye_pass_ms_in_lanes": round(sum(f_eye) / max(len(f_eye), 1), 5),
                      "lanes": ctx.last_lanes(),
                      "note": "RTM_FLAG_FUSED_SHADOW (shadow texels evaluated on demand in the eye pass, "
@@ -497,7 +514,7 @@ def main():
     if pipelined:
         # sampled launches j = 0, stride, 2*stride, ...: j = 0 is the prologue shadow pass,
         # j = steps (if sampled) the epilogue eye pass; the rest are pipelined frame launches
-        pipe = eye_ms[1:-1] if a.steps % timing_stride == 0 else eye_ms[1:]
+        pipe = eye_ms[1:-1] if nS % timing_stride == 0 else eye_ms[1:]
         pipe_ms = sum(pipe) / max(len(pipe), 1)
         avg_sh, avg_eye = sh_ms[0], 0.0
     else:
@@ -510,9 +527,9 @@ def main():
 
     if rank == 0:
         rows = shard.row_band(H, world, rank) if tile_mode else (0, H)
-        pixels = W * H * a.steps * (1 if tile_mode else world)
+        pixels = W * H * nS * (1 if tile_mode else world)
         value = pixels / elapsed / 1e6
-        s0 = scenes[a.warmup] if a.warmup < len(scenes) else scenes[0]
+        s0 = scenes[nW] if nW < len(scenes) else scenes[0]
         band_h = rows[1] - rows[0]
         st = ctx.stats(s0, eye, shadow, W, H, K, flags)
         sep = metrics.shared_z_separable(shadow)
@@ -529,7 +546,7 @@ def main():
         # the whole frame (both passes' algorithmic bytes) over the headline time per frame
         passes = [work[k] for k in ("shadow_pass", "eye_pass") if k in work]
         work["frame"] = {"ops": sum(w["ops"] for w in passes), "bytes": sum(w["bytes"] for w in passes)}
-        roof_frame = dict(metrics.roofline("frame", work, elapsed / a.steps * 1e3))  # per GPU
+        roof_frame = dict(metrics.roofline("frame", work, elapsed / nS * 1e3))  # per GPU
         roof_frame.pop("traffic", None)
         roof_frame["note"] = ("both passes' algorithmic bytes per frame / wall time per frame of the timed region"
                               + (f" ({lanes} lanes)" if lanes > 1 else ""))
@@ -553,6 +570,8 @@ def main():
             "steps": a.steps,
             "warmup": a.warmup,
             "ms_per_step": round(elapsed / a.steps * 1e3, 5),
+            "frames_per_step": F,
+            "ms_per_frame": round(elapsed / nS * 1e3, 5),
             "higher_is_better": True,
             "scaling": "strong" if tile_mode else "weak",
             "vs_baseline": None,

@@ -316,7 +316,11 @@ int rtm_render_rows_async(rtm_ctx* ctx, const rtm_scene* scene, const rtm_camera
  * maps) — correct, but measured slower on MI355X.  Each frame's
  * output is bit-identical to rtm_render.  Frames are validated as they are
  * enqueued: on an error return, the frames before the failing one may already
- * be on the stream. */
+ * be on the stream.  The march tables (built from the patches, the shadow camera
+ * and march_steps) are shared by all lanes: when a frame's tables differ from the
+ * previous frame's, the host waits for every lane's earlier work before rebuilding
+ * them, so a sequence whose patches change from frame to frame serialises the
+ * call (still correct, no longer asynchronous). */
 int rtm_render_frames_async(rtm_ctx* ctx, int32_t n_frames, const rtm_scene* scenes,
                             const rtm_camera* eye, const rtm_camera* shadow, int32_t width,
                             int32_t height, int32_t march_steps, int32_t flags,

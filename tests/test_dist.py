@@ -105,11 +105,12 @@ def test_bench_tile_gather_gloo_rehearsal_world2(fmt):
     (gloo gathers the CPU-staged bands; the 8-GPU run uses RCCL): one JSON line,
     strong scaling, both ranks' pixels counted once."""
     res = _run_bench(["--gpus", "2", "--dist-backend", "gloo", "--mode", "tile-gather", "--format", fmt,
-                      "--config", "2", "--steps", "6", "--warmup", "2", "--preroll-ms", "0", "--no-cpu-baseline",
+                      "--config", "2", "--steps", "3", "--warmup", "1", "--frames-per-step", "2", "--preroll-ms", "0", "--no-cpu-baseline",
                       "--no-alt"], 2)
     assert res["n_gpus"] == 2 and res["scaling"] == "strong" and res["value"] > 0
     assert res["tile_gather"]["format"] == fmt.upper() and "gloo" in res["tile_gather"]["gather"]
     assert res["config"]["rows_rank0"] == 540
+    assert res["frames_per_step"] == 2 and res["tile_gather"]["frames"] == 6
 
 
 @pytest.mark.gpu
@@ -118,5 +119,6 @@ def test_bench_frames_gloo_rehearsal_world2_carries_tile_gather():
     res = _run_bench(["--gpus", "2", "--dist-backend", "gloo", "--config", "2", "--steps", "20", "--warmup", "5",
                       "--preroll-ms", "20", "--tile-gather-steps", "4", "--no-cpu-baseline", "--no-alt"], 2)
     assert res["scaling"] == "weak" and res["n_gpus"] == 2
+    assert res["frames_per_step"] == 32  # auto: 64 Mpixel worth of 1920x1080 frames
     assert set(res["tile_gather"]) == {"rgba32f", "rgba8"}
     assert all(v["value"] > 0 for v in res["tile_gather"].values())

@@ -15,7 +15,7 @@ from collections import defaultdict
 
 
 def short(name):
-    m = re.search(r"(shadow_\w+_kernel|eye_pass_kernel|frame_pipe_kernel|rt_upload_kernel|"
+    m = re.search(r"(shadow_\w+_kernel|eye_\w+_kernel|frame_pipe_kernel|rt_\w+_kernel|upload_kernel|"
                   r"vp_\w+_kernel|fill_kernel|encode_rgb8_kernel|ppm_\w+_kernel)(<[^>]*>)?", name)
     return (m.group(1) + (m.group(2) or "")) if m else name[:60]
 
@@ -57,8 +57,9 @@ def main():
             d["salu_insts_per_wave"] = d.get("SQ_INSTS_SALU", 0) / d["SQ_WAVES"]
         timed_shadow = k.startswith("shadow_") and not k.startswith("shadow_pass_kernel<true")  # (<true>: stats)
         name = ("shadow_pass" if timed_shadow else
-                "eye_pass" if k.startswith("eye_pass_kernel<false, false") else
-                "eye_pass_fused" if k.startswith("eye_pass_kernel<true, false") else k)
+                "eye_pass" if k.startswith(("eye_pass_kernel<false, false", "eye_batch_kernel<false",
+                                             "eye_sdf_kernel", "eye_sdf_batch_kernel")) else
+                "eye_pass_fused" if k.startswith(("eye_pass_kernel<true, false", "eye_batch_kernel<true")) else k)
         out["kernels"][name] = d
     print(json.dumps(out, indent=1, sort_keys=True))
 

@@ -18,7 +18,7 @@ for grp in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_IN
   i=$((i+1))
   echo "=== pass $i: $grp"
   timeout -k 10 300 rocprofv3 --pmc $grp --kernel-trace --output-format csv -d "$OUT/p$i" -o run -- \
-      python3 "$ROOT/bench.py" --steps 20 --warmup 5 --no-cpu-baseline --config "$CFG" ${BENCH_ARGS:-} > "$OUT/p$i.log" 2>&1
+      python3 "$ROOT/bench.py" --steps 20 --warmup 5 --no-cpu-baseline --tile-gather-steps 0 --no-host-output --config "$CFG" ${BENCH_ARGS:-} > "$OUT/p$i.log" 2>&1
   rc=$?
   echo "pass $i rc=$rc"
   if [ $rc -ne 0 ]; then tail -20 "$OUT/p$i.log"; fi

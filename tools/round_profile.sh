@@ -6,7 +6,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 ROOT=$(pwd)
-TAG=${TAG:-r01_v14}
+TAG=${TAG:-r02_v1}
 OUT=$ROOT/gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
@@ -24,18 +24,25 @@ step() {
 [ "${SKIP_TESTS:-0}" = 1 ] || step pytest_gpu 900 python -m pytest tests -m gpu -q -p no:cacheprovider
 [ "${SKIP_TESTS:-0}" = 1 ] || step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 step bench3 600 python bench.py
+step bench3_short 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline
+step bench3_tg32 300 python bench.py --mode tile-gather --format rgba32f --no-cpu-baseline --no-host-output --tile-gather-steps 0
+step bench3_tg8 300 python bench.py --mode tile-gather --format rgba8 --no-cpu-baseline --no-host-output --tile-gather-steps 0
 step bench2 300 python bench.py --config 2 --no-alt --no-cpu-baseline
 step bench4 300 python bench.py --config 4 --no-alt --no-cpu-baseline
 step bench5 300 python bench.py --config 5 --no-alt --no-cpu-baseline
 step bench6 300 python bench.py --config 6 --no-alt
 step bench7 300 python bench.py --config 7 --no-alt --no-cpu-baseline
 step bench8 300 python bench.py --config 8 --no-alt
-step prof3 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof3" -o run --output-format csv -- python3 "$ROOT/bench.py" --steps 200 --warmup 20 --no-cpu-baseline --no-alt
-RTM_LANES=1 step prof3_one_lane 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof3_one_lane" -o run --output-format csv -- python3 "$ROOT/bench.py" --steps 200 --warmup 20 --no-cpu-baseline --no-alt
-step prof4 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof4" -o run --output-format csv -- python3 "$ROOT/bench.py" --config 4 --steps 100 --warmup 10 --no-cpu-baseline --no-alt
-step prof6 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof6" -o run --output-format csv -- python3 "$ROOT/bench.py" --config 6 --steps 200 --warmup 20 --no-cpu-baseline --no-alt
-step prof8 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof8" -o run --output-format csv -- python3 "$ROOT/bench.py" --config 8 --steps 100 --warmup 10 --no-cpu-baseline --no-alt
-if [ "${PMC:-1}" = 1 ]; then
+step bench9 300 python bench.py --config 9 --no-alt
+step prof3 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof3" -o run --output-format csv -- python3 "$ROOT/bench.py" --steps 25 --warmup 3 --no-cpu-baseline --no-alt
+RTM_LANES=1 step prof3_one_lane 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof3_one_lane" -o run --output-format csv -- python3 "$ROOT/bench.py" --steps 25 --warmup 3 --no-cpu-baseline --no-alt
+step prof4 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof4" -o run --output-format csv -- python3 "$ROOT/bench.py" --config 4 --steps 13 --warmup 2 --no-cpu-baseline --no-alt
+step prof6 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof6" -o run --output-format csv -- python3 "$ROOT/bench.py" --config 6 --steps 25 --warmup 3 --no-cpu-baseline --no-alt
+step prof2 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof2" -o run --output-format csv -- python3 "$ROOT/bench.py" --config 2 --steps 20 --warmup 5 --no-cpu-baseline --no-alt
+step prof7 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof7" -o run --output-format csv -- python3 "$ROOT/bench.py" --config 7 --steps 10 --warmup 2 --no-cpu-baseline --no-alt
+step prof9 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof9" -o run --output-format csv -- python3 "$ROOT/bench.py" --config 9 --steps 20 --warmup 5 --no-cpu-baseline --no-alt
+step prof8 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof8" -o run --output-format csv -- python3 "$ROOT/bench.py" --config 8 --steps 13 --warmup 2 --no-cpu-baseline --no-alt
+if [ "${PMC:-0}" = 1 ]; then
   TAG=$TAG CFG=3 BENCH_ARGS="--no-alt" step pmc3 1200 bash tools/profile_pmc.sh
 fi
 echo done
