@@ -675,6 +675,8 @@ struct rtm_ctx {
     DevBuf smap;    // shadow map, W*H f64
     DevBuf smap2;   // second shadow map for the pipelined frame sequence
     const double* last_smap = nullptr;
+    ShadowPart last_sh{};  // the last shadow pass's arguments (smap_fmt: how last_smap is stored)
+    DevBuf smap_dec;       // rtm_ctx_shadow_map's f64 view of a coded map
     DevBuf out;     // staging for rtm_render's host output
     DevBuf stats;
     int32_t smap_w = 0, smap_h = 0;
@@ -991,8 +993,11 @@ int enqueue_frame(rtm_ctx* ctx, FrameArgs& a, const FrameExtra* x, void* out_dev
     double* smap = nullptr;
     TimingSlot* slot = next_slot(ctx);
     if (!fused) {
+        // the map's storage: coded (1-2 B per texel) unless counting (f64)
+        a.sh.smap_fmt = stats ? SMAP_F64 : shadow_map_format(a.sh);
+        a.sh.smap_bw = (a.sh.W + 127) / 128;
         DevBuf& sb = l ? l->smap : ctx->smap;
-        if ((rc = sb.ensure(sizeof(double) * (size_t)a.sh.W * (size_t)a.sh.H, ctx->device))) return rc;
+        if ((rc = sb.ensure((size_t)smap_bytes(a.sh.smap_fmt, a.sh.W, a.sh.H), ctx->device))) return rc;
         smap = (double*)sb.p;
         ctx->smap_w = a.sh.W;
         ctx->smap_h = a.sh.H;
@@ -1001,6 +1006,7 @@ int enqueue_frame(rtm_ctx* ctx, FrameArgs& a, const FrameExtra* x, void* out_dev
         if (slot) HIP_TRY(hipEventRecord(slot->ev[1], s));
         ctx->have_shadow_pass = true;
         ctx->last_smap = smap;
+        ctx->last_sh = a.sh;
     } else {
         ctx->have_shadow_pass = false;
     }
@@ -1102,8 +1108,13 @@ int enqueue_batch(rtm_ctx* ctx, int lane, FrameArgs* fa, const FrameExtra* ex, f
     }
     BatchRing& br = *brp;
     const bool fused = (fa[0].ey.flags & RTM_FLAG_FUSED_SHADOW) != 0;
-    const size_t map_words = (size_t)fa[0].sh.W * (size_t)fa[0].sh.H;
-    if (!fused && (rc = br.smaps.ensure(sizeof(double) * map_words * (size_t)n, ctx->device))) return rc;
+    const int32_t sfmt = fused ? SMAP_F64 : shadow_map_format(fa[0].sh);
+    for (int k = 0; k < n; ++k) {
+        fa[k].sh.smap_fmt = sfmt;
+        fa[k].sh.smap_bw = (fa[k].sh.W + 127) / 128;
+    }
+    const size_t map_bytes = ((size_t)smap_bytes(sfmt, fa[0].sh.W, fa[0].sh.H) + 255) & ~(size_t)255;
+    if (!fused && (rc = br.smaps.ensure(map_bytes * (size_t)n, ctx->device))) return rc;
     // layout of the upload: the BatchFrame table, then each frame's device tables
     auto up = [](size_t v) { return (v + 255) & ~(size_t)255; };
     size_t off = up(sizeof(BatchFrame) * (size_t)n);
@@ -1134,7 +1145,7 @@ int enqueue_batch(rtm_ctx* ctx, int lane, FrameArgs* fa, const FrameExtra* ex, f
     for (int k = 0; k < n; ++k) {
         BatchFrame& bf = *(BatchFrame*)(hb + sizeof(BatchFrame) * (size_t)k);
         bf.a = fa[k];
-        bf.smap = fused ? nullptr : (double*)br.smaps.p + map_words * (size_t)k;
+        bf.smap = fused ? nullptr : (double*)((char*)br.smaps.p + map_bytes * (size_t)k);
         bf.out = outs[k];
         if ((rc = format_tabs(ctx, RTM_FORMAT_RGBA32F, fa[k].ey.W, outs[k], bf.tabs))) return rc;
         bf.tabs.rt = nullptr;
@@ -1173,7 +1184,8 @@ int enqueue_batch(rtm_ctx* ctx, int lane, FrameArgs* fa, const FrameExtra* ex, f
         if ((rc = launch_shadow_batch((const BatchFrame*)db, n, fa[0], s))) return fail(rc, "batched shadow pass failed");
         if (slot) HIP_TRY(hipEventRecord(slot->ev[1], s));
         ctx->have_shadow_pass = true;
-        ctx->last_smap = (const double*)br.smaps.p + map_words * (size_t)(n - 1);
+        ctx->last_smap = (const double*)((const char*)br.smaps.p + map_bytes * (size_t)(n - 1));
+        ctx->last_sh = fa[n - 1].sh;
         ctx->smap_w = fa[0].sh.W;
         ctx->smap_h = fa[0].sh.H;
     } else {
@@ -1366,7 +1378,15 @@ int rtm_render_async(rtm_ctx* ctx, const rtm_scene* scene, const rtm_camera* eye
 
 const double* rtm_ctx_shadow_map(rtm_ctx* ctx) {
     if (!ctx || !ctx->have_shadow_pass) return nullptr;
-    return ctx->last_smap;
+    if (ctx->last_sh.smap_fmt == SMAP_F64) return ctx->last_smap;
+    // a coded map (rtm_kernels.h): its f64 values, decoded after the frame on the
+    // context stream, then waited for
+    DeviceGuard g(ctx->device);
+    const ShadowPart& sh = ctx->last_sh;
+    if (ctx->smap_dec.ensure(sizeof(double) * (size_t)sh.W * (size_t)sh.H, ctx->device)) return nullptr;
+    if (launch_smap_decode(sh, ctx->last_smap, (double*)ctx->smap_dec.p, ctx->stream)) return nullptr;
+    if (hipStreamSynchronize(ctx->stream) != hipSuccess) return nullptr;
+    return (const double*)ctx->smap_dec.p;
 }
 
 int rtm_render_frames_async(rtm_ctx* ctx, int32_t n_frames, const rtm_scene* scenes, const rtm_camera* eye,
@@ -1538,6 +1558,7 @@ int rtm_render_frames_async(rtm_ctx* ctx, int32_t n_frames, const rtm_scene* sce
     }
     ctx->have_shadow_pass = true;
     ctx->last_smap = sm[last & 1];
+    ctx->last_sh = f[(size_t)last].sh;  // (f64 map: the pipelined kernel writes 8-byte texels)
     ctx->smap_w = width;
     ctx->smap_h = height;
     return RTM_OK;

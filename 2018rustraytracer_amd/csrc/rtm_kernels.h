@@ -91,7 +91,28 @@ struct ShadowPart {
     int32_t n_spheres, n_patches;
     int32_t steps, flags;
     int32_t cull_x0, cull_x1, cull_y0, cull_y1;  // union of the spheres' pixel ranges (see EyePart)
+    int32_t smap_fmt;  // SMAP_F64 / SMAP_U8 / SMAP_U16: how the shadow pass stores the map (shadow_map_format)
+    int32_t smap_bw;   // coded maps: blocks per block row, ceil(W / 128)
 };
+
+// The shadow map's storage.  Every texel's value is one of +INF, a sphere's
+// back-face depth at that texel, or t_k (the march's t after k advances, a table
+// entry), so a coded map stores WHICH: code k < steps = t_k, steps + i = sphere i's
+// depth there (recomputed by the reader with the writer's operations: same bits),
+// all ones = +INF.  The codes are tiled in blocks of 128 columns x 4 rows, one
+// block per shadow wave: texel (x, y) is element
+//   ((y >> 2) * smap_bw + (x >> 7)) * 512 + ((x & 127) >> 1) * 8 + (y & 3) * 2 + (x & 1)
+// (the lean tile's lane holds 4 rows x 2 columns = 8 codes, stored as 8 or 16
+// contiguous bytes).  1 or 2 bytes per texel instead of 8.
+constexpr int32_t SMAP_F64 = 0, SMAP_U8 = 1, SMAP_U16 = 2;
+constexpr int64_t smap_code_index(int x, int y, int bw) {
+    return ((int64_t)(y >> 2) * bw + (x >> 7)) * 512 + ((x & 127) >> 1) * 8 + (y & 3) * 2 + (x & 1);
+}
+// bytes of a shadow map of W x H texels in format fmt
+inline int64_t smap_bytes(int32_t fmt, int32_t W, int32_t H) {
+    if (fmt == SMAP_F64) return (int64_t)W * H * 8;
+    return (int64_t)((W + 127) / 128) * ((H + 3) / 4) * 512 * (fmt == SMAP_U8 ? 1 : 2);
+}
 
 // What the eye pass of one frame reads (eye viewport rasterize + renderColorImage).
 struct EyePart {
@@ -281,6 +302,13 @@ static_assert(sizeof(StatsK) == sizeof(rtm_stats), "StatsK layout");
 
 // Launchers (rtm_kernels.hip).  All asynchronous on `stream`.
 int launch_shadow_pass(const FrameArgs& a, double* smap, void* stream, StatsK* stats);
+// The map format the (non-counting) shadow pass writes for these arguments: a
+// coded map (SMAP_U8 when steps + n_spheres <= 254, SMAP_U16 up to 65534) for
+// the default lean tile and the generic tile, f64 for the A/B-only modes and
+// when RTM_SMAP=f64.  Set a.sh.smap_fmt / smap_bw before both passes launch.
+int32_t shadow_map_format(const ShadowPart& sh);
+// f64 values of a coded map (rtm_ctx_shadow_map's view of it), async on stream.
+int launch_smap_decode(const ShadowPart& sh, const void* codes, double* out, void* stream);
 // rt / psp != nullptr: the frame has ray-traced primitives / a PERSPECTIVE eye
 // with spheres (device RtK / PerspK, see launch_upload); either selects the
 // general eye kernel.

@@ -16,6 +16,7 @@
 #include <math.h>
 
 #include <algorithm>
+#include <string>
 #include <stdint.h>
 #include <stdlib.h>
 
@@ -132,6 +133,7 @@ struct MarchResult {
     bool hit;
     double t;
     int iters;  // loop iterations executed (stats only)
+    int k;      // hit: the advances before it (t == t_after(tb, k), the coded map's march code)
 };
 
 // t after k advances (table built on the host by sequential summation; the
@@ -200,7 +202,7 @@ __device__ __forceinline__ int first_crossing(cdouble* zt, double D, double oz, 
 template <bool COUNT>
 __device__ __forceinline__ MarchResult march_axis(double D, bool inr0, double oz, double sz, int steps,
                                                   const Tables& tb) {
-    MarchResult r{false, 0.0, 0};
+    MarchResult r{false, 0.0, 0, 0};
     int cnt = inr0 ? 0 : steps;
     const bool fast_ok = tb.z != nullptr && (!inr0 || (fabs(D) < INFINITY && D != 0.0));
     if (tb.zmono != 0 && __all(fast_ok)) {
@@ -258,6 +260,7 @@ __device__ __forceinline__ MarchResult march_axis(double D, bool inr0, double oz
     if (cnt < steps) {
         r.hit = true;
         r.t = t_after(tb, cnt);
+        r.k = cnt;
     }
     if (COUNT) r.iters = cnt < steps ? cnt + 1 : steps;
     return r;
@@ -277,7 +280,7 @@ __device__ __forceinline__ MarchResult march(double ox, double oy, double oz, do
     // General ray (x/y motion): in-range and the surface depth change per step.
     // Per 4-step chunk the hits are collected as bits; the first set bit of the
     // first non-empty chunk is the reference's first hit.
-    MarchResult r{false, 0.0, 0};
+    MarchResult r{false, 0.0, 0, 0};
     const int mask = hit_class_mask(oz - bil(p, px0, py0));
     int khit = -1;
     bool done = false;
@@ -301,6 +304,7 @@ __device__ __forceinline__ MarchResult march(double ox, double oy, double oz, do
     if (khit >= 0) {
         r.hit = true;
         r.t = t_after(tb, khit);
+        r.k = khit;
     }
     if (COUNT) r.iters = khit >= 0 ? khit + 1 : steps;
     return r;
@@ -766,8 +770,9 @@ struct ShadowCounts {
 // covers (for the per-wave cull).
 template <bool COUNT>
 __device__ __forceinline__ double shadow_texel(const ShadowPart& a, int xi, int yi, int xb, int xe, int yw,
-                                               ShadowCounts& c) {
+                                               ShadowCounts& c, int& code) {
     double zb = INFINITY;
+    code = -1;  // +INF
     if (!(a.flags & RTM_FLAG_NO_SHADOW_RASTER) && union_may_cover(a, xb, xe, yw, yw)) {
         const double x = a.tab.nx[xi];
         const double y = a.tab.ny[yi];
@@ -777,7 +782,10 @@ __device__ __forceinline__ double shadow_texel(const ShadowPart& a, int xi, int 
             if (cover(a.sph[i], x, y, h)) {
                 if (COUNT) ++c.tests;
                 const double depth = a.sph[i].z + h * a.sph[i].r;  // EnumFace::BACK (main.rs:243)
-                if (depth < zb) zb = depth;
+                if (depth < zb) {
+                    zb = depth;
+                    code = a.steps + i;
+                }
             }
         }
     }
@@ -797,7 +805,10 @@ __device__ __forceinline__ double shadow_texel(const ShadowPart& a, int xi, int 
                     c.hits += m.hit;
                     c.inrange += inr0;
                 }
-                if (m.hit && m.t < zb) zb = m.t;
+                if (m.hit && m.t < zb) {
+                    zb = m.t;
+                    code = m.k;
+                }
             }
         } else {
             double o[3], d[3];
@@ -809,11 +820,71 @@ __device__ __forceinline__ double shadow_texel(const ShadowPart& a, int xi, int 
                     c.hits += m.hit;
                     c.inrange += in01((o[0] + 1.0) * 0.5) && in01((o[1] + 1.0) * 0.5);
                 }
-                if (m.hit && m.t < zb) zb = m.t;
+                if (m.hit && m.t < zb) {
+                    zb = m.t;
+                    code = m.k;
+                }
             }
         }
     }
     return zb;
+}
+template <bool COUNT>
+__device__ __forceinline__ double shadow_texel(const ShadowPart& a, int xi, int yi, int xb, int xe, int yw,
+                                               ShadowCounts& c) {
+    int code;
+    return shadow_texel<COUNT>(a, xi, yi, xb, xe, yw, c, code);
+}
+
+// Value of a coded shadow-map texel (ShadowPart::smap_fmt != SMAP_F64): what the
+// shadow pass computed there, recomputed from its code with the writer's
+// operations (t_after; cover + the BACK-face depth of the lean and generic
+// tiles), so the same bits.
+__device__ __forceinline__ double smap_decode(const ShadowPart& sh, const void* __restrict__ map, int tx, int ty) {
+    const int64_t e = smap_code_index(tx, ty, sh.smap_bw);
+    const uint32_t code = sh.smap_fmt == SMAP_U8 ? (uint32_t)((const uint8_t*)map)[e]
+                                                 : (uint32_t)((const uint16_t*)map)[e];
+    const uint32_t inf = sh.smap_fmt == SMAP_U8 ? 0xFFu : 0xFFFFu;
+    if (code == inf) return INFINITY;
+    if ((int)code < sh.steps) return t_after(sh.tab, (int)code);
+    const RasterSphereK& sp = sh.sph[(int)code - sh.steps];
+    const double pa = ((sh.tab.nx[tx] - sp.cx) * sp.n) / sp.m;
+    const double pb = ((sh.tab.ny[ty] - sp.cy) * sp.n) / sp.m;
+    const double d = sqrt(pa * pa + pb * pb);
+    const double h = sqrt(1.0 - d * d);
+    return sp.z + h * sp.r;
+}
+
+// smap_decode for the eye pass's lookups (the active lanes of a wave, each with
+// its own texel): the code and the texel's NDC coordinates are loaded together
+// (no chain of dependent loads), and sphere codes are resolved one sphere at a
+// time with that sphere's constants as wave-uniform (scalar) values instead of a
+// per-lane indexed load of them.  Same operations as smap_decode: same bits.
+__device__ __forceinline__ double smap_decode_wave(const ShadowPart& sh, const void* __restrict__ map, int tx, int ty) {
+    const int64_t e = smap_code_index(tx, ty, sh.smap_bw);
+    const bool u8 = sh.smap_fmt == SMAP_U8;
+    const uint32_t code = u8 ? (uint32_t)((const uint8_t*)map)[e] : (uint32_t)((const uint16_t*)map)[e];
+    const double xs = sh.tab.nx[tx];
+    const double ys = sh.tab.ny[ty];
+    const uint32_t inf = u8 ? 0xFFu : 0xFFFFu;
+    const int steps = sh.steps;
+    double v = INFINITY;
+    if (code != inf && (int)code < steps) v = t_after(sh.tab, (int)code);
+    int si = (code != inf && (int)code >= steps) ? (int)code - steps : -1;
+    while (__any(si >= 0)) {
+        const unsigned long long b = __ballot(si >= 0);
+        const int i = __builtin_amdgcn_readfirstlane(__shfl(si, __builtin_ctzll(b)));
+        const RasterSphereK& sp = sh.sph[i];
+        if (si == i) {
+            const double pa = ((xs - sp.cx) * sp.n) / sp.m;
+            const double pb = ((ys - sp.cy) * sp.n) / sp.m;
+            const double d = sqrt(pa * pa + pb * pb);
+            const double h = sqrt(1.0 - d * d);
+            v = sp.z + h * sp.r;
+            si = -1;
+        }
+    }
+    return v;
 }
 
 // Generic shadow tile: 64 x TILE_Y texels, one wave per row.
@@ -825,8 +896,14 @@ __device__ __forceinline__ void shadow_tile_generic(const ShadowPart& a, double*
     const int yi = __builtin_amdgcn_readfirstlane(by * TILE_Y + (threadIdx.x >> 6));  // wave-uniform row
     ShadowCounts c;
     if (xi < a.W && yi < a.H) {
-        const double zb = shadow_texel<COUNT>(a, xi, yi, xb, xb + TILE_X - 1, yi, c);
-        smap[(int64_t)yi * a.W + xi] = zb;
+        int code;
+        const double zb = shadow_texel<COUNT>(a, xi, yi, xb, xb + TILE_X - 1, yi, c, code);
+        if (COUNT || a.smap_fmt == SMAP_F64)
+            smap[(int64_t)yi * a.W + xi] = zb;
+        else if (a.smap_fmt == SMAP_U8)
+            ((uint8_t*)smap)[smap_code_index(xi, yi, a.smap_bw)] = (uint8_t)code;  // -1: 0xFF = +INF
+        else
+            ((uint16_t*)smap)[smap_code_index(xi, yi, a.smap_bw)] = (uint16_t)code;
     }
     if (COUNT) {
         stat_add(&st->shadow_sphere_tests, c.tests);
@@ -1108,9 +1185,12 @@ __device__ unsigned long long g_phase[1 << 18];
 //   okA = !P(z_{f-1}), okB = P(z_f), entry = !P(z_0)   (monotone P)
 //   hit  = inr & fastD & okA & okB & f < steps      -> t = t_f
 //   slow = inr & (!fastD | (entry & !(okA & (f == steps | okB))))  -> exact march_axis
-template <int NR, int CW, bool INC, int FILLN = 4>
+// CODE: the map's storage (SMAP_F64, or a coded map, rtm_kernels.h): the tile
+// tracks which source won each texel beside its value.
+template <int NR, int CW, bool INC, int FILLN = 4, int CODE = SMAP_F64>
 __device__ __forceinline__ void shadow_tile_lean2(const ShadowPart& a, double* __restrict__ smap, int bx, int by,
                                                   double2* __restrict__ T, int diag) {
+    static_assert(CODE == SMAP_F64 || (NR == 4 && CW == 2), "coded maps use the 4 x 128 texel block layout");
     constexpr int TW = TILE_X * CW;
     const int lane = threadIdx.x & (TILE_X - 1);
     const int xb = bx * TW;
@@ -1173,10 +1253,14 @@ __device__ __forceinline__ void shadow_tile_lean2(const ShadowPart& a, double* _
         }
     }
     double zb[NR][CW];
+    int cd[NR][CW];  // CODE: the winning source (-1: +INF)
 #pragma unroll
     for (int r = 0; r < NR; ++r)
 #pragma unroll
-        for (int c = 0; c < CW; ++c) zb[r][c] = INFINITY;
+        for (int c = 0; c < CW; ++c) {
+            zb[r][c] = INFINITY;
+            cd[r][c] = -1;
+        }
     // shadow viewport rasterize, face BACK (main.rs:1569, 243)
     if (!(a.flags & RTM_FLAG_NO_SHADOW_RASTER) && !(diag & 1) &&
         union_may_cover(a, xb, xb + TW - 1, y0, y0 + NR - 1)) {
@@ -1211,7 +1295,9 @@ __device__ __forceinline__ void shadow_tile_lean2(const ShadowPart& a, double* _
                     const double d = sqrt(s2[c]);
                     const double h = sqrt(1.0 - d * d);
                     const double depth = sp.z + h * sp.r;
-                    zb[r][c] = ((d < 1.0) & (depth < zb[r][c])) ? depth : zb[r][c];
+                    const bool win = (d < 1.0) & (depth < zb[r][c]);
+                    zb[r][c] = win ? depth : zb[r][c];
+                    if (CODE) cd[r][c] = win ? a.steps + i : cd[r][c];
                 }
             }
         }
@@ -1283,7 +1369,9 @@ __device__ __forceinline__ void shadow_tile_lean2(const ShadowPart& a, double* _
                     const bool entry = INC ? (oz < Dv) : !(oz < Dv);
                     const bool hit = inr & fastD & okA & okB & (f < steps);
                     const double ty = e.y;
-                    zb[r][c] = (hit & (ty < zb[r][c])) ? ty : zb[r][c];
+                    const bool win = hit & (ty < zb[r][c]);
+                    zb[r][c] = win ? ty : zb[r][c];
+                    if (CODE) cd[r][c] = win ? f : cd[r][c];
                     const bool sl = inr & (!fastD | (entry & !(okA & ((f == steps) | okB))));
                     slow |= sl ? (1u << (r * CW + c)) : 0u;
                 }
@@ -1310,7 +1398,10 @@ __device__ __forceinline__ void shadow_tile_lean2(const ShadowPart& a, double* _
                     for (int r = 0; r < NR; ++r)
 #pragma unroll
                         for (int c = 0; c < CW; ++c)
-                            if (q == r * CW + c && m.hit && m.t < zb[r][c]) zb[r][c] = m.t;
+                            if (q == r * CW + c && m.hit && m.t < zb[r][c]) {
+                                zb[r][c] = m.t;
+                                if (CODE) cd[r][c] = m.k;
+                            }
                 }
             }
         }
@@ -1324,6 +1415,33 @@ __device__ __forceinline__ void shadow_tile_lean2(const ShadowPart& a, double* _
 #pragma unroll
             for (int c = 0; c < CW; ++c) any |= zb[r][c] == -12345.0;
         if (any) smap[0] = 0.0;
+        return;
+    }
+    if (CODE != SMAP_F64) {
+        // the lane's 4 rows x 2 columns as one 8- (U8) or 16-byte (U16) store into
+        // the wave's block: element lane*8 + r*2 + c (rows past H and columns past
+        // W hold codes no reader looks up; a wave whose rows all lie past H has no
+        // block: the map holds ceil(H/4) block rows)
+        const int64_t blk = (int64_t)(y0 >> 2) * a.smap_bw + (xb >> 7);
+        if (y0 >= a.H) {
+        } else if (CODE == SMAP_U8) {
+            uint32_t w[2] = {0u, 0u};
+#pragma unroll
+            for (int r = 0; r < NR; ++r)
+#pragma unroll
+                for (int c = 0; c < CW; ++c) w[r >> 1] |= ((uint32_t)cd[r][c] & 0xFFu) << (8 * ((r & 1) * 2 + c));
+            *reinterpret_cast<uint2*>((uint8_t*)smap + blk * 512 + lane * 8) = make_uint2(w[0], w[1]);
+        } else {
+            uint32_t w[NR];
+#pragma unroll
+            for (int r = 0; r < NR; ++r) w[r] = ((uint32_t)cd[r][0] & 0xFFFFu) | ((uint32_t)cd[r][1] << 16);
+            *reinterpret_cast<uint4*>((uint8_t*)smap + blk * 1024 + lane * 16) = make_uint4(w[0], w[1], w[2], w[3]);
+        }
+        RTM_PHASE(4)
+        if (diag & 8) {
+            __builtin_amdgcn_s_waitcnt(0);
+            RTM_PHASE(5)
+        }
         return;
     }
 #pragma unroll
@@ -1356,7 +1474,7 @@ __device__ __forceinline__ int hot_rows_first(int b, int n, int h0, int h1) {
     return r < h0 ? r : r + nh;
 }
 
-template <int NR, int CW, bool INC, int FILLN>
+template <int NR, int CW, bool INC, int FILLN, int CODE>
 __device__ __forceinline__ void shadow_lean2_block(const ShadowPart& sh, double* __restrict__ smap, int diag, int hot,
                                                    double2* __restrict__ lds) {
     int by = blockIdx.y;
@@ -1368,14 +1486,14 @@ __device__ __forceinline__ void shadow_lean2_block(const ShadowPart& sh, double*
         const bool none = sh.cull_x0 > sh.cull_x1 || sh.cull_y0 > sh.cull_y1 || sh.cull_y1 < 0;
         by = none ? by : hot_rows_first(by, n, h0, h1);
     }
-    shadow_tile_lean2<NR, CW, INC, FILLN>(sh, smap, blockIdx.x, by, lds, diag);
+    shadow_tile_lean2<NR, CW, INC, FILLN, CODE>(sh, smap, blockIdx.x, by, lds, diag);
 }
 
-template <int NR, int CW, bool INC, int FILLN = 4>
+template <int NR, int CW, bool INC, int FILLN = 4, int CODE = SMAP_F64>
 __global__ __launch_bounds__(BLOCK) void shadow_lean2_kernel(const FrameArgs a, double* __restrict__ smap, int diag,
                                                              int hot) {
     extern __shared__ double2 lds_zt[];
-    shadow_lean2_block<NR, CW, INC, FILLN>(a.sh, smap, diag, hot, lds_zt);
+    shadow_lean2_block<NR, CW, INC, FILLN, CODE>(a.sh, smap, diag, hot, lds_zt);
 }
 
 // Batched forms: frame blockIdx.z of a BatchFrame table in device memory.  The
@@ -1383,11 +1501,11 @@ __global__ __launch_bounds__(BLOCK) void shadow_lean2_kernel(const FrameArgs a, 
 // loads exactly like kernel arguments.
 using CBatch = const __attribute__((address_space(4))) BatchFrame;
 
-template <int NR, int CW, bool INC, int FILLN>
+template <int NR, int CW, bool INC, int FILLN, int CODE>
 __global__ __launch_bounds__(BLOCK) void shadow_lean2_batch_kernel(CBatch* __restrict__ fr, int diag, int hot) {
     extern __shared__ double2 lds_zt[];
     CBatch* f = fr + blockIdx.z;
-    shadow_lean2_block<NR, CW, INC, FILLN>(*(const ShadowPart*)&f->a.sh, f->smap, diag, hot, lds_zt);
+    shadow_lean2_block<NR, CW, INC, FILLN, CODE>(*(const ShadowPart*)&f->a.sh, f->smap, diag, hot, lds_zt);
 }
 
 
@@ -1550,8 +1668,10 @@ __device__ __forceinline__ void eye_tile(const EyePart& a, const ShadowPart& sh,
             if (ty >= 0 && ty < a.Hs && tx >= 0 && tx < a.Ws) {
                 if (FUSED)
                     dsm = shadow_texel<COUNT>(sh, (int)tx, (int)ty, (int)tx, (int)tx, (int)ty, sc);
-                else
+                else if (sh.smap_fmt == SMAP_F64)
                     dsm = smap[ty * a.Ws + tx];
+                else
+                    dsm = smap_decode_wave(sh, smap, (int)tx, (int)ty);
             }
             const bool lit = dsm > qz - 0.0;
             const double lm = lit ? 1.0 : 0.25;
@@ -1655,6 +1775,14 @@ __global__ __launch_bounds__(BLOCK) void eye_pass_kernel(const FrameArgs a, cons
                                                          void* __restrict__ out, StatsK* __restrict__ st,
                                                          const DevTabs tabs, int wide) {
     eye_tile<FUSED, COUNT, RT, FMT>(a.ey, a.sh, smap, out, blockIdx.x, blockIdx.y, st, tabs, wide);
+}
+
+// The sphere-only eye pass (RT 0, materialised map) held to 8 waves per SIMD: the
+// coded map's decode (smap_decode_wave) would otherwise take it to 66 VGPRs, 7 waves.
+template <int FMT>
+__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8))) void eye_pass8_kernel(
+    const FrameArgs a, const double* __restrict__ smap, void* __restrict__ out, const DevTabs tabs, int wide) {
+    eye_tile<false, false, 0, FMT>(a.ey, a.sh, smap, out, blockIdx.x, blockIdx.y, nullptr, tabs, wide);
 }
 
 // The SDF eye instantiation (row f-4) with a register cap: WPE waves per SIMD at least.
@@ -2054,7 +2182,18 @@ static void launch_sep(const FrameArgs& a, double* smap, hipStream_t s) {
         const int hot = lean_hot() ? 1 : 0;
 #define RTM_L2(C, I, F) \
     hipLaunchKernelGGL((shadow_lean2_kernel<NR, C, I, F>), g2, dim3(BLOCK), lsm, s, a, smap, diag_mode(), hot)
-        if (cw == 2 && fill1) {
+#define RTM_L2C(I, F, M) \
+    hipLaunchKernelGGL((shadow_lean2_kernel<4, 2, I, F, M>), g2, dim3(BLOCK), lsm, s, a, smap, diag_mode(), hot)
+        const int code = a.sh.smap_fmt;
+        if (NR == 4 && cw == 2 && code != SMAP_F64) {  // coded map (shadow_map_format)
+            if (code == SMAP_U8) {
+                if (fill1) { if (inc) RTM_L2C(true, 1, SMAP_U8); else RTM_L2C(false, 1, SMAP_U8); }
+                else { if (inc) RTM_L2C(true, 4, SMAP_U8); else RTM_L2C(false, 4, SMAP_U8); }
+            } else {
+                if (fill1) { if (inc) RTM_L2C(true, 1, SMAP_U16); else RTM_L2C(false, 1, SMAP_U16); }
+                else { if (inc) RTM_L2C(true, 4, SMAP_U16); else RTM_L2C(false, 4, SMAP_U16); }
+            }
+        } else if (cw == 2 && fill1) {
             if (inc) RTM_L2(2, true, 1);
             else RTM_L2(2, false, 1);
         } else if (cw == 2) {
@@ -2065,6 +2204,7 @@ static void launch_sep(const FrameArgs& a, double* smap, hipStream_t s) {
             else RTM_L2(1, false, 4);
         }
 #undef RTM_L2
+#undef RTM_L2C
     } else if (mode == MARCH_SEARCH)
         hipLaunchKernelGGL((shadow_sep_kernel<NR, MARCH_SEARCH>), g, dim3(BLOCK), smem, s, a, smap, diag_mode(), lds);
     else if (mode == MARCH_CMP)
@@ -2112,6 +2252,15 @@ static bool sdf_wpe5() {
     return v;
 }
 
+// The sphere-only eye pass at 8 waves/SIMD (default; RTM_EYE_WPE8=0: the compiler's allocation)
+static bool eye_wpe8() {
+    static bool v = [] {
+        const char* e = getenv("RTM_EYE_WPE8");
+        return !(e && atoi(e) == 0);
+    }();
+    return v;
+}
+
 template <int FMT>
 static void launch_eye_fmt(const FrameArgs& a, const double* smap, void* o, hipStream_t s, dim3 g, bool fused,
                            const DevTabs& tabs, int wide) {
@@ -2130,6 +2279,8 @@ static void launch_eye_fmt(const FrameArgs& a, const double* smap, void* o, hipS
         else RTM_EYE(false, 1);
     } else {
         if (fused) RTM_EYE(true, 0);
+        else if (eye_wpe8())
+            hipLaunchKernelGGL((eye_pass8_kernel<FMT>), g, dim3(BLOCK), 0, s, a, smap, o, tabs, wide);
         else RTM_EYE(false, 0);
     }
 #undef RTM_EYE
@@ -2195,14 +2346,17 @@ int launch_shadow_batch(const BatchFrame* dev, int n, const FrameArgs& a0, void*
         const bool inc = sh.tab.zmono >= 0;
         const bool fill1 = lean_fill1() && sh.steps + 1 <= BLOCK;
         const int hot = lean_hot() ? 1 : 0;
-#define RTM_LB(I, F) hipLaunchKernelGGL((shadow_lean2_batch_kernel<4, 2, I, F>), g, dim3(BLOCK), lsm, s, fr, diag_mode(), hot)
-        if (fill1) {
-            if (inc) RTM_LB(true, 1);
-            else RTM_LB(false, 1);
-        } else {
-            if (inc) RTM_LB(true, 4);
-            else RTM_LB(false, 4);
-        }
+#define RTM_LB(I, F, M) \
+    hipLaunchKernelGGL((shadow_lean2_batch_kernel<4, 2, I, F, M>), g, dim3(BLOCK), lsm, s, fr, diag_mode(), hot)
+#define RTM_LBM(M)                                              \
+    do {                                                        \
+        if (fill1) { if (inc) RTM_LB(true, 1, M); else RTM_LB(false, 1, M); } \
+        else { if (inc) RTM_LB(true, 4, M); else RTM_LB(false, 4, M); }       \
+    } while (0)
+        if (sh.smap_fmt == SMAP_U8) RTM_LBM(SMAP_U8);
+        else if (sh.smap_fmt == SMAP_U16) RTM_LBM(SMAP_U16);
+        else RTM_LBM(SMAP_F64);
+#undef RTM_LBM
 #undef RTM_LB
         return launched();
     }
@@ -2210,6 +2364,37 @@ int launch_shadow_batch(const BatchFrame* dev, int n, const FrameArgs& a0, void*
     dim3 g = grid_for(sh.W, sh.H);
     g.z = (unsigned)n;
     hipLaunchKernelGGL(shadow_pass_batch_kernel, g, dim3(BLOCK), 0, s, fr);
+    return launched();
+}
+
+// The shadow map's storage for these arguments (rtm_kernels.h): coded when the
+// default lean tile (4 rows x 2 columns per lane) or the generic tile writes it and
+// every code fits (steps + n_spheres codes plus +INF); f64 for the A/B-only
+// separable modes, and with RTM_SMAP=f64 (A/B runs: the 8-byte map).
+int32_t shadow_map_format(const ShadowPart& sh) {
+    static const bool f64_env = [] {
+        const char* e = getenv("RTM_SMAP");
+        return e && (std::string(e) == "f64" || std::string(e) == "0");
+    }();
+    if (f64_env) return SMAP_F64;
+    if (use_sep(sh) && !(sep_mode(sh) == MARCH_LEAN2 && sep_rows() == 4 && lean_cols() == 2)) return SMAP_F64;
+    const int64_t codes = (int64_t)sh.steps + sh.n_spheres;  // + the all-ones +INF code
+    if (codes <= 254) return SMAP_U8;
+    if (codes <= 65534 && sh.tab.t) return SMAP_U16;
+    return SMAP_F64;
+}
+
+__global__ __launch_bounds__(BLOCK) void smap_decode_kernel(const ShadowPart sh, const void* __restrict__ codes,
+                                                            double* __restrict__ out) {
+    const int x = blockIdx.x * BLOCK + threadIdx.x;
+    const int y = blockIdx.y;
+    if (x < sh.W) out[(int64_t)y * sh.W + x] = smap_decode(sh, codes, x, y);
+}
+
+int launch_smap_decode(const ShadowPart& sh, const void* codes, double* out, void* stream) {
+    if (sh.smap_fmt == SMAP_F64 || sh.W < 1 || sh.H < 1) return RTM_ERR_INVALID;
+    hipLaunchKernelGGL(smap_decode_kernel, dim3((unsigned)((sh.W + BLOCK - 1) / BLOCK), (unsigned)sh.H), dim3(BLOCK),
+                       0, (hipStream_t)stream, sh, codes, out);
     return launched();
 }
 

@@ -294,7 +294,7 @@ def main():
     W, H, K = cfg["width"], cfg["height"], cfg["steps"]
     # frames per step: a step renders F frames of the sequence (at least 8, and at least
     # 64 Mpixel, so a short --steps run still times milliseconds of work, not a few frames)
-    F = a.frames_per_step or min(256, max(8, -(-(1 << 26) // (W * H))))
+    F = a.frames_per_step or min(256, max(8, (1 << 26) // (W * H)))
     nW, nS = a.warmup * F, a.steps * F  # warmup / timed frames
     tile_mode = a.mode == "tile-gather"
     # tile-gather: each band evaluates only the shadow texels it reads (no cross-rank shadow map)
