@@ -1,0 +1,6 @@
+set -o pipefail
+export TMPDIR=/tmp
+O=gpurun_out/r2l; mkdir -p $O
+timeout -k 10 600 python -u -m pytest -x -q --timeout 280 --timeout-method thread tests/test_smap_codes.py tests/test_gpu_parity.py -m gpu -p no:cacheprovider > $O/pytest.log 2>&1
+rc=$?; echo "pytest rc=$rc"; tail -3 $O/pytest.log; [ $rc -ne 0 ] && exit $rc
+bash tools/ab_env.sh $O "3 2 5" "-;RTM_LEAN_MID=0" 2
