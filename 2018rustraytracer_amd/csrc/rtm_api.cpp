@@ -1376,6 +1376,12 @@ int rtm_render_async(rtm_ctx* ctx, const rtm_scene* scene, const rtm_camera* eye
                                  row_begin, row_end, out_rgba_dev);
 }
 
+int32_t rtm_ctx_shadow_map_texel_bytes(rtm_ctx* ctx) {
+    if (!ctx || !ctx->have_shadow_pass) return 0;
+    const int32_t f = ctx->last_sh.smap_fmt;
+    return f == SMAP_U8 ? 1 : f == SMAP_U16 ? 2 : 8;
+}
+
 const double* rtm_ctx_shadow_map(rtm_ctx* ctx) {
     if (!ctx || !ctx->have_shadow_pass) return nullptr;
     if (ctx->last_sh.smap_fmt == SMAP_F64) return ctx->last_smap;

@@ -8,7 +8,12 @@ off for bit parity).  Per-unit figures:
   shadow texel   4 per sphere (cull)      + 19 per covering sphere
                  32 per patch (ray origin, domain map, surface depth, entry sign,
                     in-range test, step vector, strict-min update)
-                 3 per march iteration    (z - D, class test, z += step.z)
+                 3 per march iteration    (z - D, class test, z += step.z) for a ray
+                                          without x/y motion (march_axis)
+                 16 per march iteration   for a ray that moves in x/y (the general
+                                          loop, e.g. a tilted sun): p += step (3),
+                                          bilinear (7), z - h, class test, two
+                                          in-range tests (2 each)
     separable axis-aligned shadow camera with a shared z sequence (every
     BASELINE scene): the per-wave cull is scalar, D = d0[x] + dd[x]*py[y],
     z_k is one host table for all texels, so per texel:
@@ -31,6 +36,12 @@ off for bit parity).  Per-unit figures:
                                            body quadratic 50)
                  -- per (pixel, primitive) test run: stats eye_plane_tests /
                  eye_cylinder_tests, after the PERSPECTIVE eye's per-wave cull
+    PERSPECTIVE eye without SDFs (the RT 3 kernel): every ray starts at the
+    camera, so the host evaluates calcRayPlane's numerator and iCappedCone's
+    origin-only terms once per (camera, primitive) (RtK::persp); per test:
+                 24 per circle plane      (denominator 5, its test, t, t tests 4,
+                                           hit point + radius test 15)
+                 48 per capped cylinder   (rd.ba 5, cap branch ~16, body quadratic 27)
 
 HBM bytes the two-kernel design must move:
   shadow pass    8 B per texel            (f64 shadow-map store)
@@ -52,6 +63,7 @@ SHADOW_PER_SPHERE = 4
 SHADOW_PER_COVER = 19
 SHADOW_PER_PATCH = 32
 SHADOW_PER_ITER = 3
+SHADOW_PER_ITER_MOVING = 16
 SEP_PER_PATCH = 4
 SEP_PER_ITER = 1
 SEARCH_PER_PATCH = 10
@@ -62,6 +74,8 @@ RT_RAY_ORTHO = 12
 RT_RAY_PERSP = 24
 RT_PER_PLANE = 33
 RT_PER_CYL = 88
+RT_PER_PLANE_PERSP = 24
+RT_PER_CYL_PERSP = 48
 # row f-4 (entry.frag distanceFn0 + the sphere-tracing leaf, restated in f64):
 # per (pixel, SDF): two sBox slab tests + the loop set-up; per distanceFn0
 # evaluation: sdBox 19 + udTriangleSingle's sign test 30 + its edge branch 59
@@ -83,8 +97,13 @@ def shared_z_separable(shadow_cam) -> bool:
 
 def frame_work(stats: dict, width: int, height: int, n_spheres: int, n_patches: int, flags: int = 0,
                fused: bool = False, sep: bool = False, n_planes: int = 0, n_cyls: int = 0,
-               perspective: bool = False, search: bool = False, n_sdfs: int = 0) -> dict:
-    """search: the march is the first-crossing search (monotone shared z table)."""
+               perspective: bool = False, search: bool = False, n_sdfs: int = 0, map_texel_bytes: int = 8,
+               moving: bool = False) -> dict:
+    """search: the march is the first-crossing search (monotone shared z table).
+    map_texel_bytes: the shadow map's storage per texel (8: f64; 2 or 1: the coded
+    map, rtm_ctx_shadow_map_texel_bytes) -- stored once per texel by the shadow
+    pass, gathered once per hit pixel by the eye pass.
+    moving: the shadow rays move in x/y (the general march loop)."""
     px = width * height
     no_march = bool(flags & 0x1)
     no_sraster = bool(flags & 0x2)
@@ -98,7 +117,8 @@ def frame_work(stats: dict, width: int, height: int, n_spheres: int, n_patches: 
         elif sep and not fused:
             sh_ops += texels * n_patches * SEP_PER_PATCH + SEP_PER_ITER * stats["march_iterations"]
         else:
-            sh_ops += texels * n_patches * SHADOW_PER_PATCH + SHADOW_PER_ITER * stats["march_iterations"]
+            sh_ops += texels * n_patches * SHADOW_PER_PATCH + (
+                SHADOW_PER_ITER_MOVING if moving else SHADOW_PER_ITER) * stats["march_iterations"]
     eye_ops = (px * EYE_PER_SPHERE * n_spheres + EYE_PER_COVER * stats["eye_sphere_tests"]
                + EYE_PER_HIT * stats["eye_hit_pixels"])
     if n_planes or n_cyls or n_sdfs:
@@ -106,11 +126,13 @@ def frame_work(stats: dict, width: int, height: int, n_spheres: int, n_patches: 
         # primitives no ray of a wave can reach (stats, ABI v4)
         pl_tests = stats.get("eye_plane_tests", px * n_planes)
         cy_tests = stats.get("eye_cylinder_tests", px * n_cyls)
+        hoisted = perspective and not n_sdfs  # the RT 3 kernel (host-hoisted origin terms)
         eye_ops += (px * ((RT_RAY_PERSP if perspective else RT_RAY_ORTHO) + SDF_PER_TRACE * n_sdfs)
-                    + RT_PER_PLANE * pl_tests + RT_PER_CYL * cy_tests)
+                    + (RT_PER_PLANE_PERSP if hoisted else RT_PER_PLANE) * pl_tests
+                    + (RT_PER_CYL_PERSP if hoisted else RT_PER_CYL) * cy_tests)
         eye_ops += SDF_PER_EVAL * stats.get("sdf_distance_evals", 0) + SDF_PER_HIT * stats.get("eye_sdf_pixels", 0)
-    sh_bytes = 0 if fused else 8 * px
-    eye_bytes = 16 * px + (0 if fused else 8 * stats["eye_hit_pixels"])
+    sh_bytes = 0 if fused else map_texel_bytes * px
+    eye_bytes = 16 * px + (0 if fused else map_texel_bytes * stats["eye_hit_pixels"])
     return dict(shadow_pass=dict(ops=sh_ops, bytes=sh_bytes),
                 eye_pass=dict(ops=eye_ops + (sh_ops if fused else 0), bytes=eye_bytes),
                 # software-pipelined launch: shadow pass of frame i + eye pass of frame i-1

@@ -147,6 +147,10 @@ class Context:
     def shadow_map_ptr(self) -> int:
         return _lib().rtm_ctx_shadow_map(self._h) or 0
 
+    def shadow_map_texel_bytes(self) -> int:
+        """Bytes per texel of the last shadow pass's map: 8 (f64), 2 or 1 (coded)."""
+        return int(_lib().rtm_ctx_shadow_map_texel_bytes(self._h))
+
     def stats(self, scene: Scene, eye: Camera, shadow: Camera, width: int, height: int, steps: int,
               flags: int = 0) -> dict:
         sc, keep = scene.to_c()

@@ -412,6 +412,8 @@ def main():
         barrier()
         elapsed = max_over_ranks(time.perf_counter() - t0)
 
+    # the shadow map's storage in the timed frames (coded: 1-2 B per texel; fused: none)
+    map_bytes = ctx.shadow_map_texel_bytes() or 8
     # per-kernel HIP-event durations over the timed region (ctx stream)
     n_launches = nS + 1 if pipelined else nS
     sh_ms, eye_ms = ctx.kernel_ms_history((n_launches + timing_stride - 1) // timing_stride)
@@ -538,7 +540,8 @@ def main():
                                   n_cyls=len(s0.cappedCylinderPrimitives),
                                   perspective=eye.type_ == sc.PERSPECTIVE,
                                   search=sep and os.environ.get("RTM_SEP_MODE", "2") == "2",
-                                  n_sdfs=len(s0.sdfPrimitives))
+                                  n_sdfs=len(s0.sdfPrimitives), map_texel_bytes=map_bytes,
+                                  moving=(shadow.dirNormalized[0] * 0.03 != 0.0 or shadow.dirNormalized[1] * 0.03 != 0.0))
         if band_h != H:  # rank 0 renders one band: scale the frame's work to it (approximate)
             for kk in work.values():
                 kk["ops"] = int(kk["ops"] * band_h / H)
@@ -595,6 +598,7 @@ def main():
             "roofline": roof,
             "roofline_other_kernel": roof_other,
             "roofline_frame": roof_frame,
+            "shadow_map_texel_bytes": None if fused else map_bytes,
             "lanes": lanes,
             "frames_per_launch": batch,
             "kernels_in_lanes": in_lanes,

@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define RTM_ABI_VERSION 6
+#define RTM_ABI_VERSION 7
 
 /* ---- limits: scene constants travel as kernel arguments (SGPR path) ---- */
 #define RTM_MAX_SPHERES 16
@@ -326,8 +326,15 @@ int rtm_render_frames_async(rtm_ctx* ctx, int32_t n_frames, const rtm_scene* sce
                             int32_t height, int32_t march_steps, int32_t flags,
                             float* const* out_rgba_dev);
 /* Device pointer of the context's shadow map (width*height f64) after a
- * non-fused render (NULL before the first one). */
+ * non-fused render (NULL before the first one).  The shadow pass stores a coded
+ * map (which source won each texel, 1 or 2 bytes) unless
+ * RTM_SMAP=f64: this call then decodes it into an f64 buffer of the context on
+ * its stream and waits (blocking), so the values are the shadow viewport's
+ * zBuffer bit for bit either way. */
 const double* rtm_ctx_shadow_map(rtm_ctx* ctx);
+/* ABI v7: bytes per texel the last non-fused frame's shadow pass stored: 8 (f64),
+ * 2 or 1 (coded map); 0 before any. */
+int32_t rtm_ctx_shadow_map_texel_bytes(rtm_ctx* ctx);
 
 /* Counting variant of the frame (separate, untimed kernels): the per-pass
  * work counts behind the roofline's algorithmic flop count. */

@@ -26,6 +26,7 @@ hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, cty
 u = lambda a: np.ascontiguousarray(a).view(np.uint64 if a.dtype == np.float64 else np.uint32)
 eye = sc.eye_camera()
 ctx = rtm.Context(0)
+F64 = %(f64)r
 
 def smap(c, w, h):
     m = np.empty((h, w), np.float64)
@@ -46,6 +47,8 @@ for s, shc, w, h, k in cases:
     torch.cuda.synchronize()
     ctx.render_async(s, eye, shc, w, h, k, 0, out.data_ptr())
     ctx.synchronize()
+    expect = 8 if F64 else (1 if k + len(s.spherePrimitives) <= 254 else 2)
+    assert ctx.shadow_map_texel_bytes() == expect, (ctx.shadow_map_texel_bytes(), expect, k)
     want = oracle.render(s, eye, shc, w, h, k, 0, nthreads=8, want_shadow=True)
     assert np.array_equal(u(out.cpu().numpy()), u(want["rgba"])), (w, h, k)
     assert np.array_equal(u(smap(ctx, w, h)), u(want["shadow"])), ("map", w, h, k)
@@ -73,6 +76,6 @@ def test_shadow_map_formats_in_subprocess(fmt):
     env.pop("RTM_SMAP", None)
     if fmt == "f64":
         env["RTM_SMAP"] = "f64"
-    r = subprocess.run([sys.executable, "-c", CHILD % {"root": ROOT}], env=env, capture_output=True, text=True,
+    r = subprocess.run([sys.executable, "-c", CHILD % {"root": ROOT, "f64": fmt == "f64"}], env=env, capture_output=True, text=True,
                        timeout=600)
     assert r.returncode == 0 and "smap ok" in r.stdout, r.stdout[-3000:] + r.stderr[-3000:]

@@ -58,7 +58,7 @@ def main():
         timed_shadow = k.startswith("shadow_") and not k.startswith("shadow_pass_kernel<true")  # (<true>: stats)
         name = ("shadow_pass" if timed_shadow else
                 "eye_pass" if k.startswith(("eye_pass_kernel<false, false", "eye_batch_kernel<false",
-                                             "eye_sdf_kernel", "eye_sdf_batch_kernel")) else
+                                             "eye_sdf_kernel", "eye_sdf_batch_kernel", "eye_pass8_kernel")) else
                 "eye_pass_fused" if k.startswith(("eye_pass_kernel<true, false", "eye_batch_kernel<true")) else k)
         out["kernels"][name] = d
     print(json.dumps(out, indent=1, sort_keys=True))

@@ -13,5 +13,7 @@ for c in "$@"; do
   echo "pmc $c rc=$rc"
   [ $rc -ne 0 ] && exit $rc
   cp "gpurun_out/pmc_${tag}_c$cfg/summary.json" "gpurun_out/pmc_${tag}_c$cfg.summary.json"
+  # the raw per-dispatch CSVs are large (gpurun copies back at most 64 MiB): keep the summary and logs
+  rm -rf "gpurun_out/pmc_${tag}_c$cfg"/p[0-9]*/
 done
 echo done
