@@ -1023,10 +1023,11 @@ int enqueue_frame(rtm_ctx* ctx, FrameArgs& a, const FrameExtra* x, void* out_dev
 // How many lanes a frame sequence spreads over.  Frames are independent (own
 // scene, own shadow map, own output), so frame i can run beside frame i+1: at
 // 3840x2160 one frame's two kernels leave the chip part-empty in their ramp and
-// tail (the shadow pass is latency-bound), and 3 lanes take config 3 from ~40 to
-// ~34 us per frame; at 7680x4320 the passes are long and store-bound and
-// lanes only add cache pressure (2 lanes: 133 -> 157 us), hence the size
-// limit; below 1 Mpixel the host's launch rate is the limit and switching
+// tail (the shadow pass is latency-bound): with the coded shadow map, 2 lanes take
+// config 3 from 40.1 to 33.3 us per frame (3 lanes 33.9), config 2 from 13.7 to
+// 9.5 (3 lanes 10.7) and 7680x4320 from 134 to 128 (with the 8-byte map a second
+// lane only added cache pressure there: 133 -> 157 us) (profiles/r02_ab_lanes.txt);
+// below 1 Mpixel the host's launch rate is the limit and switching
 // streams costs more than the overlap gains (512x512: 19.2 -> 14.2 Gpix/s with
 // 3 lanes) (tools/probes/two_ctx.py).  RTM_LANES=n overrides.
 // Frame i goes to lane (n-1-i) % L, so the last frame runs on lane 0 and the
@@ -1038,7 +1039,7 @@ int frame_lanes(int32_t req, int32_t n, int32_t W, int32_t H, float* const* out,
         return e ? atoi(e) : 0;
     }();
     const int64_t px = (int64_t)W * H;
-    int L = req > 0 ? req : env > 0 ? env : (px >= (1LL << 20) && px <= 3840LL * 2160 ? 3 : 1);
+    int L = req > 0 ? req : env > 0 ? env : (px >= (1LL << 20) ? 2 : 1);
     const int32_t nb = (n + B - 1) / B;  // batches of B frames; batch b runs on lane (nb-1-b) % L
     if (L > 8) L = 8;
     if (L > nb) L = nb;

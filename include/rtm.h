@@ -228,8 +228,8 @@ int rtm_ctx_kernel_ms_history(rtm_ctx* ctx, float* shadow_pass_ms, float* eye_pa
 /* Lanes of rtm_render_frames_async: independent frames spread over `lanes`
  * streams of the context (own shadow map each), so one frame's kernels run
  * beside another's; the call still completes in ctx's stream order.  0 = auto
- * (RTM_LANES from the environment, else 3 for frames of 1 Mpixel up to
- * 3840x2160, 1 otherwise);
+ * (RTM_LANES from the environment, else 2 for frames of 1 Mpixel and up,
+ * 1 below);
  * 1 = strictly one frame after another; at most 8.  With several lanes the
  * kernel durations of rtm_ctx_kernel_ms_history overlap (each is the kernel's
  * time beside the other lanes).  rtm_ctx_last_lanes: lanes the last
