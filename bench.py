@@ -74,6 +74,8 @@ def parse():
                     help="tile-gather mode: what is rendered and gathered")
     ap.add_argument("--tile-gather-steps", type=int, default=200,
                     help="frames of the secondary tile-gather measurement (0 = skip it)")
+    ap.add_argument("--tile-gather-timeout-s", type=float, default=240.0,
+                    help="watchdog of the secondary tile-gather measurement (group set-up included)")
     # The clocks ramp for tens of ms after an idle GPU: a time-based pre-roll before the
     # counted warmup makes a short --steps/--warmup run read the steady state.
     ap.add_argument("--preroll-ms", type=float, default=300.0)
@@ -83,6 +85,30 @@ def parse():
 
 
 FORMATS = {"rgba32f": 0, "rgba8": 1}
+
+
+class _Watchdog:
+    """Bounds a secondary measurement: if it has not finished after `seconds`, rank 0
+    prints the line it already holds (the secondary field marked as timed out) and
+    every rank leaves with status 0, so a stalled peer can never cost the headline."""
+
+    def __init__(self, seconds: float, res: dict | None, field: str):
+        import threading
+        self._t = threading.Timer(seconds, self._fire, args=(res, field, seconds))
+        self._t.daemon = True
+        self._t.start()
+
+    @staticmethod
+    def _fire(res, field, seconds):
+        if res is not None:
+            res[field] = {"error": f"watchdog: not finished after {seconds:.0f} s"}
+            print(json.dumps(res), flush=True)
+        sys.stderr.write(f"bench.py: {field} watchdog fired after {seconds:.0f} s\n")
+        sys.stderr.flush()
+        os._exit(0)
+
+    def cancel(self):
+        self._t.cancel()
 
 
 def tile_gather(rtm, lib, ctx, group, world, rank, dist, tdev, c_scenes, eye, shadow, W, H, K, flags, fmt, steps,
@@ -336,7 +362,10 @@ def main():
     scenes = [distinct[i % n_distinct] for i in range(total)]
     c_distinct = [s.to_c() for s in distinct]
     c_scenes = [c_distinct[i % n_distinct] for i in range(total)]
-    group = make_group(rtm, world, rank, local, dist, a.dist_backend) if (tile_mode or a.tile_gather_steps) else None
+    # the RCCL group of the tile-partitioned frame: up front when it is the primary
+    # measurement; for the secondary `tile_gather` field only after the headline frames
+    # (a group that cannot be formed must never cost the headline line)
+    group = make_group(rtm, world, rank, local, dist, a.dist_backend) if tile_mode else None
 
     # a ring of output frames (a renderer's swap chain): consecutive frames write
     # different buffers, so the library may run them side by side (rtm_api.cpp
@@ -493,25 +522,6 @@ def main():
                      "note": "RTM_FLAG_FUSED_SHADOW (shadow texels evaluated on demand in the eye pass, "
                              "bit-identical image); secondary measurement, not the headline value"}
 
-    # Secondary: the tile-partitioned, gathered frame (strong scaling) in RGBA f32 and RGBA8
-    tile = None
-    if not tile_mode and a.tile_gather_steps > 0:
-        tile = {}
-        tg_scenes = [scene_for(i) for i in range(min(total, 64))]
-        tg_c = [s.to_c() for s in tg_scenes]
-        # every band count renders the same algorithm: each band evaluates the shadow
-        # texels it reads (N = 1 included, so the N = 1 figure is the strong-scaling base)
-        tflags = cfg["flags"] | rtm.abi.RTM_FLAG_FUSED_SHADOW
-        for name, fmt in FORMATS.items():
-            try:
-                tile[name] = tile_gather(rtm, lib, ctx, group, world, rank, dist, tdev, tg_c, eye, shadow, W, H, K,
-                                         tflags, fmt, a.tile_gather_steps, min(20, a.tile_gather_steps))
-            except Exception as ex:  # a failed secondary measurement must not lose the headline line
-                tile[name] = {"error": str(ex)[:300]}
-                break
-    if group is not None:
-        group.close()
-
     pipe_ms = None
     if pipelined:
         # sampled launches j = 0, stride, 2*stride, ...: j = 0 is the prologue shadow pass,
@@ -523,10 +533,7 @@ def main():
         avg_sh = sum(sh_ms) / max(len(sh_ms), 1)
         avg_eye = sum(eye_ms) / max(len(eye_ms), 1)
 
-    host = None
-    if rank == 0 and world == 1 and not a.no_host_output and a.config == 3:
-        host = host_output(rtm, scenes[0], eye, shadow, W, H, K, cfg["flags"])
-
+    res = None
     if rank == 0:
         rows = shard.row_band(H, world, rank) if tile_mode else (0, H)
         pixels = W * H * nS * (1 if tile_mode else world)
@@ -605,12 +612,47 @@ def main():
             "one_lane": one_lane,
             "preroll": preroll,
             "alt_fused_shadow": alt_fused,
-            "tile_gather": tg_primary if tile_mode else tile,
-            "host_output": host,
+            "tile_gather": tg_primary if tile_mode else None,
+            "host_output": None,
             "parity": ("bit-exact vs CPU oracle (tests/test_gpu_parity.py)" if a.config <= 5
                        else "bit-exact vs CPU oracle (tests/test_raytrace.py)" if a.config <= 8
                        else "bit-exact vs CPU oracle (tests/test_general_march.py)"),
         }
+
+    # Secondary: the tile-partitioned, gathered frame (strong scaling) in RGBA f32 and RGBA8
+    tile = None
+    if not tile_mode and a.tile_gather_steps > 0:
+        tile = {}
+        # a watchdog for the secondary measurement: RCCL over several ranks is exercised
+        # here for the first time in a run; if it stalls, rank 0 still prints the line
+        watchdog = _Watchdog(a.tile_gather_timeout_s, res, "tile_gather")
+        try:
+            group = make_group(rtm, world, rank, local, dist, a.dist_backend)
+        except Exception as ex:
+            tile["error"] = f"group: {str(ex)[:300]}"
+        tg_scenes = [scene_for(i) for i in range(min(total, 64))]
+        tg_c = [s.to_c() for s in tg_scenes]
+        # every band count renders the same algorithm: each band evaluates the shadow
+        # texels it reads (N = 1 included, so the N = 1 figure is the strong-scaling base)
+        tflags = cfg["flags"] | rtm.abi.RTM_FLAG_FUSED_SHADOW
+        for name, fmt in FORMATS.items():
+            if "error" in tile:
+                break
+            try:
+                tile[name] = tile_gather(rtm, lib, ctx, group, world, rank, dist, tdev, tg_c, eye, shadow, W, H, K,
+                                         tflags, fmt, a.tile_gather_steps, min(20, a.tile_gather_steps))
+            except Exception as ex:  # a failed secondary measurement must not lose the headline line
+                tile[name] = {"error": str(ex)[:300]}
+                break
+        watchdog.cancel()
+        if res is not None:
+            res["tile_gather"] = tile
+    if group is not None:
+        group.close()
+
+    if rank == 0:
+        if world == 1 and not a.no_host_output and a.config == 3:
+            res["host_output"] = host_output(rtm, scenes[0], eye, shadow, W, H, K, cfg["flags"])
         if world == 1 and not a.no_cpu_baseline:
             what = ("Scene A-bench frame 100" if a.config in (2, 3, 4) else cfg["desc"].split(", ", 1)[1])
             res["cpu_baseline"] = cpu_baseline(s0, eye, shadow, W, H, K, flags, a.cpu_threads, what)

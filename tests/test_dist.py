@@ -122,3 +122,19 @@ def test_bench_frames_gloo_rehearsal_world2_carries_tile_gather():
     assert res["frames_per_step"] == 32  # auto: 64 Mpixel worth of 1920x1080 frames
     assert set(res["tile_gather"]) == {"rgba32f", "rgba8"}
     assert all(v["value"] > 0 for v in res["tile_gather"].values())
+
+
+def test_bench_watchdog_prints_the_line_and_exits_cleanly():
+    """bench.py's secondary-measurement watchdog: when it fires, rank 0 prints the
+    line it holds (the secondary field marked) and the process exits with status 0."""
+    import json
+    import subprocess
+    import sys
+    code = ("import sys, time; sys.path.insert(0, %r); import bench; "
+            "bench._Watchdog(0.2, {'value': 1.0, 'tile_gather': None}, 'tile_gather'); time.sleep(30)" % ROOT)
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stderr
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    assert d["value"] == 1.0 and "watchdog" in d["tile_gather"]["error"]
