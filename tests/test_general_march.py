@@ -81,3 +81,57 @@ def test_tilted_sun_batched_sequence(rtm, scenes, gpu_ctx):
             assert bits_equal(o.cpu().numpy(), rtm.render_frame(s, eye, sh, w, h, k))
     finally:
         gpu_ctx.set_batch(0)
+
+
+def _random_sun(rng, scenes):
+    """A seeded orthographic sun with x/y motion in any direction (signs, steep
+    and shallow angles) and an offset position."""
+    def cross(a, b):
+        return (a[1] * b[2] - a[2] * b[1], a[2] * b[0] - a[0] * b[2], a[0] * b[1] - a[1] * b[0])
+    while True:
+        v = rng.uniform(-1.0, 1.0, 3)
+        v[2] = rng.choice([-1.0, 1.0]) * rng.uniform(0.3, 1.0)
+        if abs(v[0]) > 1e-3 or abs(v[1]) > 1e-3:
+            break
+    d = scenes.normalize(tuple(float(x) for x in v))
+    s = scenes.normalize(cross((0.0, 1.0, 0.0), d))
+    u = cross(d, s)
+    pos = tuple(float(x) for x in rng.uniform(-0.3, 0.3, 3))
+    return scenes.Camera(scenes.ORTHOGONAL, pos, d, u, s)
+
+
+def _random_patches(rng, scenes, n):
+    return [scenes.Bilinear(scenes.Linear(*map(float, rng.uniform(-0.5, 2.5, 2))),
+                            scenes.Linear(*map(float, rng.uniform(-0.5, 2.5, 2)))) for _ in range(n)]
+
+
+def _frame_and_map(rtm, gpu_ctx, sc, eye, sh, w, h, k):
+    import ctypes
+    import torch
+    out = torch.empty((h, w, 4), dtype=torch.float32, device="cuda")
+    torch.cuda.synchronize()
+    gpu_ctx.render_async(sc, eye, sh, w, h, k, 0, out.data_ptr())
+    gpu_ctx.synchronize()
+    hip = ctypes.CDLL("libamdhip64.so")
+    smap = np.empty((h, w), np.float64)
+    assert hip.hipMemcpy(smap.ctypes.data_as(ctypes.c_void_p), ctypes.c_void_p(gpu_ctx.shadow_map_ptr()),
+                         ctypes.c_size_t(8 * w * h), 2) == 0
+    return out.cpu().numpy(), smap
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(8))
+def test_step_compaction_random_suns(rtm, oracle, scenes, gpu_ctx, seed):
+    """The general march under seeded suns (x/y motion in any direction), patch
+    sets of 1-3 patches and step counts that are not multiples of the 4-step
+    chunk: frame and shadow map bit-equal to the oracle."""
+    rng = np.random.default_rng(0x2018 + seed)
+    sh = _random_sun(rng, scenes)
+    k = int(rng.choice([1, 2, 3, 5, 7, 64, 131]))
+    w, h = int(rng.integers(100, 420)), int(rng.integers(3, 230))
+    sc = scenes.closely_orbiting_sphere(int(rng.integers(0, 300)), _random_patches(rng, scenes, int(rng.integers(1, 4))))
+    eye = scenes.eye_camera()
+    want = oracle.render(sc, eye, sh, w, h, k, 0, nthreads=NT, want_shadow=True, want_stats=True)
+    got, smap = _frame_and_map(rtm, gpu_ctx, sc, eye, sh, w, h, k)
+    assert bits_equal(smap, want["shadow"]), first_mismatch(smap, want["shadow"])
+    assert bits_equal(got, want["rgba"]), first_mismatch(got, want["rgba"])
