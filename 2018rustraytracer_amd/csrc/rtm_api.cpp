@@ -1073,14 +1073,22 @@ int ensure_lanes(rtm_ctx* ctx, int L) {
 // are short and the host's per-frame launches bound the rate (512x512: 12 Gpix/s
 // one frame per launch, 43 at 16; 1920x1080 on 3 lanes: 123 at 1, 181 at 4,
 // tools/probes/batch_probe.py), so 8 Mpixel worth of frames (at most 16) share
-// one launch per pass (rtm_ctx_set_batch / RTM_BATCH override; 1 = one frame per launch).
-int frame_batch(int32_t req, int32_t W, int32_t H) {
+// one launch per pass.  From 4 Mpixel up, sphere/patch frames batch to 32
+// Mpixel: a 3840x2160 launch of 4 frames runs each frame's shadow pass in 13.4
+// instead of 16.2 us and its eye pass in 21.7 instead of 25.1 (one ramp and tail
+// per 4 frames), 244 -> 251 Gpix/s on 2 lanes; 7680x4320 stays at 1
+// (profiles/r02_ab_batch.txt).  Frames with ray-traced primitives or SDFs keep the
+// 8 Mpixel rule: their batched eye pass has no per-wave primitive cull (config 6
+// at 4 frames per launch: 141 vs 90 us).  rtm_ctx_set_batch / RTM_BATCH override
+// (1 = one frame per launch).
+int frame_batch(int32_t req, int32_t W, int32_t H, bool prims) {
     static const int env = [] {
         const char* e = getenv("RTM_BATCH");
         return e ? atoi(e) : 0;
     }();
     const int64_t px = (int64_t)W * H;
-    int B = req > 0 ? req : env > 0 ? env : (int)std::max<int64_t>(1, std::min<int64_t>(16, (8LL << 20) / px));
+    const int64_t target = (!prims && px >= (4LL << 20)) ? (32LL << 20) : (8LL << 20);
+    int B = req > 0 ? req : env > 0 ? env : (int)std::max<int64_t>(1, std::min<int64_t>(16, target / px));
     return std::max(1, std::min(B, 64));
 }
 
@@ -1411,7 +1419,10 @@ int rtm_render_frames_async(rtm_ctx* ctx, int32_t n_frames, const rtm_scene* sce
         // so the GPU starts on frame 0 while the host prepares frame 1 (building all
         // frames first left the GPU idle for the whole build)
         DeviceGuard g(ctx->device);
-        int B = std::min<int32_t>(frame_batch(ctx->batch_req, width, height), n_frames);
+        bool prims = false;  // ray-traced primitives or SDFs in any frame
+        for (int32_t i = 0; i < n_frames && !prims; ++i)
+            prims = scenes[i].n_circle_planes > 0 || scenes[i].n_capped_cylinders > 0 || scenes[i].n_sdfs > 0;
+        int B = std::min<int32_t>(frame_batch(ctx->batch_req, width, height, prims), n_frames);
         int L = frame_lanes(ctx->lanes_req, n_frames, width, height, out_rgba_dev, B);
         int rc = RTM_OK;
         if (L > 1) {  // fork: the lanes start after the context stream's earlier work

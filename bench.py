@@ -236,8 +236,10 @@ def host_output(rtm, scene, eye, shadow, W, H, K, flags, frames=8):
     return res
 
 
-def _latest_traffic(cfg_id: int, kernel: str):
-    """HBM bytes per launch from the newest committed PMC summary (tools/profile.sh)."""
+def _latest_traffic(cfg_id: int, kernel: str, frames_per_launch: int = 1):
+    """HBM bytes per launch from the newest committed PMC summary (tools/profile.sh)
+    whose launches held `frames_per_launch` frames (`frames_per_launch` in the
+    summary, 1 when absent)."""
     import re
 
     def key(f):  # newest round/version first: r01_v12 after r01_v9 (not lexicographic)
@@ -250,7 +252,8 @@ def _latest_traffic(cfg_id: int, kernel: str):
             d = json.load(open(f))
         except Exception:
             continue
-        if d.get("config") == cfg_id and kernel in d.get("kernels", {}):
+        if (d.get("config") == cfg_id and kernel in d.get("kernels", {})
+                and d.get("frames_per_launch", 1) == frames_per_launch):
             return d["kernels"][kernel].get("hbm_bytes_per_launch")
     return None
 
@@ -371,11 +374,15 @@ def main():
     # different buffers, so the library may run them side by side (rtm_api.cpp
     # frame_lanes puts frame i on lane (n-1-i) % L: the ring must be a multiple of L)
     # and batch (several frames per launch, rtm_ctx_set_batch: frames of one launch need
-    # distinct outputs): 48 frames below 8 Mpixel (batches of up to 16 on up to 3 lanes)
+    # distinct outputs; batch b runs on lane (n_batches-1-b) % L, so the ring must be a
+    # multiple of frames-per-launch x lanes): 48 frames (batches of 1-16 on 1-3 lanes;
+    # 25 GB at 7680x4320, of 288 GB)
     lanes_env = int(os.environ.get("RTM_LANES", "0") or 0)
-    n_ring = 12 if lanes_env in (0, 1, 2, 3, 4, 6) else lanes_env * ((12 + lanes_env - 1) // lanes_env)
-    if W * H < (8 << 20):
-        n_ring = max(n_ring, 48 if lanes_env in (0, 1, 2, 3, 4, 6, 8, 12, 16) else 16 * max(lanes_env, 1))
+    batch_env = int(os.environ.get("RTM_BATCH", "0") or 0)
+    n_ring = 48
+    if lanes_env > 0 or batch_env > 0:
+        m = max(lanes_env, 1) * max(batch_env, 1)
+        n_ring = 48 if 48 % m == 0 else m * ((48 + m - 1) // m)
     ring = ([torch.empty((H, W, 4), dtype=torch.float32, device=f"cuda:{local}") for _ in range(n_ring)]
             if not tile_mode else [])
     sequence = not tile_mode and not a.per_frame_calls
@@ -463,6 +470,7 @@ def main():
     # batched launches (rtm_ctx_set_batch: several frames per launch): the events
     # time a launch, i.e. a batch of frames; the per-kernel figures are per frame
     batch = ctx.last_batch() if sequence else 1
+    launch_batch = batch  # frames per launch of the kernels the roofline prices
     if batch > 1:
         sh_ms, eye_ms = [v / batch for v in sh_ms], [v / batch for v in eye_ms]
 
@@ -491,6 +499,7 @@ def main():
         el1 = time.perf_counter() - t1
         sh_ms, eye_ms = ctx.kernel_ms_history((n1 + timing_stride - 1) // timing_stride)
         b1 = ctx.last_batch()
+        launch_batch = b1
         sh_ms, eye_ms = [v / b1 for v in sh_ms], [v / b1 for v in eye_ms]
         ctx.set_lanes(0)
         one_lane = {"value": round(W * H * n1 / el1 / 1e6, 2), "unit": "Mpixels/s", "frames": n1,
@@ -515,6 +524,7 @@ def main():
         barrier()
         el_f = max_over_ranks(time.perf_counter() - t1)
         _, f_eye = ctx.kernel_ms_history((nS + timing_stride - 1) // timing_stride)
+        f_eye = [v / max(ctx.last_batch(), 1) for v in f_eye]  # per frame
         alt_fused = {"value": round(W * H * nS * world / el_f / 1e6, 2), "unit": "Mpixels/s",
                      "ms_per_step": round(el_f / a.steps * 1e3, 5), "ms_per_frame": round(el_f / nS * 1e3, 5),
                      "fused_eye_pass_ms_in_lanes": round(sum(f_eye) / max(len(f_eye), 1), 5),
@@ -560,6 +570,18 @@ def main():
         roof_frame.pop("traffic", None)
         roof_frame["note"] = ("both passes' algorithmic bytes per frame / wall time per frame of the timed region"
                               + (f" ({lanes} lanes)" if lanes > 1 else ""))
+        # the kernel rooflines are per LAUNCH (what rocprofv3 and the PMC passes see): a
+        # launch of B frames (rtm_ctx_set_batch) moves B frames' bytes in its duration
+        nb = max(launch_batch, 1)
+        work_l = {k: {"ops": v["ops"] * nb, "bytes": v["bytes"] * nb} for k, v in work.items()}
+
+        def kroof(kernel, ms_per_frame):
+            r = dict(metrics.roofline(kernel, work_l, ms_per_frame * nb,
+                                      _latest_traffic(a.config, kernel, nb if kernel == "eye_pass" or
+                                                      kernel == "shadow_pass" else 1)))
+            r["frames_per_launch"] = nb
+            return r
+
         if pipelined:
             dom, dom_ms = "frame_pipe", pipe_ms
             roof = metrics.roofline(dom, work, dom_ms, _latest_traffic(a.config, dom))
@@ -567,11 +589,10 @@ def main():
         else:
             dom = "eye_pass" if (fused or avg_eye >= avg_sh) else "shadow_pass"
             dom_ms = avg_eye if dom == "eye_pass" else avg_sh
-            roof = metrics.roofline(dom, work, dom_ms, _latest_traffic(a.config, dom))
+            roof = kroof(dom, dom_ms)
             other = "shadow_pass" if dom == "eye_pass" else "eye_pass"
             other_ms = avg_sh if other == "shadow_pass" else avg_eye
-            roof_other = (metrics.roofline(other, work, other_ms, _latest_traffic(a.config, other))
-                          if other_ms > 0 else None)
+            roof_other = kroof(other, other_ms) if other_ms > 0 else None
         res = {
             "metric": cfg.get("metric", METRIC if a.config <= 5 else METRIC_F1 if a.config <= 7 else METRIC_F4),
             "value": round(value, 2),
