@@ -630,6 +630,7 @@ struct BatchRing {
     hipEvent_t copied[R] = {}, used[R] = {};
     int next = 0;
     DevBuf smaps;  // the batch's shadow maps, B x W x H f64
+    DevBuf rtmask; // per-wave primitive masks of the batch's PERSPECTIVE eye passes (row f-1)
     int device = 0;
     ~BatchRing() {
         int cur = 0;
@@ -1073,21 +1074,20 @@ int ensure_lanes(rtm_ctx* ctx, int L) {
 // are short and the host's per-frame launches bound the rate (512x512: 12 Gpix/s
 // one frame per launch, 43 at 16; 1920x1080 on 3 lanes: 123 at 1, 181 at 4,
 // tools/probes/batch_probe.py), so 8 Mpixel worth of frames (at most 16) share
-// one launch per pass.  From 4 Mpixel up, sphere/patch frames batch to 32
-// Mpixel: a 3840x2160 launch of 4 frames runs each frame's shadow pass in 13.4
-// instead of 16.2 us and its eye pass in 21.7 instead of 25.1 (one ramp and tail
-// per 4 frames), 244 -> 251 Gpix/s on 2 lanes; 7680x4320 stays at 1
-// (profiles/r02_ab_batch.txt).  Frames with ray-traced primitives or SDFs keep the
-// 8 Mpixel rule: their batched eye pass has no per-wave primitive cull (config 6
-// at 4 frames per launch: 141 vs 90 us).  rtm_ctx_set_batch / RTM_BATCH override
+// one launch per pass.  From 4 Mpixel up frames batch to 32 Mpixel: a 3840x2160
+// launch of 4 frames runs each frame's shadow pass in 13.4 instead of 16.2 us and
+// its eye pass in 21.7 instead of 25.1 (one ramp and tail per 4 frames), 244 ->
+// 251 Gpix/s on 2 lanes; ray-traced frames (config 6, with the batched per-wave
+// primitive cull) eye 90 -> 83 us per frame, SDF frames neutral; 7680x4320 stays
+// at 1 (profiles/r02_ab_batch.txt).  rtm_ctx_set_batch / RTM_BATCH override
 // (1 = one frame per launch).
-int frame_batch(int32_t req, int32_t W, int32_t H, bool prims) {
+int frame_batch(int32_t req, int32_t W, int32_t H) {
     static const int env = [] {
         const char* e = getenv("RTM_BATCH");
         return e ? atoi(e) : 0;
     }();
     const int64_t px = (int64_t)W * H;
-    const int64_t target = (!prims && px >= (4LL << 20)) ? (32LL << 20) : (8LL << 20);
+    const int64_t target = px >= (4LL << 20) ? (32LL << 20) : (8LL << 20);
     int B = req > 0 ? req : env > 0 ? env : (int)std::max<int64_t>(1, std::min<int64_t>(16, target / px));
     return std::max(1, std::min(B, 64));
 }
@@ -1182,6 +1182,18 @@ int enqueue_batch(rtm_ctx* ctx, int lane, FrameArgs* fa, const FrameExtra* ex, f
     }
     // a frame without ray-traced primitives in a RT 3 batch: every frame shares the eye camera
     t0.rt_persp = t0.rt ? t0.rt_persp : 0;
+    if (t0.rt && t0.rt_persp && !t0.sdf && eye_wave_cull_on()) {
+        // per-wave primitive masks (rt_cull_batch_kernel) for every frame with primitives,
+        // ceil(W/64) * rows words each; stream-ordered reuse on this lane
+        const size_t nw = (size_t)((fa[0].ey.W + 63) / 64) * (size_t)(fa[0].ey.row_end - fa[0].ey.row_begin);
+        if ((rc = br.rtmask.ensure(sizeof(uint32_t) * nw * (size_t)n, ctx->device))) return rc;
+        for (int k = 0; k < n; ++k)
+            if (ex[k].has_rt) {
+                BatchFrame& bf = *(BatchFrame*)(hb + sizeof(BatchFrame) * (size_t)k);
+                bf.tabs.rtmask = (uint32_t*)br.rtmask.p + nw * (size_t)k;
+            }
+        t0.rtmask = (uint32_t*)br.rtmask.p;
+    }
     t0.fmt = RTM_FORMAT_RGBA32F;
     HIP_TRY(hipStreamWaitEvent(br.copy, br.used[j], 0));  // the device slot is free
     HIP_TRY(hipMemcpyAsync(db, hb, bytes, hipMemcpyHostToDevice, br.copy));
@@ -1419,10 +1431,7 @@ int rtm_render_frames_async(rtm_ctx* ctx, int32_t n_frames, const rtm_scene* sce
         // so the GPU starts on frame 0 while the host prepares frame 1 (building all
         // frames first left the GPU idle for the whole build)
         DeviceGuard g(ctx->device);
-        bool prims = false;  // ray-traced primitives or SDFs in any frame
-        for (int32_t i = 0; i < n_frames && !prims; ++i)
-            prims = scenes[i].n_circle_planes > 0 || scenes[i].n_capped_cylinders > 0 || scenes[i].n_sdfs > 0;
-        int B = std::min<int32_t>(frame_batch(ctx->batch_req, width, height, prims), n_frames);
+        int B = std::min<int32_t>(frame_batch(ctx->batch_req, width, height), n_frames);
         int L = frame_lanes(ctx->lanes_req, n_frames, width, height, out_rgba_dev, B);
         int rc = RTM_OK;
         if (L > 1) {  // fork: the lanes start after the context stream's earlier work

@@ -320,6 +320,8 @@ int launch_eye_pass(const FrameArgs& a, const double* smap, void* out, void* str
 // a batch shares the shapes, flags, tables and kernel variant).
 int launch_shadow_batch(const BatchFrame* dev, int n, const FrameArgs& a0, void* stream);
 int launch_eye_batch(const BatchFrame* dev, int n, const FrameArgs& a0, const DevTabs& t0, void* stream);
+// The eye pass's per-wave primitive cull is on (RTM_EYE_MODE bit 2 clear).
+bool eye_wave_cull_on();
 bool shadow_batchable(const ShadowPart& sh);
 // Stream-ordered copy of host bytes into device memory by kernels whose
 // arguments carry the bytes (<= 3968 per launch), so the host copy is consumed

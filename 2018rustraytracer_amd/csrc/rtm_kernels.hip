@@ -1823,10 +1823,9 @@ __global__ void upload_kernel(const UploadChunk k, uint64_t* __restrict__ dst, i
 // pixels bx*64 .. bx*64+63 of row row_begin + yl), so the cone set-up and the
 // bounding-sphere tests run once per wave instead of on every lane of it.  The
 // same operations, hence the same masks.
-__global__ __launch_bounds__(BLOCK) void rt_cull_kernel(const CamK c, const RtK* __restrict__ rt, int W, int H,
-                                                        int row_begin, int rows, uint32_t* __restrict__ masks) {
+__device__ __forceinline__ void rt_cull_wave(const CamK& c, const RtK* __restrict__ rt, int W, int H, int row_begin,
+                                             int rows, uint32_t* __restrict__ masks, int t) {
     const int gx = (W + TILE_X - 1) / TILE_X;
-    const int t = blockIdx.x * BLOCK + threadIdx.x;
     if (t >= gx * rows) return;
     const int xb = (t % gx) * TILE_X, yi = row_begin + t / gx;
     const RayCone k = ray_cone(c, min(xb, W - 1), min(xb + TILE_X - 1, W - 1), min(yi, H - 1), W, H);
@@ -1839,6 +1838,23 @@ __global__ __launch_bounds__(BLOCK) void rt_cull_kernel(const CamK c, const RtK*
         if (cone_culls(k, c, C, R, cullable)) m &= ~(1u << l);
     }
     masks[t] = m;
+}
+
+__global__ __launch_bounds__(BLOCK) void rt_cull_kernel(const CamK c, const RtK* __restrict__ rt, int W, int H,
+                                                        int row_begin, int rows, uint32_t* __restrict__ masks) {
+    rt_cull_wave(c, rt, W, H, row_begin, rows, masks, blockIdx.x * BLOCK + threadIdx.x);
+}
+
+// rt_cull_kernel for a batch: frame blockIdx.z's masks (frames with ray-traced
+// primitives under a PERSPECTIVE eye get a mask buffer from the host; the others
+// have none and skip).
+__global__ __launch_bounds__(BLOCK) void rt_cull_batch_kernel(CBatch* __restrict__ fr) {
+    CBatch* f = fr + blockIdx.z;
+    uint32_t* masks = f->tabs.rtmask;
+    const RtK* rt = f->tabs.rt;
+    if (!masks || !rt) return;
+    const EyePart& e = *(const EyePart*)&f->a.ey;
+    rt_cull_wave(e.eye, rt, e.W, e.H, e.row_begin, e.row_end - e.row_begin, masks, blockIdx.x * BLOCK + threadIdx.x);
 }
 
 // Timing diagnostic only (RTM_DIAG_EYE=1): the eye pass's stores without its work.
@@ -2403,11 +2419,19 @@ bool shadow_batchable(const ShadowPart& sh) {
     return !use_sep(sh) || (sep_mode(sh) == MARCH_LEAN2 && sep_rows() == 4 && lean_cols() == 2);
 }
 
+bool eye_wave_cull_on() { return !(eye_wide() & 4); }
+
 int launch_eye_batch(const BatchFrame* dev, int n, const FrameArgs& a0, const DevTabs& t0, void* stream) {
     hipStream_t s = (hipStream_t)stream;
     CBatch* fr = (CBatch*)dev;
     const int rows = a0.ey.row_end - a0.ey.row_begin;
     const int wide = eye_wide();
+    if (t0.rtmask) {  // the batch's per-wave primitive masks first (RT 3)
+        const int nw = ((a0.ey.W + TILE_X - 1) / TILE_X) * rows;
+        hipLaunchKernelGGL(rt_cull_batch_kernel, dim3((unsigned)((nw + BLOCK - 1) / BLOCK), 1, (unsigned)n),
+                           dim3(BLOCK), 0, s, fr);
+        if (launched()) return RTM_ERR_HIP;
+    }
     dim3 g = (wide & 1) ? dim3((unsigned)((a0.ey.W + BLOCK - 1) / BLOCK), (unsigned)rows) : grid_for(a0.ey.W, rows);
     g.z = (unsigned)n;
     const bool fused = (a0.ey.flags & RTM_FLAG_FUSED_SHADOW) != 0;

@@ -241,8 +241,8 @@ int rtm_ctx_last_lanes(rtm_ctx* ctx, int32_t* lanes);
  * dimension; each frame's constants come from a table uploaded per batch), so
  * small frames stop paying a launch per pass per frame.  0 = auto (RTM_BATCH
  * from the environment, else as many frames as make 8 Mpixel, at most 16: 16 at
- * 512x512, 4 at 1920x1080; from 4 Mpixel up, frames without ray-traced
- * primitives or SDFs batch to 32 Mpixel: 4 at 3840x2160, 1 at 7680x4320);
+ * 512x512, 4 at 1920x1080; from 4 Mpixel up 32 Mpixel: 4 at 3840x2160, 1 at
+ * 7680x4320);
  * 1 = one frame per launch; at most 64.  Frames with overlapping outputs never share a launch (a repeated output
  * pointer still ends with the later frame).  Batches are spread over the lanes.  Kernel durations of
  * rtm_ctx_kernel_ms_history are then per launch, i.e. per batch;

@@ -359,3 +359,31 @@ def test_viewport_outliving_its_context(rtm, scenes):
     with pytest.raises(abi.RtmError):
         vp.zBuffer()
     vp.close()
+
+
+@pytest.mark.parametrize("batch,lanes", [(3, 1), (4, 2), (16, 1)])
+def test_batched_perspective_raytraced_frames(rtm, scenes, gpu_ctx, batch, lanes):
+    """Batched launches of PERSPECTIVE-eye frames with ray-traced primitives: the
+    per-wave primitive masks are computed per frame of the batch
+    (rt_cull_batch_kernel) and every frame == rtm_render bit for bit, including
+    frames without primitives and with spheres only inside the same batch."""
+    import torch
+    w, h, k = 512, 384, 64
+    eye, sh = scenes.perspective_eye_camera(), scenes.shadow_camera()
+    frames = [scenes.raytracing_plane0(), scenes.scene_r_bench(), scenes.raytracing_plane0(True),
+              scenes.perspective_simple1(), scenes.scene_r_bench(), scenes.raytracing_plane0(),
+              scenes.perspective_simple2(), scenes.raytracing_plane0(True)]
+    outs = [torch.empty((h, w, 4), dtype=torch.float32, device="cuda") for _ in frames]
+    try:
+        gpu_ctx.set_batch(batch)
+        gpu_ctx.set_lanes(lanes)
+        torch.cuda.synchronize()
+        gpu_ctx.render_frames_async(frames, eye, sh, w, h, k, scenes.RAYTRACING_FLAGS, [o.data_ptr() for o in outs])
+        gpu_ctx.synchronize()
+        assert gpu_ctx.last_batch() == min(batch, len(frames))
+        for s, o in zip(frames, outs):
+            want = rtm.render_frame(s, eye, sh, w, h, k, scenes.RAYTRACING_FLAGS)
+            assert bits_equal(o.cpu().numpy(), want)
+    finally:
+        gpu_ctx.set_lanes(0)
+        gpu_ctx.set_batch(0)
