@@ -15,6 +15,7 @@
 #include <memory>
 #include <string>
 #include <thread>
+#include <limits>
 #include <vector>
 
 #include "rtm_encode.h"
@@ -357,10 +358,34 @@ void build_extra(const rtm_scene* scene, const rtm_camera* eye, int32_t W, int32
 // positive, +inf or NaN): r NaN -> NaN (both tests always pass), r < 0 -> -1 (both
 // always fail for non-NaN s), r = +inf -> +inf; otherwise a search over the ordered
 // bit patterns of [+0, +inf).
+// The boundary is searched first next to r*r (sqrt(fl(r*r)) is within an ulp or
+// so of r: a few steps), which the per-frame host build of a ray-traced frame pays
+// per circle plane; any start gives the same boundary (the set {s : sqrt(s) <= r}
+// is a prefix of the ordered bit patterns), and a start that needs more than 64
+// steps falls back to the full bisection.
 double sqrt_le_threshold(double r) {
     if (r != r) return r;
     if (r < 0.0) return -1.0;
     if (std::sqrt(INFINITY) <= r) return INFINITY;
+    {
+        double g = r * r;
+        uint64_t b;
+        if (!(g < INFINITY)) g = std::numeric_limits<double>::max();
+        std::memcpy(&b, &g, sizeof b);
+        auto ok = [r](uint64_t bits) {
+            double v;
+            std::memcpy(&v, &bits, sizeof v);
+            return std::sqrt(v) <= r;
+        };
+        int n = 0;
+        while (n < 64 && !ok(b)) --b, ++n;                                // b = +0 is always ok
+        while (n < 64 && b + 1u < 0x7FF0000000000000ull && ok(b + 1u)) ++b, ++n;
+        if (n < 64) {
+            double t;
+            std::memcpy(&t, &b, sizeof t);
+            return t;
+        }
+    }
     uint64_t lo = 0u, hi = 0x7FF0000000000000ull;  // sqrt(+0) <= r (r >= +-0), sqrt(+inf) > r
     while (hi - lo > 1u) {
         const uint64_t mid = lo + (hi - lo) / 2u;
@@ -663,6 +688,11 @@ struct rtm_ctx {
     hipStream_t stream = nullptr;
     std::vector<std::unique_ptr<Lane>> lanes;  // extra lanes 1..n (lane 0 is the context itself)
     hipEvent_t fork = nullptr;                 // lanes wait on the context stream's earlier work
+    // lane stagger (rtm_render_frames_async): recorded after the first launch's shadow
+    // pass; the second lane's first launch waits for it, so one lane's shadow pass runs
+    // beside the other's eye pass instead of both lanes running the same pass at once
+    hipEvent_t stagger = nullptr;
+    bool stagger_arm = false;
     int32_t lanes_req = 0;                     // rtm_ctx_set_lanes (0 = auto)
     int32_t lanes_last = 0;                    // lanes of the last frame-sequence call
     int32_t batch_req = 0;                     // rtm_ctx_set_batch (0 = auto)
@@ -1004,6 +1034,10 @@ int enqueue_frame(rtm_ctx* ctx, FrameArgs& a, const FrameExtra* x, void* out_dev
         ctx->smap_h = a.sh.H;
         if (slot) HIP_TRY(hipEventRecord(slot->ev[0], s));
         if ((rc = launch_shadow_pass(a, smap, s, stats))) return fail(rc, "shadow pass launch failed");
+        if (ctx->stagger_arm) {
+            HIP_TRY(hipEventRecord(ctx->stagger, s));
+            ctx->stagger_arm = false;
+        }
         if (slot) HIP_TRY(hipEventRecord(slot->ev[1], s));
         ctx->have_shadow_pass = true;
         ctx->last_smap = smap;
@@ -1028,9 +1062,9 @@ int enqueue_frame(rtm_ctx* ctx, FrameArgs& a, const FrameExtra* x, void* out_dev
 // config 3 from 40.1 to 33.3 us per frame (3 lanes 33.9), config 2 from 13.7 to
 // 9.5 (3 lanes 10.7) and 7680x4320 from 134 to 128 (with the 8-byte map a second
 // lane only added cache pressure there: 133 -> 157 us) (profiles/r02_ab_lanes.txt);
-// below 1 Mpixel the host's launch rate is the limit and switching
-// streams costs more than the overlap gains (512x512: 19.2 -> 14.2 Gpix/s with
-// 3 lanes) (tools/probes/two_ctx.py).  RTM_LANES=n overrides.
+// at 512x512 with 64 frames per launch 60 -> 80 Gpix/s (one frame per launch,
+// round 1, lanes had lost there: the host's launch rate was the limit).  RTM_LANES=n
+// overrides.
 // Frame i goes to lane (n-1-i) % L, so the last frame runs on lane 0 and the
 // context's shadow map holds its shadow pass, as on one lane.  Lanes stay at 1
 // when two frames of different lanes write overlapping output.
@@ -1039,8 +1073,7 @@ int frame_lanes(int32_t req, int32_t n, int32_t W, int32_t H, float* const* out,
         const char* e = getenv("RTM_LANES");
         return e ? atoi(e) : 0;
     }();
-    const int64_t px = (int64_t)W * H;
-    int L = req > 0 ? req : env > 0 ? env : (px >= (1LL << 20) ? 2 : 1);
+    int L = req > 0 ? req : env > 0 ? env : 2;
     const int32_t nb = (n + B - 1) / B;  // batches of B frames; batch b runs on lane (nb-1-b) % L
     if (L > 8) L = 8;
     if (L > nb) L = nb;
@@ -1074,7 +1107,10 @@ int ensure_lanes(rtm_ctx* ctx, int L) {
 // are short and the host's per-frame launches bound the rate (512x512: 12 Gpix/s
 // one frame per launch, 43 at 16; 1920x1080 on 3 lanes: 123 at 1, 181 at 4,
 // tools/probes/batch_probe.py), so 8 Mpixel worth of frames (at most 16) share
-// one launch per pass.  From 4 Mpixel up frames batch to 32 Mpixel: a 3840x2160
+// one launch per pass; below 1 Mpixel 32 Mpixel worth, at most 64: main()'s own
+// scene (raytracingPlane0, 512x512) 50.7 Gpix/s at 16 frames per launch on one
+// lane, 80 at 64 on two lanes (profiles/r02_ab_batch.txt).  From 4 Mpixel up
+// frames batch to 32 Mpixel: a 3840x2160
 // launch of 4 frames runs each frame's shadow pass in 13.4 instead of 16.2 us and
 // its eye pass in 21.7 instead of 25.1 (one ramp and tail per 4 frames), 244 ->
 // 251 Gpix/s on 2 lanes; ray-traced frames (config 6, with the batched per-wave
@@ -1087,8 +1123,10 @@ int frame_batch(int32_t req, int32_t W, int32_t H) {
         return e ? atoi(e) : 0;
     }();
     const int64_t px = (int64_t)W * H;
-    const int64_t target = px >= (4LL << 20) ? (32LL << 20) : (8LL << 20);
-    int B = req > 0 ? req : env > 0 ? env : (int)std::max<int64_t>(1, std::min<int64_t>(16, target / px));
+    // below 1 Mpixel 32 Mpixel worth, at most 64 (512x512: 64 frames per launch)
+    const int64_t target = (px >= (4LL << 20) || px < (1LL << 20)) ? (32LL << 20) : (8LL << 20);
+    const int64_t cap = px < (1LL << 20) ? 64 : 16;
+    int B = req > 0 ? req : env > 0 ? env : (int)std::max<int64_t>(1, std::min<int64_t>(cap, target / px));
     return std::max(1, std::min(B, 64));
 }
 
@@ -1195,14 +1233,27 @@ int enqueue_batch(rtm_ctx* ctx, int lane, FrameArgs* fa, const FrameExtra* ex, f
         t0.rtmask = (uint32_t*)br.rtmask.p;
     }
     t0.fmt = RTM_FORMAT_RGBA32F;
-    HIP_TRY(hipStreamWaitEvent(br.copy, br.used[j], 0));  // the device slot is free
-    HIP_TRY(hipMemcpyAsync(db, hb, bytes, hipMemcpyHostToDevice, br.copy));
-    HIP_TRY(hipEventRecord(br.copied[j], br.copy));
-    HIP_TRY(hipStreamWaitEvent(s, br.copied[j], 0));
+    static const bool copy_stream = [] {  // RTM_BATCH_COPY=stream: upload on the lane's own stream (A/B)
+        const char* e = getenv("RTM_BATCH_COPY");
+        return !(e && std::string(e) == "stream");
+    }();
+    if (copy_stream) {
+        HIP_TRY(hipStreamWaitEvent(br.copy, br.used[j], 0));  // the device slot is free
+        HIP_TRY(hipMemcpyAsync(db, hb, bytes, hipMemcpyHostToDevice, br.copy));
+        HIP_TRY(hipEventRecord(br.copied[j], br.copy));
+        HIP_TRY(hipStreamWaitEvent(s, br.copied[j], 0));
+    } else {  // in stream order after the lane's earlier batches (which read the older slots)
+        HIP_TRY(hipMemcpyAsync(db, hb, bytes, hipMemcpyHostToDevice, s));
+        HIP_TRY(hipEventRecord(br.copied[j], s));
+    }
     TimingSlot* slot = next_slot(ctx);
     if (!fused) {
         if (slot) HIP_TRY(hipEventRecord(slot->ev[0], s));
         if ((rc = launch_shadow_batch((const BatchFrame*)db, n, fa[0], s))) return fail(rc, "batched shadow pass failed");
+        if (ctx->stagger_arm) {
+            HIP_TRY(hipEventRecord(ctx->stagger, s));
+            ctx->stagger_arm = false;
+        }
         if (slot) HIP_TRY(hipEventRecord(slot->ev[1], s));
         ctx->have_shadow_pass = true;
         ctx->last_smap = (const double*)((const char*)br.smaps.p + map_bytes * (size_t)(n - 1));
@@ -1294,6 +1345,7 @@ void rtm_ctx_destroy(rtm_ctx* ctx) {
         ctx->lanes.clear();
         ctx->batch.reset();
         if (ctx->fork) (void)hipEventDestroy(ctx->fork);
+        if (ctx->stagger) (void)hipEventDestroy(ctx->stagger);
         for (auto& sl : ctx->ring)
             for (auto& e : sl.ev)
                 if (e) (void)hipEventDestroy(e);
@@ -1444,9 +1496,29 @@ int rtm_render_frames_async(rtm_ctx* ctx, int32_t n_frames, const rtm_scene* sce
         const int32_t nb = (n_frames + B - 1) / B;
         std::vector<FrameArgs> fa((size_t)B);
         std::vector<FrameExtra> fx((size_t)B);
+        // RTM_STAGGER=1 (A/B only): the second lane starts after the first lane's first
+        // shadow pass, so one lane's shadow pass runs beside the other's eye pass.  Off by
+        // default: the lanes do better in step at 3840x2160 (262 vs 254 Gpix/s: a shadow
+        // pass beside the other lane's eye-pass store stream waits longer on its loads)
+        // and at 512x512 (80 vs 68); +3 % at 1920x1080 (profiles/r02_ab_batch.txt)
+        static const bool stagger_on = [] {
+            const char* e = getenv("RTM_STAGGER");
+            return e && atoi(e) != 0;
+        }();
+        bool stagger = stagger_on && L > 1 && !ctx->stagger_arm;
+        if (stagger && !ctx->stagger) HIP_TRY(hipEventCreateWithFlags(&ctx->stagger, hipEventDisableTiming));
         for (int32_t b = 0; b < nb && !rc; ++b) {
             const int32_t i0 = b * B, nf = std::min(B, n_frames - i0);
             const int lane = (nb - 1 - b) % L;
+            if (stagger && b == 0) ctx->stagger_arm = true;  // the first launch records it after its shadow pass
+            if (stagger && b == 1) {
+                ctx->stagger_arm = false;
+                hipStream_t ls = lane > 0 ? ctx->lanes[(size_t)lane - 1]->stream : ctx->stream;
+                if (hipStreamWaitEvent(ls, ctx->stagger, 0) != hipSuccess) {
+                    rc = fail(RTM_ERR_HIP, "lane stagger wait failed");
+                    break;
+                }
+            }
             for (int32_t k = 0; k < nf && !rc; ++k) {
                 rc = build_frame(fa[(size_t)k], &scenes[i0 + k], eye, shadow, width, height, march_steps, flags);
                 if (!rc) build_extra(&scenes[i0 + k], eye, width, height, fx[(size_t)k]);
@@ -1485,6 +1557,7 @@ int rtm_render_frames_async(rtm_ctx* ctx, int32_t n_frames, const rtm_scene* sce
                 k = e;
             }
         }
+        ctx->stagger_arm = false;
         // join every lane (also after an error, so the context stream still covers what
         // was enqueued); the first error, of the frames or of a join, is returned
         const std::string frame_err = rc ? g_last_error : std::string();
