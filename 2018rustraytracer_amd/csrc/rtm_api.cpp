@@ -1073,7 +1073,7 @@ int frame_lanes(int32_t req, int32_t n, int32_t W, int32_t H, float* const* out,
         const char* e = getenv("RTM_LANES");
         return e ? atoi(e) : 0;
     }();
-    int L = req > 0 ? req : env > 0 ? env : 2;
+    int L = req > 0 ? req : env > 0 ? env : ((int64_t)W * H >= (16LL << 20) ? 3 : 2);
     const int32_t nb = (n + B - 1) / B;  // batches of B frames; batch b runs on lane (nb-1-b) % L
     if (L > 8) L = 8;
     if (L > nb) L = nb;
@@ -1103,28 +1103,30 @@ int ensure_lanes(rtm_ctx* ctx, int L) {
     return RTM_OK;
 }
 
-// Frames per launch of a frame sequence: below 8 Mpixel a frame's two kernels
-// are short and the host's per-frame launches bound the rate (512x512: 12 Gpix/s
-// one frame per launch, 43 at 16; 1920x1080 on 3 lanes: 123 at 1, 181 at 4,
-// tools/probes/batch_probe.py), so 8 Mpixel worth of frames (at most 16) share
-// one launch per pass; below 1 Mpixel 32 Mpixel worth, at most 64: main()'s own
-// scene (raytracingPlane0, 512x512) 50.7 Gpix/s at 16 frames per launch on one
-// lane, 80 at 64 on two lanes (profiles/r02_ab_batch.txt).  From 4 Mpixel up
-// frames batch to 32 Mpixel: a 3840x2160
-// launch of 4 frames runs each frame's shadow pass in 13.4 instead of 16.2 us and
-// its eye pass in 21.7 instead of 25.1 (one ramp and tail per 4 frames), 244 ->
-// 251 Gpix/s on 2 lanes; ray-traced frames (config 6, with the batched per-wave
-// primitive cull) eye 90 -> 83 us per frame, SDF frames neutral; 7680x4320 stays
-// at 1 (profiles/r02_ab_batch.txt).  rtm_ctx_set_batch / RTM_BATCH override
-// (1 = one frame per launch).
+// Frames per launch of a frame sequence (profiles/r02_ab_batch.txt).  One frame
+// per launch leaves small frames bound by the host's per-frame launches
+// (512x512: 12 Gpix/s at one frame per launch, 43 at 16; 1920x1080: 123 at 1, 181
+// at 4, tools/probes/batch_probe.py), and a big frame's two kernels pay a ramp and
+// a tail each.  Auto: below 1 Mpixel 32 Mpixel worth of frames, at most 64
+// (main()'s own scene, raytracingPlane0 at 512x512: 50.7 Gpix/s at 16 on one
+// lane, 80 at 64 on two); 1-4 Mpixel 8 Mpixel worth, at most 16 (1920x1080: 4;
+// 8 and 16 were no faster); 4-16 Mpixel 32 Mpixel worth (3840x2160: 4 frames, each
+// frame's shadow pass 13.4 instead of 16.2 us, its eye pass 21.7 instead of 25.1,
+// 244 -> 251-256 Gpix/s; ray-traced frames with the batched per-wave primitive cull
+// eye 90 -> 83 us per frame; SDF frames neutral); from 16 Mpixel 64 Mpixel worth
+// (7680x4320: 2 frames on 3 lanes, config 4 260 -> 270-273 Gpix/s in three runs,
+// config 5 neutral).  rtm_ctx_set_batch / RTM_BATCH override (1 = one frame per
+// launch).
 int frame_batch(int32_t req, int32_t W, int32_t H) {
     static const int env = [] {
         const char* e = getenv("RTM_BATCH");
         return e ? atoi(e) : 0;
     }();
     const int64_t px = (int64_t)W * H;
-    // below 1 Mpixel 32 Mpixel worth, at most 64 (512x512: 64 frames per launch)
-    const int64_t target = (px >= (4LL << 20) || px < (1LL << 20)) ? (32LL << 20) : (8LL << 20);
+    // below 1 Mpixel 32 Mpixel worth, at most 64 (512x512: 64 frames per launch);
+    // from 16 Mpixel 64 Mpixel worth (7680x4320: 2 frames per launch, on 3 lanes)
+    const int64_t target = px >= (16LL << 20) ? (64LL << 20)
+                           : (px >= (4LL << 20) || px < (1LL << 20)) ? (32LL << 20) : (8LL << 20);
     const int64_t cap = px < (1LL << 20) ? 64 : 16;
     int B = req > 0 ? req : env > 0 ? env : (int)std::max<int64_t>(1, std::min<int64_t>(cap, target / px));
     return std::max(1, std::min(B, 64));

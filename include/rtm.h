@@ -228,7 +228,7 @@ int rtm_ctx_kernel_ms_history(rtm_ctx* ctx, float* shadow_pass_ms, float* eye_pa
 /* Lanes of rtm_render_frames_async: independent frames spread over `lanes`
  * streams of the context (own shadow map each), so one frame's kernels run
  * beside another's; the call still completes in ctx's stream order.  0 = auto
- * (RTM_LANES from the environment, else 2);
+ * (RTM_LANES from the environment, else 2; 3 from 16 Mpixel up);
  * 1 = strictly one frame after another; at most 8.  With several lanes the
  * kernel durations of rtm_ctx_kernel_ms_history overlap (each is the kernel's
  * time beside the other lanes).  rtm_ctx_last_lanes: lanes the last
@@ -241,7 +241,8 @@ int rtm_ctx_last_lanes(rtm_ctx* ctx, int32_t* lanes);
  * small frames stop paying a launch per pass per frame.  0 = auto (RTM_BATCH
  * from the environment, else as many frames as make 32 Mpixel below 1 Mpixel
  * (at most 64: 64 at 512x512), 8 Mpixel from 1 to 4 Mpixel (at most 16: 4 at
- * 1920x1080) and 32 Mpixel from 4 Mpixel up (4 at 3840x2160, 1 at 7680x4320));
+ * 1920x1080), 32 Mpixel from 4 Mpixel up (4 at 3840x2160) and 64 Mpixel from
+ * 16 Mpixel up (2 at 7680x4320));
  * 1 = one frame per launch; at most 64.  Frames with overlapping outputs never share a launch (a repeated output
  * pointer still ends with the later frame).  Batches are spread over the lanes.  Kernel durations of
  * rtm_ctx_kernel_ms_history are then per launch, i.e. per batch;
