@@ -365,18 +365,44 @@ __device__ __forceinline__ bool plane_hit_persp(const PlaneK& p, const double o[
     return !(qx * qx + qy * qy + qz * qz > p.r2max);
 }
 
+// iCappedCone (main.rs:2889-2959) split in two: the t test per (ray, cylinder)
+// and the hit normal, evaluated only for the cylinder that finally takes the pixel
+// (trace_pixel): a cylinder hit behind a known intersection, or one a later
+// primitive overrides, no longer pays the body normal's sqrt and division.  The
+// normal is recomputed from the same inputs (ray, cylinder, t, part) with the same
+// operations in the same order, so it has the same bits as if computed at the hit.
+// part: 1 = cap at pa, 2 = cap at pb, 3 = body.
+constexpr int CY_CAP_A = 1, CY_CAP_B = 2, CY_BODY = 3;
+
+// The body normal of iCappedCone (main.rs:2950-2958): y = oaba + rdba*t, then
+// normalize(baba*(baba*(oa + rd*t) - ba*rr*ra) - ba*hy*y).
+__device__ __forceinline__ void icapped_body_normal(const CylK& c, const double oa[3], double oaba, double rdba,
+                                                    const double rd[3], double t, double n[3]) {
+    const double y = oaba + rdba * t;
+    const double rra = c.rr * c.ra, hyy = c.hy * y;
+    double v[3];
+    for (int k = 0; k < 3; ++k) v[k] = ((oa[k] + rd[k] * t) * c.baba - c.ba[k] * rra) * c.baba - c.ba[k] * hyy;
+    const double m = sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);  // normalize (main.rs:105-108)
+    const double inv = 1.0 / m;
+    for (int k = 0; k < 3; ++k) n[k] = v[k] * inv;
+}
+
+__device__ __forceinline__ void icapped_cap_normal(const CylK& c, int part, double n[3]) {
+    const double sc = part == CY_CAP_A ? -c.isq : c.isq;
+    for (int k = 0; k < 3; ++k) n[k] = c.ba[k] * sc;
+}
+
 // icapped for a ray from the PERSPECTIVE camera position (RtK::persp): oa, ob,
 // oaba, obba, oc, ocba, baba*baba and k0 are the host's constants (the same
 // operations in the same order), so the cap branches are uniform and only the
-// terms with rd remain per pixel.
-__device__ __forceinline__ double icapped_persp(const CylK& c, const double rd[3], double n[3]) {
+// terms with rd remain per pixel.  t (-1: miss) and the part hit.
+__device__ __forceinline__ double icapped_persp_t(const CylK& c, const double rd[3], int& part) {
     const double rdba = rd[0] * c.ba[0] + rd[1] * c.ba[1] + rd[2] * c.ba[2];
     if (c.oaba < 0.0) {
         double w[3];
         for (int k = 0; k < 3; ++k) w[k] = c.oa[k] * rdba - rd[k] * c.oaba;
         if (w[0] * w[0] + w[1] * w[1] + w[2] * w[2] < c.ra * c.ra * rdba * rdba) {
-            const double sc = -c.isq;
-            for (int k = 0; k < 3; ++k) n[k] = c.ba[k] * sc;
+            part = CY_CAP_A;
             return -c.oaba / rdba;
         }
     } else if (c.obba > 0.0) {
@@ -384,7 +410,7 @@ __device__ __forceinline__ double icapped_persp(const CylK& c, const double rd[3
         double w[3];
         for (int k = 0; k < 3; ++k) w[k] = c.ob[k] + rd[k] * t;
         if (w[0] * w[0] + w[1] * w[1] + w[2] * w[2] < c.rb * c.rb) {
-            for (int k = 0; k < 3; ++k) n[k] = c.ba[k] * c.isq;
+            part = CY_CAP_B;
             return t;
         }
     }
@@ -397,21 +423,26 @@ __device__ __forceinline__ double icapped_persp(const CylK& c, const double rd[3
     const double t = (-k1 - sg * sqrt(h)) / (k2 * c.rr);
     const double y = c.oaba + rdba * t;
     if (y > 0.0 && y < c.baba) {
-        const double rra = c.rr * c.ra, hyy = c.hy * y;
-        double v[3];
-        for (int k = 0; k < 3; ++k) v[k] = ((c.oa[k] + rd[k] * t) * c.baba - c.ba[k] * rra) * c.baba - c.ba[k] * hyy;
-        const double m = sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
-        const double inv = 1.0 / m;
-        for (int k = 0; k < 3; ++k) n[k] = v[k] * inv;
+        part = CY_BODY;
         return t;
     }
     return -1.0;
 }
 
+__device__ __forceinline__ void icapped_persp_normal(const CylK& c, const double rd[3], double t, int part,
+                                                     double n[3]) {
+    if (part != CY_BODY) {
+        icapped_cap_normal(c, part, n);
+        return;
+    }
+    const double rdba = rd[0] * c.ba[0] + rd[1] * c.ba[1] + rd[2] * c.ba[2];
+    icapped_body_normal(c, c.oa, c.oaba, rdba, rd, t, n);
+}
+
 // iCappedCone (main.rs:2889-2959) in the reference's operation order; the
 // ray-independent terms (ba, baba, rr, hy, inversesqrt(baba)) come from the
-// host.  Returns t (-1 on a miss) and the hit normal in n.
-__device__ __forceinline__ double icapped(const CylK& c, const double ro[3], const double rd[3], double n[3]) {
+// host.  t (-1: miss) and the part hit.
+__device__ __forceinline__ double icapped_t(const CylK& c, const double ro[3], const double rd[3], int& part) {
     double oa[3], ob[3];
     for (int k = 0; k < 3; ++k) {
         oa[k] = ro[k] - c.pa[k];
@@ -425,8 +456,7 @@ __device__ __forceinline__ double icapped(const CylK& c, const double ro[3], con
         double w[3];
         for (int k = 0; k < 3; ++k) w[k] = oa[k] * rdba - rd[k] * oaba;
         if (w[0] * w[0] + w[1] * w[1] + w[2] * w[2] < c.ra * c.ra * rdba * rdba) {
-            const double sc = -c.isq;
-            for (int k = 0; k < 3; ++k) n[k] = c.ba[k] * sc;
+            part = CY_CAP_A;
             return -oaba / rdba;
         }
     } else if (obba > 0.0) {
@@ -434,7 +464,7 @@ __device__ __forceinline__ double icapped(const CylK& c, const double ro[3], con
         double w[3];
         for (int k = 0; k < 3; ++k) w[k] = ob[k] + rd[k] * t;
         if (w[0] * w[0] + w[1] * w[1] + w[2] * w[2] < c.rb * c.rb) {
-            for (int k = 0; k < 3; ++k) n[k] = c.ba[k] * c.isq;
+            part = CY_CAP_B;
             return t;
         }
     }
@@ -454,15 +484,23 @@ __device__ __forceinline__ double icapped(const CylK& c, const double ro[3], con
     const double t = (-k1 - sg * sqrt(h)) / (k2 * c.rr);
     const double y = oaba + rdba * t;
     if (y > 0.0 && y < c.baba) {
-        const double rra = c.rr * c.ra, hyy = c.hy * y;
-        double v[3];
-        for (int k = 0; k < 3; ++k) v[k] = ((oa[k] + rd[k] * t) * c.baba - c.ba[k] * rra) * c.baba - c.ba[k] * hyy;
-        const double m = sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);  // normalize (main.rs:105-108)
-        const double inv = 1.0 / m;
-        for (int k = 0; k < 3; ++k) n[k] = v[k] * inv;
+        part = CY_BODY;
         return t;
     }
     return -1.0;
+}
+
+__device__ __forceinline__ void icapped_normal(const CylK& c, const double ro[3], const double rd[3], double t,
+                                               int part, double n[3]) {
+    if (part != CY_BODY) {
+        icapped_cap_normal(c, part, n);
+        return;
+    }
+    double oa[3];
+    for (int k = 0; k < 3; ++k) oa[k] = ro[k] - c.pa[k];
+    const double rdba = rd[0] * c.ba[0] + rd[1] * c.ba[1] + rd[2] * c.ba[2];
+    const double oaba = oa[0] * c.ba[0] + oa[1] * c.ba[1] + oa[2] * c.ba[2];
+    icapped_body_normal(c, oa, oaba, rdba, rd, t, n);
 }
 
 // ---- row f-4: the GL preview's SDF, the f64 restatement of oracle/rtm_oracle.c ----
@@ -733,19 +771,23 @@ __device__ __forceinline__ void trace_pixel(const RtK* __restrict__ rt, const do
             zb = t;
         }
     }
+    int cyi = -1, cypart = 0;  // the cylinder that takes the pixel: its normal afterwards
     for (int i = 0; i < ncy; ++i) {
         if (!((mask >> (16 + i)) & 1u)) continue;  // wave-uniform
-        double n[3];
-        const double t = persp ? icapped_persp(rt->cy[i], d, n) : icapped(rt->cy[i], o, d, n);
+        int part = 0;
+        const double t = persp ? icapped_persp_t(rt->cy[i], d, part) : icapped_t(rt->cy[i], o, d, part);
         if (t < 0.0) continue;  // behind the camera (and misses)
         if (t > zb) continue;   // behind a known intersection
         hit.kind = 3;
         hit.id = rt->cy[i].id;
         hit.t = t;
-        hit.n[0] = n[0];
-        hit.n[1] = n[1];
-        hit.n[2] = n[2];
+        cyi = i;
+        cypart = part;
         zb = t;
+    }
+    if (cyi >= 0) {
+        if (persp) icapped_persp_normal(rt->cy[cyi], d, hit.t, cypart, hit.n);
+        else icapped_normal(rt->cy[cyi], o, d, hit.t, cypart, hit.n);
     }
     zb_io = zb;
 }
