@@ -146,6 +146,8 @@ struct rtm_group {
     std::vector<Member> m;
     bool aborted = false;
     bool root_staging = false;
+    void* root_frame = nullptr;  // rtm_group_render: the assembled frame on the root's device
+    size_t root_frame_bytes = 0;
 };
 
 namespace {
@@ -171,6 +173,15 @@ void release(rtm_group* g, bool destroy_comms) {
         mb.xfer = nullptr;
         if (mb.ctx) rtm_ctx_destroy(mb.ctx);
         mb.ctx = nullptr;
+    }
+    if (g->root_frame) {
+        for (Member& mb : g->m)
+            if (mb.rank == 0) {
+                Guard d(mb.device);
+                (void)hipFree(g->root_frame);
+            }
+        g->root_frame = nullptr;
+        g->root_frame_bytes = 0;
     }
 }
 
@@ -467,6 +478,45 @@ int rtm_group_render_frames_async(rtm_group* g, int32_t n_frames, const rtm_scen
         if ((rc = group_frame(g, pf.get(), width, height, format, root, out_dev[i]))) return rc;
     }
     return RTM_OK;
+}
+
+int rtm_group_render(rtm_group* g, const rtm_scene* scene, const rtm_camera* eye, const rtm_camera* shadow,
+                     int32_t width, int32_t height, int32_t march_steps, int32_t flags, int32_t format,
+                     void* out_host) {
+    if (!g) return set_error(RTM_ERR_INVALID, "group is NULL");
+    const int32_t bpp = rtm::internal::bytes_per_pixel(format);
+    if (!bpp) return set_error(RTM_ERR_INVALID, "unknown output format");
+    if (width <= 0 || height <= 0 || width > RTM_MAX_DIM || height > RTM_MAX_DIM)
+        return set_error(RTM_ERR_INVALID, "image size outside [1, RTM_MAX_DIM]");
+    Member* root = nullptr;
+    for (Member& mb : g->m)
+        if (mb.rank == 0) root = &mb;
+    const size_t bytes = (size_t)bpp * (size_t)width * (size_t)height;
+    if (root) {
+        if (!out_host) return set_error(RTM_ERR_INVALID, "out_host is NULL on the root");
+        if (g->root_frame_bytes < bytes) {
+            Guard d(root->device);
+            GHIP_TRY(hipStreamSynchronize(root->xfer));
+            if (g->root_frame) (void)hipFree(g->root_frame);
+            g->root_frame = nullptr;
+            g->root_frame_bytes = 0;
+            if (hipMalloc(&g->root_frame, bytes) != hipSuccess)
+                return set_error(RTM_ERR_OOM, "root frame allocation failed");
+            g->root_frame_bytes = bytes;
+        }
+    }
+    void* outs[1] = {root ? g->root_frame : nullptr};
+    int rc = rtm_group_render_frames_async(g, 1, scene, eye, shadow, width, height, march_steps, flags, format, 0,
+                                           outs);
+    if (rc) return rc;
+    if (root) {  // the frame is complete in the root's transfer-stream order
+        Guard d(root->device);
+        GHIP_TRY(hipMemcpyAsync(out_host, g->root_frame, bytes, hipMemcpyDeviceToHost, root->xfer));
+        // wait in the runtime (a pageable copy is staged by the waiting thread: polling
+        // the stream instead took 23 ms per 4K frame instead of 2.4)
+        GHIP_TRY(hipStreamSynchronize(root->xfer));
+    }
+    return rtm_group_synchronize(g, 0);
 }
 
 void* rtm_group_stream(rtm_group* g) {

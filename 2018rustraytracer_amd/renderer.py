@@ -335,6 +335,21 @@ class Group:
         lib = _lib()
         abi.check(lib, lib.rtm_group_synchronize(self._h, timeout_ms), "rtm_group_synchronize")
 
+    def render(self, scene: Scene, eye: Camera, shadow: Camera, width: int, height: int, steps: int,
+               flags: int = 0, fmt: int = abi.RTM_FORMAT_RGBA32F, out=None):
+        """rtm_group_render: the tile-partitioned, gathered frame in host memory
+        (blocking): (H, W, 4) float32 for RGBA32F, (H, W, 4|3) uint8 for RGBA8 / RGB8."""
+        import numpy as np
+        if out is None:
+            out = (np.empty((height, width, 4), np.float32) if fmt == abi.RTM_FORMAT_RGBA32F
+                   else np.empty((height, width, 4 if fmt == abi.RTM_FORMAT_RGBA8 else 3), np.uint8))
+        sc, keep = scene.to_c()
+        e, s = eye.to_c(), shadow.to_c()
+        lib = _lib()
+        abi.check(lib, lib.rtm_group_render(self._h, C.byref(sc), C.byref(e), C.byref(s), width, height, steps,
+                                            flags, fmt, out.ctypes.data_as(C.c_void_p)), "rtm_group_render")
+        return out
+
     def close(self):
         if self._h:
             _lib().rtm_group_destroy(self._h)

@@ -8,7 +8,7 @@
  * plain C ABI: it includes only rtm.h and links only librtm.so.
  *
  *   rtm_cli [-s SCENE] [-w W] [-h H] [-k STEPS] [-f FIRST_FRAME] [-n FRAMES] [-b]
- *           [--ppm PATH] [--ppm-gpu PATH] [--raw PATH]
+ *           [-g N] [--ppm PATH] [--ppm-gpu PATH] [--raw PATH]
  *
  *   -s SCENE    orbit   testscene_closelyOrbitingSphere (main.rs:1468-1633, default)
  *               plane0  testscene_raytracingPlane0, main()'s default scene
@@ -22,6 +22,11 @@
  *               RTM_FLAG_NO_SHADOW_RASTER, and -k is ignored.
  *   -b          Scene A-bench's tilted patch instead of the
  *               reference's hard-coded one (main.rs:2024-2029)
+ *   -g N        render every frame through an RCCL group of devices 0..N-1
+ *               (rtm_group_create: ncclCommInitAll in this process; each device renders
+ *               a row band, ONE gather assembles the frame on device 0,
+ *               rtm_group_render returns it to host memory): the north star's
+ *               tile-partitioned frame, called as a Rust host would call it
  *   --ppm PATH  writeColorImage of the last frame (P3 text, main.rs:660-704),
  *               encoded on the host from rtm_encode_thresholds
  *   --ppm-gpu PATH  the same file from the library's RGB8 output format
@@ -185,7 +190,7 @@ static double now(void) {
 }
 
 int main(int argc, char** argv) {
-    int w = 512, h = 512, steps = 500, first = 0, frames = 1, bench_patch = 0;
+    int w = 512, h = 512, steps = 500, first = 0, frames = 1, bench_patch = 0, group_n = 0;
     const char *ppm = NULL, *ppm_gpu = NULL, *raw = NULL, *scene_name = "orbit";
     for (int i = 1; i < argc; i++) {
         const char* a = argv[i];
@@ -196,6 +201,7 @@ int main(int argc, char** argv) {
         else if (!strcmp(a, "-f") && more) first = atoi(argv[++i]);
         else if (!strcmp(a, "-n") && more) frames = atoi(argv[++i]);
         else if (!strcmp(a, "-b")) bench_patch = 1;
+        else if (!strcmp(a, "-g") && more) group_n = atoi(argv[++i]);
         else if (!strcmp(a, "-s") && more) scene_name = argv[++i];
         else if (!strcmp(a, "--ppm-gpu") && more) ppm_gpu = argv[++i];
         else if (!strcmp(a, "--ppm") && more) ppm = argv[++i];
@@ -203,7 +209,7 @@ int main(int argc, char** argv) {
         else {
             fprintf(stderr,
                     "usage: %s [-s orbit|plane0|plane0-disc|persp1|persp2] [-w W] [-h H] [-k STEPS] [-f FIRST] "
-                    "[-n FRAMES] [-b] [--ppm P] [--ppm-gpu P] [--raw P]\n",
+                    "[-n FRAMES] [-b] [-g N] [--ppm P] [--ppm-gpu P] [--raw P]\n",
                     argv[0]);
             return 2;
         }
@@ -237,6 +243,15 @@ int main(int argc, char** argv) {
     }
     float* img = (float*)malloc((size_t)w * h * 4 * sizeof(float));
     if (!img) return 1;
+    rtm_group* group = NULL;
+    if (group_n > 0) {
+        const int rc = rtm_group_create(group_n, NULL, &group);
+        if (rc != RTM_OK) {
+            fprintf(stderr, "rtm_group_create: %d (%s)\n", rc, rtm_last_error());
+            free(img);
+            return 1;
+        }
+    }
     double t0 = 0.0;
     rtm_scene sc;
     rtm_sphere sph[3];
@@ -252,18 +267,22 @@ int main(int argc, char** argv) {
             sc = other;
         }
         if (i == 1 || frames == 1) t0 = now(); /* frame 0 pays the context/table set-up when frames > 1 */
-        const int rc = rtm_render(&sc, &eye, &shadow, w, h, steps, flags, img);
+        const int rc = group ? rtm_group_render(group, &sc, &eye, &shadow, w, h, steps, flags, RTM_FORMAT_RGBA32F, img)
+                             : rtm_render(&sc, &eye, &shadow, w, h, steps, flags, img);
         if (rc != RTM_OK) {
-            fprintf(stderr, "rtm_render: %d (%s)\n", rc, rtm_last_error());
+            fprintf(stderr, "%s: %d (%s)\n", group ? "rtm_group_render" : "rtm_render", rc, rtm_last_error());
+            if (group) rtm_group_destroy(group);
             free(img);
             return 1;
         }
     }
     const double dt = now() - t0;
+    if (group) rtm_group_destroy(group); /* (ncclCommDestroy: ~0.5 s, outside the timed frames) */
     const int timed = frames > 1 ? frames - 1 : 1;
     printf("{\"scene\": \"%s\", \"frames\": %d, \"width\": %d, \"height\": %d, \"steps\": %d, "
-           "\"seconds\": %.6f, \"mpixels_per_s\": %.2f, \"path\": \"rtm_render (host output)\"}\n",
-           scene_name, timed, w, h, steps, dt, (double)w * h * timed / dt / 1e6);
+           "\"seconds\": %.6f, \"mpixels_per_s\": %.2f, \"path\": \"%s (host output)\", \"gpus\": %d}\n",
+           scene_name, timed, w, h, steps, dt, (double)w * h * timed / dt / 1e6,
+           group_n > 0 ? "rtm_group_render" : "rtm_render", group_n > 0 ? group_n : 1);
     int rc = 0;
     if (ppm_gpu) {
         uint8_t* rgb = (uint8_t*)malloc((size_t)w * h * 3);

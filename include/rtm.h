@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define RTM_ABI_VERSION 7
+#define RTM_ABI_VERSION 8
 
 /* ---- limits: scene constants travel as kernel arguments (SGPR path) ---- */
 #define RTM_MAX_SPHERES 16
@@ -390,6 +390,16 @@ int rtm_group_render_frames_async(rtm_group* g, int32_t n_frames, const rtm_scen
                                   const rtm_camera* eye, const rtm_camera* shadow, int32_t width, int32_t height,
                                   int32_t march_steps, int32_t flags, int32_t format, int32_t root,
                                   void* const* out_dev);
+/* ABI v8: the drop-in form for a host that owns no device memory (the Rust
+ * crate): one frame, tile-partitioned over the group and gathered to rank 0 as
+ * above, into a device buffer the group owns on rank 0's device, then copied
+ * into out_host (width*height pixels of rtm_format_bytes(format) bytes; direct
+ * DMA when registered with rtm_host_register).  Blocking: returns when out_host
+ * holds the frame (on the process holding rank 0; elsewhere when this rank's
+ * band has been sent, out_host ignored). */
+int rtm_group_render(rtm_group* g, const rtm_scene* scene, const rtm_camera* eye, const rtm_camera* shadow,
+                     int32_t width, int32_t height, int32_t march_steps, int32_t flags, int32_t format,
+                     void* out_host);
 /* hipStream_t (as void*) in whose order a frame gathered to rank 0 is complete on
  * this process (the root's transfer stream; on other ranks, where their sends run) */
 void* rtm_group_stream(rtm_group* g);

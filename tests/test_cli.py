@@ -101,3 +101,23 @@ def test_cli_scene_switch(oracle, scenes, tmp_path, name):
     text = oracle.write_ppm(want)
     assert ppm.read_bytes() == text
     assert ppm_gpu.read_bytes() == text
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("frame,sha", [(0, "cf557d736f83a4f6"), (100, "cb7008f728da5208")])
+def test_cli_group_frames(oracle, scenes, tmp_path, frame, sha):
+    """rtm_cli -g 1: every frame through an RCCL group (ncclCommInitAll over the
+    box's device, rtm_group_render to host memory), the reference's frames bit for
+    bit and the survey's hashes, exactly as the single-device path."""
+    raw = tmp_path / "g.raw"
+    p = subprocess.run([CLI, "-w", "512", "-h", "512", "-k", "500", "-f", str(frame), "-n", "2", "-g", "1",
+                        "--raw", str(raw)], capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0, p.stderr
+    assert '"path": "rtm_group_render (host output)"' in p.stdout
+    got = np.fromfile(raw, dtype=np.float32).reshape(512, 512, 4)
+    want = oracle.render(scenes.closely_orbiting_sphere(frame + 1), scenes.eye_camera(), scenes.shadow_camera(),
+                         512, 512, 500, 0)["rgba"]
+    assert bits_equal(got, want), first_mismatch(got, want)
+    one = oracle.render(scenes.closely_orbiting_sphere(frame), scenes.eye_camera(), scenes.shadow_camera(),
+                        512, 512, 500, 0)["rgba"]
+    assert _sha16_rgb(one) == sha

@@ -243,3 +243,26 @@ def test_group_rejects_bad_input_before_enqueue(rtm, scenes):
         g.render_async(bad, eye, sh, 8, 8, 8, 0, 0, 0, out.data_ptr())
     g.synchronize(10000)  # nothing was enqueued: returns at once
     g.close()
+
+
+@pytest.mark.parametrize("staging", [False, True], ids=["in-place", "rccl-self-gather"])
+@pytest.mark.parametrize("fmt", [0, 1, 2])
+def test_group_render_host_output(rtm, oracle, scenes, fmt, staging):
+    """rtm_group_render (ABI v8, the form a host without device memory calls): the
+    gathered frame in host memory, pageable and registered, sizes that change from
+    call to call (the group's root buffer grows), bit-equal to the oracle."""
+    g = rtm.Group(n_devices=1)
+    g.set_root_staging(staging)
+    eye, sh = scenes.eye_camera(), scenes.shadow_camera()
+    for (w, h, f) in ((320, 180, 10), (517, 299, 60), (320, 180, 90)):
+        s = scenes.scene_a_bench(f)
+        want = want_frame(oracle, s, eye, sh, w, h, 64, 0, fmt, rtm.abi)
+        got = g.render(s, eye, sh, w, h, 64, 0, fmt)
+        assert np.array_equal(got.view(np.uint8), want.view(np.uint8))
+        buf = np.zeros_like(want)
+        with rtm.HostRegistration(buf):
+            g.render(s, eye, sh, w, h, 64, 0, fmt, out=buf)
+        assert np.array_equal(buf.view(np.uint8), want.view(np.uint8))
+    with pytest.raises(rtm.RtmError):
+        g.render(scenes.scene_a_bench(), eye, sh, 8, 8, 8, 0, 9)  # unknown format
+    g.close()
