@@ -1134,7 +1134,8 @@ int frame_batch(int32_t req, int32_t W, int32_t H) {
 
 // Enqueue frames [0, n) of `fa` (same tables, flags and sizes) as ONE batched
 // launch per pass on `lane`; a frame's output is outs[k] (RGBA f32).
-int enqueue_batch(rtm_ctx* ctx, int lane, FrameArgs* fa, const FrameExtra* ex, float* const* outs, int n) {
+int enqueue_batch(rtm_ctx* ctx, int lane, FrameArgs* fa, const FrameExtra* ex, void* const* outs, int n,
+                  int32_t fmt = RTM_FORMAT_RGBA32F) {
     int rc;
     if ((rc = frame_tables(ctx, fa[0]))) return rc;
     for (int k = 1; k < n; ++k) {
@@ -1196,7 +1197,7 @@ int enqueue_batch(rtm_ctx* ctx, int lane, FrameArgs* fa, const FrameExtra* ex, f
         bf.a = fa[k];
         bf.smap = fused ? nullptr : (double*)((char*)br.smaps.p + map_bytes * (size_t)k);
         bf.out = outs[k];
-        if ((rc = format_tabs(ctx, RTM_FORMAT_RGBA32F, fa[k].ey.W, outs[k], bf.tabs))) return rc;
+        if ((rc = format_tabs(ctx, fmt, fa[k].ey.W, outs[k], bf.tabs))) return rc;
         bf.tabs.rt = nullptr;
         bf.tabs.psp = nullptr;
         bf.tabs.sdf = nullptr;
@@ -1234,7 +1235,7 @@ int enqueue_batch(rtm_ctx* ctx, int lane, FrameArgs* fa, const FrameExtra* ex, f
             }
         t0.rtmask = (uint32_t*)br.rtmask.p;
     }
-    t0.fmt = RTM_FORMAT_RGBA32F;
+    t0.fmt = fmt;
     static const bool copy_stream = [] {  // RTM_BATCH_COPY=stream: upload on the lane's own stream (A/B)
         const char* e = getenv("RTM_BATCH_COPY");
         return !(e && std::string(e) == "stream");
@@ -1548,7 +1549,8 @@ int rtm_render_frames_async(rtm_ctx* ctx, int32_t n_frames, const rtm_scene* sce
                     ++e;
                 if (e - k >= 2 && shadow_batchable(fa[(size_t)k].sh)) {
                     if (!(rc = frame_tables(ctx, fa[(size_t)k])) && shadow_batchable(fa[(size_t)k].sh))
-                        rc = enqueue_batch(ctx, lane, &fa[(size_t)k], &fx[(size_t)k], out_rgba_dev + i0 + k, e - k);
+                        rc = enqueue_batch(ctx, lane, &fa[(size_t)k], &fx[(size_t)k],
+                                           reinterpret_cast<void* const*>(out_rgba_dev + i0 + k), e - k);
                     else if (!rc)
                         for (int32_t q = k; q < e && !rc; ++q)
                             rc = enqueue_frame(ctx, fa[(size_t)q], &fx[(size_t)q], out_rgba_dev[i0 + q], nullptr, lane);
@@ -2107,6 +2109,51 @@ int enqueue_prepared(rtm_ctx* ctx, const PreparedFrame* f, int32_t format, int32
     DeviceGuard g(ctx->device);
     return enqueue_frame(ctx, a, &f->x, out_dev, nullptr, 0, format);
 }
+
+int enqueue_prepared_batch(rtm_ctx* ctx, const PreparedFrame* const* fs, int n, int32_t format, int32_t row_begin,
+                           int32_t row_end, void* const* outs) {
+    if (!ctx || !fs || !outs || n < 1) return fail(RTM_ERR_INVALID, "bad arguments");
+    if (n == 1) return enqueue_prepared(ctx, fs[0], format, row_begin, row_end, outs[0]);
+    int rc;
+    for (int k = 0; k < n; ++k) {
+        if (!fs[k] || !outs[k]) return fail(RTM_ERR_INVALID, "bad arguments");
+        if ((rc = validate_format(format, outs[k]))) return rc;
+    }
+    const FrameArgs& a0 = fs[0]->a;
+    if (row_begin < 0 || row_end > a0.ey.H || row_begin >= row_end)
+        return fail(RTM_ERR_INVALID, "row range [%d,%d) outside [0,%d)", row_begin, row_end, a0.ey.H);
+    // one launch per pass needs the same march tables (patches) and sizes in every frame
+    bool same = true;
+    for (int k = 1; k < n && same; ++k) {
+        const FrameArgs& b = fs[k]->a;
+        same = b.sh.n_patches == a0.sh.n_patches && b.ey.W == a0.ey.W && b.ey.H == a0.ey.H &&
+               b.sh.steps == a0.sh.steps && b.ey.flags == a0.ey.flags &&
+               std::memcmp(b.sh.patch, a0.sh.patch, sizeof(PatchK) * (size_t)a0.sh.n_patches) == 0;
+    }
+    DeviceGuard g(ctx->device);
+    if (!same) {
+        for (int k = 0; k < n; ++k)
+            if ((rc = enqueue_prepared(ctx, fs[k], format, row_begin, row_end, outs[k]))) return rc;
+        return RTM_OK;
+    }
+    std::vector<FrameArgs> fa((size_t)n);
+    std::vector<FrameExtra> fx((size_t)n);
+    for (int k = 0; k < n; ++k) {
+        fa[(size_t)k] = fs[k]->a;
+        fa[(size_t)k].ey.row_begin = row_begin;
+        fa[(size_t)k].ey.row_end = row_end;
+        fx[(size_t)k] = fs[k]->x;
+    }
+    if ((rc = frame_tables(ctx, fa[0]))) return rc;
+    if (!(fa[0].ey.flags & RTM_FLAG_FUSED_SHADOW) && !shadow_batchable(fa[0].sh)) {
+        for (int k = 0; k < n; ++k)
+            if ((rc = enqueue_frame(ctx, fa[(size_t)k], &fx[(size_t)k], outs[k], nullptr, 0, format))) return rc;
+        return RTM_OK;
+    }
+    return enqueue_batch(ctx, 0, fa.data(), fx.data(), outs, n, format);
+}
+
+int auto_frames_per_launch(int32_t width, int32_t rows) { return frame_batch(0, width, rows); }
 
 int32_t bytes_per_pixel(int32_t format) { return format_bytes(format); }
 

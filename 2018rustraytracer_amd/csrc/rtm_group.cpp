@@ -331,73 +331,83 @@ int rtm_group_set_root_staging(rtm_group* g, int32_t on) {
 
 namespace {
 
-// One frame of the group, its inputs already validated and prepared.  Per member:
-// the band renders on the member's context stream (the root's in place into
-// out_dev, the others' into staging slot s); the transfer stream waits for the
-// render and then carries the gather, so a context stream never waits for a
-// transfer and frame i+1 renders while frame i is in flight.  The frame is
-// complete in the root's transfer stream order (rtm_group_stream).
-int group_frame(rtm_group* g, const rtm::internal::PreparedFrame* pf, int32_t width, int32_t height, int32_t format,
-                int32_t root, void* out_dev) {
+// A chunk of nf frames of the group (1 <= nf <= the staging slot's frame count),
+// their inputs already validated and prepared.  Per member: the bands of all nf
+// frames render on the member's context stream in one launch per pass (the batched
+// kernels; the root's bands in place into out_dev[j], the others' into staging slot
+// s, band j at offset j*band_bytes); the transfer stream waits for the render and
+// then carries one gather per frame, so a context stream never waits for a
+// transfer and the next chunk renders while this one is in flight.  Frame j is
+// complete in the root's transfer-stream order (rtm_group_stream).
+int group_chunk(rtm_group* g, const rtm::internal::PreparedFrame* const* pf, int nf, int32_t width, int32_t height,
+                int32_t format, int32_t root, void* const* out_dev) {
     const int32_t n = g->n_ranks;
     const size_t row_bytes = (size_t)rtm::internal::bytes_per_pixel(format) * (size_t)width;
+    int32_t b0, b1;
+    band_rows(height, n, 0, &b0, &b1);
+    const size_t band_bytes = row_bytes * (size_t)(b1 - b0);
     int rc;
-    // 1. every local member renders its band
+    std::vector<void*> outs((size_t)nf);
+    // 1. every local member renders its bands of the chunk's frames
     for (Member& mb : g->m) {
         int32_t r0, r1;
         band_rows(height, n, mb.rank, &r0, &r1);
         Guard d(mb.device);
         hipStream_t rs = rtm::internal::ctx_stream(mb.ctx);
         const bool staged = mb.rank != root || g->root_staging;
-        if (r0 < r1 && !staged) {
-            rc = rtm::internal::enqueue_prepared(mb.ctx, pf, format, r0, r1, (char*)out_dev + row_bytes * (size_t)r0);
-            if (rc) return rc;
-        } else if (r0 < r1) {
+        if (r0 < r1) {
             const int s = mb.slot;
-            GHIP_TRY(hipStreamWaitEvent(rs, mb.sent[s], 0));  // stage[s]'s previous send has read it
-            rc = rtm::internal::enqueue_prepared(mb.ctx, pf, format, r0, r1, mb.stage[s]);
+            if (staged) GHIP_TRY(hipStreamWaitEvent(rs, mb.sent[s], 0));  // slot s's previous sends have read it
+            for (int j = 0; j < nf; ++j)
+                outs[(size_t)j] = staged ? (void*)((char*)mb.stage[s] + band_bytes * (size_t)j)
+                                         : (void*)((char*)out_dev[j] + row_bytes * (size_t)r0);
+            rc = rtm::internal::enqueue_prepared_batch(mb.ctx, pf, nf, format, r0, r1, outs.data());
             if (rc) return rc;
-            GHIP_TRY(hipEventRecord(mb.ready[s], rs));
-            GHIP_TRY(hipStreamWaitEvent(mb.xfer, mb.ready[s], 0));
+            if (staged) {
+                GHIP_TRY(hipEventRecord(mb.ready[s], rs));
+                GHIP_TRY(hipStreamWaitEvent(mb.xfer, mb.ready[s], 0));
+            }
         }
-        if (mb.rank == root && !staged) {  // the root's own band, in the frame's completion order
+        if (mb.rank == root && !staged) {  // the root's own bands, in the frames' completion order
             GHIP_TRY(hipEventRecord(mb.start, rs));
             GHIP_TRY(hipStreamWaitEvent(mb.xfer, mb.start, 0));
         }
     }
-    // 2. ONE gather: the root receives every other band in place, the others send
-    //    theirs (nothing to move for a one-rank group rendering in place)
+    // 2. ONE gather per frame: the root receives every other band in place, the
+    //    others send theirs (nothing to move for a one-rank group rendering in place)
     if (n > 1 || g->root_staging) {
         const Rccl& R = rccl();
-        NCCL_TRY(R.GroupStart());
-        for (Member& mb : g->m) {
-            if (mb.rank == root) {
-                for (int32_t p = 0; p < n; ++p) {
-                    if (p == root && !g->root_staging) continue;
-                    int32_t r0, r1;
-                    band_rows(height, n, p, &r0, &r1);
-                    if (r0 >= r1) continue;
-                    ncclResult_t r = R.Recv((char*)out_dev + row_bytes * (size_t)r0, row_bytes * (size_t)(r1 - r0),
-                                            ncclUint8, p, mb.comm, mb.xfer);
+        for (int j = 0; j < nf; ++j) {
+            NCCL_TRY(R.GroupStart());
+            for (Member& mb : g->m) {
+                if (mb.rank == root) {
+                    for (int32_t p = 0; p < n; ++p) {
+                        if (p == root && !g->root_staging) continue;
+                        int32_t r0, r1;
+                        band_rows(height, n, p, &r0, &r1);
+                        if (r0 >= r1) continue;
+                        ncclResult_t r = R.Recv((char*)out_dev[j] + row_bytes * (size_t)r0,
+                                                row_bytes * (size_t)(r1 - r0), ncclUint8, p, mb.comm, mb.xfer);
+                        if (r != ncclSuccess) {
+                            (void)R.GroupEnd();
+                            return comm_fail("ncclRecv", r);
+                        }
+                    }
+                }
+                int32_t r0, r1;
+                band_rows(height, n, mb.rank, &r0, &r1);
+                const bool staged = mb.rank != root || g->root_staging;
+                if (staged && r0 < r1) {
+                    ncclResult_t r = R.Send((char*)mb.stage[mb.slot] + band_bytes * (size_t)j,
+                                            row_bytes * (size_t)(r1 - r0), ncclUint8, root, mb.comm, mb.xfer);
                     if (r != ncclSuccess) {
                         (void)R.GroupEnd();
-                        return comm_fail("ncclRecv", r);
+                        return comm_fail("ncclSend", r);
                     }
                 }
             }
-            int32_t r0, r1;
-            band_rows(height, n, mb.rank, &r0, &r1);
-            const bool staged = mb.rank != root || g->root_staging;
-            if (staged && r0 < r1) {
-                ncclResult_t r =
-                    R.Send(mb.stage[mb.slot], row_bytes * (size_t)(r1 - r0), ncclUint8, root, mb.comm, mb.xfer);
-                if (r != ncclSuccess) {
-                    (void)R.GroupEnd();
-                    return comm_fail("ncclSend", r);
-                }
-            }
+            NCCL_TRY(R.GroupEnd());
         }
-        NCCL_TRY(R.GroupEnd());
     }
     // 3. staging slots: free again once their sends have read them
     for (Member& mb : g->m) {
@@ -417,8 +427,9 @@ struct PreparedDeleter {
     void operator()(rtm::internal::PreparedFrame* f) const { rtm::internal::delete_prepared(f); }
 };
 
-// Shared checks of the frame calls; allocates the staging buffers.
-int group_begin(rtm_group* g, int32_t width, int32_t height, int32_t format, int32_t root) {
+// Shared checks of the frame calls; allocates the staging buffers (two slots of
+// `frames` bands each).
+int group_begin(rtm_group* g, int32_t width, int32_t height, int32_t format, int32_t root, int32_t frames) {
     if (!g) return set_error(RTM_ERR_INVALID, "group is NULL");
     if (g->aborted) return set_error(RTM_ERR_COMM, "group was aborted");
     if (root < 0 || root >= g->n_ranks) return set_error(RTM_ERR_INVALID, "root outside [0, n_ranks)");
@@ -431,7 +442,8 @@ int group_begin(rtm_group* g, int32_t width, int32_t height, int32_t format, int
     for (Member& mb : g->m) {
         const bool staged = mb.rank != root || g->root_staging;
         int rc;
-        if (staged && (rc = ensure_stage(mb, (size_t)bpp * (size_t)width * (size_t)(b1 - b0)))) return rc;
+        if (staged && (rc = ensure_stage(mb, (size_t)bpp * (size_t)width * (size_t)(b1 - b0) * (size_t)frames)))
+            return rc;
     }
     return RTM_OK;
 }
@@ -459,23 +471,58 @@ int rtm_group_render_async(rtm_group* g, const rtm_scene* scene, const rtm_camer
 int rtm_group_render_frames_async(rtm_group* g, int32_t n_frames, const rtm_scene* scenes, const rtm_camera* eye,
                                   const rtm_camera* shadow, int32_t width, int32_t height, int32_t march_steps,
                                   int32_t flags, int32_t format, int32_t root, void* const* out_dev) {
-    int rc = group_begin(g, width, height, format, root);
-    if (rc) return rc;
+    if (!g) return set_error(RTM_ERR_INVALID, "group is NULL");
     if (n_frames < 1 || !scenes || !out_dev) return set_error(RTM_ERR_INVALID, "bad frame list");
+    if (width <= 0 || height <= 0 || width > RTM_MAX_DIM || height > RTM_MAX_DIM)
+        return set_error(RTM_ERR_INVALID, "image size outside [1, RTM_MAX_DIM]");
+    // frames per launch: the library's auto rule for a band (every rank's bands of a
+    // chunk render in one launch per pass), the same on every rank
+    int32_t b0, b1;
+    band_rows(height, g->n_ranks > 0 ? g->n_ranks : 1, 0, &b0, &b1);
+    const int32_t B = std::max(1, std::min<int32_t>(n_frames, rtm::internal::auto_frames_per_launch(width, b1 - b0)));
+    int rc = group_begin(g, width, height, format, root, B);
+    if (rc) return rc;
     // more than one band: each evaluates the shadow texels it reads (same image bits)
     const int32_t f = flags | (g->n_ranks > 1 ? RTM_FLAG_FUSED_SHADOW : 0);
-    std::unique_ptr<rtm::internal::PreparedFrame, PreparedDeleter> pf(rtm::internal::new_prepared());
-    if (!pf) return set_error(RTM_ERR_OOM, "host allocation failed");
     // Everything that can fail for the caller's inputs is checked before the first
     // enqueue: a rank that stopped half-way would leave its peers' transfers unmatched.
     for (int32_t i = 0; i < n_frames; ++i) {
         if ((rc = rtm::internal::check_frame(&scenes[i], eye, shadow, width, height, march_steps, f))) return rc;
         if ((rc = check_root_out(g, format, root, out_dev[i]))) return rc;
     }
-    for (int32_t i = 0; i < n_frames; ++i) {
-        if ((rc = rtm::internal::prepare_frame(pf.get(), &scenes[i], eye, shadow, width, height, march_steps, f)))
-            return rc;
-        if ((rc = group_frame(g, pf.get(), width, height, format, root, out_dev[i]))) return rc;
+    std::vector<std::unique_ptr<rtm::internal::PreparedFrame, PreparedDeleter>> pf((size_t)B);
+    std::vector<const rtm::internal::PreparedFrame*> pp((size_t)B);
+    for (int32_t k = 0; k < B; ++k) {
+        pf[(size_t)k].reset(rtm::internal::new_prepared());
+        if (!pf[(size_t)k]) return set_error(RTM_ERR_OOM, "host allocation failed");
+        pp[(size_t)k] = pf[(size_t)k].get();
+    }
+    bool holds_root = false;
+    for (const Member& mb : g->m) holds_root |= mb.rank == root;
+    const uintptr_t frame_bytes = (uintptr_t)rtm::internal::bytes_per_pixel(format) * (uintptr_t)width * height;
+    for (int32_t i0 = 0; i0 < n_frames;) {
+        int nf = std::min<int32_t>(B, n_frames - i0);
+        // on the root, a chunk's frames need disjoint outputs (they render side by side);
+        // a repeated output starts the next chunk, so the later frame still lands last
+        // (chunking is local: every frame's gather is its own matched send/receive set)
+        if (holds_root)
+            for (int k = 1; k < nf; ++k) {
+                bool clash = false;
+                for (int q = 0; q < k && !clash; ++q) {
+                    const uintptr_t a = (uintptr_t)out_dev[i0 + k], b = (uintptr_t)out_dev[i0 + q];
+                    clash = a < b + frame_bytes && b < a + frame_bytes;
+                }
+                if (clash) {
+                    nf = k;
+                    break;
+                }
+            }
+        for (int k = 0; k < nf; ++k)
+            if ((rc = rtm::internal::prepare_frame(pf[(size_t)k].get(), &scenes[i0 + k], eye, shadow, width, height,
+                                                   march_steps, f)))
+                return rc;
+        if ((rc = group_chunk(g, pp.data(), nf, width, height, format, root, out_dev + i0))) return rc;
+        i0 += nf;
     }
     return RTM_OK;
 }

@@ -23,6 +23,13 @@ int prepare_frame(PreparedFrame* f, const rtm_scene* scene, const rtm_camera* ey
 // rows [row_begin, row_end) in `format` into out_dev, on ctx's stream
 int enqueue_prepared(rtm_ctx* ctx, const PreparedFrame* f, int32_t format, int32_t row_begin, int32_t row_end,
                      void* out_dev);
+// n frames' rows [row_begin, row_end) in `format`, frame k into outs[k], on ctx's
+// stream: one launch per pass when the frames share their march tables
+// (rtm_ctx_set_batch's batched kernels), else frame by frame
+int enqueue_prepared_batch(rtm_ctx* ctx, const PreparedFrame* const* fs, int n, int32_t format, int32_t row_begin,
+                           int32_t row_end, void* const* outs);
+// frames per launch the library's auto rule picks for width x rows frames
+int auto_frames_per_launch(int32_t width, int32_t rows);
 // bytes per pixel of an RTM_FORMAT_* (0: unknown)
 int32_t bytes_per_pixel(int32_t format);
 // set rtm_last_error and return code

@@ -125,17 +125,20 @@ def tile_gather(rtm, lib, ctx, group, world, rank, dist, tdev, c_scenes, eye, sh
     r0, r1 = shard.row_band(H, world, rank)
     e_c, s_c = eye.to_c(), shadow.to_c()
     if group is not None:
-        # two output frames on the root (a swap chain): frame i+1 renders while frame i is gathered
-        outs = ([torch.empty(W * H * bpp, dtype=torch.uint8, device=dev) for _ in range(2)] if rank == 0
-                else [None, None])
+        # a swap chain of output frames on the root: the library renders a band of up to
+        # 16 frames per launch (distinct outputs), frame i+1.. render while frame i is
+        # gathered
+        n_out = 32
+        outs = ([torch.empty(W * H * bpp, dtype=torch.uint8, device=dev) for _ in range(n_out)] if rank == 0
+                else [None] * n_out)
         arr = (rtm.abi.rtm_scene * len(c_scenes))(*[c[0] for c in c_scenes])
-        ptrs = (C.c_void_p * 2)(*[C.c_void_p(o.data_ptr() if o is not None else 0) for o in outs])
+        ptrs = (C.c_void_p * n_out)(*[C.c_void_p(o.data_ptr() if o is not None else 0) for o in outs])
 
         def run(first, n):  # one rtm_group_render_frames_async call per <= len(c_scenes) frames
             done = 0
             while done < n:
                 k = min(n - done, len(c_scenes))
-                ov = (C.c_void_p * k)(*[ptrs[(first + done + j) % 2] for j in range(k)])
+                ov = (C.c_void_p * k)(*[ptrs[(first + done + j) % n_out] for j in range(k)])
                 rc = lib.rtm_group_render_frames_async(group.handle, k, arr, C.byref(e_c), C.byref(s_c), W, H, K,
                                                        flags, fmt, 0, ov)
                 rtm.abi.check(lib, rc, "rtm_group_render_frames_async")

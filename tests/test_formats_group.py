@@ -266,3 +266,30 @@ def test_group_render_host_output(rtm, oracle, scenes, fmt, staging):
     with pytest.raises(rtm.RtmError):
         g.render(scenes.scene_a_bench(), eye, sh, 8, 8, 8, 0, 9)  # unknown format
     g.close()
+
+
+@pytest.mark.parametrize("staging", [False, True], ids=["in-place", "rccl-self-gather"])
+@pytest.mark.parametrize("fmt", [0, 1])
+def test_group_frame_sequence_batched(rtm, oracle, scenes, fmt, staging):
+    """rtm_group_render_frames_async over 10 frames: the bands of a chunk render in
+    one launch per pass (auto: 16 frames of 256x144 per launch), a repeated output
+    pointer cuts the chunk so the later frame lands last; every output holds the
+    oracle's frame (and encode) of the last frame written into it."""
+    import torch
+    g = rtm.Group(n_devices=1)
+    g.set_root_staging(staging)
+    w, h, k = 256, 144, 64
+    eye, sh = scenes.eye_camera(), scenes.shadow_camera()
+    frames = [scenes.scene_a_bench(7 * i) for i in range(10)]
+    bufs = [(torch.empty((h, w, 4), dtype=torch.float32, device="cuda") if fmt == 0 else
+             torch.empty(h * w * rtm.abi.FORMAT_BYTES[fmt], dtype=torch.uint8, device="cuda")) for _ in range(4)]
+    order = [0, 1, 2, 3, 0, 1, 2, 3, 1, 2]   # the last writers: buf0 <- 4, buf1 <- 8, buf2 <- 9, buf3 <- 7
+    torch.cuda.synchronize()
+    g.render_frames_async(frames, eye, sh, w, h, k, 0, fmt, 0, [bufs[o].data_ptr() for o in order])
+    g.synchronize(60000)
+    last = {o: i for i, o in enumerate(order)}
+    for b, i in last.items():
+        got = to_host(bufs[b], h, w, fmt, rtm.abi)
+        want = want_frame(oracle, frames[i], eye, sh, w, h, k, 0, fmt, rtm.abi)
+        assert np.array_equal(got.view(np.uint8), want.view(np.uint8)), (b, i)
+    g.close()
