@@ -2128,6 +2128,8 @@ int enqueue_prepared_batch(rtm_ctx* ctx, const PreparedFrame* const* fs, int n, 
         const FrameArgs& b = fs[k]->a;
         same = b.sh.n_patches == a0.sh.n_patches && b.ey.W == a0.ey.W && b.ey.H == a0.ey.H &&
                b.sh.steps == a0.sh.steps && b.ey.flags == a0.ey.flags &&
+               std::memcmp(&b.sh.cam, &a0.sh.cam, sizeof(CamK)) == 0 &&
+               std::memcmp(&b.ey.eye, &a0.ey.eye, sizeof(CamK)) == 0 &&
                std::memcmp(b.sh.patch, a0.sh.patch, sizeof(PatchK) * (size_t)a0.sh.n_patches) == 0;
     }
     DeviceGuard g(ctx->device);
