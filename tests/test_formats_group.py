@@ -293,3 +293,28 @@ def test_group_frame_sequence_batched(rtm, oracle, scenes, fmt, staging):
         want = want_frame(oracle, frames[i], eye, sh, w, h, k, 0, fmt, rtm.abi)
         assert np.array_equal(got.view(np.uint8), want.view(np.uint8)), (b, i)
     g.close()
+
+
+@pytest.mark.parametrize("fmt", [0, 2])
+def test_group_frame_sequence_raytraced_perspective(rtm, scenes, fmt):
+    """The group's batched bands with ray-traced primitives under a PERSPECTIVE eye
+    (the batched per-wave primitive cull) and perspective spheres, in one chunk:
+    every frame equals the single-device rtm_render_ex bytes."""
+    import torch
+    g = rtm.Group(n_devices=1)
+    g.set_root_staging(True)
+    w, h = 320, 240
+    eye, sh = scenes.perspective_eye_camera(), scenes.shadow_camera()
+    fl = scenes.RAYTRACING_FLAGS
+    frames = [scenes.raytracing_plane0(), scenes.scene_r_bench(), scenes.perspective_simple1(),
+              scenes.raytracing_plane0(True), scenes.scene_r_bench(), scenes.perspective_simple2()]
+    bufs = [(torch.empty((h, w, 4), dtype=torch.float32, device="cuda") if fmt == 0 else
+             torch.empty(h * w * rtm.abi.FORMAT_BYTES[fmt], dtype=torch.uint8, device="cuda")) for _ in frames]
+    torch.cuda.synchronize()
+    g.render_frames_async(frames, eye, sh, w, h, 0, fl, fmt, 0, [b.data_ptr() for b in bufs])
+    g.synchronize(60000)
+    for s, b in zip(frames, bufs):
+        want = rtm.render_frame_ex(s, eye, sh, w, h, 0, fl, fmt)
+        got = to_host(b, h, w, fmt, rtm.abi)
+        assert np.array_equal(got.view(np.uint8), want.view(np.uint8))
+    g.close()
