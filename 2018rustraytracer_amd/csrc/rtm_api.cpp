@@ -12,6 +12,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <ctime>
 #include <memory>
 #include <string>
 #include <thread>
@@ -57,6 +58,48 @@ int fail(int code, const char* fmt, ...) {
     g_last_error = buf;
     return code;
 }
+
+// RTM_HOST_PROF=1 (diagnostic only): host wall time of rtm_render_frames_async by
+// phase, summed over the process and printed to stderr at exit.  Off: one branch
+// on a static per phase.
+struct HostProf {
+    enum { BUILD, SCAN, FILL, SYNC, UPLOAD, LAUNCH, N };
+    const bool on = [] {
+        const char* e = getenv("RTM_HOST_PROF");
+        return e && atoi(e) != 0;
+    }();
+    double s[N] = {};
+    long frames = 0, calls = 0, batches = 0;
+    static double now() {
+        timespec ts;
+        clock_gettime(CLOCK_MONOTONIC, &ts);
+        return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
+    }
+    ~HostProf() {
+        if (!on || !frames) return;
+        static const char* names[N] = {"build", "scan", "fill", "sync", "upload", "launch"};
+        s[SCAN] -= s[FILL] + s[SYNC] + s[UPLOAD] + s[LAUNCH];  // enqueue_batch runs inside the scan phase
+        fprintf(stderr, "RTM_HOST_PROF calls=%ld batches=%ld frames=%ld us/frame:", calls, batches, frames);
+        for (int i = 0; i < N; ++i) fprintf(stderr, " %s=%.3f", names[i], s[i] * 1e6 / (double)frames);
+        fprintf(stderr, "\n");
+    }
+};
+HostProf g_hprof;
+struct HostPhase {  // adds the scope's wall time to one phase when RTM_HOST_PROF is on
+    int ph;
+    double t0;
+    explicit HostPhase(int p) : ph(p), t0(g_hprof.on ? HostProf::now() : 0.0) {}
+    void next(int p) {
+        if (!g_hprof.on) return;
+        const double t = HostProf::now();
+        g_hprof.s[ph] += t - t0;
+        t0 = t;
+        ph = p;
+    }
+    ~HostPhase() {
+        if (g_hprof.on) g_hprof.s[ph] += HostProf::now() - t0;
+    }
+};
 
 #define HIP_TRY(expr)                                                                    \
     do {                                                                                 \
@@ -1137,6 +1180,8 @@ int frame_batch(int32_t req, int32_t W, int32_t H) {
 int enqueue_batch(rtm_ctx* ctx, int lane, FrameArgs* fa, const FrameExtra* ex, void* const* outs, int n,
                   int32_t fmt = RTM_FORMAT_RGBA32F) {
     int rc;
+    HostPhase hp(HostProf::FILL);
+    if (g_hprof.on) g_hprof.batches++;
     if ((rc = frame_tables(ctx, fa[0]))) return rc;
     for (int k = 1; k < n; ++k) {
         fa[k].sh.tab = fa[0].sh.tab;
@@ -1169,15 +1214,36 @@ int enqueue_batch(rtm_ctx* ctx, int lane, FrameArgs* fa, const FrameExtra* ex, v
     auto up = [](size_t v) { return (v + 255) & ~(size_t)255; };
     size_t off = up(sizeof(BatchFrame) * (size_t)n);
     std::vector<size_t> o_rt((size_t)n, 0), o_psp((size_t)n, 0), o_sdf((size_t)n, 0);
+    // a table equal to the previous frame's (a static scene, or primitives that did not
+    // move) is uploaded once and shared: same bytes, so the same bits
+    std::vector<char> fresh_rt((size_t)n, 1), fresh_psp((size_t)n, 1), fresh_sdf((size_t)n, 1);
     for (int k = 0; k < n; ++k) {
-        if (ex[k].has_rt) { o_rt[(size_t)k] = off; off = up(off + sizeof(RtK)); }
-        if (ex[k].has_psp) { o_psp[(size_t)k] = off; off = up(off + sizeof(PerspK)); }
-        if (ex[k].has_sdf) { o_sdf[(size_t)k] = off; off = up(off + sizeof(SdfTabK)); }
+        const FrameExtra* pv = k > 0 ? &ex[k - 1] : nullptr;
+        if (ex[k].has_rt) {
+            if (pv && pv->has_rt && std::memcmp(&pv->rt, &ex[k].rt, sizeof(RtK)) == 0) {
+                o_rt[(size_t)k] = o_rt[(size_t)k - 1];
+                fresh_rt[(size_t)k] = 0;
+            } else { o_rt[(size_t)k] = off; off = up(off + sizeof(RtK)); }
+        }
+        if (ex[k].has_psp) {
+            if (pv && pv->has_psp && std::memcmp(&pv->psp, &ex[k].psp, sizeof(PerspK)) == 0) {
+                o_psp[(size_t)k] = o_psp[(size_t)k - 1];
+                fresh_psp[(size_t)k] = 0;
+            } else { o_psp[(size_t)k] = off; off = up(off + sizeof(PerspK)); }
+        }
+        if (ex[k].has_sdf) {
+            if (pv && pv->has_sdf && std::memcmp(&pv->sdf, &ex[k].sdf, sizeof(SdfTabK)) == 0) {
+                o_sdf[(size_t)k] = o_sdf[(size_t)k - 1];
+                fresh_sdf[(size_t)k] = 0;
+            } else { o_sdf[(size_t)k] = off; off = up(off + sizeof(SdfTabK)); }
+        }
     }
     const size_t bytes = off;
     const int j = br.next;
     br.next = (br.next + 1) % BatchRing::R;
+    hp.next(HostProf::SYNC);
     HIP_TRY(hipEventSynchronize(br.copied[j]));  // the slot's previous upload has left the host buffer
+    hp.next(HostProf::FILL);
     if (br.host_bytes[j] < bytes) {
         if (br.host[j]) HIP_TRY(hipHostFree(br.host[j]));
         br.host[j] = nullptr;
@@ -1204,19 +1270,19 @@ int enqueue_batch(rtm_ctx* ctx, int lane, FrameArgs* fa, const FrameExtra* ex, v
         bf.tabs.rtmask = nullptr;
         bf.tabs.rt_persp = 0;
         if (ex[k].has_rt) {
-            std::memcpy(hb + o_rt[(size_t)k], &ex[k].rt, sizeof(RtK));
+            if (fresh_rt[(size_t)k]) std::memcpy(hb + o_rt[(size_t)k], &ex[k].rt, sizeof(RtK));
             bf.tabs.rt = (const RtK*)(db + o_rt[(size_t)k]);
             bf.tabs.rt_persp = ex[k].rt.persp;
             t0.rt = bf.tabs.rt;
             t0.rt_persp = ex[k].rt.persp;
         }
         if (ex[k].has_psp) {
-            std::memcpy(hb + o_psp[(size_t)k], &ex[k].psp, sizeof(PerspK));
+            if (fresh_psp[(size_t)k]) std::memcpy(hb + o_psp[(size_t)k], &ex[k].psp, sizeof(PerspK));
             bf.tabs.psp = (const PerspK*)(db + o_psp[(size_t)k]);
             t0.psp = bf.tabs.psp;
         }
         if (ex[k].has_sdf) {
-            std::memcpy(hb + o_sdf[(size_t)k], &ex[k].sdf, sizeof(SdfTabK));
+            if (fresh_sdf[(size_t)k]) std::memcpy(hb + o_sdf[(size_t)k], &ex[k].sdf, sizeof(SdfTabK));
             bf.tabs.sdf = (const SdfTabK*)(db + o_sdf[(size_t)k]);
             t0.sdf = bf.tabs.sdf;
         }
@@ -1236,6 +1302,7 @@ int enqueue_batch(rtm_ctx* ctx, int lane, FrameArgs* fa, const FrameExtra* ex, v
         t0.rtmask = (uint32_t*)br.rtmask.p;
     }
     t0.fmt = fmt;
+    hp.next(HostProf::UPLOAD);
     static const bool copy_stream = [] {  // RTM_BATCH_COPY=stream: upload on the lane's own stream (A/B)
         const char* e = getenv("RTM_BATCH_COPY");
         return !(e && std::string(e) == "stream");
@@ -1249,6 +1316,7 @@ int enqueue_batch(rtm_ctx* ctx, int lane, FrameArgs* fa, const FrameExtra* ex, v
         HIP_TRY(hipMemcpyAsync(db, hb, bytes, hipMemcpyHostToDevice, s));
         HIP_TRY(hipEventRecord(br.copied[j], s));
     }
+    hp.next(HostProf::LAUNCH);
     TimingSlot* slot = next_slot(ctx);
     if (!fused) {
         if (slot) HIP_TRY(hipEventRecord(slot->ev[0], s));
@@ -1510,6 +1578,8 @@ int rtm_render_frames_async(rtm_ctx* ctx, int32_t n_frames, const rtm_scene* sce
         }();
         bool stagger = stagger_on && L > 1 && !ctx->stagger_arm;
         if (stagger && !ctx->stagger) HIP_TRY(hipEventCreateWithFlags(&ctx->stagger, hipEventDisableTiming));
+        HostPhase hp(HostProf::SCAN);
+        if (g_hprof.on) g_hprof.calls++, g_hprof.frames += n_frames;
         for (int32_t b = 0; b < nb && !rc; ++b) {
             const int32_t i0 = b * B, nf = std::min(B, n_frames - i0);
             const int lane = (nb - 1 - b) % L;
@@ -1522,10 +1592,12 @@ int rtm_render_frames_async(rtm_ctx* ctx, int32_t n_frames, const rtm_scene* sce
                     break;
                 }
             }
+            hp.next(HostProf::BUILD);
             for (int32_t k = 0; k < nf && !rc; ++k) {
                 rc = build_frame(fa[(size_t)k], &scenes[i0 + k], eye, shadow, width, height, march_steps, flags);
                 if (!rc) build_extra(&scenes[i0 + k], eye, width, height, fx[(size_t)k]);
             }
+            hp.next(HostProf::SCAN);
             if (rc) break;
             // runs of frames with the same march tables (patches) and disjoint outputs share
             // one launch per pass (frames of one launch run concurrently, so a repeated

@@ -138,11 +138,21 @@ class Context:
         frame i goes to device pointer out_ptrs[i]."""
         arr, keep = prepared if prepared is not None else self.prepare_frames(scenes)  # scenes unused if prepared
         n = len(arr)
-        outs = (C.c_void_p * n)(*[C.c_void_p(p) for p in out_ptrs])
+        outs = Context.out_array(out_ptrs)
+        if len(outs) != n:
+            raise ValueError(f"{len(outs)} output pointers for {n} frames")
         e, s = eye.to_c(), shadow.to_c()
         lib = _lib()
         abi.check(lib, lib.rtm_render_frames_async(self._h, n, arr, C.byref(e), C.byref(s), width, height, steps,
                                                    flags, outs), "rtm_render_frames_async")
+
+    @staticmethod
+    def out_array(out_ptrs):
+        """The float* const* of rtm_render_frames_async: a ctypes array built once
+        (a swap chain reused call after call) passes through as it is."""
+        if isinstance(out_ptrs, C.Array):
+            return out_ptrs
+        return (C.c_void_p * len(out_ptrs))(*[C.c_void_p(p) for p in out_ptrs])
 
     def shadow_map_ptr(self) -> int:
         return _lib().rtm_ctx_shadow_map(self._h) or 0

@@ -387,3 +387,37 @@ def test_batched_perspective_raytraced_frames(rtm, scenes, gpu_ctx, batch, lanes
     finally:
         gpu_ctx.set_lanes(0)
         gpu_ctx.set_batch(0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["rt", "sdf"])
+def test_batched_repeated_frames_share_tables(rtm, scenes, gpu_ctx, kind):
+    """A batch whose consecutive frames carry equal primitive tables uploads each
+    run of equal tables once and points the frames at it (enqueue_batch); runs of
+    repeats, changes back and forth and a lone last frame all == rtm_render bit for
+    bit."""
+    import torch
+    w, h, k = 256, 192, 64
+    if kind == "rt":
+        eye, flags = scenes.perspective_eye_camera(), scenes.RAYTRACING_FLAGS
+        a, b, c = scenes.raytracing_plane0(), scenes.scene_r_bench(), scenes.perspective_simple1()
+    else:
+        eye, flags = scenes.sdf_eye_camera(), 0
+        a, b, c = scenes.sdf_preview_scene(), scenes.sdf_bench_scene(), scenes.mixed_sdf(101)
+    sh = scenes.shadow_camera()
+    frames = [a, a, a, b, b, a, c, c, b, a]
+    outs = [torch.empty((h, w, 4), dtype=torch.float32, device="cuda") for _ in frames]
+    try:
+        gpu_ctx.set_batch(len(frames))
+        gpu_ctx.set_lanes(1)
+        torch.cuda.synchronize()
+        gpu_ctx.render_frames_async(frames, eye, sh, w, h, k, flags, [o.data_ptr() for o in outs])
+        gpu_ctx.synchronize()
+        assert gpu_ctx.last_batch() == len(frames)
+        for i, (s, o) in enumerate(zip(frames, outs)):
+            want = rtm.render_frame(s, eye, sh, w, h, k, flags)
+            got = o.cpu().numpy()
+            assert bits_equal(got, want), (i, first_mismatch(got, want))
+    finally:
+        gpu_ctx.set_lanes(0)
+        gpu_ctx.set_batch(0)
