@@ -559,13 +559,27 @@ def main():
         band_h = rows[1] - rows[0]
         st = ctx.stats(s0, eye, shadow, W, H, K, flags)
         sep = metrics.shared_z_separable(shadow)
-        work = metrics.frame_work(st, W, H, len(s0.spherePrimitives), len(s0.patches), flags, fused=fused,
-                                  sep=sep, n_planes=len(s0.circlePlanePrimitives),
-                                  n_cyls=len(s0.cappedCylinderPrimitives),
-                                  perspective=eye.type_ == sc.PERSPECTIVE,
-                                  search=sep and os.environ.get("RTM_SEP_MODE", "2") == "2",
-                                  n_sdfs=len(s0.sdfPrimitives), map_texel_bytes=map_bytes,
-                                  moving=(shadow.dirNormalized[0] * 0.03 != 0.0 or shadow.dirNormalized[1] * 0.03 != 0.0))
+        def frame_work(fused_):
+            return metrics.frame_work(st, W, H, len(s0.spherePrimitives), len(s0.patches), flags, fused=fused_,
+                                      sep=sep, n_planes=len(s0.circlePlanePrimitives),
+                                      n_cyls=len(s0.cappedCylinderPrimitives),
+                                      perspective=eye.type_ == sc.PERSPECTIVE,
+                                      search=sep and os.environ.get("RTM_SEP_MODE", "2") == "2",
+                                      n_sdfs=len(s0.sdfPrimitives), map_texel_bytes=map_bytes,
+                                      moving=(shadow.dirNormalized[0] * 0.03 != 0.0
+                                              or shadow.dirNormalized[1] * 0.03 != 0.0))
+
+        work = frame_work(fused)
+        if alt_fused is not None and band_h == H:
+            # the fused frame is one kernel (the eye pass evaluating the shadow texels its
+            # hit pixels read): its algorithmic bytes and ops per frame over its wall time
+            # per frame in the same run
+            rf = dict(metrics.roofline("eye_pass", frame_work(True), alt_fused["ms_per_frame"]))
+            rf.pop("traffic", None)
+            rf["kernel"] = "frame (fused shadow: one eye-pass kernel per frame)"
+            rf["note"] = ("algorithmic bytes per frame (16 B/px store, no map) / wall time per frame "
+                          f"of the alt_fused_shadow run ({alt_fused['lanes']} lanes); PMC: profiles/*pmc_fused*")
+            alt_fused["roofline_frame"] = rf
         if band_h != H:  # rank 0 renders one band: scale the frame's work to it (approximate)
             for kk in work.values():
                 kk["ops"] = int(kk["ops"] * band_h / H)

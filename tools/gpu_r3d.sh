@@ -18,12 +18,9 @@ run() {
 for r in 1 2; do
   for c in ${CFGS:-7}; do
     CFG=$c
-    run c${c}_base_$r X=1
-    run c${c}_hwq8_$r GPU_MAX_HW_QUEUES=8
-    run c${c}_hwq16_$r GPU_MAX_HW_QUEUES=16
-    run c${c}_copystream_$r RTM_BATCH_COPY=stream
-    run c${c}_hwq8_copystream_$r GPU_MAX_HW_QUEUES=8 RTM_BATCH_COPY=stream
-    run c${c}_lanes1_$r RTM_LANES=1
+    for v in ${VARIANTS:-X=1}; do
+      run c${c}_${v//[=,]/_}_$r $v
+    done
   done
 done
 echo done
