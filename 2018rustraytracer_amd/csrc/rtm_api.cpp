@@ -689,10 +689,28 @@ struct TimingSlot {
 // its previous upload has completed (copied[j]), its device side once the
 // kernels that read it have run (used[j]); the upload runs on its own stream, so
 // batch i+1's table crosses PCIe while batch i renders.
+// How a batch's frame table reaches the device (RTM_BATCH_COPY, A/B): "pull" (default)
+// a kernel on the lane's stream reads the pinned slot; "copy" hipMemcpyAsync on a
+// copy stream with event waits both ways (round 2 until r02_v9); "stream"
+// hipMemcpyAsync on the lane's stream.  Past a few tens of KB the async copy goes to a
+// copy engine: 8 frames per launch at 3840x2160 (32 KB) ran at 91 instead of 248
+// Gpix/s with kernels of the same duration (profiles/r02_ab_batch_pull.txt).
+enum { UPLOAD_PULL, UPLOAD_COPY_STREAM, UPLOAD_LANE_STREAM };
+int batch_upload_mode() {
+    static const int m = [] {
+        const char* e = getenv("RTM_BATCH_COPY");
+        if (e && std::string(e) == "copy") return (int)UPLOAD_COPY_STREAM;
+        if (e && std::string(e) == "stream") return (int)UPLOAD_LANE_STREAM;
+        return (int)UPLOAD_PULL;
+    }();
+    return m;
+}
+
 struct BatchRing {
     static constexpr int R = 4;
     hipStream_t copy = nullptr;
     void* host[R] = {};
+    void* host_dev[R] = {};  // the pinned host slot's device address (the pull kernel reads it)
     size_t host_bytes[R] = {};
     DevBuf dev[R];
     hipEvent_t copied[R] = {}, used[R] = {};
@@ -1146,30 +1164,28 @@ int ensure_lanes(rtm_ctx* ctx, int L) {
     return RTM_OK;
 }
 
-// Frames per launch of a frame sequence (profiles/r02_ab_batch.txt).  One frame
-// per launch leaves small frames bound by the host's per-frame launches
-// (512x512: 12 Gpix/s at one frame per launch, 43 at 16; 1920x1080: 123 at 1, 181
-// at 4, tools/probes/batch_probe.py), and a big frame's two kernels pay a ramp and
-// a tail each.  Auto: below 1 Mpixel 32 Mpixel worth of frames, at most 64
-// (main()'s own scene, raytracingPlane0 at 512x512: 50.7 Gpix/s at 16 on one
-// lane, 80 at 64 on two); 1-4 Mpixel 8 Mpixel worth, at most 16 (1920x1080: 4;
-// 8 and 16 were no faster); 4-16 Mpixel 32 Mpixel worth (3840x2160: 4 frames, each
-// frame's shadow pass 13.4 instead of 16.2 us, its eye pass 21.7 instead of 25.1,
-// 244 -> 251-256 Gpix/s; ray-traced frames with the batched per-wave primitive cull
-// eye 90 -> 83 us per frame; SDF frames neutral); from 16 Mpixel 64 Mpixel worth
-// (7680x4320: 2 frames on 3 lanes, config 4 260 -> 270-273 Gpix/s in three runs,
-// config 5 neutral).  rtm_ctx_set_batch / RTM_BATCH override (1 = one frame per
-// launch).
+// Frames per launch of a frame sequence (profiles/r02_ab_batch.txt,
+// r02_ab_batch_pull.txt).  One frame per launch leaves small frames bound by the
+// host's per-frame launches (512x512: 12 Gpix/s at one frame per launch, 43 at 16;
+// 1920x1080: 123 at 1, 181 at 4, tools/probes/batch_probe.py), and a big frame's two
+// kernels pay a ramp and a tail each (3840x2160 at 4 frames: each frame's shadow pass
+// 13.4 instead of 16.2 us, its eye pass 21.7 instead of 25.1).  Until r02_v10 the rule
+// was 8 Mpixel worth from 1 to 4 Mpixel and 32 Mpixel worth from 4 to 16: bigger
+// tables went through a copy engine.  rtm_ctx_set_batch / RTM_BATCH override (1 = one
+// frame per launch).
 int frame_batch(int32_t req, int32_t W, int32_t H) {
     static const int env = [] {
         const char* e = getenv("RTM_BATCH");
         return e ? atoi(e) : 0;
     }();
     const int64_t px = (int64_t)W * H;
-    // below 1 Mpixel 32 Mpixel worth, at most 64 (512x512: 64 frames per launch);
-    // from 16 Mpixel 64 Mpixel worth (7680x4320: 2 frames per launch, on 3 lanes)
-    const int64_t target = px >= (16LL << 20) ? (64LL << 20)
-                           : (px >= (4LL << 20) || px < (1LL << 20)) ? (32LL << 20) : (8LL << 20);
+    // 64 Mpixel worth of frames, at most 64 below 1 Mpixel (512x512: 64 frames per
+    // launch) and 16 above (1920x1080: 16, 3840x2160: 8, 7680x4320: 2).  With the
+    // batch table pulled by the lane's stream (r02_v10) bigger batches pay: 3840x2160
+    // 250 -> 262 Gpix/s at 8 frames, 1920x1080 218 -> 248 at 16; with the async copy
+    // the larger table went to a copy engine and 8 frames ran at 91-150 Gpix/s
+    // (profiles/r02_ab_batch_pull.txt).
+    const int64_t target = 64LL << 20;
     const int64_t cap = px < (1LL << 20) ? 64 : 16;
     int B = req > 0 ? req : env > 0 ? env : (int)std::max<int64_t>(1, std::min<int64_t>(cap, target / px));
     return std::max(1, std::min(B, 64));
@@ -1194,7 +1210,7 @@ int enqueue_batch(rtm_ctx* ctx, int lane, FrameArgs* fa, const FrameExtra* ex, v
     if (!brp) {
         std::unique_ptr<BatchRing> b(new BatchRing);
         b->device = ctx->device;
-        HIP_TRY(hipStreamCreateWithFlags(&b->copy, hipStreamNonBlocking));
+        if (batch_upload_mode() == UPLOAD_COPY_STREAM) HIP_TRY(hipStreamCreateWithFlags(&b->copy, hipStreamNonBlocking));
         for (int j = 0; j < BatchRing::R; ++j) {
             HIP_TRY(hipEventCreateWithFlags(&b->copied[j], hipEventDisableTiming));
             HIP_TRY(hipEventCreateWithFlags(&b->used[j], hipEventDisableTiming));
@@ -1250,6 +1266,7 @@ int enqueue_batch(rtm_ctx* ctx, int lane, FrameArgs* fa, const FrameExtra* ex, v
         br.host_bytes[j] = 0;
         HIP_TRY(hipHostMalloc(&br.host[j], bytes, hipHostMallocDefault));
         br.host_bytes[j] = bytes;
+        HIP_TRY(hipHostGetDevicePointer(&br.host_dev[j], br.host[j], 0));
     }
     if (br.dev[j].bytes < bytes) {
         HIP_TRY(hipEventSynchronize(br.used[j]));  // no kernel still reads the old device slot
@@ -1303,11 +1320,14 @@ int enqueue_batch(rtm_ctx* ctx, int lane, FrameArgs* fa, const FrameExtra* ex, v
     }
     t0.fmt = fmt;
     hp.next(HostProf::UPLOAD);
-    static const bool copy_stream = [] {  // RTM_BATCH_COPY=stream: upload on the lane's own stream (A/B)
-        const char* e = getenv("RTM_BATCH_COPY");
-        return !(e && std::string(e) == "stream");
-    }();
-    if (copy_stream) {
+    const int mode = batch_upload_mode();
+    if (mode == UPLOAD_PULL) {
+        // the lane's stream pulls the table from the pinned slot: in stream order after the
+        // lane's earlier batches (the previous readers of this device slot), and copied[j]
+        // tells the host when the slot may be refilled
+        if ((rc = launch_pull(br.host_dev[j], bytes, db, s))) return fail(rc, "batch table pull failed");
+        HIP_TRY(hipEventRecord(br.copied[j], s));
+    } else if (mode == UPLOAD_COPY_STREAM) {
         HIP_TRY(hipStreamWaitEvent(br.copy, br.used[j], 0));  // the device slot is free
         HIP_TRY(hipMemcpyAsync(db, hb, bytes, hipMemcpyHostToDevice, br.copy));
         HIP_TRY(hipEventRecord(br.copied[j], br.copy));

@@ -327,6 +327,8 @@ bool shadow_batchable(const ShadowPart& sh);
 // arguments carry the bytes (<= 3968 per launch), so the host copy is consumed
 // at launch: no pinned staging, no host synchronisation.  bytes % 8 == 0.
 int launch_upload(const void* src, size_t bytes, void* dst, void* stream);
+// bytes (a multiple of 16, 16-byte aligned) from pinned, device-accessible host memory
+int launch_pull(const void* src_host, size_t bytes, void* dst, void* stream);
 // Software-pipelined frame step: the shadow pass of a.sh into smap_w and the eye
 // pass of a.ey (the previous frame) from smap_r into out, in ONE launch whose
 // workgroups interleave the two roles (VALU-bound and HBM-store-bound tiles

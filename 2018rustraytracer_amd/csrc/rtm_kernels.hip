@@ -1860,6 +1860,14 @@ __global__ void upload_kernel(const UploadChunk k, uint64_t* __restrict__ dst, i
     for (int i = threadIdx.x; i < n; i += blockDim.x) dst[i] = k.w[i];
 }
 
+// launch_pull: a batch table pulled from pinned host memory by the device, in the
+// lane's stream order (16 bytes per thread, vector loads over PCIe, vector stores):
+// one launch instead of an async copy, which goes to a copy engine (with its
+// cross-queue waits) once the table passes a few tens of KB.
+__global__ __launch_bounds__(BLOCK) void pull_kernel(const uint4* __restrict__ src, uint4* __restrict__ dst, int n) {
+    for (int i = blockIdx.x * BLOCK + threadIdx.x; i < n; i += gridDim.x * BLOCK) dst[i] = src[i];
+}
+
 // Per-wave primitive masks of an eye pass under a PERSPECTIVE eye (RT 3): the
 // cone cull of rt_wave_mask, one thread per wave of the eye pass (wave (bx, yl):
 // pixels bx*64 .. bx*64+63 of row row_begin + yl), so the cone set-up and the
@@ -2494,6 +2502,16 @@ int launch_eye_batch(const BatchFrame* dev, int n, const FrameArgs& a0, const De
     else RTM_EBF(RTM_FORMAT_RGBA32F);
 #undef RTM_EBF
 #undef RTM_EB
+    return launched();
+}
+
+int launch_pull(const void* src_host, size_t bytes, void* dst, void* stream) {
+    if (bytes % 16 || ((uintptr_t)src_host & 15) || ((uintptr_t)dst & 15)) return RTM_ERR_INVALID;
+    const int n = (int)(bytes / 16);
+    if (n == 0) return 0;
+    const int blocks = std::min((n + BLOCK - 1) / BLOCK, 64);
+    hipLaunchKernelGGL(pull_kernel, dim3((unsigned)blocks), dim3(BLOCK), 0, (hipStream_t)stream,
+                       (const uint4*)src_host, (uint4*)dst, n);
     return launched();
 }
 

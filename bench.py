@@ -379,13 +379,13 @@ def main():
     # and batch (several frames per launch, rtm_ctx_set_batch: frames of one launch need
     # distinct outputs; batch b runs on lane (n_batches-1-b) % L, so the ring must be a
     # multiple of frames-per-launch x lanes): 48 frames from 4 Mpixel up (the auto
-    # batches of 1-4 frames on 1-3 lanes; 25 GB at 7680x4320, of 288 GB), 128 below
+    # batches of 2-8 frames on 2-3 lanes; 25 GB at 7680x4320, of 288 GB), 128 below
     # (batches of up to 64 frames on 2 lanes)
     lanes_env = int(os.environ.get("RTM_LANES", "0") or 0)
     batch_env = int(os.environ.get("RTM_BATCH", "0") or 0)
     n_ring = 48 if W * H >= (4 << 20) else 128
     if lanes_env > 0 or batch_env > 0:
-        m = max(lanes_env, 1) * max(batch_env, 1)
+        m = (lanes_env if lanes_env > 0 else 3 if W * H >= (16 << 20) else 2) * max(batch_env, 1)
         n_ring = n_ring if n_ring % m == 0 else m * ((n_ring + m - 1) // m)
     ring = ([torch.empty((H, W, 4), dtype=torch.float32, device=f"cuda:{local}") for _ in range(n_ring)]
             if not tile_mode else [])

@@ -239,10 +239,9 @@ int rtm_ctx_last_lanes(rtm_ctx* ctx, int32_t* lanes);
  * the same patches share ONE launch per pass (the frame index is the grid's z
  * dimension; each frame's constants come from a table uploaded per batch), so
  * small frames stop paying a launch per pass per frame.  0 = auto (RTM_BATCH
- * from the environment, else as many frames as make 32 Mpixel below 1 Mpixel
- * (at most 64: 64 at 512x512), 8 Mpixel from 1 to 4 Mpixel (at most 16: 4 at
- * 1920x1080), 32 Mpixel from 4 Mpixel up (4 at 3840x2160) and 64 Mpixel from
- * 16 Mpixel up (2 at 7680x4320));
+ * from the environment, else as many frames as make 64 Mpixel, at most 64 below
+ * 1 Mpixel (64 at 512x512) and 16 from 1 Mpixel up (16 at 1920x1080, 8 at
+ * 3840x2160, 2 at 7680x4320));
  * 1 = one frame per launch; at most 64.  Frames with overlapping outputs never share a launch (a repeated output
  * pointer still ends with the later frame).  Batches are spread over the lanes.  Kernel durations of
  * rtm_ctx_kernel_ms_history are then per launch, i.e. per batch;

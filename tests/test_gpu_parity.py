@@ -630,16 +630,16 @@ def test_set_batch_api(rtm, gpu_ctx):
 
 @pytest.mark.parametrize("kind", ["spheres", "raytraced"])
 def test_auto_batch_at_4k(rtm, scenes, gpu_ctx, kind):
-    """The auto frames-per-launch rule at 3840x2160: 4 frames share a launch (2
+    """The auto frames-per-launch rule at 3840x2160: 8 frames share a launch (2
     lanes), spheres + patches or ray-traced primitives alike; every frame ==
     rtm_render bit for bit."""
     import torch
     w, h, k = 3840, 2160, 64
     eye, sh = scenes.eye_camera(), scenes.shadow_camera()
     if kind == "spheres":
-        frames = [scenes.scene_a_bench(100 + i) for i in range(8)]
+        frames = [scenes.scene_a_bench(100 + i) for i in range(16)]
     else:
-        frames = [scenes.mixed_rt(10 * i) for i in range(8)]
+        frames = [scenes.mixed_rt(10 * i) for i in range(16)]
     outs = [torch.empty((h, w, 4), dtype=torch.float32, device="cuda") for _ in frames]
     try:
         gpu_ctx.set_batch(0)
@@ -647,7 +647,7 @@ def test_auto_batch_at_4k(rtm, scenes, gpu_ctx, kind):
         torch.cuda.synchronize()
         gpu_ctx.render_frames_async(frames, eye, sh, w, h, k, 0, [o.data_ptr() for o in outs])
         gpu_ctx.synchronize()
-        assert gpu_ctx.last_batch() == 4
+        assert gpu_ctx.last_batch() == 8
         assert gpu_ctx.last_lanes() == 2
         for s, o in zip(frames, outs):
             assert bits_equal(o.cpu().numpy(), rtm.render_frame(s, eye, sh, w, h, k)), "frame differs"
