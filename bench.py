@@ -409,12 +409,14 @@ def main():
         outp = [ring[i % n_ring].data_ptr() for i in range(max(nW, nS, 1))]
 
     # clock ramp: frames for at least --preroll-ms of wall time before the counted warmup
+    # (in chunks of one step, so its launches carry full batches like the timed ones: the
+    # PMC passes average a kernel's counters over all of its launches)
     preroll_frames, t_pre = 0, time.perf_counter()
+    n_pre = min(F, total)
+    pre = ctx.prepare_frames(scenes[:n_pre]) if sequence and not tile_mode else None
     while (time.perf_counter() - t_pre) * 1e3 < a.preroll_ms and not tile_mode:
-        n_pre = min(20, total)
         if sequence:
-            ctx.render_frames_async([0] * n_pre, eye, shadow, W, H, K, flags, outp[:n_pre],
-                                    ctx.prepare_frames(scenes[:n_pre]))
+            ctx.render_frames_async([0] * n_pre, eye, shadow, W, H, K, flags, outp[:n_pre], pre)
         else:
             for i in range(n_pre):
                 frames_step(i)
@@ -494,8 +496,8 @@ def main():
                     "note": "HIP-event kernel durations in the timed region, kernels of other lanes alongside"}
         n1 = min(nS, 400)
         ctx.set_lanes(1)
-        ctx.render_frames_async([0] * min(nW, 50), eye, shadow, W, H, K, flags, outp[:min(nW, 50)],
-                                ctx.prepare_frames(scenes[:min(nW, 50)]))
+        ctx.render_frames_async([0] * min(nW, F), eye, shadow, W, H, K, flags, outp[:min(nW, F)],
+                                ctx.prepare_frames(scenes[:min(nW, F)]))
         ctx.set_timing_capacity(max(1, n1 // timing_stride))
         one = ctx.prepare_frames(scenes[nW:nW + n1])
         outs_one = ctx.out_array(outp[:n1])
@@ -523,8 +525,8 @@ def main():
     if sequence and not pipelined and not a.no_alt and not fused:
         fflags = flags | rtm.abi.RTM_FLAG_FUSED_SHADOW
         ctx.set_timing_capacity(max(1, nS // timing_stride))
-        ctx.render_frames_async([0] * min(nW, 5), eye, shadow, W, H, K, fflags, outp[:min(nW, 5)],
-                                ctx.prepare_frames(scenes[:min(nW, 5)]))
+        ctx.render_frames_async([0] * min(nW, F), eye, shadow, W, H, K, fflags, outp[:min(nW, F)],
+                                ctx.prepare_frames(scenes[:min(nW, F)]))
         barrier()
         ctx.set_timing_stride(timing_stride)
         t1 = time.perf_counter()
