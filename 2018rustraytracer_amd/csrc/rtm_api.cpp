@@ -1134,7 +1134,11 @@ int frame_lanes(int32_t req, int32_t n, int32_t W, int32_t H, float* const* out,
         const char* e = getenv("RTM_LANES");
         return e ? atoi(e) : 0;
     }();
-    int L = req > 0 ? req : env > 0 ? env : ((int64_t)W * H >= (16LL << 20) ? 3 : 2);
+    // auto: 4 lanes below 16 Mpixel, 3 from 16 Mpixel up.  With the batch tables pulled
+    // by the lanes (r02_v10), more lanes pay: 3840x2160 263 -> 276 Gpix/s at 4 (274-276
+    // at 3, 268-273 at 6), 1920x1080 259 -> 267 (3 and 4), 512x512 119 -> 141,
+    // 7680x4320 best at 3 (profiles/r02_ab_lanes_v12.txt)
+    int L = req > 0 ? req : env > 0 ? env : ((int64_t)W * H >= (16LL << 20) ? 3 : 4);
     const int32_t nb = (n + B - 1) / B;  // batches of B frames; batch b runs on lane (nb-1-b) % L
     if (L > 8) L = 8;
     if (L > nb) L = nb;

@@ -385,9 +385,11 @@ def main():
     lanes_env = int(os.environ.get("RTM_LANES", "0") or 0)
     batch_env = int(os.environ.get("RTM_BATCH", "0") or 0)
     n_ring = 48 if W * H >= (4 << 20) else 128
-    if lanes_env > 0 or batch_env > 0:
-        m = (lanes_env if lanes_env > 0 else 3 if W * H >= (16 << 20) else 2) * max(batch_env, 1)
-        n_ring = n_ring if n_ring % m == 0 else m * ((n_ring + m - 1) // m)
+    # the library's auto rules (rtm_api.cpp frame_lanes / frame_batch), for overrides of one
+    lanes_auto = 3 if W * H >= (16 << 20) else 4
+    batch_auto = max(1, min(64 if W * H < (1 << 20) else 16, (64 << 20) // (W * H)))
+    m = (lanes_env if lanes_env > 0 else lanes_auto) * (batch_env if batch_env > 0 else batch_auto)
+    n_ring = n_ring if n_ring % m == 0 else m * ((n_ring + m - 1) // m)
     ring = ([torch.empty((H, W, 4), dtype=torch.float32, device=f"cuda:{local}") for _ in range(n_ring)]
             if not tile_mode else [])
     sequence = not tile_mode and not a.per_frame_calls

@@ -228,7 +228,7 @@ int rtm_ctx_kernel_ms_history(rtm_ctx* ctx, float* shadow_pass_ms, float* eye_pa
 /* Lanes of rtm_render_frames_async: independent frames spread over `lanes`
  * streams of the context (own shadow map each), so one frame's kernels run
  * beside another's; the call still completes in ctx's stream order.  0 = auto
- * (RTM_LANES from the environment, else 2; 3 from 16 Mpixel up);
+ * (RTM_LANES from the environment, else 4; 3 from 16 Mpixel up);
  * 1 = strictly one frame after another; at most 8.  With several lanes the
  * kernel durations of rtm_ctx_kernel_ms_history overlap (each is the kernel's
  * time beside the other lanes).  rtm_ctx_last_lanes: lanes the last
