@@ -1223,7 +1223,13 @@ int enqueue_batch(rtm_ctx* ctx, int lane, FrameArgs* fa, const FrameExtra* ex, v
     }
     BatchRing& br = *brp;
     const bool fused = (fa[0].ey.flags & RTM_FLAG_FUSED_SHADOW) != 0;
-    const int32_t sfmt = fused ? SMAP_F64 : shadow_map_format(fa[0].sh);
+    // One storage for the whole launch (the batched shadow kernel is instantiated per
+    // storage), so it must hold every frame's codes: steps + the most spheres of any
+    // frame (frames of a batch may differ in sphere count; a byte map chosen for
+    // frame 0 alone would truncate a later frame's sphere codes).
+    ShadowPart widest = fa[0].sh;
+    for (int k = 1; k < n; ++k) widest.n_spheres = std::max(widest.n_spheres, fa[k].sh.n_spheres);
+    const int32_t sfmt = fused ? SMAP_F64 : shadow_map_format(widest);
     for (int k = 0; k < n; ++k) {
         fa[k].sh.smap_fmt = sfmt;
         fa[k].sh.smap_bw = (fa[k].sh.W + 127) / 128;

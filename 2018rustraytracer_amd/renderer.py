@@ -231,11 +231,30 @@ def _host_frame(height: int, width: int, fmt: int) -> np.ndarray:
     return np.empty((height, width, abi.FORMAT_BYTES[fmt]), np.uint8)
 
 
+def _check_host_out(out, height: int, width: int, fmt: int) -> np.ndarray:
+    """A caller-supplied host frame: the C side writes width*height*bytes(fmt)
+    contiguous bytes through its base pointer, so a short, strided or mistyped
+    buffer would be overrun or scattered.  Raise instead."""
+    if fmt not in abi.FORMAT_BYTES:
+        raise ValueError(f"unknown output format {fmt}")
+    if not isinstance(out, np.ndarray):
+        raise ValueError("out must be a numpy array")
+    want = np.float32 if fmt == abi.RTM_FORMAT_RGBA32F else np.uint8
+    if out.dtype != want:
+        raise ValueError(f"out has dtype {out.dtype}, format {fmt} needs {np.dtype(want)}")
+    if not out.flags.c_contiguous:
+        raise ValueError("out must be C-contiguous")
+    need = width * height * abi.FORMAT_BYTES[fmt]
+    if out.nbytes < need:
+        raise ValueError(f"out holds {out.nbytes} bytes, the frame needs {need}")
+    return out
+
+
 def render_frame_ex(scene: Scene, eye: Camera, shadow: Camera, width: int, height: int, steps: int,
                     flags: int = 0, fmt: int = abi.RTM_FORMAT_RGBA32F, n_gpus: int = 0, out=None) -> np.ndarray:
     """rtm_render_ex (n_gpus == 0) or rtm_render_multi_ex: the frame in output format
     `fmt` into host memory: (H, W, 4) f32, (H, W, 4) u8 (RGBA8) or (H, W, 3) u8 (RGB8)."""
-    out = _host_frame(height, width, fmt) if out is None else out
+    out = _host_frame(height, width, fmt) if out is None else _check_host_out(out, height, width, fmt)
     sc, keep = scene.to_c()
     e, s = eye.to_c(), shadow.to_c()
     lib = _lib()
@@ -329,6 +348,8 @@ class Group:
         """rtm_group_render_frames_async: frame i into out_ptrs[i] (ignored off the root)."""
         arr, keep = prepared if prepared is not None else Context.prepare_frames(None, scenes)
         n = len(arr)
+        if len(out_ptrs) != n:
+            raise ValueError(f"{len(out_ptrs)} output pointers for {n} frames")
         outs = (C.c_void_p * n)(*[C.c_void_p(p or 0) for p in out_ptrs])
         e, s = eye.to_c(), shadow.to_c()
         lib = _lib()
@@ -349,10 +370,7 @@ class Group:
                flags: int = 0, fmt: int = abi.RTM_FORMAT_RGBA32F, out=None):
         """rtm_group_render: the tile-partitioned, gathered frame in host memory
         (blocking): (H, W, 4) float32 for RGBA32F, (H, W, 4|3) uint8 for RGBA8 / RGB8."""
-        import numpy as np
-        if out is None:
-            out = (np.empty((height, width, 4), np.float32) if fmt == abi.RTM_FORMAT_RGBA32F
-                   else np.empty((height, width, 4 if fmt == abi.RTM_FORMAT_RGBA8 else 3), np.uint8))
+        out = _host_frame(height, width, fmt) if out is None else _check_host_out(out, height, width, fmt)
         sc, keep = scene.to_c()
         e, s = eye.to_c(), shadow.to_c()
         lib = _lib()

@@ -350,12 +350,14 @@ def test_pipelined_frames_differing_patches_fallback(rtm, scenes, gpu_ctx):
     _frames_vs_single(rtm, scenes, gpu_ctx, frames, scenes.eye_camera(), scenes.shadow_camera(), 640, 360, 64)
 
 
-@pytest.mark.parametrize("lanes", [1, 2, 3, 4])
-def test_frame_lanes_in_subprocess(rtm, scenes, lanes):
+@pytest.mark.parametrize("lanes,batch", [(1, 1), (2, 1), (3, 1), (4, 1), (3, 2), (4, 2)])
+def test_frame_lanes_in_subprocess(rtm, scenes, lanes, batch):
     """RTM_LANES=n (read once per process): the frame sequence spread over n
     streams, each with its own shadow map, == frame-by-frame rtm_render; the
     context's shadow map then holds the LAST frame's shadow pass; a sequence whose
-    frames share one output falls back to one lane (the last frame's image wins)."""
+    frames share one output falls back to one lane (the last frame's image wins).
+    Lanes spread batches, so the batch is fixed (1 or 2 frames per launch: 8 or 4
+    batches of the 8 frames) and the lane count the call used is asserted."""
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -367,6 +369,7 @@ rtm = importlib.import_module("2018rustraytracer_amd")
 sc = importlib.import_module("2018rustraytracer_amd.scenes")
 eye, sh = sc.eye_camera(), sc.shadow_camera()
 ctx = rtm.Context(0)
+ctx.set_batch(BATCH)
 w, h, k = 960, 540, 64
 frames = [sc.scene_a_bench(100 + 5 * i) for i in range(7)] + [sc.scene_b()]
 u32 = lambda a: a.view(np.uint32)
@@ -374,6 +377,8 @@ outs = [torch.empty((h, w, 4), dtype=torch.float32, device="cuda") for _ in fram
 torch.cuda.synchronize()
 ctx.render_frames_async(frames, eye, sh, w, h, k, 0, [o.data_ptr() for o in outs])
 ctx.synchronize()
+assert ctx.last_lanes() == LANES, (ctx.last_lanes(), LANES)
+assert ctx.last_batch() == BATCH, (ctx.last_batch(), BATCH)
 last_map = torch.empty((h, w), dtype=torch.float64, device="cuda")
 hip = ctypes.CDLL("libamdhip64.so")
 hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
@@ -391,8 +396,9 @@ torch.cuda.synchronize()
 ctx.render_frames_async(frames, eye, sh, w, h, k, 0, [shared.data_ptr()] * len(frames))
 ctx.synchronize()
 assert np.array_equal(u32(shared.cpu().numpy()), u32(rtm.render_frame(frames[-1], eye, sh, w, h, k, 0)))
+assert ctx.last_lanes() == 1
 print("lanes ok")
-''' % root
+'''.replace("LANES", str(lanes)).replace("BATCH", str(batch)) % root
     env = dict(os.environ, RTM_LANES=str(lanes))
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0 and "lanes ok" in r.stdout, r.stdout + r.stderr
@@ -630,9 +636,10 @@ def test_set_batch_api(rtm, gpu_ctx):
 
 @pytest.mark.parametrize("kind", ["spheres", "raytraced"])
 def test_auto_batch_at_4k(rtm, scenes, gpu_ctx, kind):
-    """The auto frames-per-launch rule at 3840x2160: 8 frames share a launch (2
-    lanes), spheres + patches or ray-traced primitives alike; every frame ==
-    rtm_render bit for bit."""
+    """The auto frames-per-launch rule at 3840x2160: 8 frames share a launch; 16
+    frames make 2 batches, so 2 of the auto 4 lanes run (the full 4-lane headline
+    is pinned to the oracle in test_headline_mode.py), spheres + patches or
+    ray-traced primitives alike; every frame == rtm_render bit for bit."""
     import torch
     w, h, k = 3840, 2160, 64
     eye, sh = scenes.eye_camera(), scenes.shadow_camera()
