@@ -12,7 +12,7 @@ _PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 # RTM_LIB: another build of the same library (A/B timing runs only, tools/ab_bench.py)
 LIB_PATH = os.environ.get("RTM_LIB") or os.path.join(_PKG_DIR, "librtm.so")
 
-RTM_ABI_VERSION = 8
+RTM_ABI_VERSION = 9
 RTM_MAX_SPHERES = 16
 RTM_MAX_PATCHES = 4
 RTM_MAX_CIRCLE_PLANES = 16
@@ -169,6 +169,8 @@ ABI_SYMBOLS = [
     ("rtm_group_stream", _P, [_P]),
     ("rtm_group_synchronize", C.c_int, [_P, _I32]),
     ("rtm_group_set_root_staging", C.c_int, [_P, _I32]),
+    ("rtm_group_create_loopback", C.c_int, [_I32, C.POINTER(_I32), C.POINTER(_P)]),
+    ("rtm_group_set_host_direct", C.c_int, [_P, _I32]),
     ("rtm_viewport_create", C.c_int, [_P, _I32, _I32, _I32, C.POINTER(rtm_camera), C.POINTER(_P)]),
     ("rtm_viewport_destroy", None, [_P]),
     ("rtm_viewport_rasterize", C.c_int, [_P, C.POINTER(rtm_scene)]),

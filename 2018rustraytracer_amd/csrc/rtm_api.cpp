@@ -785,6 +785,8 @@ struct rtm_ctx {
     int64_t tab_nt = 0, tab_nz = 0, tab_nd = 0;
     int32_t tab_w = 0, tab_h = 0, tab_np = 0, tab_zmono = 0;
     double tab_z0 = 0.0;
+    double tab_inv_sz = 0.0;
+    int64_t tab_rec = -1;  // offset (doubles) of the coded tile's records, -1: none
     bool tab_hast = false, tab_sep = false;
 };
 
@@ -846,6 +848,9 @@ bool separable(const rtm_camera* c, int32_t W, std::vector<double>& colx, double
 
 inline bool in01(double v) { return std::fabs(v - 0.5) <= 0.5; }
 
+// An f32 index-guess term of the coded shadow tile, clamped to +-2^24 (NaN -> 0).
+inline double guess_term(double v) { return v != v ? 0.0 : std::min(std::max(v, -16777216.0), 16777216.0); }
+
 // Build (or reuse) the context's lookup tables for (steps, W, H, march camera, patches).
 int ensure_tables(rtm_ctx* ctx, int32_t steps, int32_t W, int32_t H, const rtm_camera* march_cam,
                   const PatchK* patches, int32_t n_patches, Tables* out) {
@@ -889,7 +894,11 @@ int ensure_tables(rtm_ctx* ctx, int32_t steps, int32_t W, int32_t H, const rtm_c
         const int64_t nsep = with_sep ? (int64_t)H + 2 * (int64_t)n_patches * W : 0;
         const int64_t nd = nt + W + H + nz + nsep;
         const int64_t nok = with_sep ? (int64_t)W + H : 0;
-        std::vector<double> h((size_t)nd + (size_t)(nok + 1) / 2);
+        // the coded shadow tile's records (rtm_kernels.h ZRecK / ColRecK / RowRecK), 32-byte aligned
+        const bool with_rec = with_sep && zmono != 0 && nt >= 1;
+        const int64_t rec_at = ((nd + (nok + 1) / 2) + 3) / 4 * 4;
+        const int64_t nrec = with_rec ? 4 * (nt + 1) + 4 * (int64_t)n_patches * W + 2 * (int64_t)H : 0;
+        std::vector<double> h((size_t)(with_rec ? rec_at + nrec : nd + (nok + 1) / 2));
         double t = 0.0;  // raymarchPatch: t = 0.0; ... t += magnitudeOfStepsize (main.rs:2237, 2273)
         for (int64_t k = 0; k < nt; ++k) {
             h[(size_t)k] = t;
@@ -920,6 +929,47 @@ int ensure_tables(rtm_ctx* ctx, int32_t steps, int32_t W, int32_t H, const rtm_c
                 }
             }
         }
+        if (with_rec) {
+            const double* py = &h[(size_t)(nt + W + H + nz)];
+            const double* d0 = py + H;
+            const double* dd = d0 + (int64_t)n_patches * W;
+            const int32_t* ok = (const int32_t*)&h[(size_t)nd];
+            ZRecK* zr = reinterpret_cast<ZRecK*>(&h[(size_t)rec_at]);
+            ColRecK* cr = reinterpret_cast<ColRecK*>(zr + nt + 1);
+            RowRecK* rr = reinterpret_cast<RowRecK*>(cr + (int64_t)n_patches * W);
+            const double past = zmono > 0 ? INFINITY : -INFINITY;  // compares as "past the surface"
+            for (int64_t k = 0; k <= nt; ++k) {
+                zr[k].zprev = zt[(size_t)(k > 0 ? k - 1 : 0)];
+                zr[k].z = k < nt ? zt[(size_t)k] : past;
+                zr[k].t = k < nt ? h[(size_t)k] : INFINITY;
+                zr[k].pad = 0.0;
+            }
+            const double inv_sz = 1.0 / sz;
+            for (int32_t k = 0; k < n_patches; ++k)
+                for (int32_t i = 0; i < W; ++i) {
+                    ColRecK& c = cr[(int64_t)k * W + i];
+                    c.d0 = d0[(int64_t)k * W + i];
+                    c.dd = dd[(int64_t)k * W + i];
+                    if (!ok[i]) {
+                        // a column outside inRange01 never hits (main.rs:2249): a finite
+                        // surface depth "before the start" for the table's direction makes
+                        // the tile's check neither hit nor go slow there (see the kernel)
+                        c.d0 = zmono > 0 ? -1.0e300 : 1.0e300;
+                        c.dd = 0.0;
+                    }
+                    // bounded and finite, so the kernel's f32 -> int conversion of
+                    // g0 + g1*pyf is always defined (|pyf| <= 4 below)
+                    c.g0 = (float)guess_term((c.d0 - z0) * inv_sz + 1.0);
+                    c.g1 = (float)guess_term(c.dd * inv_sz);
+                    c.ok = ok[i];
+                    c.pad = 0;
+                }
+            for (int32_t j = 0; j < H; ++j) {
+                rr[j].py = py[j];
+                rr[j].pyf = py[j] != py[j] ? 0.0f : (float)std::min(std::max(py[j], -4.0), 4.0);  // a guess term
+                rr[j].ok = ok[W + j];
+            }
+        }
         HIP_TRY(hipStreamSynchronize(ctx->stream));  // earlier launches may still read the old tables
         for (auto& l : ctx->lanes) HIP_TRY(hipStreamSynchronize(l->stream));
         int rc = ctx->tabs.ensure(h.size() * sizeof(double), ctx->device);
@@ -936,6 +986,8 @@ int ensure_tables(rtm_ctx* ctx, int32_t steps, int32_t W, int32_t H, const rtm_c
         ctx->tab_np = n_patches;
         ctx->tab_zmono = zmono;
         ctx->tab_z0 = nz ? zt[0] : 0.0;
+        ctx->tab_rec = with_rec ? rec_at : -1;
+        ctx->tab_inv_sz = nz ? 1.0 / sz : 0.0;
     }
     const double* base = (const double*)ctx->tabs.p;
     const int64_t nt2 = ctx->tab_nt, nz2 = ctx->tab_nz;
@@ -945,6 +997,7 @@ int ensure_tables(rtm_ctx* ctx, int32_t steps, int32_t W, int32_t H, const rtm_c
     out->z = nz2 ? base + nt2 + W + H : nullptr;
     out->zmono = nz2 ? ctx->tab_zmono : 0;
     out->z0 = nz2 ? ctx->tab_z0 : 0.0;
+    out->inv_sz = nz2 ? ctx->tab_inv_sz : 0.0;
     if (ctx->tab_sep) {
         out->py = base + nt2 + W + H + nz2;
         out->d0 = out->py + H;
@@ -953,6 +1006,15 @@ int ensure_tables(rtm_ctx* ctx, int32_t steps, int32_t W, int32_t H, const rtm_c
     } else {
         out->py = out->d0 = out->dd = nullptr;
         out->ok = nullptr;
+    }
+    if (ctx->tab_rec >= 0) {
+        out->zrec = reinterpret_cast<const ZRecK*>(base + ctx->tab_rec);
+        out->col = reinterpret_cast<const ColRecK*>(out->zrec + nt2 + 1);
+        out->row = reinterpret_cast<const RowRecK*>(out->col + (int64_t)ctx->tab_np * W);
+    } else {
+        out->zrec = nullptr;
+        out->col = nullptr;
+        out->row = nullptr;
     }
     return RTM_OK;
 }

@@ -18,6 +18,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <string>
@@ -136,6 +137,8 @@ struct Member {
     hipEvent_t ready[2] = {nullptr, nullptr};  // band rendered into stage[s]
     hipEvent_t sent[2] = {nullptr, nullptr};   // stage[s] read by its send
     hipEvent_t done = nullptr;       // the frame's transfers on this member are finished
+    hipEvent_t lb_sent = nullptr;    // loopback transport: this member's send is posted
+    hipEvent_t lb_recv = nullptr;    // loopback transport: the root's copy of it has run
     void* stage[2] = {nullptr, nullptr};
     size_t stage_bytes = 0;
     int slot = 0;
@@ -146,6 +149,8 @@ struct rtm_group {
     std::vector<Member> m;
     bool aborted = false;
     bool root_staging = false;
+    bool loopback = false;     // transport: device copies on the root's stream instead of RCCL
+    bool host_direct = false;  // rtm_group_render: every band straight to the host, no gather
     void* root_frame = nullptr;  // rtm_group_render: the assembled frame on the root's device
     size_t root_frame_bytes = 0;
 };
@@ -159,7 +164,8 @@ void release(rtm_group* g, bool destroy_comms) {
         if (mb.xfer) (void)hipStreamSynchronize(mb.xfer);
         if (mb.comm && destroy_comms && R.CommDestroy) (void)R.CommDestroy(mb.comm);
         mb.comm = nullptr;
-        for (hipEvent_t* e : {&mb.start, &mb.ready[0], &mb.ready[1], &mb.sent[0], &mb.sent[1], &mb.done})
+        for (hipEvent_t* e : {&mb.start, &mb.ready[0], &mb.ready[1], &mb.sent[0], &mb.sent[1], &mb.done,
+                              &mb.lb_sent, &mb.lb_recv})
             if (*e) {
                 (void)hipEventDestroy(*e);
                 *e = nullptr;
@@ -192,7 +198,8 @@ int setup_members(rtm_group* g) {
         if (rc) return rc;
         Guard d(mb.device);
         GHIP_TRY(hipStreamCreateWithFlags(&mb.xfer, hipStreamNonBlocking));
-        for (hipEvent_t* e : {&mb.start, &mb.ready[0], &mb.ready[1], &mb.sent[0], &mb.sent[1], &mb.done})
+        for (hipEvent_t* e : {&mb.start, &mb.ready[0], &mb.ready[1], &mb.sent[0], &mb.sent[1], &mb.done,
+                              &mb.lb_sent, &mb.lb_recv})
             GHIP_TRY(hipEventCreateWithFlags(e, hipEventDisableTiming));
     }
     return RTM_OK;
@@ -267,6 +274,31 @@ int rtm_group_create(int32_t n_devices, const int32_t* devices, rtm_group** out)
     return RTM_OK;
 }
 
+int rtm_group_create_loopback(int32_t n_members, const int32_t* devices, rtm_group** out) {
+    if (!out) return set_error(RTM_ERR_INVALID, "out is NULL");
+    *out = nullptr;
+    const int nd = rtm_device_count();
+    if (nd <= 0) return set_error(RTM_ERR_NO_DEVICE, "no HIP device visible");
+    if (n_members < 1 || n_members > 64) return set_error(RTM_ERR_INVALID, "n_members outside [1, 64]");
+    std::unique_ptr<rtm_group> g(new rtm_group);
+    g->n_ranks = n_members;
+    g->loopback = true;
+    g->m.resize((size_t)n_members);
+    for (int i = 0; i < n_members; ++i) {
+        const int d = devices ? devices[i] : 0;
+        if (d < 0 || d >= nd) return set_error(RTM_ERR_INVALID, "device id out of range");
+        g->m[(size_t)i].device = d;
+        g->m[(size_t)i].rank = i;
+    }
+    int rc = setup_members(g.get());
+    if (rc) {
+        release(g.get(), false);
+        return rc;
+    }
+    *out = g.release();
+    return RTM_OK;
+}
+
 int rtm_group_create_rank(int32_t device, int32_t n_ranks, int32_t rank, const uint8_t id[128], rtm_group** out) {
     if (!out || !id) return set_error(RTM_ERR_INVALID, "out/id is NULL");
     *out = nullptr;
@@ -305,7 +337,14 @@ int rtm_group_create_rank(int32_t device, int32_t n_ranks, int32_t rank, const u
 
 void rtm_group_destroy(rtm_group* g) {
     if (!g) return;
-    if (!g->aborted) (void)rtm_group_synchronize(g, 0);
+    // bounded: a peer that never posts its matching transfer would otherwise hang
+    // the caller (and interpreter shutdown); past the limit the communicators are
+    // aborted (RTM_GROUP_DESTROY_TIMEOUT_MS, default 120 s; <= 0 waits indefinitely)
+    static const int32_t limit_ms = [] {
+        const char* e = getenv("RTM_GROUP_DESTROY_TIMEOUT_MS");
+        return e ? (int32_t)atoi(e) : 120000;
+    }();
+    if (!g->aborted) (void)rtm_group_synchronize(g, limit_ms);
     release(g, !g->aborted);
     delete g;
 }
@@ -375,7 +414,30 @@ int group_chunk(rtm_group* g, const rtm::internal::PreparedFrame* const* pf, int
     }
     // 2. ONE gather per frame: the root receives every other band in place, the
     //    others send theirs (nothing to move for a one-rank group rendering in place)
-    if (n > 1 || g->root_staging) {
+    if ((n > 1 || g->root_staging) && g->loopback) {
+        // the same matched pairs with device copies on the root's transfer stream:
+        // the copy runs after the sender's transfer stream reached its send (band
+        // rendered), and the sender's stream moves past its send only once the copy
+        // has read the band -- RCCL's completion order for a send/receive pair
+        Member* rm = nullptr;
+        for (Member& mb : g->m)
+            if (mb.rank == root) rm = &mb;
+        for (int j = 0; j < nf; ++j)
+            for (Member& mb : g->m) {
+                const bool staged = mb.rank != root || g->root_staging;
+                int32_t r0, r1;
+                band_rows(height, n, mb.rank, &r0, &r1);
+                if (!staged || r0 >= r1) continue;
+                const size_t bytes = row_bytes * (size_t)(r1 - r0);
+                GHIP_TRY(hipEventRecord(mb.lb_sent, mb.xfer));
+                GHIP_TRY(hipStreamWaitEvent(rm->xfer, mb.lb_sent, 0));
+                GHIP_TRY(hipMemcpyAsync((char*)out_dev[j] + row_bytes * (size_t)r0,
+                                        (char*)mb.stage[mb.slot] + band_bytes * (size_t)j, bytes,
+                                        hipMemcpyDeviceToDevice, rm->xfer));
+                GHIP_TRY(hipEventRecord(mb.lb_recv, rm->xfer));
+                GHIP_TRY(hipStreamWaitEvent(mb.xfer, mb.lb_recv, 0));
+            }
+    } else if (n > 1 || g->root_staging) {
         const Rccl& R = rccl();
         for (int j = 0; j < nf; ++j) {
             NCCL_TRY(R.GroupStart());
@@ -527,14 +589,93 @@ int rtm_group_render_frames_async(rtm_group* g, int32_t n_frames, const rtm_scen
     return RTM_OK;
 }
 
+namespace {
+
+// rtm_group_render with host_direct: every member renders its band into its own
+// staging buffer and copies it from its device straight into its rows of out_host
+// (one host thread per member: a pageable copy blocks its caller, and into a
+// registered buffer each copy is DMA over that device's own PCIe link) -- N links
+// into host memory instead of a gather into one device and that device's link.
+int group_render_direct(rtm_group* g, const rtm_scene* scene, const rtm_camera* eye, const rtm_camera* shadow,
+                        int32_t width, int32_t height, int32_t march_steps, int32_t flags, int32_t format,
+                        void* out_host) {
+    if ((int32_t)g->m.size() != g->n_ranks)
+        return set_error(RTM_ERR_UNSUPPORTED, "direct host delivery needs every rank in this process");
+    if (!out_host) return set_error(RTM_ERR_INVALID, "out_host is NULL");
+    int rc = rtm_group_synchronize(g, 0);  // staging buffers idle
+    if (rc) return rc;
+    const int32_t n = g->n_ranks;
+    const size_t row_bytes = (size_t)rtm::internal::bytes_per_pixel(format) * (size_t)width;
+    const int32_t f = flags | (n > 1 ? RTM_FLAG_FUSED_SHADOW : 0);
+    if ((rc = rtm::internal::check_frame(scene, eye, shadow, width, height, march_steps, f))) return rc;
+    int32_t b0, b1;
+    band_rows(height, n, 0, &b0, &b1);
+    for (Member& mb : g->m)
+        if ((rc = ensure_stage(mb, row_bytes * (size_t)(b1 - b0)))) return rc;
+    for (Member& mb : g->m) {
+        int32_t r0, r1;
+        band_rows(height, n, mb.rank, &r0, &r1);
+        if (r0 >= r1) continue;
+        Guard d(mb.device);
+        if ((rc = rtm_render_rows_async(mb.ctx, scene, eye, shadow, width, height, march_steps, f, format, r0, r1,
+                                        mb.stage[0])))
+            return rc;
+    }
+    std::vector<int> rcs(g->m.size(), RTM_OK);
+    std::vector<std::string> errs(g->m.size());
+    auto copy_band = [&](size_t i) {
+        Member& mb = g->m[i];
+        int32_t r0, r1;
+        band_rows(height, n, mb.rank, &r0, &r1);
+        Guard d(mb.device);
+        hipStream_t rs = rtm::internal::ctx_stream(mb.ctx);
+        hipError_t e = hipMemcpyAsync((char*)out_host + row_bytes * (size_t)r0, mb.stage[0],
+                                      row_bytes * (size_t)(r1 - r0), hipMemcpyDeviceToHost, rs);
+        if (e == hipSuccess) e = hipStreamSynchronize(rs);
+        if (e != hipSuccess) {
+            rcs[i] = RTM_ERR_HIP;
+            errs[i] = std::string("band copy from device ") + std::to_string(mb.device) + ": " + hipGetErrorString(e);
+        }
+    };
+    std::vector<size_t> live;
+    for (size_t i = 0; i < g->m.size(); ++i) {
+        int32_t r0, r1;
+        band_rows(height, n, g->m[i].rank, &r0, &r1);
+        if (r0 < r1) live.push_back(i);
+    }
+    if (live.size() <= 1) {
+        for (size_t i : live) copy_band(i);
+    } else {
+        std::vector<std::thread> th;
+        for (size_t i : live) th.emplace_back(copy_band, i);
+        for (auto& t : th) t.join();
+    }
+    for (size_t i = 0; i < g->m.size(); ++i)
+        if (rcs[i]) return set_error(rcs[i], errs[i].c_str());
+    return RTM_OK;
+}
+
+}  // namespace
+
+int rtm_group_set_host_direct(rtm_group* g, int32_t on) {
+    if (!g) return set_error(RTM_ERR_INVALID, "group is NULL");
+    if (on && (int32_t)g->m.size() != g->n_ranks)
+        return set_error(RTM_ERR_UNSUPPORTED, "direct host delivery needs every rank in this process");
+    g->host_direct = on != 0;
+    return RTM_OK;
+}
+
 int rtm_group_render(rtm_group* g, const rtm_scene* scene, const rtm_camera* eye, const rtm_camera* shadow,
                      int32_t width, int32_t height, int32_t march_steps, int32_t flags, int32_t format,
                      void* out_host) {
     if (!g) return set_error(RTM_ERR_INVALID, "group is NULL");
+    if (g->aborted) return set_error(RTM_ERR_COMM, "group was aborted");
     const int32_t bpp = rtm::internal::bytes_per_pixel(format);
     if (!bpp) return set_error(RTM_ERR_INVALID, "unknown output format");
     if (width <= 0 || height <= 0 || width > RTM_MAX_DIM || height > RTM_MAX_DIM)
         return set_error(RTM_ERR_INVALID, "image size outside [1, RTM_MAX_DIM]");
+    if (g->host_direct) return group_render_direct(g, scene, eye, shadow, width, height, march_steps, flags, format,
+                                                   out_host);
     Member* root = nullptr;
     for (Member& mb : g->m)
         if (mb.rank == 0) root = &mb;

@@ -66,7 +66,35 @@ struct PatchK {
 //   so the surface depth is D = d0 + dd * py (main.rs:2077, one mul + one add).
 // z_{k+1} = fl(z_k + step.z) is monotone in k (rounding is monotone), which the
 // host re-checks entry by entry before setting zmono.
+// Records of the coded shadow tile (shadow_tile_coded), host-built with the tables
+// below when the march camera is separable and the z table monotone:
+//   ZRecK[k], k in [0, steps]: (z_{k-1}, z_k, t_k) -- one LDS read yields both table
+//     entries the first-crossing check compares and the hit's t.  k == steps holds
+//     z = +-INF (the side "past the surface" for the table's direction) and t = +INF,
+//     so a guess of `steps` is never a winning hit and needs no separate test.
+//   ColRecK[p*W + i]: patch p's column terms d0, dd (below) + the f32 guess terms
+//     g0 = (d0 - z0)/sz + 1, g1 = dd/sz (index guess trunc(g0 + g1*py) ~ ceil of
+//     (D - z0)/sz: a guess only, checked against the table) + inRange01 of the column.
+//   RowRecK[j]: py[j], (f32) py[j], inRange01 of the row.
+struct ZRecK {
+    double zprev, z, t, pad;
+};
+struct ColRecK {
+    double d0, dd;
+    float g0, g1;
+    int32_t ok, pad;
+};
+struct RowRecK {
+    double py;
+    float pyf;
+    int32_t ok;
+};
+static_assert(sizeof(ZRecK) == 32 && sizeof(ColRecK) == 32 && sizeof(RowRecK) == 16, "record layouts");
+
 struct Tables {
+    const ZRecK* zrec;    // coded-tile records (see above), or nullptr
+    const ColRecK* col;   // n_patches*W, or nullptr
+    const RowRecK* row;   // H, or nullptr
     const double* t;   // steps entries, or nullptr when steps > RTM_T_TABLE_MAX
     const double* nx;  // W entries
     const double* ny;  // H entries
@@ -78,6 +106,7 @@ struct Tables {
     int32_t zmono;     // z table (first `steps` entries) is non-decreasing (+1) / non-increasing (-1)
     int32_t pad;
     double z0;         // z[0] when z != nullptr (a kernarg copy: no dependent global load for it)
+    double inv_sz;     // 1.0 / step.z when z != nullptr (the first-crossing guess's scale)
 };
 #define RTM_T_TABLE_MAX 65536
 

@@ -16,6 +16,7 @@
 #include <math.h>
 
 #include <algorithm>
+#include <type_traits>
 #include <string>
 #include <stdint.h>
 #include <stdlib.h>
@@ -207,7 +208,7 @@ __device__ __forceinline__ MarchResult march_axis(double D, bool inr0, double oz
     const bool fast_ok = tb.z != nullptr && (!inr0 || (fabs(D) < INFINITY && D != 0.0));
     if (tb.zmono != 0 && __all(fast_ok)) {
         // monotone table (host-checked): locate the first crossing directly
-        if (inr0) cnt = first_crossing((cdouble*)tb.z, D, oz, 1.0 / sz, tb.zmono > 0, steps);
+        if (inr0) cnt = first_crossing((cdouble*)tb.z, D, oz, tb.inv_sz, tb.zmono > 0, steps);
     } else if (__any(inr0) && __all(fast_ok)) {
         cdouble* zt = (cdouble*)tb.z;
         const bool epos = !(oz < D);  // entry class POS <=> z0 >= D
@@ -1550,6 +1551,259 @@ __global__ __launch_bounds__(BLOCK) void shadow_lean2_batch_kernel(CBatch* __res
     shadow_lean2_block<NR, CW, INC, FILLN, CODE>(*(const ShadowPart*)&f->a.sh, f->smap, diag, hot, lds_zt);
 }
 
+// The coded shadow tile (the default for every coded map, rtm_kernels.h): the
+// texels and codes of shadow_tile_lean2<4, 2, INC, *, CODE> with NB 4-row blocks
+// per wave (a wave covers 128 columns x 4*NB rows, lane l columns xb + 2l, +1),
+// rebuilt around host-built records (ZRecK / ColRecK / RowRecK) so that the
+// per-texel work is only what the first-crossing check needs:
+//   D = d0 + dd*py (exact, 2 f64 ops); "D finite and nonzero" (one class test);
+//   f = clamp(trunc(g0 + g1*py), 1, steps) (an f32 index guess, checked below);
+//   one LDS record T[f] = (z_{f-1}, z_f, t_f), and with P(z) = INC ? !(z < D) : (z < D)
+//   okA = !P(z_{f-1}), okB = P(z_f), entry = !P(z_0)   (P monotone over the table)
+//   hit  = inr & fastD & okA & okB          (T[steps] = (z_{steps-1}, past, +INF):
+//                                            a guess of `steps` never wins)
+//   slow = inr & (!fastD | (entry & !(okA & okB)))  -> the exact march_axis
+// The slow texels are rare (a guess within f32 error of a step boundary, or a
+// non-finite/zero D): the wave only records THAT one exists, and its slow path
+// re-derives which.  The last patch updates only the codes (zb is dead after it).
+// Needs 1 <= steps <= CODED_MAX_STEPS (LDS) when marching, and a coded map.
+constexpr int CODED_MAX_STEPS = 1023;  // (steps + 1) * 32 B <= 32 KiB of LDS
+template <bool INC, int CODE, int NB>
+__device__ __forceinline__ void shadow_tile_coded(const ShadowPart& a, void* __restrict__ map, int bx, int by,
+                                                  ZRecK* __restrict__ T) {
+    constexpr int NR = 4 * NB;
+    const int lane = threadIdx.x & (TILE_X - 1);
+    const int xb = bx * 128;
+    const int x0 = xb + lane * 2;
+    const int y0 = __builtin_amdgcn_readfirstlane(by * (TILE_Y * NR) + (threadIdx.x >> 6) * NR);
+    const int W = a.W, H = a.H, steps = a.steps;
+    const bool march = !(a.flags & RTM_FLAG_NO_MARCH) && a.n_patches > 0 && steps > 0;
+    // the LDS records: one per thread, loaded now, written after the raster
+    // (as double2 halves: a ZRecK value would be kept in scratch)
+    const double2* zsrc = reinterpret_cast<const double2*>(a.tab.zrec);
+    double2 rec0 = make_double2(0.0, 0.0), rec1 = rec0;
+    const bool fill1 = march && steps + 1 <= BLOCK;
+    if (fill1 && (int)threadIdx.x <= steps) {
+        rec0 = zsrc[2 * threadIdx.x];
+        rec1 = zsrc[2 * threadIdx.x + 1];
+    }
+    const int xs0 = min(x0, W - 1), xs1 = min(x0 + 1, W - 1);
+    ColRecK c0{}, c1{};
+    if (march) {
+        c0 = a.tab.col[xs0];
+        c1 = a.tab.col[xs1];
+    }
+    double xc[2];
+    xc[0] = a.tab.nx[xs0];
+    xc[1] = a.tab.nx[xs1];
+    double zb[NR][2];
+    int cd[NR][2];
+#pragma unroll
+    for (int r = 0; r < NR; ++r)
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            zb[r][c] = INFINITY;
+            cd[r][c] = -1;
+        }
+    // shadow viewport rasterize, face BACK (main.rs:1569, 243): as the lean tile
+    if (!(a.flags & RTM_FLAG_NO_SHADOW_RASTER) && union_may_cover(a, xb, xb + 127, y0, y0 + NR - 1)) {
+        uint32_t live = wave_sphere_mask(a.sph, a.n_spheres, xb, xb + 127, y0, y0 + NR - 1);
+        while (live) {
+            const int i = __builtin_ctz(live);
+            live &= live - 1u;
+            const RasterSphereK& sp = a.sph[i];
+            double pa[2];
+#pragma unroll
+            for (int c = 0; c < 2; ++c) pa[c] = ((xc[c] - sp.cx) * sp.n) / sp.m;
+#pragma unroll
+            for (int r = 0; r < NR; ++r) {
+                const int y = y0 + r;
+                if (y >= H || y < sp.iy0 || y > sp.iy1) continue;  // wave-uniform
+                const double pb = ((((cdouble*)a.tab.ny)[y] - sp.cy) * sp.n) / sp.m;
+                double s2[2];
+                bool in = false;
+#pragma unroll
+                for (int c = 0; c < 2; ++c) {
+                    s2[c] = pa[c] * pa[c] + pb * pb;
+                    in |= s2[c] < 1.0;
+                }
+                if (!__any(in)) continue;  // d < 1 implies s2 < 1 (sqrt monotone, sqrt(1) == 1)
+#pragma unroll
+                for (int c = 0; c < 2; ++c) {
+                    const double d = sqrt(s2[c]);
+                    const double h = sqrt(1.0 - d * d);
+                    const double depth = sp.z + h * sp.r;
+                    const bool win = (d < 1.0) & (depth < zb[r][c]);
+                    zb[r][c] = win ? depth : zb[r][c];
+                    cd[r][c] = win ? steps + i : cd[r][c];
+                }
+            }
+        }
+    }
+    if (march) {
+        double2* T2 = reinterpret_cast<double2*>(T);
+        if (fill1) {
+            if ((int)threadIdx.x <= steps) {
+                T2[2 * threadIdx.x] = rec0;
+                T2[2 * threadIdx.x + 1] = rec1;
+            }
+        } else {
+            for (int k = threadIdx.x; k <= steps; k += BLOCK) {
+                T2[2 * k] = zsrc[2 * k];
+                T2[2 * k + 1] = zsrc[2 * k + 1];
+            }
+        }
+        __syncthreads();
+        using CRow = const __attribute__((address_space(4))) RowRecK;
+        double py[NR];
+        float pyf[NR];
+        bool rowok[NR];
+        uint32_t rowbits = 0;  // (wave-uniform: bit r = row r marches: in range and < H)
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {
+            const int yr = min(y0 + r, H - 1);  // wave-uniform: scalar loads
+            CRow& rr = ((CRow*)a.tab.row)[yr];
+            py[r] = rr.py;
+            pyf[r] = rr.pyf;
+            rowok[r] = (y0 + r < H) & (rr.ok != 0);
+            rowbits |= rowok[r] ? 1u << r : 0u;
+        }
+        rowbits = __builtin_amdgcn_readfirstlane(rowbits);
+        const double oz = a.tab.z0;
+        const int np = a.n_patches;
+        const float fsteps = (float)steps;
+        for (int k = 0; k < np; ++k) {
+            if (k > 0) {
+                c0 = a.tab.col[k * W + xs0];
+                c1 = a.tab.col[k * W + xs1];
+            }
+            const double d0[2] = {c0.d0, c1.d0};
+            const double dd[2] = {c0.dd, c1.dd};
+            const float g0[2] = {c0.g0, c1.g0};
+            const float g1[2] = {c0.g1, c1.g1};
+            // A column outside inRange01 has the host record d0 = "before the start"
+            // (finite), dd = 0: entry and okA are false there, so it neither hits nor
+            // goes slow -- no per-texel in-range test.  Rows are wave-uniform.
+            bool sany = false;  // a texel the check cannot decide
+            // MASKED: skip rows outside inRange01 or past H (wave-uniform); the
+            // common case (every row marches) runs without the row tests
+            auto check = [&](auto masked) {
+                constexpr bool MASKED = decltype(masked)::value;
+#pragma unroll
+                for (int r = 0; r < NR; ++r) {
+                    if (MASKED && !((rowbits >> r) & 1u)) continue;
+#pragma unroll
+                    for (int c = 0; c < 2; ++c) {
+                        const double Dv = d0[c] + dd[c] * py[r];
+                        const bool fastD = __builtin_amdgcn_class(Dv, 0x198);  // finite, nonzero
+                        // g0, g1, pyf are host-bounded finite values: the median and the
+                        // conversion of a value in [1, steps] are exact and defined
+                        const int f = (int)__builtin_amdgcn_fmed3f(__builtin_fmaf(g1[c], pyf[r], g0[c]), 1.0f, fsteps);
+                        const double zp = T[f].zprev, zf = T[f].z, tf = T[f].t;
+                        const bool okA = INC ? (zp < Dv) : !(zp < Dv);
+                        const bool okB = INC ? !(zf < Dv) : (zf < Dv);
+                        const bool entry = INC ? (oz < Dv) : !(oz < Dv);
+                        const bool win = fastD & okA & okB & (tf < zb[r][c]);
+                        zb[r][c] = win ? tf : zb[r][c];
+                        cd[r][c] = win ? f : cd[r][c];
+                        sany |= !fastD | (entry & !(okA & okB));
+                    }
+                }
+            };
+            if (rowbits == (1u << NR) - 1u) check(std::false_type{});
+            else check(std::true_type{});
+            if (__any(sany)) {
+                // exact per-texel march (march_axis) for the texels the check cannot decide
+                const double sz = a.cam.dir[2] * 0.03;
+#pragma unroll 1
+                for (int q = 0; q < NR * 2; ++q) {
+                    const int qr = q >> 1, qc = q & 1;
+                    double pyq = py[0];
+                    float pyfq = pyf[0];
+                    bool rokq = rowok[0];
+#pragma unroll
+                    for (int r = 1; r < NR; ++r) {
+                        pyq = qr == r ? py[r] : pyq;
+                        pyfq = qr == r ? pyf[r] : pyfq;
+                        rokq = qr == r ? rowok[r] : rokq;
+                    }
+                    // (selects, not indexing: a dynamically indexed array would live in scratch)
+                    const double d0q = qc ? d0[1] : d0[0], ddq = qc ? dd[1] : dd[0];
+                    const float g0q = qc ? g0[1] : g0[0], g1q = qc ? g1[1] : g1[0];
+                    const double Dv = d0q + ddq * pyq;
+                    const bool inr = rokq;
+                    const bool fastD = __builtin_amdgcn_class(Dv, 0x198);
+                    const int f = (int)__builtin_amdgcn_fmed3f(__builtin_fmaf(g1q, pyfq, g0q), 1.0f, fsteps);
+                    const double zp = T[f].zprev, zf = T[f].z;
+                    const bool okA = INC ? (zp < Dv) : !(zp < Dv);
+                    const bool okB = INC ? !(zf < Dv) : (zf < Dv);
+                    const bool entry = INC ? (oz < Dv) : !(oz < Dv);
+                    const bool sl = inr & (!fastD | (entry & !(okA & okB)));
+                    if (!__any(sl)) continue;
+                    MarchResult m{false, 0.0, 0, 0};
+                    if (sl) m = march_axis<false>(Dv, true, oz, sz, steps, a.tab);
+#pragma unroll
+                    for (int r = 0; r < NR; ++r)
+#pragma unroll
+                        for (int c = 0; c < 2; ++c)
+                            if (q == r * 2 + c && sl && m.hit && m.t < zb[r][c]) {
+                                zb[r][c] = m.t;
+                                cd[r][c] = m.k;
+                            }
+                }
+            }
+        }
+    }
+    // the lane's 4 rows x 2 columns of each block as one 8- (U8) or 16-byte (U16)
+    // store: element lane*8 + r*2 + c of block (y >> 2, xb >> 7) (rows past H hold
+    // codes no reader looks up; a block wholly past H does not exist)
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+        const int yb = y0 + 4 * b;
+        if (yb >= H) break;
+        const int64_t blk = (int64_t)(yb >> 2) * a.smap_bw + (xb >> 7);
+        if (CODE == SMAP_U8) {
+            uint32_t w[2] = {0u, 0u};
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+#pragma unroll
+                for (int c = 0; c < 2; ++c)
+                    w[r >> 1] |= ((uint32_t)cd[4 * b + r][c] & 0xFFu) << (8 * ((r & 1) * 2 + c));
+            *reinterpret_cast<uint2*>((uint8_t*)map + blk * 512 + lane * 8) = make_uint2(w[0], w[1]);
+        } else {
+            uint32_t w[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                w[r] = ((uint32_t)cd[4 * b + r][0] & 0xFFFFu) | ((uint32_t)cd[4 * b + r][1] << 16);
+            *reinterpret_cast<uint4*>((uint8_t*)map + blk * 1024 + lane * 16) = make_uint4(w[0], w[1], w[2], w[3]);
+        }
+    }
+}
+
+template <bool INC, int CODE, int NB>
+__device__ __forceinline__ void shadow_coded_block(const ShadowPart& sh, void* __restrict__ map, ZRecK* __restrict__ lds) {
+    constexpr int TR = TILE_Y * 4 * NB;
+    const int n = (int)gridDim.y;
+    const int h0 = max(sh.cull_y0, 0) / TR;
+    const int h1 = min(min(sh.cull_y1, sh.H - 1) / TR, n - 1);
+    const bool none = sh.cull_x0 > sh.cull_x1 || sh.cull_y0 > sh.cull_y1 || sh.cull_y1 < 0;
+    const int by = none ? (int)blockIdx.y : hot_rows_first((int)blockIdx.y, n, h0, h1);
+    shadow_tile_coded<INC, CODE, NB>(sh, map, blockIdx.x, by, lds);
+}
+
+template <bool INC, int CODE, int NB>
+__global__ __launch_bounds__(BLOCK) void shadow_coded_kernel(const FrameArgs a, double* __restrict__ smap) {
+    extern __shared__ ZRecK lds_rec[];
+    shadow_coded_block<INC, CODE, NB>(a.sh, smap, lds_rec);
+}
+
+template <bool INC, int CODE, int NB>
+__global__ __launch_bounds__(BLOCK) void shadow_coded_batch_kernel(CBatch* __restrict__ fr) {
+    extern __shared__ ZRecK lds_rec[];
+    CBatch* f = fr + blockIdx.z;
+    shadow_coded_block<INC, CODE, NB>(*(const ShadowPart*)&f->a.sh, f->smap, lds_rec);
+}
+
 
 // Eye tile: 64 x TILE_Y pixels: eye viewport rasterize (face FRONT, main.rs:1616)
 // [+ processRaytracingRays when RT, main.rs:1035] + renderColorImage
@@ -2225,6 +2479,49 @@ static bool lean_hot() {
     return v;
 }
 
+// The coded shadow tile (shadow_tile_coded): 4-row blocks per wave, RTM_CODED=1|2
+// (default 1); RTM_CODED=0 keeps the lean tile for coded maps (A/B runs).
+static int coded_blocks() {
+    static int v = [] {
+        const char* e = getenv("RTM_CODED");
+        const int b = e ? atoi(e) : 1;
+        return (b == 0 || b == 2) ? b : 1;
+    }();
+    return v;
+}
+
+// Does this frame's (lean, coded) shadow pass take shadow_tile_coded?
+static bool coded_ok(const ShadowPart& sh) {
+    const bool march = !(sh.flags & RTM_FLAG_NO_MARCH) && sh.n_patches > 0 && sh.steps > 0;
+    return coded_blocks() > 0 && sh.smap_fmt != SMAP_F64 &&
+           (!march || (sh.tab.zrec && sh.tab.col && sh.tab.row && sh.steps <= CODED_MAX_STEPS));
+}
+
+// Launch the coded tile for one frame (FrameArgs) or a batch (fr != nullptr, n frames).
+static void launch_coded(const ShadowPart& sh, const FrameArgs* a, double* smap, CBatch* fr, int n, hipStream_t s) {
+    const bool march = !(sh.flags & RTM_FLAG_NO_MARCH) && sh.n_patches > 0 && sh.steps > 0;
+    const size_t lsm = march ? sizeof(ZRecK) * (size_t)(sh.steps + 1) : 0;
+    const int nb = coded_blocks();
+    dim3 g((unsigned)((sh.W + 127) / 128), (unsigned)((sh.H + TILE_Y * 4 * nb - 1) / (TILE_Y * 4 * nb)),
+           (unsigned)(fr ? n : 1));
+    const bool inc = sh.tab.zmono >= 0;  // (no march: either instantiation is exact)
+#define RTM_CK(I, M, B)                                                                             \
+    do {                                                                                            \
+        if (fr) hipLaunchKernelGGL((shadow_coded_batch_kernel<I, M, B>), g, dim3(BLOCK), lsm, s, fr); \
+        else hipLaunchKernelGGL((shadow_coded_kernel<I, M, B>), g, dim3(BLOCK), lsm, s, *a, smap);    \
+    } while (0)
+#define RTM_CKB(I, M) do { if (nb == 2) RTM_CK(I, M, 2); else RTM_CK(I, M, 1); } while (0)
+    if (sh.smap_fmt == SMAP_U8) {
+        if (inc) RTM_CKB(true, SMAP_U8);
+        else RTM_CKB(false, SMAP_U8);
+    } else {
+        if (inc) RTM_CKB(true, SMAP_U16);
+        else RTM_CKB(false, SMAP_U16);
+    }
+#undef RTM_CKB
+#undef RTM_CK
+}
+
 template <int NR>
 static void launch_sep(const FrameArgs& a, double* smap, hipStream_t s) {
     dim3 g((unsigned)((a.sh.W + TILE_X - 1) / TILE_X), (unsigned)((a.sh.H + TILE_Y * NR - 1) / (TILE_Y * NR)));
@@ -2251,7 +2548,9 @@ static void launch_sep(const FrameArgs& a, double* smap, hipStream_t s) {
 #define RTM_L2C(I, F, M) \
     hipLaunchKernelGGL((shadow_lean2_kernel<4, 2, I, F, M>), g2, dim3(BLOCK), lsm, s, a, smap, diag_mode(), hot)
         const int code = a.sh.smap_fmt;
-        if (NR == 4 && cw == 2 && code != SMAP_F64) {  // coded map (shadow_map_format)
+        if (NR == 4 && cw == 2 && code != SMAP_F64 && coded_ok(a.sh)) {
+            launch_coded(a.sh, &a, smap, nullptr, 1, s);
+        } else if (NR == 4 && cw == 2 && code != SMAP_F64) {  // coded map (shadow_map_format)
             if (code == SMAP_U8) {
                 if (fill1) { if (inc) RTM_L2C(true, 1, SMAP_U8); else RTM_L2C(false, 1, SMAP_U8); }
                 else { if (inc) RTM_L2C(true, 4, SMAP_U8); else RTM_L2C(false, 4, SMAP_U8); }
@@ -2404,6 +2703,10 @@ int launch_shadow_batch(const BatchFrame* dev, int n, const FrameArgs& a0, void*
     hipStream_t s = (hipStream_t)stream;
     CBatch* fr = (CBatch*)dev;
     const ShadowPart& sh = a0.sh;
+    if (use_sep(sh) && sep_mode(sh) == MARCH_LEAN2 && sep_rows() == 4 && lean_cols() == 2 && coded_ok(sh)) {
+        launch_coded(sh, nullptr, nullptr, fr, n, s);
+        return launched();
+    }
     if (use_sep(sh) && sep_mode(sh) == MARCH_LEAN2 && sep_rows() == 4 && lean_cols() == 2) {
         const bool march = !(sh.flags & RTM_FLAG_NO_MARCH) && sh.n_patches > 0 && sh.steps > 0;
         const size_t lsm = march ? sizeof(double2) * (size_t)(sh.steps + 1) : 0;

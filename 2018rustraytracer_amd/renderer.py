@@ -225,7 +225,14 @@ def render_frame_multi(scene: Scene, eye: Camera, shadow: Camera, width: int, he
     return out
 
 
+def _unknown_format(fmt: int):
+    # the library's answer to an unknown format (RTM_ERR_INVALID), before any buffer is sized
+    return abi.RtmError(abi.RTM_ERR_INVALID, "host frame", f"unknown output format {fmt}")
+
+
 def _host_frame(height: int, width: int, fmt: int) -> np.ndarray:
+    if fmt not in abi.FORMAT_BYTES:
+        raise _unknown_format(fmt)
     if fmt == abi.RTM_FORMAT_RGBA32F:
         return np.empty((height, width, 4), np.float32)
     return np.empty((height, width, abi.FORMAT_BYTES[fmt]), np.uint8)
@@ -236,7 +243,7 @@ def _check_host_out(out, height: int, width: int, fmt: int) -> np.ndarray:
     contiguous bytes through its base pointer, so a short, strided or mistyped
     buffer would be overrun or scattered.  Raise instead."""
     if fmt not in abi.FORMAT_BYTES:
-        raise ValueError(f"unknown output format {fmt}")
+        raise _unknown_format(fmt)
     if not isinstance(out, np.ndarray):
         raise ValueError("out must be a numpy array")
     want = np.float32 if fmt == abi.RTM_FORMAT_RGBA32F else np.uint8
@@ -296,10 +303,17 @@ class Group:
     process per GPU (ncclCommInitRank, uid from Group.unique_id() on rank 0)."""
 
     def __init__(self, n_devices: int | None = None, devices=None, *, device: int | None = None,
-                 n_ranks: int | None = None, rank: int | None = None, uid: bytes | None = None):
+                 n_ranks: int | None = None, rank: int | None = None, uid: bytes | None = None,
+                 loopback: bool = False):
         self._h = C.c_void_p()
         lib = _lib()
-        if device is not None:
+        if loopback:
+            # test transport (rtm_group_create_loopback): device copies instead of RCCL,
+            # members may share a device (devices None: all on device 0)
+            n = n_devices if n_devices is not None else len(devices)
+            devs = (C.c_int32 * n)(*devices) if devices is not None else None
+            abi.check(lib, lib.rtm_group_create_loopback(n, devs, C.byref(self._h)), "rtm_group_create_loopback")
+        elif device is not None:
             u = (C.c_uint8 * 128).from_buffer_copy(uid)
             abi.check(lib, lib.rtm_group_create_rank(device, n_ranks, rank, u, C.byref(self._h)),
                       "rtm_group_create_rank")
@@ -333,6 +347,12 @@ class Group:
     def set_root_staging(self, on: bool):
         lib = _lib()
         abi.check(lib, lib.rtm_group_set_root_staging(self._h, 1 if on else 0), "rtm_group_set_root_staging")
+
+    def set_host_direct(self, on: bool):
+        """rtm_group_set_host_direct: render() copies every band from its own device
+        straight into the host frame (N links) instead of gathering to rank 0."""
+        lib = _lib()
+        abi.check(lib, lib.rtm_group_set_host_direct(self._h, 1 if on else 0), "rtm_group_set_host_direct")
 
     def render_async(self, scene: Scene, eye: Camera, shadow: Camera, width: int, height: int, steps: int,
                      flags: int, fmt: int, root: int, out_ptr: int, prepared=None):

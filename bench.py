@@ -111,8 +111,42 @@ class _Watchdog:
         self._t.cancel()
 
 
+def band_times(rtm, lib, ctx, world, rank, dist, tdev, c_scene, eye, shadow, W, H, K, flags, fmt, reps=6):
+    """Every rank's own band render (what it renders in the tile-partitioned frame,
+    each band evaluating the shadow texels it reads), timed alone with HIP events on
+    its context's stream; rank 0 gets the list (SURVEY.md §8e-1 imbalance)."""
+    import ctypes as C
+    import torch
+
+    shard = importlib.import_module("2018rustraytracer_amd.shard")
+    r0, r1 = shard.row_band(H, world, rank)
+    ms = 0.0
+    if r1 > r0:
+        e_c, s_c = eye.to_c(), shadow.to_c()
+        buf = torch.empty((r1 - r0) * W * rtm.abi.FORMAT_BYTES[fmt] + 16, dtype=torch.uint8,
+                          device=torch.device("cuda", torch.cuda.current_device()))
+        st = torch.cuda.ExternalStream(ctx.stream)
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        fl = flags | (rtm.abi.RTM_FLAG_FUSED_SHADOW if world > 1 else 0)
+        for it in range(2 + reps):
+            if it == 2:
+                ev0.record(st)
+            rc = lib.rtm_render_rows_async(ctx.handle, C.byref(c_scene[0]), C.byref(e_c), C.byref(s_c), W, H, K,
+                                           fl, fmt, r0, r1, C.c_void_p(buf.data_ptr()))
+            rtm.abi.check(lib, rc, "rtm_render_rows_async")
+        ev1.record(st)
+        ev1.synchronize()
+        ms = ev0.elapsed_time(ev1) / reps
+    if world == 1:
+        return [ms]
+    t = torch.zeros(world, dtype=torch.float64, device=tdev)
+    t[rank] = ms
+    dist.all_reduce(t)
+    return [float(v) for v in t.cpu()]
+
+
 def tile_gather(rtm, lib, ctx, group, world, rank, dist, tdev, c_scenes, eye, shadow, W, H, K, flags, fmt, steps,
-                warmup, timeout_ms=120000):
+                warmup, timeout_ms=120000, bands=False):
     """The tile-partitioned frame: N row bands, one gather into rank
     0.  RCCL (librtm rtm_group) with the nccl backend; with gloo the bands go to the
     CPU and gloo gathers them (the rehearsal of this path on one GPU)."""
@@ -188,14 +222,26 @@ def tile_gather(rtm, lib, ctx, group, world, rank, dist, tdev, c_scenes, eye, sh
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
     r00, r01 = shard.row_band(H, world, 0)
+    if group is None:
+        gather = "gloo gather of CPU-staged bands (rehearsal, not RCCL)"
+    elif world == 1:
+        gather = "none: one band, rendered in place into the output (no transfer at N = 1)"
+    else:
+        gather = "RCCL: ncclSend/ncclRecv in one group into rank 0's device buffer (librtm rtm_group)"
+    extra = {}
+    if bands:
+        bt = band_times(rtm, lib, ctx, world, rank, dist, tdev, c_scenes[0], eye, shadow, W, H, K, flags, fmt)
+        mean = sum(bt) / len(bt)
+        extra = {"band_ms": [round(v, 4) for v in bt],
+                 "band_max_over_mean": round(max(bt) / mean, 4) if mean > 0 else None,
+                 "band_note": "each rank's own band alone (fused shadow), HIP events on its context stream"}
     return {"value": round(W * H * steps / el / 1e6, 2), "unit": "Mpixels/s", "frames": steps,
             "ms_per_step": round(el / steps * 1e3, 5), "scaling": "strong",
             "format": {0: "RGBA32F", 1: "RGBA8", 2: "RGB8"}[fmt], "bytes_per_pixel": bpp,
             "root_ingress_bytes_per_frame": int(W * (H - (r01 - r00)) * bpp),
-            "gather": ("RCCL: ncclSend/ncclRecv in one group into rank 0's device buffer (librtm rtm_group)"
-                       if group is not None else "gloo gather of CPU-staged bands (rehearsal, not RCCL)"),
+            "gather": gather,
             "shadow": ("fused: each band evaluates the shadow texels it reads" if world > 1 or flags & 4
-                       else "two-pass (one band: the whole shadow map)")}
+                       else "two-pass (one band: the whole shadow map)"), **extra}
 
 
 def make_group(rtm, world, rank, local, dist, backend):
@@ -213,9 +259,13 @@ def make_group(rtm, world, rank, local, dist, backend):
     return rtm.Group(device=local, n_ranks=world, rank=rank, uid=bytes(uid.cpu().numpy().tobytes()))
 
 
-def host_output(rtm, scene, eye, shadow, W, H, K, flags, frames=8):
+def host_output(rtm, scene, eye, shadow, W, H, K, flags, frames=8, n_gpus=0):
     """The drop-in's host-output rate (PCIe included; never `value`): rtm_render_ex
-    into pageable and registered host memory, RGBA f32 and writeColorImage's RGB8."""
+    into pageable and registered host memory, RGBA f32 and writeColorImage's RGB8.
+    n_gpus > 0: rtm_render_multi_ex over devices 0..n_gpus-1 from this process (the
+    Rust host's multi-GPU frame, = rtm_group_render with rtm_group_set_host_direct):
+    every device renders its row band and copies it over its own PCIe link into its
+    rows of the host frame, no device-to-device hop."""
     import numpy as np
     res = {}
     for fmt, name in ((0, "rgba32f"), (2, "rgb8")):
@@ -223,10 +273,11 @@ def host_output(rtm, scene, eye, shadow, W, H, K, flags, frames=8):
             buf = np.empty((H, W, 4), np.float32) if fmt == 0 else np.empty((H, W, 3), np.uint8)
             r = rtm.HostRegistration(buf) if reg else None
             try:
-                rtm.render_frame_ex(scene, eye, shadow, W, H, K, flags, fmt, out=buf)
+                kw = {"n_gpus": n_gpus} if n_gpus else {}
+                rtm.render_frame_ex(scene, eye, shadow, W, H, K, flags, fmt, out=buf, **kw)
                 t0 = time.perf_counter()
                 for _ in range(frames):
-                    rtm.render_frame_ex(scene, eye, shadow, W, H, K, flags, fmt, out=buf)
+                    rtm.render_frame_ex(scene, eye, shadow, W, H, K, flags, fmt, out=buf, **kw)
                 el = (time.perf_counter() - t0) / frames
             finally:
                 if r is not None:
@@ -234,7 +285,9 @@ def host_output(rtm, scene, eye, shadow, W, H, K, flags, frames=8):
             res[f"{name}_{'registered' if reg else 'pageable'}"] = {
                 "value": round(W * H / el / 1e6, 2), "unit": "Mpixels/s", "ms_per_frame": round(el * 1e3, 4),
                 "bytes_per_frame": int(buf.nbytes), "GB_per_s": round(buf.nbytes / el / 1e9, 2)}
-    res["note"] = ("rtm_render_ex: blocking, the frame copied to host memory by every call, one frame at a time "
+    res["note"] = ((f"rtm_render_multi_ex over {n_gpus} devices (row bands, fused shadow, each band over its "
+                    "own device's PCIe link)" if n_gpus else "rtm_render_ex")
+                   + ": blocking, the frame copied to host memory by every call, one frame at a time "
                    f"({frames} frames); registered = a buffer pinned once with rtm_host_register (direct DMA)")
     return res
 
@@ -437,7 +490,7 @@ def main():
             preroll_frames += 50
         preroll["ms"], preroll["frames"] = round((time.perf_counter() - t_pre) * 1e3, 1), preroll_frames
         tg_primary = tile_gather(rtm, lib, ctx, group, world, rank, dist, tdev, c_scenes, eye, shadow, W, H, K,
-                                 flags, fmt, nS, nW)
+                                 flags, fmt, nS, nW, bands=True)
         elapsed = tg_primary["ms_per_step"] * nS / 1e3
     else:
         if sequence:
@@ -687,7 +740,8 @@ def main():
                 break
             try:
                 tile[name] = tile_gather(rtm, lib, ctx, group, world, rank, dist, tdev, tg_c, eye, shadow, W, H, K,
-                                         tflags, fmt, a.tile_gather_steps, min(20, a.tile_gather_steps))
+                                         tflags, fmt, a.tile_gather_steps, min(20, a.tile_gather_steps),
+                                         bands=name == "rgba32f")
             except Exception as ex:  # a failed secondary measurement must not lose the headline line
                 tile[name] = {"error": str(ex)[:300]}
                 break
@@ -697,6 +751,19 @@ def main():
     if group is not None:
         group.close()
 
+    if world > 1 and not a.no_host_output and a.config in (3, 4):
+        # the N-link host frame: rank 0 drives all N devices while the others wait
+        barrier()
+        if rank == 0:
+            if torch.cuda.device_count() >= world:
+                try:
+                    res["host_output"] = host_output(rtm, scenes[0], eye, shadow, W, H, K, cfg["flags"],
+                                                     n_gpus=world)
+                except Exception as ex:
+                    res["host_output"] = {"error": str(ex)[:300]}
+            else:
+                res["host_output"] = {"skipped": f"{torch.cuda.device_count()} visible devices < {world} ranks"}
+        barrier()
     if rank == 0:
         if world == 1 and not a.no_host_output and a.config == 3:
             res["host_output"] = host_output(rtm, scenes[0], eye, shadow, W, H, K, cfg["flags"])

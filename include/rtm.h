@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define RTM_ABI_VERSION 8
+#define RTM_ABI_VERSION 9
 
 /* ---- limits: scene constants travel as kernel arguments (SGPR path) ---- */
 #define RTM_MAX_SPHERES 16
@@ -410,6 +410,19 @@ int rtm_group_synchronize(rtm_group* g, int32_t timeout_ms);
 /* Test hook: 1 = the root also stages its band and sends it to itself through
  * RCCL (exercises the transfer path on a one-device group); 0 = in place (default). */
 int rtm_group_set_root_staging(rtm_group* g, int32_t on);
+/* ABI v9, test transport: a group of n_members ranks in this process whose gather
+ * runs as device copies on the root's transfer stream (the matched send/receive
+ * pairs' completion order kept with events) instead of RCCL, so members may share
+ * a device (devices NULL: all on device 0).  Exercises the N-rank band, staging and
+ * receive paths of the frame calls on one GPU; not a transport for production. */
+int rtm_group_create_loopback(int32_t n_members, const int32_t* devices, rtm_group** out);
+/* ABI v9: 1 = rtm_group_render delivers the frame over N host links: every member
+ * renders its band and copies it from its own device straight into its rows of
+ * out_host (registered with rtm_host_register: DMA on each device's PCIe link), no
+ * gather -- the Rust host's multi-GPU frame at N links' rate (main.rs:710, 896-901).
+ * Needs every rank in this process (rtm_group_create / _loopback; else
+ * RTM_ERR_UNSUPPORTED).  0 = gather to rank 0, then one copy (default). */
+int rtm_group_set_host_direct(rtm_group* g, int32_t on);
 
 /* ---- output encoding: writeColorImage (main.rs:660-704), BASELINE row f-2 ----
  * Per channel: c.max(0.0).min(1.0), f32::powf(v, 1.0/2.2), (v * 255.0) as i64,

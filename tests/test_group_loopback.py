@@ -1,0 +1,161 @@
+"""The multi-rank frame of rtm_group run on the box's one GPU.
+
+rtm_group_create_loopback builds an N-member group in one process whose gather
+is a device copy per matched send/receive pair (same event ordering as the RCCL
+pairs) instead of RCCL, so members may share a device.  Everything else is the
+production path: N row bands of ceil(H/N) rows, each band rendered with the fused
+shadow on its own context, double-buffered staging, the root's receive loop over
+peers, chunked frame sequences.  Every frame is compared with the CPU oracle
+(oracle.render, then its writeColorImage encode) bit for bit.
+
+Also rtm_group_set_host_direct (ABI v9): rtm_group_render delivers the frame over
+N host links, each band copied from its own device into its rows of the host
+frame (the reference returns the owned image to the host, main.rs:710, 896-901).
+"""
+import os
+
+import numpy as np
+import pytest
+
+from test_formats_group import to_host, want_frame
+
+pytestmark = pytest.mark.gpu
+
+NT = min(16, os.cpu_count() or 1)
+_WANT = {}
+
+
+def want_cached(oracle, rtm, scenes, cfg, frame, fmt):
+    key = (cfg, frame, fmt)
+    if key not in _WANT:
+        c = scenes.CONFIGS[cfg]
+        s = scenes.scene_a_bench(frame) if c["scene"] is scenes.scene_a_bench else c["scene"]()
+        _WANT[key] = want_frame(oracle, s, scenes.eye_camera(), scenes.shadow_camera(), c["width"], c["height"],
+                                c["steps"], c["flags"], fmt, rtm.abi)
+    return _WANT[key]
+
+
+def device_out(torch, rtm, h, w, fmt):
+    if fmt == 0:
+        return torch.empty((h, w, 4), dtype=torch.float32, device="cuda")
+    return torch.empty(h * w * rtm.abi.FORMAT_BYTES[fmt], dtype=torch.uint8, device="cuda")
+
+
+CASES = [
+    # (config, members, format, root, root staged)
+    (4, 2, 0, 0, False),
+    (4, 3, 0, 0, False),
+    (4, 4, 0, 2, False),
+    (4, 8, 0, 0, False),
+    (4, 8, 1, 5, True),
+    (5, 2, 2, 0, True),
+    (5, 8, 0, 7, False),
+    (2, 3, 0, 1, True),
+    (2, 8, 1, 0, False),
+    (2, 8, 2, 3, True),
+]
+
+
+@pytest.mark.parametrize("case", CASES, ids=[f"cfg{c[0]}-n{c[1]}-fmt{c[2]}-root{c[3]}{'-staged' if c[4] else ''}"
+                                             for c in CASES])
+def test_loopback_group_frame_matches_oracle(rtm, oracle, scenes, case):
+    """One frame over N members (the root's band in place or staged, any root): the
+    assembled frame == the oracle's, bit for bit, at the BASELINE sizes."""
+    import torch
+    cfg, n, fmt, root, staged = case
+    c = scenes.CONFIGS[cfg]
+    w, h, k = c["width"], c["height"], c["steps"]
+    s = scenes.scene_a_bench(100) if cfg != 5 else c["scene"]()
+    g = rtm.Group(n_devices=n, loopback=True)
+    try:
+        assert g.info() == (n, n, 0)
+        g.set_root_staging(staged)
+        out = device_out(torch, rtm, h, w, fmt)
+        out.fill_(0xAB if fmt else 7.0)
+        torch.cuda.synchronize()
+        g.render_async(s, scenes.eye_camera(), scenes.shadow_camera(), w, h, k, c["flags"], fmt, root,
+                       out.data_ptr())
+        g.synchronize(120000)
+        got = to_host(out, h, w, fmt, rtm.abi)
+        want = want_cached(oracle, rtm, scenes, cfg, 100, fmt)
+        bad = got.view(np.uint8) != want.view(np.uint8)
+        assert not bad.any(), f"{int(bad.sum())} bytes differ, first rows {sorted(set(np.argwhere(bad)[:, 0]))[:5]}"
+    finally:
+        g.close()
+        torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("n,staged", [(4, False), (3, True), (8, False)])
+def test_loopback_group_frame_sequence_reuses_staging(rtm, oracle, scenes, n, staged):
+    """12 frames at 1920x1080 (auto frames per launch on a band), outputs reused so
+    chunks are cut and both staging slots of every member are reused several
+    times; each output holds the oracle's frame of its last writer."""
+    import torch
+    w, h, k = 1920, 1080, 32
+    eye, sh = scenes.eye_camera(), scenes.shadow_camera()
+    frames = [scenes.scene_a_bench(11 * i) for i in range(12)]
+    order = [0, 1, 2, 0, 3, 1, 2, 3, 0, 1, 2, 3]
+    g = rtm.Group(n_devices=n, loopback=True)
+    try:
+        g.set_root_staging(staged)
+        bufs = [device_out(torch, rtm, h, w, 0) for _ in range(4)]
+        torch.cuda.synchronize()
+        g.render_frames_async(frames, eye, sh, w, h, k, 0, 0, 0, [bufs[o].data_ptr() for o in order])
+        g.synchronize(120000)
+        last = {o: i for i, o in enumerate(order)}
+        for b, i in last.items():
+            want = oracle.render(frames[i], eye, sh, w, h, k, 0, nthreads=NT)["rgba"]
+            got = to_host(bufs[b], h, w, 0, rtm.abi)
+            assert np.array_equal(got.view(np.uint32), want.view(np.uint32)), (b, i)
+    finally:
+        g.close()
+
+
+@pytest.mark.parametrize("n", [1, 3, 8])
+@pytest.mark.parametrize("fmt", [0, 1, 2])
+def test_group_render_host_direct(rtm, oracle, scenes, n, fmt):
+    """rtm_group_render with direct host delivery: every band from its own member
+    into its rows of the host frame (pageable, then registered), == the oracle;
+    the gathered form of the same group gives the same bytes."""
+    g = rtm.Group(n_devices=n, loopback=True)
+    try:
+        eye, sh = scenes.eye_camera(), scenes.shadow_camera()
+        for (w, h, f) in ((1920, 1080, 100), (517, 299, 60)):
+            s = scenes.scene_a_bench(f)
+            want = want_frame(oracle, s, eye, sh, w, h, 64, 0, fmt, rtm.abi)
+            g.set_host_direct(True)
+            got = g.render(s, eye, sh, w, h, 64, 0, fmt)
+            assert np.array_equal(got.view(np.uint8), want.view(np.uint8))
+            buf = np.zeros_like(want)
+            with rtm.HostRegistration(buf):
+                g.render(s, eye, sh, w, h, 64, 0, fmt, out=buf)
+            assert np.array_equal(buf.view(np.uint8), want.view(np.uint8))
+            g.set_host_direct(False)
+            got = g.render(s, eye, sh, w, h, 64, 0, fmt)
+            assert np.array_equal(got.view(np.uint8), want.view(np.uint8))
+    finally:
+        g.close()
+
+
+def test_group_host_direct_rccl_one_device(rtm, oracle, scenes):
+    """The RCCL group (ncclCommInitAll over the one device) in direct mode."""
+    g = rtm.Group(n_devices=1)
+    try:
+        g.set_host_direct(True)
+        eye, sh = scenes.eye_camera(), scenes.shadow_camera()
+        s = scenes.scene_a_bench(100)
+        want = want_frame(oracle, s, eye, sh, 3840, 2160, 64, 0, 2, rtm.abi)
+        got = g.render(s, eye, sh, 3840, 2160, 64, 0, 2)
+        assert np.array_equal(got, want)
+    finally:
+        g.close()
+
+
+def test_loopback_rejects_bad_members(rtm):
+    lib = rtm.load_library()
+    import ctypes as C
+    h = C.c_void_p()
+    assert lib.rtm_group_create_loopback(0, None, C.byref(h)) == rtm.abi.RTM_ERR_INVALID
+    devs = (C.c_int32 * 2)(0, 99)
+    assert lib.rtm_group_create_loopback(2, devs, C.byref(h)) == rtm.abi.RTM_ERR_INVALID
+    assert not h.value

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""One line per bench log of an A/B directory (tools/ab_env.sh, gpu_r2*.sh): value,
+"""One line per bench log of an A/B directory (tools/ab_env.sh): value,
 us/frame, kernel durations, one-lane value."""
 import glob
 import json
