@@ -767,6 +767,7 @@ struct rtm_ctx {
     DevBuf smap;    // shadow map, W*H f64
     DevBuf smap2;   // second shadow map for the pipelined frame sequence
     const double* last_smap = nullptr;
+    bool last_trivial = false;  // the last frame's shadow viewport was all +INF and not materialised
     ShadowPart last_sh{};  // the last shadow pass's arguments (smap_fmt: how last_smap is stored)
     DevBuf smap_dec;       // rtm_ctx_shadow_map's f64 view of a coded map
     DevBuf out;     // staging for rtm_render's host output
@@ -959,7 +960,7 @@ int ensure_tables(rtm_ctx* ctx, int32_t steps, int32_t W, int32_t H, const rtm_c
                     }
                     // bounded and finite, so the kernel's f32 -> int conversion of
                     // g0 + g1*pyf is always defined (|pyf| <= 4 below)
-                    c.g0 = (float)guess_term((c.d0 - z0) * inv_sz + 1.0);
+                    c.g0 = (float)guess_term((c.d0 - z0) * inv_sz);
                     c.g1 = (float)guess_term(c.dd * inv_sz);
                     c.ok = ok[i];
                     c.pad = 0;
@@ -1119,6 +1120,29 @@ int upload_sdf(rtm_ctx* ctx, DevBuf& buf, hipStream_t s, const SdfTabK& k, const
     return RTM_OK;
 }
 
+// A frame with RTM_FLAG_NO_MARCH | RTM_FLAG_NO_SHADOW_RASTER (main()'s own scene,
+// main.rs:910-1046) has an all-+INF shadow viewport: it skips the shadow pass and its
+// eye pass takes the fused path, whose on-demand texel is +INF at once -- the same
+// bits, one kernel instead of two.  rtm_ctx_shadow_map then materialises the +INF
+// map on request.  RTM_TRIVIAL_SHADOW=0 keeps the two-pass frame (A/B runs).
+bool trivial_shadow(int32_t flags) {
+    static const bool on = [] {
+        const char* e = getenv("RTM_TRIVIAL_SHADOW");
+        return !(e && atoi(e) == 0);
+    }();
+    const int32_t both = RTM_FLAG_NO_MARCH | RTM_FLAG_NO_SHADOW_RASTER;
+    return on && (flags & both) == both && !(flags & RTM_FLAG_FUSED_SHADOW);
+}
+
+void note_trivial(rtm_ctx* ctx, const ShadowPart& sh) {
+    ctx->have_shadow_pass = true;
+    ctx->last_trivial = true;
+    ctx->last_smap = nullptr;
+    ctx->last_sh = sh;
+    ctx->smap_w = sh.W;
+    ctx->smap_h = sh.H;
+}
+
 // lane 0: the context's own stream and buffers; lane k > 0: ctx->lanes[k-1]
 int enqueue_frame(rtm_ctx* ctx, FrameArgs& a, const FrameExtra* x, void* out_dev, StatsK* stats, int lane = 0,
                   int32_t fmt = RTM_FORMAT_RGBA32F) {
@@ -1143,6 +1167,8 @@ int enqueue_frame(rtm_ctx* ctx, FrameArgs& a, const FrameExtra* x, void* out_dev
         if ((rc = mb.ensure(words * sizeof(uint32_t), ctx->device))) return rc;
         tabs.rtmask = (uint32_t*)mb.p;
     }
+    const bool trivial = !stats && trivial_shadow(a.ey.flags);
+    if (trivial) a.ey.flags |= RTM_FLAG_FUSED_SHADOW;
     const bool fused = (a.ey.flags & RTM_FLAG_FUSED_SHADOW) != 0;
     double* smap = nullptr;
     TimingSlot* slot = next_slot(ctx);
@@ -1163,8 +1189,11 @@ int enqueue_frame(rtm_ctx* ctx, FrameArgs& a, const FrameExtra* x, void* out_dev
         }
         if (slot) HIP_TRY(hipEventRecord(slot->ev[1], s));
         ctx->have_shadow_pass = true;
+        ctx->last_trivial = false;
         ctx->last_smap = smap;
         ctx->last_sh = a.sh;
+    } else if (trivial) {
+        note_trivial(ctx, a.sh);
     } else {
         ctx->have_shadow_pass = false;
     }
@@ -1284,6 +1313,9 @@ int enqueue_batch(rtm_ctx* ctx, int lane, FrameArgs* fa, const FrameExtra* ex, v
         brp = std::move(b);
     }
     BatchRing& br = *brp;
+    const bool trivial = trivial_shadow(fa[0].ey.flags);  // (a batch shares its flags)
+    if (trivial)
+        for (int k = 0; k < n; ++k) fa[k].ey.flags |= RTM_FLAG_FUSED_SHADOW;
     const bool fused = (fa[0].ey.flags & RTM_FLAG_FUSED_SHADOW) != 0;
     // One storage for the whole launch (the batched shadow kernel is instantiated per
     // storage), so it must hold every frame's codes: steps + the most spheres of any
@@ -1419,10 +1451,13 @@ int enqueue_batch(rtm_ctx* ctx, int lane, FrameArgs* fa, const FrameExtra* ex, v
         }
         if (slot) HIP_TRY(hipEventRecord(slot->ev[1], s));
         ctx->have_shadow_pass = true;
+        ctx->last_trivial = false;
         ctx->last_smap = (const double*)((const char*)br.smaps.p + map_bytes * (size_t)(n - 1));
         ctx->last_sh = fa[n - 1].sh;
         ctx->smap_w = fa[0].sh.W;
         ctx->smap_h = fa[0].sh.H;
+    } else if (trivial) {
+        note_trivial(ctx, fa[n - 1].sh);
     } else {
         ctx->have_shadow_pass = false;
     }
@@ -1613,13 +1648,22 @@ int rtm_render_async(rtm_ctx* ctx, const rtm_scene* scene, const rtm_camera* eye
 }
 
 int32_t rtm_ctx_shadow_map_texel_bytes(rtm_ctx* ctx) {
-    if (!ctx || !ctx->have_shadow_pass) return 0;
+    if (!ctx || !ctx->have_shadow_pass || ctx->last_trivial) return 0;
     const int32_t f = ctx->last_sh.smap_fmt;
     return f == SMAP_U8 ? 1 : f == SMAP_U16 ? 2 : 8;
 }
 
 const double* rtm_ctx_shadow_map(rtm_ctx* ctx) {
     if (!ctx || !ctx->have_shadow_pass) return nullptr;
+    if (ctx->last_trivial) {
+        // the all-+INF viewport of a frame without shadow raster and march, materialised now
+        DeviceGuard g(ctx->device);
+        const int64_t n = (int64_t)ctx->last_sh.W * ctx->last_sh.H;
+        if (ctx->smap_dec.ensure(sizeof(double) * (size_t)n, ctx->device)) return nullptr;
+        if (launch_fill((double*)ctx->smap_dec.p, n, INFINITY, nullptr, 0, ctx->stream)) return nullptr;
+        if (hipStreamSynchronize(ctx->stream) != hipSuccess) return nullptr;
+        return (const double*)ctx->smap_dec.p;
+    }
     if (ctx->last_sh.smap_fmt == SMAP_F64) return ctx->last_smap;
     // a coded map (rtm_kernels.h): its f64 values, decoded after the frame on the
     // context stream, then waited for

@@ -73,8 +73,8 @@ struct PatchK {
 //     z = +-INF (the side "past the surface" for the table's direction) and t = +INF,
 //     so a guess of `steps` is never a winning hit and needs no separate test.
 //   ColRecK[p*W + i]: patch p's column terms d0, dd (below) + the f32 guess terms
-//     g0 = (d0 - z0)/sz + 1, g1 = dd/sz (index guess trunc(g0 + g1*py) ~ ceil of
-//     (D - z0)/sz: a guess only, checked against the table) + inRange01 of the column.
+//     g0 = (d0 - z0)/sz, g1 = dd/sz (index guess ceil(g0 + g1*py) ~ the first k with
+//     z_k past D: a guess only, checked against the table) + inRange01 of the column.
 //   RowRecK[j]: py[j], (f32) py[j], inRange01 of the row.
 struct ZRecK {
     double zprev, z, t, pad;

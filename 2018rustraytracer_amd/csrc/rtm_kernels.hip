@@ -1557,7 +1557,9 @@ __global__ __launch_bounds__(BLOCK) void shadow_lean2_batch_kernel(CBatch* __res
 // rebuilt around host-built records (ZRecK / ColRecK / RowRecK) so that the
 // per-texel work is only what the first-crossing check needs:
 //   D = d0 + dd*py (exact, 2 f64 ops); "D finite and nonzero" (one class test);
-//   f = clamp(trunc(g0 + g1*py), 1, steps) (an f32 index guess, checked below);
+//   f = ceil(clamp(g0 + g1*py, 1, steps)) (an f32 index guess, checked below; ceil,
+//     not trunc(x) + 1: an x that rounds to an integer in f32 is common and would be
+//     mis-guessed by one, sending its wave down the slow path);
 //   one LDS record T[f] = (z_{f-1}, z_f, t_f), and with P(z) = INC ? !(z < D) : (z < D)
 //   okA = !P(z_{f-1}), okB = P(z_f), entry = !P(z_0)   (P monotone over the table)
 //   hit  = inr & fastD & okA & okB          (T[steps] = (z_{steps-1}, past, +INF):
@@ -1698,7 +1700,8 @@ __device__ __forceinline__ void shadow_tile_coded(const ShadowPart& a, void* __r
                         const bool fastD = __builtin_amdgcn_class(Dv, 0x198);  // finite, nonzero
                         // g0, g1, pyf are host-bounded finite values: the median and the
                         // conversion of a value in [1, steps] are exact and defined
-                        const int f = (int)__builtin_amdgcn_fmed3f(__builtin_fmaf(g1[c], pyf[r], g0[c]), 1.0f, fsteps);
+                        const int f = (int)ceilf(__builtin_amdgcn_fmed3f(__builtin_fmaf(g1[c], pyf[r], g0[c]), 1.0f,
+                                                                         fsteps));
                         const double zp = T[f].zprev, zf = T[f].z, tf = T[f].t;
                         const bool okA = INC ? (zp < Dv) : !(zp < Dv);
                         const bool okB = INC ? !(zf < Dv) : (zf < Dv);
@@ -1733,7 +1736,7 @@ __device__ __forceinline__ void shadow_tile_coded(const ShadowPart& a, void* __r
                     const double Dv = d0q + ddq * pyq;
                     const bool inr = rokq;
                     const bool fastD = __builtin_amdgcn_class(Dv, 0x198);
-                    const int f = (int)__builtin_amdgcn_fmed3f(__builtin_fmaf(g1q, pyfq, g0q), 1.0f, fsteps);
+                    const int f = (int)ceilf(__builtin_amdgcn_fmed3f(__builtin_fmaf(g1q, pyfq, g0q), 1.0f, fsteps));
                     const double zp = T[f].zprev, zf = T[f].z;
                     const bool okA = INC ? (zp < Dv) : !(zp < Dv);
                     const bool okB = INC ? !(zf < Dv) : (zf < Dv);

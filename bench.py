@@ -512,7 +512,11 @@ def main():
         barrier()
         elapsed = max_over_ranks(time.perf_counter() - t0)
 
-    # the shadow map's storage in the timed frames (coded: 1-2 B per texel; fused: none)
+    # the shadow map's storage in the timed frames (coded: 1-2 B per texel; fused: none).
+    # A frame without shadow raster and march (config 7, main()'s scene) has an all-+INF
+    # shadow viewport: the library runs no shadow pass and its eye pass evaluates the
+    # +INF texels on demand (rtm_api.cpp trivial_shadow), i.e. the fused frame's work
+    trivial = (flags & 3) == 3 and not fused and os.environ.get("RTM_TRIVIAL_SHADOW", "1") != "0"
     map_bytes = ctx.shadow_map_texel_bytes() or 8
     # per-kernel HIP-event durations over the timed region (ctx stream)
     n_launches = nS + 1 if pipelined else nS
@@ -577,7 +581,7 @@ def main():
     # texels the eye pass looks up instead of materialising the whole shadow map.
     # Bit-identical image (tests/test_gpu_parity.py::test_fused_shadow_identical).
     alt_fused = None
-    if sequence and not pipelined and not a.no_alt and not fused:
+    if sequence and not pipelined and not a.no_alt and not fused and not trivial:
         fflags = flags | rtm.abi.RTM_FLAG_FUSED_SHADOW
         ctx.set_timing_capacity(max(1, nS // timing_stride))
         ctx.render_frames_async([0] * min(nW, F), eye, shadow, W, H, K, fflags, outp[:min(nW, F)],
@@ -627,7 +631,7 @@ def main():
                                       moving=(shadow.dirNormalized[0] * 0.03 != 0.0
                                               or shadow.dirNormalized[1] * 0.03 != 0.0))
 
-        work = frame_work(fused)
+        work = frame_work(fused or trivial)
         if alt_fused is not None and band_h == H:
             # the fused frame is one kernel (the eye pass evaluating the shadow texels its
             # hit pixels read): its algorithmic bytes and ops per frame over its wall time
@@ -666,12 +670,12 @@ def main():
             roof = metrics.roofline(dom, work, dom_ms, _latest_traffic(a.config, dom))
             roof_other = None
         else:
-            dom = "eye_pass" if (fused or avg_eye >= avg_sh) else "shadow_pass"
+            dom = "eye_pass" if (fused or trivial or avg_eye >= avg_sh) else "shadow_pass"
             dom_ms = avg_eye if dom == "eye_pass" else avg_sh
             roof = kroof(dom, dom_ms)
             other = "shadow_pass" if dom == "eye_pass" else "eye_pass"
             other_ms = avg_sh if other == "shadow_pass" else avg_eye
-            roof_other = kroof(other, other_ms) if other_ms > 0 else None
+            roof_other = kroof(other, other_ms) if other_ms > 0 and not trivial else None
         res = {
             "metric": cfg.get("metric", METRIC if a.config <= 5 else METRIC_F1 if a.config <= 7 else METRIC_F4),
             "value": round(value, 2),
@@ -692,7 +696,8 @@ def main():
                      else "synthetic: row f-4 Scene S-bench (scenes.py), f64 scene built on host" if a.config == 8
                      else "synthetic: " + cfg["desc"]),
             "config": {"workload": cfg["desc"], "config_id": a.config, "width": W, "height": H,
-                       "march_steps": K, "mode": a.mode, "shadow": "fused" if fused else "two-pass",
+                       "march_steps": K, "mode": a.mode, "shadow": ("fused" if fused else "none: all-+INF viewport (no shadow raster or march), "
+                                 "eye pass only" if trivial else "two-pass"),
                        "pipelined": pipelined,
                        "parallelism": (f"frame-parallel x{world}" if not tile_mode
                                        else f"row-bands x{world} + one gather ({a.format})"),
@@ -705,7 +710,7 @@ def main():
             "roofline": roof,
             "roofline_other_kernel": roof_other,
             "roofline_frame": roof_frame,
-            "shadow_map_texel_bytes": None if fused else map_bytes,
+            "shadow_map_texel_bytes": None if (fused or trivial) else map_bytes,
             "lanes": lanes,
             "frames_per_launch": batch,
             "kernels_in_lanes": in_lanes,

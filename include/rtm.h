@@ -333,7 +333,10 @@ int rtm_render_frames_async(rtm_ctx* ctx, int32_t n_frames, const rtm_scene* sce
  * zBuffer bit for bit either way. */
 const double* rtm_ctx_shadow_map(rtm_ctx* ctx);
 /* ABI v7: bytes per texel the last non-fused frame's shadow pass stored: 8 (f64),
- * 2 or 1 (coded map); 0 before any. */
+ * 2 or 1 (coded map); 0 before any, and 0 after a frame with RTM_FLAG_NO_MARCH |
+ * RTM_FLAG_NO_SHADOW_RASTER: its shadow viewport is all +INF, so no shadow pass runs
+ * (the eye pass evaluates its +INF texels on demand; rtm_ctx_shadow_map still
+ * returns the +INF map). */
 int32_t rtm_ctx_shadow_map_texel_bytes(rtm_ctx* ctx);
 
 /* Counting variant of the frame (separate, untimed kernels): the per-pass
