@@ -898,7 +898,8 @@ int ensure_tables(rtm_ctx* ctx, int32_t steps, int32_t W, int32_t H, const rtm_c
         // the coded shadow tile's records (rtm_kernels.h ZRecK / ColRecK / RowRecK), 32-byte aligned
         const bool with_rec = with_sep && zmono != 0 && nt >= 1;
         const int64_t rec_at = ((nd + (nok + 1) / 2) + 3) / 4 * 4;
-        const int64_t nrec = with_rec ? 4 * (nt + 1) + 4 * (int64_t)n_patches * W + 2 * (int64_t)H : 0;
+        const int64_t h_pad = ((int64_t)H + 63) / 64 * 64;  // row records padded (RowRecK)
+        const int64_t nrec = with_rec ? 4 * (nt + 1) + 4 * (int64_t)n_patches * W + 2 * h_pad : 0;
         std::vector<double> h((size_t)(with_rec ? rec_at + nrec : nd + (nok + 1) / 2));
         double t = 0.0;  // raymarchPatch: t = 0.0; ... t += magnitudeOfStepsize (main.rs:2237, 2273)
         for (int64_t k = 0; k < nt; ++k) {
@@ -965,10 +966,11 @@ int ensure_tables(rtm_ctx* ctx, int32_t steps, int32_t W, int32_t H, const rtm_c
                     c.ok = ok[i];
                     c.pad = 0;
                 }
-            for (int32_t j = 0; j < H; ++j) {
-                rr[j].py = py[j];
-                rr[j].pyf = py[j] != py[j] ? 0.0f : (float)std::min(std::max(py[j], -4.0), 4.0);  // a guess term
-                rr[j].ok = ok[W + j];
+            for (int64_t j = 0; j < h_pad; ++j) {
+                const int32_t jj = (int32_t)std::min<int64_t>(j, H - 1);  // padding: row H-1's terms, no march
+                rr[j].py = py[jj];
+                rr[j].pyf = py[jj] != py[jj] ? 0.0f : (float)std::min(std::max(py[jj], -4.0), 4.0);  // a guess term
+                rr[j].ok = j < H ? ok[W + jj] : 0;
             }
         }
         HIP_TRY(hipStreamSynchronize(ctx->stream));  // earlier launches may still read the old tables

@@ -75,7 +75,8 @@ struct PatchK {
 //   ColRecK[p*W + i]: patch p's column terms d0, dd (below) + the f32 guess terms
 //     g0 = (d0 - z0)/sz, g1 = dd/sz (index guess ceil(g0 + g1*py) ~ the first k with
 //     z_k past D: a guess only, checked against the table) + inRange01 of the column.
-//   RowRecK[j]: py[j], (f32) py[j], inRange01 of the row.
+//   RowRecK[j]: py[j], (f32) py[j], inRange01 of the row; the table is padded to a
+//     multiple of 64 rows with rows that do not march (ok = 0).
 struct ZRecK {
     double zprev, z, t, pad;
 };
@@ -89,12 +90,16 @@ struct RowRecK {
     float pyf;
     int32_t ok;
 };
-static_assert(sizeof(ZRecK) == 32 && sizeof(ColRecK) == 32 && sizeof(RowRecK) == 16, "record layouts");
+struct RowRec4K {  // the 4 rows of a coded-map block: one 64-byte scalar load
+    RowRecK r[4];
+};
+static_assert(sizeof(ZRecK) == 32 && sizeof(ColRecK) == 32 && sizeof(RowRecK) == 16 && sizeof(RowRec4K) == 64,
+              "record layouts");
 
 struct Tables {
     const ZRecK* zrec;    // coded-tile records (see above), or nullptr
     const ColRecK* col;   // n_patches*W, or nullptr
-    const RowRecK* row;   // H, or nullptr
+    const RowRecK* row;   // H rounded up to 64 (padding: ok = 0), or nullptr
     const double* t;   // steps entries, or nullptr when steps > RTM_T_TABLE_MAX
     const double* nx;  // W entries
     const double* ny;  // H entries

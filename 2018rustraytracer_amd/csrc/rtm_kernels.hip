@@ -1570,9 +1570,12 @@ __global__ __launch_bounds__(BLOCK) void shadow_lean2_batch_kernel(CBatch* __res
 // re-derives which.  The last patch updates only the codes (zb is dead after it).
 // Needs 1 <= steps <= CODED_MAX_STEPS (LDS) when marching, and a coded map.
 constexpr int CODED_MAX_STEPS = 1023;  // (steps + 1) * 32 B <= 32 KiB of LDS
-template <bool INC, int CODE, int NB>
+// WL: every wave fills its own copy of the LDS records (no workgroup barrier;
+// steps <= CODED_WL_MAX_STEPS), else the workgroup shares one copy.
+constexpr int CODED_WL_MAX_STEPS = 255;  // 4 copies of (steps + 1) * 32 B <= 32 KiB
+template <bool INC, int CODE, int NB, bool WL = false, bool EB = false>
 __device__ __forceinline__ void shadow_tile_coded(const ShadowPart& a, void* __restrict__ map, int bx, int by,
-                                                  ZRecK* __restrict__ T) {
+                                                  ZRecK* __restrict__ T, int diag) {
     constexpr int NR = 4 * NB;
     const int lane = threadIdx.x & (TILE_X - 1);
     const int xb = bx * 128;
@@ -1584,20 +1587,38 @@ __device__ __forceinline__ void shadow_tile_coded(const ShadowPart& a, void* __r
     // (as double2 halves: a ZRecK value would be kept in scratch)
     const double2* zsrc = reinterpret_cast<const double2*>(a.tab.zrec);
     double2 rec0 = make_double2(0.0, 0.0), rec1 = rec0;
-    const bool fill1 = march && steps + 1 <= BLOCK;
-    if (fill1 && (int)threadIdx.x <= steps) {
-        rec0 = zsrc[2 * threadIdx.x];
-        rec1 = zsrc[2 * threadIdx.x + 1];
+    const int fid = WL ? lane : (int)threadIdx.x;  // this thread's first record
+    const bool fill1 = march && steps + 1 <= (WL ? TILE_X : BLOCK);
+    if (march && fid <= steps) {
+        rec0 = zsrc[2 * fid];
+        rec1 = zsrc[2 * fid + 1];
     }
+    if (WL) T += (threadIdx.x >> 6) * (steps + 1);  // the wave's copy
     const int xs0 = min(x0, W - 1), xs1 = min(x0 + 1, W - 1);
     ColRecK c0{}, c1{};
     if (march) {
         c0 = a.tab.col[xs0];
         c1 = a.tab.col[xs1];
     }
-    double xc[2];
-    xc[0] = a.tab.nx[xs0];
-    xc[1] = a.tab.nx[xs1];
+    // the wave's row records: 4 rows per 64-byte scalar load, issued now (the host pads
+    // the table with non-marching rows to a multiple of 64 rows: no clamp, no H test)
+    using CRow4 = const __attribute__((address_space(4))) RowRec4K;
+    double py[NR];
+    float pyf[NR];
+    uint32_t rowbits = 0;  // (wave-uniform: bit r = row r marches: inRange01 and < H)
+    if (march) {
+#pragma unroll
+        for (int b = 0; b < NB; ++b) {
+            CRow4& r4 = ((CRow4*)a.tab.row)[(y0 >> 2) + b];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                py[4 * b + r] = r4.r[r].py;
+                pyf[4 * b + r] = r4.r[r].pyf;
+                rowbits |= r4.r[r].ok != 0 ? 1u << (4 * b + r) : 0u;
+            }
+        }
+    }
+    RTM_PHASE(0)
     double zb[NR][2];
     int cd[NR][2];
 #pragma unroll
@@ -1607,9 +1628,41 @@ __device__ __forceinline__ void shadow_tile_coded(const ShadowPart& a, void* __r
             zb[r][c] = INFINITY;
             cd[r][c] = -1;
         }
+    // the records into LDS (all threads) + the barrier: EB = before the sphere raster
+    // (waves without spheres then do not wait at the barrier for the raster of waves
+    // with spheres), else after it (the record loads in flight during the raster)
+    auto fill_lds = [&]() {
+        double2* T2 = reinterpret_cast<double2*>(T);
+        if (fid <= steps) {
+            T2[2 * fid] = rec0;
+            T2[2 * fid + 1] = rec1;
+        }
+        if (!fill1) {
+            const int stride = WL ? TILE_X : BLOCK;
+            for (int k = fid + stride; k <= steps; k += stride) {
+                T2[2 * k] = zsrc[2 * k];
+                T2[2 * k + 1] = zsrc[2 * k + 1];
+            }
+        }
+        RTM_PHASE(1)
+        if (WL) {
+            // the wave's own copy: its LDS writes complete before its reads (in order per
+            // wave); the fence keeps the compiler from moving reads above the writes
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        } else {
+            __syncthreads();
+        }
+        RTM_PHASE(2)
+    };
+    if (EB && march) fill_lds();
     // shadow viewport rasterize, face BACK (main.rs:1569, 243): as the lean tile
     if (!(a.flags & RTM_FLAG_NO_SHADOW_RASTER) && union_may_cover(a, xb, xb + 127, y0, y0 + NR - 1)) {
         uint32_t live = wave_sphere_mask(a.sph, a.n_spheres, xb, xb + 127, y0, y0 + NR - 1);
+        double xc[2] = {0.0, 0.0};  // the columns' NDC x, only where a sphere may cover
+        if (live) {
+            xc[0] = a.tab.nx[xs0];
+            xc[1] = a.tab.nx[xs1];
+        }
         while (live) {
             const int i = __builtin_ctz(live);
             live &= live - 1u;
@@ -1643,34 +1696,7 @@ __device__ __forceinline__ void shadow_tile_coded(const ShadowPart& a, void* __r
         }
     }
     if (march) {
-        double2* T2 = reinterpret_cast<double2*>(T);
-        if (fill1) {
-            if ((int)threadIdx.x <= steps) {
-                T2[2 * threadIdx.x] = rec0;
-                T2[2 * threadIdx.x + 1] = rec1;
-            }
-        } else {
-            for (int k = threadIdx.x; k <= steps; k += BLOCK) {
-                T2[2 * k] = zsrc[2 * k];
-                T2[2 * k + 1] = zsrc[2 * k + 1];
-            }
-        }
-        __syncthreads();
-        using CRow = const __attribute__((address_space(4))) RowRecK;
-        double py[NR];
-        float pyf[NR];
-        bool rowok[NR];
-        uint32_t rowbits = 0;  // (wave-uniform: bit r = row r marches: in range and < H)
-#pragma unroll
-        for (int r = 0; r < NR; ++r) {
-            const int yr = min(y0 + r, H - 1);  // wave-uniform: scalar loads
-            CRow& rr = ((CRow*)a.tab.row)[yr];
-            py[r] = rr.py;
-            pyf[r] = rr.pyf;
-            rowok[r] = (y0 + r < H) & (rr.ok != 0);
-            rowbits |= rowok[r] ? 1u << r : 0u;
-        }
-        rowbits = __builtin_amdgcn_readfirstlane(rowbits);
+        if (!EB) fill_lds();
         const double oz = a.tab.z0;
         const int np = a.n_patches;
         const float fsteps = (float)steps;
@@ -1723,12 +1749,11 @@ __device__ __forceinline__ void shadow_tile_coded(const ShadowPart& a, void* __r
                     const int qr = q >> 1, qc = q & 1;
                     double pyq = py[0];
                     float pyfq = pyf[0];
-                    bool rokq = rowok[0];
+                    const bool rokq = (rowbits >> qr) & 1u;
 #pragma unroll
                     for (int r = 1; r < NR; ++r) {
                         pyq = qr == r ? py[r] : pyq;
                         pyfq = qr == r ? pyf[r] : pyfq;
-                        rokq = qr == r ? rowok[r] : rokq;
                     }
                     // (selects, not indexing: a dynamically indexed array would live in scratch)
                     const double d0q = qc ? d0[1] : d0[0], ddq = qc ? dd[1] : dd[0];
@@ -1757,6 +1782,7 @@ __device__ __forceinline__ void shadow_tile_coded(const ShadowPart& a, void* __r
             }
         }
     }
+    RTM_PHASE(3)
     // the lane's 4 rows x 2 columns of each block as one 8- (U8) or 16-byte (U16)
     // store: element lane*8 + r*2 + c of block (y >> 2, xb >> 7) (rows past H hold
     // codes no reader looks up; a block wholly past H does not exist)
@@ -1781,30 +1807,36 @@ __device__ __forceinline__ void shadow_tile_coded(const ShadowPart& a, void* __r
             *reinterpret_cast<uint4*>((uint8_t*)map + blk * 1024 + lane * 16) = make_uint4(w[0], w[1], w[2], w[3]);
         }
     }
+    RTM_PHASE(4)
+    if (diag & 8) {
+        __builtin_amdgcn_s_waitcnt(0);  // (diagnostic only: when this wave's stores have left)
+        RTM_PHASE(5)
+    }
 }
 
-template <bool INC, int CODE, int NB>
-__device__ __forceinline__ void shadow_coded_block(const ShadowPart& sh, void* __restrict__ map, ZRecK* __restrict__ lds) {
+template <bool INC, int CODE, int NB, bool WL, bool EB>
+__device__ __forceinline__ void shadow_coded_block(const ShadowPart& sh, void* __restrict__ map, ZRecK* __restrict__ lds,
+                                                   int diag) {
     constexpr int TR = TILE_Y * 4 * NB;
     const int n = (int)gridDim.y;
     const int h0 = max(sh.cull_y0, 0) / TR;
     const int h1 = min(min(sh.cull_y1, sh.H - 1) / TR, n - 1);
     const bool none = sh.cull_x0 > sh.cull_x1 || sh.cull_y0 > sh.cull_y1 || sh.cull_y1 < 0;
     const int by = none ? (int)blockIdx.y : hot_rows_first((int)blockIdx.y, n, h0, h1);
-    shadow_tile_coded<INC, CODE, NB>(sh, map, blockIdx.x, by, lds);
+    shadow_tile_coded<INC, CODE, NB, WL, EB>(sh, map, blockIdx.x, by, lds, diag);
 }
 
-template <bool INC, int CODE, int NB>
-__global__ __launch_bounds__(BLOCK) void shadow_coded_kernel(const FrameArgs a, double* __restrict__ smap) {
+template <bool INC, int CODE, int NB, bool WL, bool EB>
+__global__ __launch_bounds__(BLOCK) void shadow_coded_kernel(const FrameArgs a, double* __restrict__ smap, int diag) {
     extern __shared__ ZRecK lds_rec[];
-    shadow_coded_block<INC, CODE, NB>(a.sh, smap, lds_rec);
+    shadow_coded_block<INC, CODE, NB, WL, EB>(a.sh, smap, lds_rec, diag);
 }
 
-template <bool INC, int CODE, int NB>
-__global__ __launch_bounds__(BLOCK) void shadow_coded_batch_kernel(CBatch* __restrict__ fr) {
+template <bool INC, int CODE, int NB, bool WL, bool EB>
+__global__ __launch_bounds__(BLOCK) void shadow_coded_batch_kernel(CBatch* __restrict__ fr, int diag) {
     extern __shared__ ZRecK lds_rec[];
     CBatch* f = fr + blockIdx.z;
-    shadow_coded_block<INC, CODE, NB>(*(const ShadowPart*)&f->a.sh, f->smap, lds_rec);
+    shadow_coded_block<INC, CODE, NB, WL, EB>(*(const ShadowPart*)&f->a.sh, f->smap, lds_rec, diag);
 }
 
 
@@ -2482,13 +2514,14 @@ static bool lean_hot() {
     return v;
 }
 
-// The coded shadow tile (shadow_tile_coded): 4-row blocks per wave, RTM_CODED=1|2
-// (default 1); RTM_CODED=0 keeps the lean tile for coded maps (A/B runs).
+// The coded shadow tile (shadow_tile_coded), default; RTM_CODED=0 keeps the lean tile
+// for coded maps (A/B runs).  (Measured and dropped from the dispatch: 2 blocks per
+// wave, 281.9 vs 305.5 Gpix/s, and per-wave record copies without the workgroup
+// barrier, 295.7: profiles/r03_ab_coded_variants.txt.)
 static int coded_blocks() {
     static int v = [] {
         const char* e = getenv("RTM_CODED");
-        const int b = e ? atoi(e) : 1;
-        return (b == 0 || b == 2) ? b : 1;
+        return (e && atoi(e) == 0) ? 0 : 1;
     }();
     return v;
 }
@@ -2503,17 +2536,21 @@ static bool coded_ok(const ShadowPart& sh) {
 // Launch the coded tile for one frame (FrameArgs) or a batch (fr != nullptr, n frames).
 static void launch_coded(const ShadowPart& sh, const FrameArgs* a, double* smap, CBatch* fr, int n, hipStream_t s) {
     const bool march = !(sh.flags & RTM_FLAG_NO_MARCH) && sh.n_patches > 0 && sh.steps > 0;
+    // record fill + barrier before the sphere raster (RTM_CODED_EB=1) or after it (default)
+    static const bool eb = [] {
+        const char* e = getenv("RTM_CODED_EB");
+        return e && atoi(e) != 0;
+    }();
     const size_t lsm = march ? sizeof(ZRecK) * (size_t)(sh.steps + 1) : 0;
-    const int nb = coded_blocks();
-    dim3 g((unsigned)((sh.W + 127) / 128), (unsigned)((sh.H + TILE_Y * 4 * nb - 1) / (TILE_Y * 4 * nb)),
-           (unsigned)(fr ? n : 1));
+    dim3 g((unsigned)((sh.W + 127) / 128), (unsigned)((sh.H + TILE_Y * 4 - 1) / (TILE_Y * 4)), (unsigned)(fr ? n : 1));
     const bool inc = sh.tab.zmono >= 0;  // (no march: either instantiation is exact)
-#define RTM_CK(I, M, B)                                                                             \
-    do {                                                                                            \
-        if (fr) hipLaunchKernelGGL((shadow_coded_batch_kernel<I, M, B>), g, dim3(BLOCK), lsm, s, fr); \
-        else hipLaunchKernelGGL((shadow_coded_kernel<I, M, B>), g, dim3(BLOCK), lsm, s, *a, smap);    \
+    const int dg = diag_mode() & 8;       // per-wave phase timestamps only (no result change)
+#define RTM_CK(I, M, E)                                                                                     \
+    do {                                                                                                    \
+        if (fr) hipLaunchKernelGGL((shadow_coded_batch_kernel<I, M, 1, false, E>), g, dim3(BLOCK), lsm, s, fr, dg); \
+        else hipLaunchKernelGGL((shadow_coded_kernel<I, M, 1, false, E>), g, dim3(BLOCK), lsm, s, *a, smap, dg);    \
     } while (0)
-#define RTM_CKB(I, M) do { if (nb == 2) RTM_CK(I, M, 2); else RTM_CK(I, M, 1); } while (0)
+#define RTM_CKB(I, M) do { if (eb) RTM_CK(I, M, true); else RTM_CK(I, M, false); } while (0)
     if (sh.smap_fmt == SMAP_U8) {
         if (inc) RTM_CKB(true, SMAP_U8);
         else RTM_CKB(false, SMAP_U8);

@@ -35,7 +35,11 @@ def main():
     t = buf.reshape(n_waves, 8)[:, :6].astype(np.int64)
     t -= t[:, 0].min()
     ph = np.diff(t, axis=1)
-    names = ["fill-load+raster", "LDS write+barrier", "march", "stores issued", "stores drained"]
+    # coded tile (default; RTM_CODED=0: the lean tile's points): 0 loads issued, 1 raster
+    # done + LDS written, 2 past the barrier, 3 march done, 4 stores issued, 5 drained
+    names = (["loads+raster+LDS write", "barrier", "march", "stores issued", "stores drained"]
+             if os.environ.get("RTM_CODED", "1") != "0" else
+             ["fill-load+raster", "LDS write+barrier", "march", "stores issued", "stores drained"])
     res = {"waves": n_waves, "kernel_span_ticks": int(t[:, 5].max() - t[:, 0].min()),
            "lifetime_ticks": {"mean": float((t[:, 5] - t[:, 0]).mean()),
                               "p50": float(np.median(t[:, 5] - t[:, 0])),
