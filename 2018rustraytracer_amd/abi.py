@@ -171,6 +171,11 @@ ABI_SYMBOLS = [
     ("rtm_group_set_root_staging", C.c_int, [_P, _I32]),
     ("rtm_group_create_loopback", C.c_int, [_I32, C.POINTER(_I32), C.POINTER(_P)]),
     ("rtm_group_set_host_direct", C.c_int, [_P, _I32]),
+    ("rtm_group_set_partition", C.c_int, [_P, _I32]),
+    ("rtm_group_partition", C.c_int32, [_P]),
+    ("rtm_render_stripes_async", C.c_int, [_P, C.POINTER(rtm_scene), C.POINTER(rtm_camera), C.POINTER(rtm_camera),
+                                           _I32, _I32, _I32, _I32, _I32, _I32, _I32, _I32, _P]),
+    ("rtm_stripe_rows", C.c_int32, [_I32, _I32, _I32, _I32]),
     ("rtm_viewport_create", C.c_int, [_P, _I32, _I32, _I32, C.POINTER(rtm_camera), C.POINTER(_P)]),
     ("rtm_viewport_destroy", None, [_P]),
     ("rtm_viewport_rasterize", C.c_int, [_P, C.POINTER(rtm_scene)]),

@@ -2306,32 +2306,54 @@ int prepare_frame(PreparedFrame* f, const rtm_scene* scene, const rtm_camera* ey
     return RTM_OK;
 }
 
+int32_t stripe_rows_of(int32_t H, int32_t n, int32_t S, int32_t r) {
+    const int32_t full = H / S, tail = H % S;  // stripes j = 0 .. ceil(H/S)-1, stripe j to rank j % n
+    int32_t rows = (full / n + (r < full % n ? 1 : 0)) * S;
+    if (tail && full % n == r) rows += tail;  // the last, short stripe is number `full`
+    return rows;
+}
+
+void apply_rows(EyePart& ey, int32_t row_begin, int32_t row_end, const RowMap* m) {
+    ey.row_begin = row_begin;
+    ey.row_end = row_end;
+    ey.stripe_rows = m ? m->stripe_rows : 0;
+    ey.stripe_stride = m ? m->stride : 0;
+    ey.stripe_phase = m ? m->phase : 0;
+    ey.out_global = m ? m->out_global : 0;
+}
+
+int check_rows(const FrameArgs& a, int32_t row_begin, int32_t row_end, const RowMap* m) {
+    if (row_begin < 0 || row_end > a.ey.H || row_begin >= row_end)
+        return fail(RTM_ERR_INVALID, "row range [%d,%d) outside [0,%d)", row_begin, row_end, a.ey.H);
+    if (m && m->stripe_rows > 0 && (row_begin != 0 || m->stride < m->stripe_rows || m->phase < 0 ||
+                                    m->phase % m->stripe_rows != 0 || m->phase >= m->stride))
+        return fail(RTM_ERR_INVALID, "bad row stripes");
+    return RTM_OK;
+}
+
 int enqueue_prepared(rtm_ctx* ctx, const PreparedFrame* f, int32_t format, int32_t row_begin, int32_t row_end,
-                     void* out_dev) {
+                     void* out_dev, const RowMap* map) {
     if (!ctx || !f || !out_dev) return fail(RTM_ERR_INVALID, "bad arguments");
     int rc = validate_format(format, out_dev);
     if (rc) return rc;
-    if (row_begin < 0 || row_end > f->a.ey.H || row_begin >= row_end)
-        return fail(RTM_ERR_INVALID, "row range [%d,%d) outside [0,%d)", row_begin, row_end, f->a.ey.H);
+    if ((rc = check_rows(f->a, row_begin, row_end, map))) return rc;
     FrameArgs a = f->a;
-    a.ey.row_begin = row_begin;
-    a.ey.row_end = row_end;
+    apply_rows(a.ey, row_begin, row_end, map);
     DeviceGuard g(ctx->device);
     return enqueue_frame(ctx, a, &f->x, out_dev, nullptr, 0, format);
 }
 
 int enqueue_prepared_batch(rtm_ctx* ctx, const PreparedFrame* const* fs, int n, int32_t format, int32_t row_begin,
-                           int32_t row_end, void* const* outs) {
+                           int32_t row_end, void* const* outs, const RowMap* map) {
     if (!ctx || !fs || !outs || n < 1) return fail(RTM_ERR_INVALID, "bad arguments");
-    if (n == 1) return enqueue_prepared(ctx, fs[0], format, row_begin, row_end, outs[0]);
+    if (n == 1) return enqueue_prepared(ctx, fs[0], format, row_begin, row_end, outs[0], map);
     int rc;
     for (int k = 0; k < n; ++k) {
         if (!fs[k] || !outs[k]) return fail(RTM_ERR_INVALID, "bad arguments");
         if ((rc = validate_format(format, outs[k]))) return rc;
     }
     const FrameArgs& a0 = fs[0]->a;
-    if (row_begin < 0 || row_end > a0.ey.H || row_begin >= row_end)
-        return fail(RTM_ERR_INVALID, "row range [%d,%d) outside [0,%d)", row_begin, row_end, a0.ey.H);
+    if ((rc = check_rows(a0, row_begin, row_end, map))) return rc;
     // one launch per pass needs the same march tables (patches) and sizes in every frame
     bool same = true;
     for (int k = 1; k < n && same; ++k) {
@@ -2345,15 +2367,14 @@ int enqueue_prepared_batch(rtm_ctx* ctx, const PreparedFrame* const* fs, int n, 
     DeviceGuard g(ctx->device);
     if (!same) {
         for (int k = 0; k < n; ++k)
-            if ((rc = enqueue_prepared(ctx, fs[k], format, row_begin, row_end, outs[k]))) return rc;
+            if ((rc = enqueue_prepared(ctx, fs[k], format, row_begin, row_end, outs[k], map))) return rc;
         return RTM_OK;
     }
     std::vector<FrameArgs> fa((size_t)n);
     std::vector<FrameExtra> fx((size_t)n);
     for (int k = 0; k < n; ++k) {
         fa[(size_t)k] = fs[k]->a;
-        fa[(size_t)k].ey.row_begin = row_begin;
-        fa[(size_t)k].ey.row_end = row_end;
+        apply_rows(fa[(size_t)k].ey, row_begin, row_end, map);
         fx[(size_t)k] = fs[k]->x;
     }
     if ((rc = frame_tables(ctx, fa[0]))) return rc;
@@ -2377,3 +2398,31 @@ hipStream_t ctx_stream(const rtm_ctx* ctx) { return ctx->stream; }
 
 }  // namespace internal
 }  // namespace rtm
+
+extern "C" {
+
+int rtm_render_stripes_async(rtm_ctx* ctx, const rtm_scene* scene, const rtm_camera* eye, const rtm_camera* shadow,
+                             int32_t width, int32_t height, int32_t march_steps, int32_t flags, int32_t format,
+                             int32_t stripe_rows, int32_t n_parts, int32_t part, void* out_dev) {
+    if (!ctx) return fail(RTM_ERR_INVALID, "ctx is NULL");
+    if (stripe_rows < 1 || n_parts < 1 || part < 0 || part >= n_parts)
+        return fail(RTM_ERR_INVALID, "stripes: stripe_rows %d, part %d of %d", stripe_rows, part, n_parts);
+    if ((int64_t)stripe_rows * n_parts > RTM_MAX_DIM * 8LL) return fail(RTM_ERR_INVALID, "stripe period too large");
+    internal::PreparedFrame f;
+    int rc = internal::prepare_frame(&f, scene, eye, shadow, width, height, march_steps, flags);
+    if (rc) return rc;
+    const int32_t rows = internal::stripe_rows_of(height, n_parts, stripe_rows, part);
+    if (rows <= 0) return RTM_OK;  // a part with no rows (more parts than stripes)
+    internal::RowMap m;
+    m.stripe_rows = stripe_rows;
+    m.stride = n_parts * stripe_rows;
+    m.phase = part * stripe_rows;
+    return internal::enqueue_prepared(ctx, &f, format, 0, rows, out_dev, &m);
+}
+
+int32_t rtm_stripe_rows(int32_t height, int32_t stripe_rows, int32_t n_parts, int32_t part) {
+    if (height < 1 || stripe_rows < 1 || n_parts < 1 || part < 0 || part >= n_parts) return -1;
+    return internal::stripe_rows_of(height, n_parts, stripe_rows, part);
+}
+
+}  // extern "C"

@@ -124,6 +124,62 @@ inline void band_rows(int32_t H, int32_t n, int32_t r, int32_t* r0, int32_t* r1)
     *r1 = std::min<int64_t>(H, (int64_t)(r + 1) * band);
 }
 
+// The partition's stripe height: RTM_GROUP_STRIPE=S overrides (0: contiguous bands);
+// default 8-row cyclic stripes once there are several ranks.  Contiguous bands of
+// ceil(H/N) rows were measured 1.26-1.56x max/mean band time at N = 4-8 (the spheres
+// sit mid-frame, and a band's cost follows its hit pixels); 8-row stripes model at
+// 1.01-1.06 (tools/band_balance.py, profiles/r03_band_balance.json).
+int32_t default_stripe(int32_t n) {
+    static const int env = [] {
+        const char* e = getenv("RTM_GROUP_STRIPE");
+        return e ? atoi(e) : -1;
+    }();
+    if (env >= 0) return env;
+    return n > 1 ? 8 : 0;
+}
+
+// Rank r's rows of an H-row frame: contiguous [r0, r0 + rows) or S-row cyclic stripes
+// (local row j = image row r*S + (j / S)*N*S + j % S).
+struct Part {
+    int32_t rows = 0, r0 = 0;
+    rtm::internal::RowMap map;
+};
+
+Part part_of(int32_t H, int32_t n, int32_t S, int32_t r) {
+    Part p;
+    if (S > 0 && n > 1) {
+        p.rows = rtm::internal::stripe_rows_of(H, n, S, r);
+        p.map.stripe_rows = S;
+        p.map.stride = n * S;
+        p.map.phase = r * S;
+    } else {
+        int32_t r1;
+        band_rows(H, n, r, &p.r0, &r1);
+        p.rows = r1 - p.r0;
+    }
+    return p;
+}
+
+// Place a part's compact rows (src) at their image rows of the frame dst: one copy for
+// a contiguous band, a 2-D copy (S rows per stripe, pitch N*S rows) plus the short
+// tail stripe for stripes.
+hipError_t place_rows(void* dst, const void* src, const Part& p, size_t row_bytes, hipMemcpyKind kind,
+                      hipStream_t s) {
+    if (p.rows <= 0) return hipSuccess;
+    if (p.map.stripe_rows <= 0)
+        return hipMemcpyAsync((char*)dst + row_bytes * (size_t)p.r0, src, row_bytes * (size_t)p.rows, kind, s);
+    const int32_t S = p.map.stripe_rows, full = p.rows / S, tail = p.rows % S;
+    char* d0 = (char*)dst + row_bytes * (size_t)p.map.phase;
+    hipError_t e = hipSuccess;
+    if (full > 0)
+        e = hipMemcpy2DAsync(d0, row_bytes * (size_t)p.map.stride, src, row_bytes * (size_t)S, row_bytes * (size_t)S,
+                             (size_t)full, kind, s);
+    if (e == hipSuccess && tail > 0)
+        e = hipMemcpyAsync(d0 + row_bytes * (size_t)p.map.stride * (size_t)full,
+                           (const char*)src + row_bytes * (size_t)S * (size_t)full, row_bytes * (size_t)tail, kind, s);
+    return e;
+}
+
 }  // namespace
 
 // One local device of the group.
@@ -151,6 +207,10 @@ struct rtm_group {
     bool root_staging = false;
     bool loopback = false;     // transport: device copies on the root's stream instead of RCCL
     bool host_direct = false;  // rtm_group_render: every band straight to the host, no gather
+    int32_t stripe = -1;       // partition: S-row cyclic stripes (S > 0) or contiguous bands (0); -1: default
+    void* recv = nullptr;      // the root's receive staging for striped RCCL gathers (n_ranks parts)
+    size_t recv_bytes = 0;
+    int recv_device = 0;
     void* root_frame = nullptr;  // rtm_group_render: the assembled frame on the root's device
     size_t root_frame_bytes = 0;
 };
@@ -188,6 +248,12 @@ void release(rtm_group* g, bool destroy_comms) {
             }
         g->root_frame = nullptr;
         g->root_frame_bytes = 0;
+    }
+    if (g->recv) {
+        Guard d(g->recv_device);
+        (void)hipFree(g->recv);
+        g->recv = nullptr;
+        g->recv_bytes = 0;
     }
 }
 
@@ -378,90 +444,112 @@ namespace {
 // then carries one gather per frame, so a context stream never waits for a
 // transfer and the next chunk renders while this one is in flight.  Frame j is
 // complete in the root's transfer-stream order (rtm_group_stream).
+int group_stripe(const rtm_group* g) { return g->stripe >= 0 ? g->stripe : default_stripe(g->n_ranks); }
+
+// The root's receive staging for striped RCCL gathers: one part per rank (its compact
+// rows land here, then place_rows scatters them), on the root's device.
+int ensure_recv(rtm_group* g, Member& rm, size_t bytes) {
+    if (bytes <= g->recv_bytes) return RTM_OK;
+    Guard d(rm.device);
+    GHIP_TRY(hipStreamSynchronize(rm.xfer));
+    if (g->recv) (void)hipFree(g->recv);
+    g->recv = nullptr;
+    g->recv_bytes = 0;
+    if (hipMalloc(&g->recv, bytes) != hipSuccess) return set_error(RTM_ERR_OOM, "receive staging allocation failed");
+    g->recv_bytes = bytes;
+    g->recv_device = rm.device;
+    return RTM_OK;
+}
+
 int group_chunk(rtm_group* g, const rtm::internal::PreparedFrame* const* pf, int nf, int32_t width, int32_t height,
                 int32_t format, int32_t root, void* const* out_dev) {
     const int32_t n = g->n_ranks;
+    const int32_t S = group_stripe(g);
     const size_t row_bytes = (size_t)rtm::internal::bytes_per_pixel(format) * (size_t)width;
-    int32_t b0, b1;
-    band_rows(height, n, 0, &b0, &b1);
-    const size_t band_bytes = row_bytes * (size_t)(b1 - b0);
+    const size_t part_bytes = row_bytes * (size_t)part_of(height, n, S, 0).rows;  // rank 0 holds the most rows
     int rc;
     std::vector<void*> outs((size_t)nf);
-    // 1. every local member renders its bands of the chunk's frames
+    // 1. every local member renders its rows of the chunk's frames
     for (Member& mb : g->m) {
-        int32_t r0, r1;
-        band_rows(height, n, mb.rank, &r0, &r1);
+        Part pt = part_of(height, n, S, mb.rank);
         Guard d(mb.device);
         hipStream_t rs = rtm::internal::ctx_stream(mb.ctx);
         const bool staged = mb.rank != root || g->root_staging;
-        if (r0 < r1) {
-            const int s = mb.slot;
-            if (staged) GHIP_TRY(hipStreamWaitEvent(rs, mb.sent[s], 0));  // slot s's previous sends have read it
+        if (pt.rows > 0) {
+            const int sl = mb.slot;
+            if (staged) GHIP_TRY(hipStreamWaitEvent(rs, mb.sent[sl], 0));  // slot sl's previous sends have read it
+            const bool stripes = pt.map.stripe_rows > 0;
+            // the root in place: its stripes straight at their image rows (out_global)
+            pt.map.out_global = (!staged && stripes) ? 1 : 0;
             for (int j = 0; j < nf; ++j)
-                outs[(size_t)j] = staged ? (void*)((char*)mb.stage[s] + band_bytes * (size_t)j)
-                                         : (void*)((char*)out_dev[j] + row_bytes * (size_t)r0);
-            rc = rtm::internal::enqueue_prepared_batch(mb.ctx, pf, nf, format, r0, r1, outs.data());
+                outs[(size_t)j] = staged ? (void*)((char*)mb.stage[sl] + part_bytes * (size_t)j)
+                                         : stripes ? out_dev[j]
+                                                   : (void*)((char*)out_dev[j] + row_bytes * (size_t)pt.r0);
+            rc = stripes ? rtm::internal::enqueue_prepared_batch(mb.ctx, pf, nf, format, 0, pt.rows, outs.data(),
+                                                                 &pt.map)
+                         : rtm::internal::enqueue_prepared_batch(mb.ctx, pf, nf, format, pt.r0, pt.r0 + pt.rows,
+                                                                 outs.data());
             if (rc) return rc;
             if (staged) {
-                GHIP_TRY(hipEventRecord(mb.ready[s], rs));
-                GHIP_TRY(hipStreamWaitEvent(mb.xfer, mb.ready[s], 0));
+                GHIP_TRY(hipEventRecord(mb.ready[sl], rs));
+                GHIP_TRY(hipStreamWaitEvent(mb.xfer, mb.ready[sl], 0));
             }
         }
-        if (mb.rank == root && !staged) {  // the root's own bands, in the frames' completion order
+        if (mb.rank == root && !staged) {  // the root's own rows, in the frames' completion order
             GHIP_TRY(hipEventRecord(mb.start, rs));
             GHIP_TRY(hipStreamWaitEvent(mb.xfer, mb.start, 0));
         }
     }
-    // 2. ONE gather per frame: the root receives every other band in place, the
-    //    others send theirs (nothing to move for a one-rank group rendering in place)
+    // 2. ONE gather per frame: the root receives every other part, the others send
+    //    theirs (nothing to move for a one-rank group rendering in place)
+    Member* rm = nullptr;
+    for (Member& mb : g->m)
+        if (mb.rank == root) rm = &mb;
     if ((n > 1 || g->root_staging) && g->loopback) {
         // the same matched pairs with device copies on the root's transfer stream:
-        // the copy runs after the sender's transfer stream reached its send (band
+        // the copy runs after the sender's transfer stream reached its send (part
         // rendered), and the sender's stream moves past its send only once the copy
-        // has read the band -- RCCL's completion order for a send/receive pair
-        Member* rm = nullptr;
-        for (Member& mb : g->m)
-            if (mb.rank == root) rm = &mb;
+        // has read the part -- RCCL's completion order for a send/receive pair
         for (int j = 0; j < nf; ++j)
             for (Member& mb : g->m) {
                 const bool staged = mb.rank != root || g->root_staging;
-                int32_t r0, r1;
-                band_rows(height, n, mb.rank, &r0, &r1);
-                if (!staged || r0 >= r1) continue;
-                const size_t bytes = row_bytes * (size_t)(r1 - r0);
+                const Part pt = part_of(height, n, S, mb.rank);
+                if (!staged || pt.rows <= 0) continue;
                 GHIP_TRY(hipEventRecord(mb.lb_sent, mb.xfer));
                 GHIP_TRY(hipStreamWaitEvent(rm->xfer, mb.lb_sent, 0));
-                GHIP_TRY(hipMemcpyAsync((char*)out_dev[j] + row_bytes * (size_t)r0,
-                                        (char*)mb.stage[mb.slot] + band_bytes * (size_t)j, bytes,
-                                        hipMemcpyDeviceToDevice, rm->xfer));
+                GHIP_TRY(place_rows(out_dev[j], (char*)mb.stage[mb.slot] + part_bytes * (size_t)j, pt, row_bytes,
+                                    hipMemcpyDeviceToDevice, rm->xfer));
                 GHIP_TRY(hipEventRecord(mb.lb_recv, rm->xfer));
                 GHIP_TRY(hipStreamWaitEvent(mb.xfer, mb.lb_recv, 0));
             }
     } else if (n > 1 || g->root_staging) {
         const Rccl& R = rccl();
+        const bool stripes = S > 0 && n > 1;
+        if (stripes && rm && (rc = ensure_recv(g, *rm, part_bytes * (size_t)n))) return rc;
         for (int j = 0; j < nf; ++j) {
             NCCL_TRY(R.GroupStart());
             for (Member& mb : g->m) {
                 if (mb.rank == root) {
                     for (int32_t p = 0; p < n; ++p) {
                         if (p == root && !g->root_staging) continue;
-                        int32_t r0, r1;
-                        band_rows(height, n, p, &r0, &r1);
-                        if (r0 >= r1) continue;
-                        ncclResult_t r = R.Recv((char*)out_dev[j] + row_bytes * (size_t)r0,
-                                                row_bytes * (size_t)(r1 - r0), ncclUint8, p, mb.comm, mb.xfer);
+                        const Part pt = part_of(height, n, S, p);
+                        if (pt.rows <= 0) continue;
+                        // a contiguous band lands in place; stripes land compact in the
+                        // receive staging and are placed after the group
+                        void* dst = stripes ? (void*)((char*)g->recv + part_bytes * (size_t)p)
+                                            : (void*)((char*)out_dev[j] + row_bytes * (size_t)pt.r0);
+                        ncclResult_t r = R.Recv(dst, row_bytes * (size_t)pt.rows, ncclUint8, p, mb.comm, mb.xfer);
                         if (r != ncclSuccess) {
                             (void)R.GroupEnd();
                             return comm_fail("ncclRecv", r);
                         }
                     }
                 }
-                int32_t r0, r1;
-                band_rows(height, n, mb.rank, &r0, &r1);
+                const Part pt = part_of(height, n, S, mb.rank);
                 const bool staged = mb.rank != root || g->root_staging;
-                if (staged && r0 < r1) {
-                    ncclResult_t r = R.Send((char*)mb.stage[mb.slot] + band_bytes * (size_t)j,
-                                            row_bytes * (size_t)(r1 - r0), ncclUint8, root, mb.comm, mb.xfer);
+                if (staged && pt.rows > 0) {
+                    ncclResult_t r = R.Send((char*)mb.stage[mb.slot] + part_bytes * (size_t)j,
+                                            row_bytes * (size_t)pt.rows, ncclUint8, root, mb.comm, mb.xfer);
                     if (r != ncclSuccess) {
                         (void)R.GroupEnd();
                         return comm_fail("ncclSend", r);
@@ -469,14 +557,21 @@ int group_chunk(rtm_group* g, const rtm::internal::PreparedFrame* const* pf, int
                 }
             }
             NCCL_TRY(R.GroupEnd());
+            if (stripes && rm) {  // the received parts to their image rows, in the root's transfer order
+                Guard d(rm->device);
+                for (int32_t p = 0; p < n; ++p) {
+                    if (p == root && !g->root_staging) continue;
+                    GHIP_TRY(place_rows(out_dev[j], (char*)g->recv + part_bytes * (size_t)p, part_of(height, n, S, p),
+                                        row_bytes, hipMemcpyDeviceToDevice, rm->xfer));
+                }
+            }
         }
     }
     // 3. staging slots: free again once their sends have read them
     for (Member& mb : g->m) {
-        int32_t r0, r1;
-        band_rows(height, n, mb.rank, &r0, &r1);
+        const Part pt = part_of(height, n, S, mb.rank);
         const bool staged = mb.rank != root || g->root_staging;
-        if (staged && r0 < r1) {
+        if (staged && pt.rows > 0) {
             Guard d(mb.device);
             GHIP_TRY(hipEventRecord(mb.sent[mb.slot], mb.xfer));
             mb.slot ^= 1;
@@ -499,12 +594,11 @@ int group_begin(rtm_group* g, int32_t width, int32_t height, int32_t format, int
     if (!bpp) return set_error(RTM_ERR_INVALID, "unknown output format");
     if (width <= 0 || height <= 0 || width > RTM_MAX_DIM || height > RTM_MAX_DIM)
         return set_error(RTM_ERR_INVALID, "image size outside [1, RTM_MAX_DIM]");
-    int32_t b0, b1;
-    band_rows(height, g->n_ranks, 0, &b0, &b1);
+    const int32_t rows0 = part_of(height, g->n_ranks, group_stripe(g), 0).rows;  // the largest part
     for (Member& mb : g->m) {
         const bool staged = mb.rank != root || g->root_staging;
         int rc;
-        if (staged && (rc = ensure_stage(mb, (size_t)bpp * (size_t)width * (size_t)(b1 - b0) * (size_t)frames)))
+        if (staged && (rc = ensure_stage(mb, (size_t)bpp * (size_t)width * (size_t)rows0 * (size_t)frames)))
             return rc;
     }
     return RTM_OK;
@@ -539,9 +633,8 @@ int rtm_group_render_frames_async(rtm_group* g, int32_t n_frames, const rtm_scen
         return set_error(RTM_ERR_INVALID, "image size outside [1, RTM_MAX_DIM]");
     // frames per launch: the library's auto rule for a band (every rank's bands of a
     // chunk render in one launch per pass), the same on every rank
-    int32_t b0, b1;
-    band_rows(height, g->n_ranks > 0 ? g->n_ranks : 1, 0, &b0, &b1);
-    const int32_t B = std::max(1, std::min<int32_t>(n_frames, rtm::internal::auto_frames_per_launch(width, b1 - b0)));
+    const int32_t rows0 = part_of(height, g->n_ranks > 0 ? g->n_ranks : 1, group_stripe(g), 0).rows;
+    const int32_t B = std::max(1, std::min<int32_t>(n_frames, rtm::internal::auto_frames_per_launch(width, rows0)));
     int rc = group_begin(g, width, height, format, root, B);
     if (rc) return rc;
     // more than one band: each evaluates the shadow texels it reads (same image bits)
@@ -608,29 +701,29 @@ int group_render_direct(rtm_group* g, const rtm_scene* scene, const rtm_camera* 
     const size_t row_bytes = (size_t)rtm::internal::bytes_per_pixel(format) * (size_t)width;
     const int32_t f = flags | (n > 1 ? RTM_FLAG_FUSED_SHADOW : 0);
     if ((rc = rtm::internal::check_frame(scene, eye, shadow, width, height, march_steps, f))) return rc;
-    int32_t b0, b1;
-    band_rows(height, n, 0, &b0, &b1);
+    const int32_t S = group_stripe(g);
     for (Member& mb : g->m)
-        if ((rc = ensure_stage(mb, row_bytes * (size_t)(b1 - b0)))) return rc;
+        if ((rc = ensure_stage(mb, row_bytes * (size_t)part_of(height, n, S, 0).rows))) return rc;
+    std::unique_ptr<rtm::internal::PreparedFrame, PreparedDeleter> pf(rtm::internal::new_prepared());
+    if (!pf) return set_error(RTM_ERR_OOM, "host allocation failed");
+    if ((rc = rtm::internal::prepare_frame(pf.get(), scene, eye, shadow, width, height, march_steps, f))) return rc;
     for (Member& mb : g->m) {
-        int32_t r0, r1;
-        band_rows(height, n, mb.rank, &r0, &r1);
-        if (r0 >= r1) continue;
+        const Part pt = part_of(height, n, S, mb.rank);
+        if (pt.rows <= 0) continue;
         Guard d(mb.device);
-        if ((rc = rtm_render_rows_async(mb.ctx, scene, eye, shadow, width, height, march_steps, f, format, r0, r1,
-                                        mb.stage[0])))
-            return rc;
+        rc = pt.map.stripe_rows > 0
+                 ? rtm::internal::enqueue_prepared(mb.ctx, pf.get(), format, 0, pt.rows, mb.stage[0], &pt.map)
+                 : rtm::internal::enqueue_prepared(mb.ctx, pf.get(), format, pt.r0, pt.r0 + pt.rows, mb.stage[0]);
+        if (rc) return rc;
     }
     std::vector<int> rcs(g->m.size(), RTM_OK);
     std::vector<std::string> errs(g->m.size());
-    auto copy_band = [&](size_t i) {
+    auto copy_part = [&](size_t i) {
         Member& mb = g->m[i];
-        int32_t r0, r1;
-        band_rows(height, n, mb.rank, &r0, &r1);
         Guard d(mb.device);
         hipStream_t rs = rtm::internal::ctx_stream(mb.ctx);
-        hipError_t e = hipMemcpyAsync((char*)out_host + row_bytes * (size_t)r0, mb.stage[0],
-                                      row_bytes * (size_t)(r1 - r0), hipMemcpyDeviceToHost, rs);
+        hipError_t e = place_rows(out_host, mb.stage[0], part_of(height, n, S, mb.rank), row_bytes,
+                                  hipMemcpyDeviceToHost, rs);
         if (e == hipSuccess) e = hipStreamSynchronize(rs);
         if (e != hipSuccess) {
             rcs[i] = RTM_ERR_HIP;
@@ -638,16 +731,13 @@ int group_render_direct(rtm_group* g, const rtm_scene* scene, const rtm_camera* 
         }
     };
     std::vector<size_t> live;
-    for (size_t i = 0; i < g->m.size(); ++i) {
-        int32_t r0, r1;
-        band_rows(height, n, g->m[i].rank, &r0, &r1);
-        if (r0 < r1) live.push_back(i);
-    }
+    for (size_t i = 0; i < g->m.size(); ++i)
+        if (part_of(height, n, S, g->m[i].rank).rows > 0) live.push_back(i);
     if (live.size() <= 1) {
-        for (size_t i : live) copy_band(i);
+        for (size_t i : live) copy_part(i);
     } else {
         std::vector<std::thread> th;
-        for (size_t i : live) th.emplace_back(copy_band, i);
+        for (size_t i : live) th.emplace_back(copy_part, i);
         for (auto& t : th) t.join();
     }
     for (size_t i = 0; i < g->m.size(); ++i)
@@ -656,6 +746,17 @@ int group_render_direct(rtm_group* g, const rtm_scene* scene, const rtm_camera* 
 }
 
 }  // namespace
+
+int rtm_group_set_partition(rtm_group* g, int32_t stripe_rows) {
+    if (!g) return set_error(RTM_ERR_INVALID, "group is NULL");
+    if (stripe_rows < -1 || stripe_rows > RTM_MAX_DIM) return set_error(RTM_ERR_INVALID, "stripe_rows outside [-1, RTM_MAX_DIM]");
+    const int rc = rtm_group_synchronize(g, 0);  // frames in flight keep the partition they were issued with
+    if (rc) return rc;
+    g->stripe = stripe_rows;
+    return RTM_OK;
+}
+
+int32_t rtm_group_partition(rtm_group* g) { return g ? group_stripe(g) : -1; }
 
 int rtm_group_set_host_direct(rtm_group* g, int32_t on) {
     if (!g) return set_error(RTM_ERR_INVALID, "group is NULL");

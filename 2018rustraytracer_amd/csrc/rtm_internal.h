@@ -20,14 +20,24 @@ PreparedFrame* new_prepared();
 void delete_prepared(PreparedFrame* f);
 int prepare_frame(PreparedFrame* f, const rtm_scene* scene, const rtm_camera* eye, const rtm_camera* shadow,
                   int32_t width, int32_t height, int32_t march_steps, int32_t flags);
-// rows [row_begin, row_end) in `format` into out_dev, on ctx's stream
+// Cyclic row stripes (the multi-GPU frame's balanced partition): a launch of local
+// rows [0, rows) renders image row phase + (j / stripe_rows) * stride + j % stripe_rows
+// for local row j (rows past H skipped); out_global: the output buffer is the whole
+// image (rows land at their image rows), else the launch's compact rows.
+struct RowMap {
+    int32_t stripe_rows = 0, stride = 0, phase = 0, out_global = 0;
+};
+// image rows of rank r of n under S-row cyclic stripes (the local row count)
+int32_t stripe_rows_of(int32_t H, int32_t n, int32_t S, int32_t r);
+// rows [row_begin, row_end) in `format` into out_dev, on ctx's stream (map: stripes,
+// row_begin = 0 and row_end = the local row count then)
 int enqueue_prepared(rtm_ctx* ctx, const PreparedFrame* f, int32_t format, int32_t row_begin, int32_t row_end,
-                     void* out_dev);
+                     void* out_dev, const RowMap* map = nullptr);
 // n frames' rows [row_begin, row_end) in `format`, frame k into outs[k], on ctx's
 // stream: one launch per pass when the frames share their march tables
 // (rtm_ctx_set_batch's batched kernels), else frame by frame
 int enqueue_prepared_batch(rtm_ctx* ctx, const PreparedFrame* const* fs, int n, int32_t format, int32_t row_begin,
-                           int32_t row_end, void* const* outs);
+                           int32_t row_end, void* const* outs, const RowMap* map = nullptr);
 // frames per launch the library's auto rule picks for width x rows frames
 int auto_frames_per_launch(int32_t width, int32_t rows);
 // bytes per pixel of an RTM_FORMAT_* (0: unknown)

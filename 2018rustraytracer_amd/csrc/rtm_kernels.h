@@ -162,6 +162,12 @@ struct EyePart {
     // union of the spheres' pixel ranges (empty: cull_x0 > cull_x1): a wave
     // outside it skips the per-sphere culls
     int32_t cull_x0, cull_x1, cull_y0, cull_y1;
+    // [row_begin, row_end) are the launch's local rows; local row j renders image row
+    // eye_row(j) = row_begin + j, or with cyclic stripes (stripe_rows > 0: the multi-GPU
+    // frame's balanced partition, rtm_group) stripe_phase + (j / stripe_rows) *
+    // stripe_stride + j % stripe_rows, clipped to H.  out_global: the output is the
+    // whole image (row eye_row(j) of it), else the launch's rows (row j).
+    int32_t stripe_rows, stripe_stride, stripe_phase, out_global;
 };
 
 // One launch's arguments: the shadow pass of frame i and the eye pass of frame

@@ -1847,6 +1847,11 @@ __global__ __launch_bounds__(BLOCK) void shadow_coded_batch_kernel(CBatch* __res
 // RT: 0 spheres only, 1 + ray-traced planes/cylinders and PERSPECTIVE spheres,
 // 2 + SDFs (its own instantiation: the sphere-trace loop's registers would
 // otherwise lower the occupancy of every ray-traced frame).
+// Image row of the launch's local row j (EyePart: contiguous rows or cyclic stripes).
+__device__ __forceinline__ int eye_row(int row_begin, int S, int stride, int phase, int j) {
+    return S > 0 ? phase + (j / S) * stride + j % S : row_begin + j;
+}
+
 template <bool FUSED, bool COUNT, int RT, int FMT = RTM_FORMAT_RGBA32F>
 __device__ __forceinline__ void eye_tile(const EyePart& a, const ShadowPart& sh, const double* __restrict__ smap,
                                          void* __restrict__ out, int bx, int by, StatsK* __restrict__ st,
@@ -1863,8 +1868,9 @@ __device__ __forceinline__ void eye_tile(const EyePart& a, const ShadowPart& sh,
     const int xb = __builtin_amdgcn_readfirstlane((wide & 1) ? (bx * TILE_Y + wv) * TILE_X : bx * TILE_X);
     const int xi = xb + (threadIdx.x & (TILE_X - 1));
     const int yl = __builtin_amdgcn_readfirstlane((wide & 1) ? by : by * TILE_Y + wv);
-    const int yi = a.row_begin + yl;
-    const bool live = xi < a.W && yi < a.row_end;
+    const int yi = __builtin_amdgcn_readfirstlane(eye_row(a.row_begin, a.stripe_rows, a.stripe_stride, a.stripe_phase, yl));
+    const int yo = a.out_global ? yi : yl;  // the output row
+    const bool live = xi < a.W && a.row_begin + yl < a.row_end && yi < a.H;
     unsigned long long n_tests = 0, n_hit = 0, n_lit = 0, n_pl_tests = 0, n_cy_tests = 0;
     ShadowCounts sc;
     int hit_kind = 0, hit_id = -1;
@@ -2024,9 +2030,9 @@ __device__ __forceinline__ void eye_tile(const EyePart& a, const ShadowPart& sh,
         if (live) {
             if (wide & 2)  // non-temporal: the frame's stores do not allocate in the caches
                 __builtin_nontemporal_store(f32x4{c.x, c.y, c.z, c.w},
-                                            reinterpret_cast<f32x4*>(&o[(int64_t)yl * a.W + xi]));
+                                            reinterpret_cast<f32x4*>(&o[(int64_t)yo * a.W + xi]));
             else
-                o[(int64_t)yl * a.W + xi] = c;
+                o[(int64_t)yo * a.W + xi] = c;
         }
     } else {
         uint32_t e = tabs.bg;  // background: one host-encoded constant
@@ -2037,9 +2043,9 @@ __device__ __forceinline__ void eye_tile(const EyePart& a, const ShadowPart& sh,
         }
         if (FMT == RTM_FORMAT_RGBA8) {  // alpha 1.0 -> 255; one dword per pixel, 256 B per wave
             uint32_t* o = reinterpret_cast<uint32_t*>(out);
-            if (live) __builtin_nontemporal_store(e | 0xFF000000u, &o[(int64_t)yl * a.W + xi]);
+            if (live) __builtin_nontemporal_store(e | 0xFF000000u, &o[(int64_t)yo * a.W + xi]);
         } else {  // RGB8: the wave's 64 pixels are 192 contiguous bytes = 48 dwords
-            uint8_t* row = reinterpret_cast<uint8_t*>(out) + (int64_t)yl * a.W * 3;
+            uint8_t* row = reinterpret_cast<uint8_t*>(out) + (int64_t)yo * a.W * 3;
             if (tabs.fmt & FMT_RGB8_DWORDS) {
                 // dword j of the wave's segment: bytes 4j..4j+3 = the tail of pixel L (from
                 // byte o = 4j - 3L) and the head of pixel L + 1
@@ -2050,7 +2056,7 @@ __device__ __forceinline__ void eye_tile(const EyePart& a, const ShadowPart& sh,
                 const uint32_t p1 = (uint32_t)__shfl((int)e, min(L + 1, TILE_X - 1));
                 const uint32_t w = (p0 >> (8 * o)) | (p1 << (8 * (3 - o)));
                 const int nv = min(TILE_X, a.W - xb);  // W % 4 == 0 (host-checked): 3*nv/4 whole dwords
-                if (yi < a.row_end && j < (3 * nv) >> 2)
+                if (a.row_begin + yl < a.row_end && yi < a.H && j < (3 * nv) >> 2)
                     __builtin_nontemporal_store(w, reinterpret_cast<uint32_t*>(row + 3 * (int64_t)xb) + j);
             } else if (live) {
                 row[3 * (int64_t)xi + 0] = (uint8_t)e;
@@ -2163,10 +2169,10 @@ __global__ __launch_bounds__(BLOCK) void pull_kernel(const uint4* __restrict__ s
 // bounding-sphere tests run once per wave instead of on every lane of it.  The
 // same operations, hence the same masks.
 __device__ __forceinline__ void rt_cull_wave(const CamK& c, const RtK* __restrict__ rt, int W, int H, int row_begin,
-                                             int rows, uint32_t* __restrict__ masks, int t) {
+                                             int rows, int4 stripes, uint32_t* __restrict__ masks, int t) {
     const int gx = (W + TILE_X - 1) / TILE_X;
     if (t >= gx * rows) return;
-    const int xb = (t % gx) * TILE_X, yi = row_begin + t / gx;
+    const int xb = (t % gx) * TILE_X, yi = eye_row(row_begin, stripes.x, stripes.y, stripes.z, t / gx);
     const RayCone k = ray_cone(c, min(xb, W - 1), min(xb + TILE_X - 1, W - 1), min(yi, H - 1), W, H);
     uint32_t m = ~0u;
     for (int l = 0; l < 32; ++l) {
@@ -2180,8 +2186,9 @@ __device__ __forceinline__ void rt_cull_wave(const CamK& c, const RtK* __restric
 }
 
 __global__ __launch_bounds__(BLOCK) void rt_cull_kernel(const CamK c, const RtK* __restrict__ rt, int W, int H,
-                                                        int row_begin, int rows, uint32_t* __restrict__ masks) {
-    rt_cull_wave(c, rt, W, H, row_begin, rows, masks, blockIdx.x * BLOCK + threadIdx.x);
+                                                        int row_begin, int rows, int4 stripes,
+                                                        uint32_t* __restrict__ masks) {
+    rt_cull_wave(c, rt, W, H, row_begin, rows, stripes, masks, blockIdx.x * BLOCK + threadIdx.x);
 }
 
 // rt_cull_kernel for a batch: frame blockIdx.z's masks (frames with ray-traced
@@ -2193,7 +2200,8 @@ __global__ __launch_bounds__(BLOCK) void rt_cull_batch_kernel(CBatch* __restrict
     const RtK* rt = f->tabs.rt;
     if (!masks || !rt) return;
     const EyePart& e = *(const EyePart*)&f->a.ey;
-    rt_cull_wave(e.eye, rt, e.W, e.H, e.row_begin, e.row_end - e.row_begin, masks, blockIdx.x * BLOCK + threadIdx.x);
+    rt_cull_wave(e.eye, rt, e.W, e.H, e.row_begin, e.row_end - e.row_begin,
+                 make_int4(e.stripe_rows, e.stripe_stride, e.stripe_phase, 0), masks, blockIdx.x * BLOCK + threadIdx.x);
 }
 
 // Timing diagnostic only (RTM_DIAG_EYE=1): the eye pass's stores without its work.
@@ -2728,7 +2736,8 @@ int launch_eye_pass(const FrameArgs& a, const double* smap, void* out, void* str
         if (t.rtmask && !(wide & 4)) {
             const int n = ((a.ey.W + TILE_X - 1) / TILE_X) * rows;
             hipLaunchKernelGGL(rt_cull_kernel, dim3((unsigned)((n + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, s, a.ey.eye,
-                               t.rt, a.ey.W, a.ey.H, a.ey.row_begin, rows, t.rtmask);
+                               t.rt, a.ey.W, a.ey.H, a.ey.row_begin, rows,
+                               make_int4(a.ey.stripe_rows, a.ey.stripe_stride, a.ey.stripe_phase, 0), t.rtmask);
         } else {
             t.rtmask = nullptr;
         }

@@ -157,5 +157,8 @@ def roofline(kernel: str, work: dict, ms: float, traffic_bytes=None) -> dict:
     main["other_roof"] = other
     main["algorithmic_bytes_per_launch"] = w["bytes"]
     main["algorithmic_f64_ops_per_launch"] = w["ops"]
+    main["ops_basis"] = ("reference-equivalent: every f64 add/sub/mul/div/sqrt/compare/class test/abs of the "
+                         "restated algorithm (module docstring) counts 1, priced at the non-FMA f64 peak; "
+                         "compares and abs are not FMA-pipe flops, so `pmc` beside it gives the issued view")
     main["avg_launch_ms"] = round(ms, 5)
     return main

@@ -120,6 +120,17 @@ class Context:
                                                  flags, fmt, row_begin, row_end, C.c_void_p(out_ptr)),
                   "rtm_render_rows_async")
 
+    def render_stripes_async(self, scene: Scene, eye: Camera, shadow: Camera, width: int, height: int, steps: int,
+                             flags: int, fmt: int, stripe_rows: int, n_parts: int, part: int, out_ptr: int):
+        """rtm_render_stripes_async: part `part` of n_parts under stripe_rows-row cyclic
+        stripes, compact rows (stripe_rows_of(...) of them) into the device buffer."""
+        sc, keep = scene.to_c()
+        e, s = eye.to_c(), shadow.to_c()
+        lib = _lib()
+        abi.check(lib, lib.rtm_render_stripes_async(self._h, C.byref(sc), C.byref(e), C.byref(s), width, height,
+                                                    steps, flags, fmt, stripe_rows, n_parts, part,
+                                                    C.c_void_p(out_ptr)), "rtm_render_stripes_async")
+
     def prepare_frames(self, scenes):
         """ctypes array of rtm_scene for render_frames_async (+ keepalive)."""
         arr = (abi.rtm_scene * len(scenes))()
@@ -347,6 +358,16 @@ class Group:
     def set_root_staging(self, on: bool):
         lib = _lib()
         abi.check(lib, lib.rtm_group_set_root_staging(self._h, 1 if on else 0), "rtm_group_set_root_staging")
+
+    def set_partition(self, stripe_rows: int):
+        """rtm_group_set_partition: S-row cyclic stripes (S > 0), contiguous bands (0),
+        the library default (-1: 8-row stripes for N > 1)."""
+        lib = _lib()
+        abi.check(lib, lib.rtm_group_set_partition(self._h, stripe_rows), "rtm_group_set_partition")
+
+    @property
+    def partition(self) -> int:
+        return int(_lib().rtm_group_partition(self._h))
 
     def set_host_direct(self, on: bool):
         """rtm_group_set_host_direct: render() copies every band from its own device

@@ -32,6 +32,22 @@ def row_bands(height: int, world: int) -> List[Tuple[int, int]]:
     return [row_band(height, world, r) for r in range(world)]
 
 
+def stripe_rows_of(height: int, world: int, stripe: int, rank: int) -> int:
+    """Rows of rank `rank` under `stripe`-row cyclic stripes (stripe j -> rank j % world);
+    mirrors rtm_stripe_rows / rtm_api.cpp stripe_rows_of."""
+    full, tail = divmod(height, stripe)
+    rows = (full // world + (1 if rank < full % world else 0)) * stripe
+    if tail and full % world == rank:
+        rows += tail
+    return rows
+
+
+def stripe_image_rows(height: int, world: int, stripe: int, rank: int) -> List[int]:
+    """The image rows of rank `rank`'s stripes, in its local (compact) order."""
+    return [y for j in range(rank, (height + stripe - 1) // stripe, world)
+            for y in range(j * stripe, min((j + 1) * stripe, height))]
+
+
 def frames_for_rank(n_frames: int, rank: int, world: int) -> List[int]:
     return list(range(rank, n_frames, world))
 

@@ -292,10 +292,10 @@ def host_output(rtm, scene, eye, shadow, W, H, K, flags, frames=8, n_gpus=0):
     return res
 
 
-def _latest_traffic(cfg_id: int, kernel: str, frames_per_launch: int = 1):
-    """HBM bytes per launch from the newest committed PMC summary (tools/profile.sh)
-    whose launches held `frames_per_launch` frames (`frames_per_launch` in the
-    summary, 1 when absent)."""
+def _latest_pmc(cfg_id: int, kernel: str, frames_per_launch: int = 1):
+    """(file, per-launch counters) of `kernel` from the newest committed PMC summary
+    (tools/profile_pmc.sh) whose launches held `frames_per_launch` frames
+    (`frames_per_launch` in the summary, 1 when absent); (None, None) if none."""
     import re
 
     def key(f):  # newest round/version first: r01_v12 after r01_v9 (not lexicographic)
@@ -310,8 +310,35 @@ def _latest_traffic(cfg_id: int, kernel: str, frames_per_launch: int = 1):
             continue
         if (d.get("config") == cfg_id and kernel in d.get("kernels", {})
                 and d.get("frames_per_launch", 1) == frames_per_launch):
-            return d["kernels"][kernel].get("hbm_bytes_per_launch")
-    return None
+            return os.path.relpath(f, ROOT), d["kernels"][kernel]
+    return None, None
+
+
+def _latest_traffic(cfg_id: int, kernel: str, frames_per_launch: int = 1):
+    """HBM bytes per launch from the newest committed PMC summary (see _latest_pmc)."""
+    _, k = _latest_pmc(cfg_id, kernel, frames_per_launch)
+    return k.get("hbm_bytes_per_launch") if k else None
+
+
+def pmc_fractions(cfg_id: int, kernel: str, frames_per_launch: int, alg_ops: int):
+    """The counters' view of a kernel next to the algorithmic roofline (VERDICT r02
+    item 6): issued f64 lane-ops (SQ_INSTS_VALU_{ADD,MUL,FMA,TRANS}_F64 x 64) over the
+    PMC run's own average duration against the non-FMA f64 peak, and the VALU issue
+    fraction: issued wave-instructions x 2 cycles / (1024 SIMDs x 2.4 GHz x duration)."""
+    src, k = _latest_pmc(cfg_id, kernel, frames_per_launch)
+    if not k or not k.get("avg_duration_ns_profiled"):
+        return None
+    dur = k["avg_duration_ns_profiled"] * 1e-9
+    f64 = 64.0 * sum(k.get(c, 0.0) for c in ("SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64",
+                                              "SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_TRANS_F64"))
+    valu = k.get("SQ_INSTS_VALU", 0.0)
+    waves = k.get("SQ_WAVES", 0.0) or 1.0
+    return {"source": src, "kernel_name": k.get("kernel_name"), "duration_ns": round(k["avg_duration_ns_profiled"]),
+            "issued_f64_lane_ops": int(f64), "issued_f64_frac": round(f64 / dur / 39.3e12, 4),
+            "valu_issue_frac": round(valu * 2 / (1024 * 2.4e9 * dur), 4),
+            "valu_insts_per_wave": round(valu / waves, 1), "salu_insts_per_wave": round(k.get("SQ_INSTS_SALU", 0.0) / waves, 1),
+            "algorithmic_over_issued_f64": round(alg_ops / f64, 3) if f64 else None,
+            "note": "counters from the committed PMC summary of this config (same kernel, same frames per launch)"}
 
 
 def cpu_baseline(scene, eye, shadow, w, h, k, flags, threads, what):
@@ -659,10 +686,10 @@ def main():
         work_l = {k: {"ops": v["ops"] * nb, "bytes": v["bytes"] * nb} for k, v in work.items()}
 
         def kroof(kernel, ms_per_frame):
-            r = dict(metrics.roofline(kernel, work_l, ms_per_frame * nb,
-                                      _latest_traffic(a.config, kernel, nb if kernel == "eye_pass" or
-                                                      kernel == "shadow_pass" else 1)))
+            fpl = nb if kernel in ("eye_pass", "shadow_pass") else 1
+            r = dict(metrics.roofline(kernel, work_l, ms_per_frame * nb, _latest_traffic(a.config, kernel, fpl)))
             r["frames_per_launch"] = nb
+            r["pmc"] = pmc_fractions(a.config, kernel, fpl, work_l[kernel]["ops"])
             return r
 
         if pipelined:

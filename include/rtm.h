@@ -347,8 +347,8 @@ int rtm_render_stats(rtm_ctx* ctx, const rtm_scene* scene, const rtm_camera* eye
 
 /* ---- multi-GPU frame over RCCL (BASELINE north star) ----
  * A group is N ranks, one device each, joined by one RCCL communicator.  A frame
- * is tile-partitioned into N row bands of ceil(H/N) rows (rank r: rows
- * [r*band, min(H,(r+1)*band))); every rank renders its band (each band evaluates
+ * is tile-partitioned over the N ranks: 8-row cyclic stripes by default, or N row
+ * bands of ceil(H/N) rows (rtm_group_set_partition); every rank renders its rows (each band evaluates
  * the shadow texels it reads: RTM_FLAG_FUSED_SHADOW, same image bits), and ONE
  * gather (ncclSend/ncclRecv in one ncclGroupStart/End, rccl.h:700-745: RCCL's own
  * ncclGather is this same pattern, but needs equal counts and the last band may
@@ -413,6 +413,23 @@ int rtm_group_synchronize(rtm_group* g, int32_t timeout_ms);
 /* Test hook: 1 = the root also stages its band and sends it to itself through
  * RCCL (exercises the transfer path on a one-device group); 0 = in place (default). */
 int rtm_group_set_root_staging(rtm_group* g, int32_t on);
+/* ABI v9: the frame's partition over the group's ranks.  stripe_rows = S > 0: cyclic
+ * S-row stripes (stripe j = rows [j*S, (j+1)*S) goes to rank j % N; each rank renders
+ * its stripes compact and the root places them: a 2-D copy per part); 0: contiguous
+ * bands of ceil(H/N) rows (SURVEY.md §8e's first form); -1: the default, 8-row
+ * stripes for N > 1 (bands measured 1.26-1.56x max/mean band time at N = 4-8, the
+ * spheres sit mid-frame; stripes even it out).  RTM_GROUP_STRIPE overrides the
+ * default.  Waits for the group's work first.  rtm_group_partition: the S in use. */
+int rtm_group_set_partition(rtm_group* g, int32_t stripe_rows);
+int32_t rtm_group_partition(rtm_group* g);
+/* ABI v9: part `part` of n_parts of the frame under stripe_rows-row cyclic stripes
+ * (the rows a group rank renders), compact rows into out_dev (rtm_stripe_rows(...)
+ * rows), on ctx's stream; rtm_stripe_rows: that row count (-1: bad arguments). */
+int rtm_render_stripes_async(rtm_ctx* ctx, const rtm_scene* scene, const rtm_camera* eye,
+                             const rtm_camera* shadow, int32_t width, int32_t height, int32_t march_steps,
+                             int32_t flags, int32_t format, int32_t stripe_rows, int32_t n_parts, int32_t part,
+                             void* out_dev);
+int32_t rtm_stripe_rows(int32_t height, int32_t stripe_rows, int32_t n_parts, int32_t part);
 /* ABI v9, test transport: a group of n_members ranks in this process whose gather
  * runs as device copies on the root's transfer stream (the matched send/receive
  * pairs' completion order kept with events) instead of RCCL, so members may share

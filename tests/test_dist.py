@@ -138,3 +138,23 @@ def test_bench_watchdog_prints_the_line_and_exits_cleanly():
     assert len(lines) == 1
     d = json.loads(lines[0])
     assert d["value"] == 1.0 and "watchdog" in d["tile_gather"]["error"]
+
+
+def test_stripe_partition_mirrors_library():
+    """shard.stripe_rows_of / stripe_image_rows (the multi-GPU frame's cyclic stripes)
+    agree with the library's rtm_stripe_rows (a host-only call) and tile every image
+    row exactly once."""
+    import importlib
+    shard = importlib.import_module("2018rustraytracer_amd.shard")
+    rtm = importlib.import_module("2018rustraytracer_amd")
+    lib = rtm.load_library()
+    for H in (1, 7, 8, 9, 255, 1080, 2160, 4320):
+        for n in (1, 2, 3, 4, 7, 8):
+            for S in (1, 3, 8, 64):
+                rows = [shard.stripe_rows_of(H, n, S, r) for r in range(n)]
+                assert sum(rows) == H
+                assert rows == [lib.rtm_stripe_rows(H, S, n, r) for r in range(n)]
+                seen = sorted(y for r in range(n) for y in shard.stripe_image_rows(H, n, S, r))
+                assert seen == list(range(H))
+                assert all(len(shard.stripe_image_rows(H, n, S, r)) == rows[r] for r in range(n))
+    assert lib.rtm_stripe_rows(10, 0, 2, 0) == -1 and lib.rtm_stripe_rows(10, 8, 2, 2) == -1

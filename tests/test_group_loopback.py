@@ -3,9 +3,11 @@
 rtm_group_create_loopback builds an N-member group in one process whose gather
 is a device copy per matched send/receive pair (same event ordering as the RCCL
 pairs) instead of RCCL, so members may share a device.  Everything else is the
-production path: N row bands of ceil(H/N) rows, each band rendered with the fused
-shadow on its own context, double-buffered staging, the root's receive loop over
-peers, chunked frame sequences.  Every frame is compared with the CPU oracle
+production path: the frame partitioned over N ranks (8-row cyclic stripes by
+default, contiguous bands of ceil(H/N) rows, other stripe heights), each part
+rendered with the fused shadow on its own context, double-buffered staging, the
+root's receive loop over peers and its 2-D placement of striped parts, chunked
+frame sequences.  Every frame is compared with the CPU oracle
 (oracle.render, then its writeColorImage encode) bit for bit.
 
 Also rtm_group_set_host_direct (ABI v9): rtm_group_render delivers the frame over
@@ -159,3 +161,67 @@ def test_loopback_rejects_bad_members(rtm):
     devs = (C.c_int32 * 2)(0, 99)
     assert lib.rtm_group_create_loopback(2, devs, C.byref(h)) == rtm.abi.RTM_ERR_INVALID
     assert not h.value
+
+
+PARTS = [
+    # (config, members, format, root, staged, stripe rows): contiguous bands (0), odd stripes,
+    # stripe periods that do not divide H, more ranks than stripes
+    (4, 8, 0, 0, False, 0),
+    (4, 4, 1, 3, True, 0),
+    (2, 3, 0, 1, False, 7),
+    (2, 8, 2, 0, True, 3),
+    (5, 7, 0, 2, False, 8),
+    (2, 8, 1, 5, False, 256),
+]
+
+
+@pytest.mark.parametrize("case", PARTS, ids=[f"cfg{c[0]}-n{c[1]}-fmt{c[2]}-root{c[3]}{'-staged' if c[4] else ''}-S{c[5]}"
+                                             for c in PARTS])
+def test_loopback_group_partitions(rtm, oracle, scenes, case):
+    """Both partitions (contiguous bands, S-row cyclic stripes placed by the root's 2-D
+    copies; the root's own stripes in place) give the oracle's frame."""
+    import torch
+    cfg, n, fmt, root, staged, S = case
+    c = scenes.CONFIGS[cfg]
+    w, h, k = c["width"], c["height"], c["steps"]
+    s = scenes.scene_a_bench(100) if cfg != 5 else c["scene"]()
+    g = rtm.Group(n_devices=n, loopback=True)
+    try:
+        assert g.partition == 8  # the default for N > 1
+        g.set_partition(S)
+        assert g.partition == S
+        g.set_root_staging(staged)
+        out = device_out(torch, rtm, h, w, fmt)
+        out.fill_(0xAB if fmt else 7.0)
+        torch.cuda.synchronize()
+        g.render_async(s, scenes.eye_camera(), scenes.shadow_camera(), w, h, k, c["flags"], fmt, root,
+                       out.data_ptr())
+        g.synchronize(120000)
+        got = to_host(out, h, w, fmt, rtm.abi)
+        want = want_cached(oracle, rtm, scenes, cfg, 100, fmt)
+        bad = got.view(np.uint8) != want.view(np.uint8)
+        assert not bad.any(), f"{int(bad.sum())} bytes differ, first rows {sorted(set(np.argwhere(bad)[:, 0]))[:5]}"
+    finally:
+        g.close()
+        torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("S,n", [(8, 8), (3, 5), (64, 3)])
+def test_render_stripes_matches_oracle_rows(rtm, oracle, scenes, gpu_ctx, S, n):
+    """rtm_render_stripes_async: every part's compact rows are the oracle's image rows
+    of that part (RGBA f32 and RGB8), fused shadow as the group renders them."""
+    import torch
+    shard = __import__("importlib").import_module("2018rustraytracer_amd.shard")
+    w, h, k = 1920, 1080, 32
+    s, eye, sh = scenes.scene_a_bench(100), scenes.eye_camera(), scenes.shadow_camera()
+    fl = rtm.abi.RTM_FLAG_FUSED_SHADOW
+    want = {f: want_frame(oracle, s, eye, sh, w, h, k, fl, f, rtm.abi) for f in (0, 2)}
+    for f in (0, 2):
+        for r in range(n):
+            rows = shard.stripe_rows_of(h, n, S, r)
+            out = device_out(torch, rtm, rows, w, f)
+            torch.cuda.synchronize()
+            gpu_ctx.render_stripes_async(s, eye, sh, w, h, k, fl, f, S, n, r, out.data_ptr())
+            gpu_ctx.synchronize()
+            got = to_host(out, rows, w, f, rtm.abi)
+            assert np.array_equal(got.view(np.uint8), want[f][shard.stripe_image_rows(h, n, S, r)].view(np.uint8)), (f, r)
