@@ -111,19 +111,22 @@ class _Watchdog:
         self._t.cancel()
 
 
-def band_times(rtm, lib, ctx, world, rank, dist, tdev, c_scene, eye, shadow, W, H, K, flags, fmt, reps=6):
-    """Every rank's own band render (what it renders in the tile-partitioned frame,
-    each band evaluating the shadow texels it reads), timed alone with HIP events on
-    its context's stream; rank 0 gets the list (SURVEY.md §8e-1 imbalance)."""
+def band_times(rtm, lib, ctx, world, rank, dist, tdev, c_scene, eye, shadow, W, H, K, flags, fmt, stripe=0,
+               reps=6):
+    """Every rank's own part of the tile-partitioned frame (its band, or with stripe
+    > 0 its cyclic stripes: what the group renders on it, each part evaluating the
+    shadow texels it reads), timed alone with HIP events on its context's stream;
+    rank 0 gets the list (SURVEY.md §8e-1 imbalance)."""
     import ctypes as C
     import torch
 
     shard = importlib.import_module("2018rustraytracer_amd.shard")
     r0, r1 = shard.row_band(H, world, rank)
+    rows = shard.stripe_rows_of(H, world, stripe, rank) if stripe > 0 and world > 1 else r1 - r0
     ms = 0.0
-    if r1 > r0:
+    if rows > 0:
         e_c, s_c = eye.to_c(), shadow.to_c()
-        buf = torch.empty((r1 - r0) * W * rtm.abi.FORMAT_BYTES[fmt] + 16, dtype=torch.uint8,
+        buf = torch.empty(rows * W * rtm.abi.FORMAT_BYTES[fmt] + 16, dtype=torch.uint8,
                           device=torch.device("cuda", torch.cuda.current_device()))
         st = torch.cuda.ExternalStream(ctx.stream)
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -131,9 +134,13 @@ def band_times(rtm, lib, ctx, world, rank, dist, tdev, c_scene, eye, shadow, W, 
         for it in range(2 + reps):
             if it == 2:
                 ev0.record(st)
-            rc = lib.rtm_render_rows_async(ctx.handle, C.byref(c_scene[0]), C.byref(e_c), C.byref(s_c), W, H, K,
-                                           fl, fmt, r0, r1, C.c_void_p(buf.data_ptr()))
-            rtm.abi.check(lib, rc, "rtm_render_rows_async")
+            if stripe > 0 and world > 1:
+                rc = lib.rtm_render_stripes_async(ctx.handle, C.byref(c_scene[0]), C.byref(e_c), C.byref(s_c), W, H,
+                                                  K, fl, fmt, stripe, world, rank, C.c_void_p(buf.data_ptr()))
+            else:
+                rc = lib.rtm_render_rows_async(ctx.handle, C.byref(c_scene[0]), C.byref(e_c), C.byref(s_c), W, H, K,
+                                               fl, fmt, r0, r1, C.c_void_p(buf.data_ptr()))
+            rtm.abi.check(lib, rc, "band render")
         ev1.record(st)
         ev1.synchronize()
         ms = ev0.elapsed_time(ev1) / reps
@@ -228,17 +235,21 @@ def tile_gather(rtm, lib, ctx, group, world, rank, dist, tdev, c_scenes, eye, sh
         gather = "none: one band, rendered in place into the output (no transfer at N = 1)"
     else:
         gather = "RCCL: ncclSend/ncclRecv in one group into rank 0's device buffer (librtm rtm_group)"
-    extra = {}
+    stripe = group.partition if group is not None else 0
+    extra = {"partition": (f"{stripe}-row cyclic stripes" if stripe > 0 and world > 1 else
+                           f"contiguous bands of ceil(H/{world}) rows")}
     if bands:
-        bt = band_times(rtm, lib, ctx, world, rank, dist, tdev, c_scenes[0], eye, shadow, W, H, K, flags, fmt)
+        bt = band_times(rtm, lib, ctx, world, rank, dist, tdev, c_scenes[0], eye, shadow, W, H, K, flags, fmt,
+                        stripe if group is not None else 0)
         mean = sum(bt) / len(bt)
-        extra = {"band_ms": [round(v, 4) for v in bt],
-                 "band_max_over_mean": round(max(bt) / mean, 4) if mean > 0 else None,
-                 "band_note": "each rank's own band alone (fused shadow), HIP events on its context stream"}
+        extra.update({"band_ms": [round(v, 4) for v in bt],
+                      "band_max_over_mean": round(max(bt) / mean, 4) if mean > 0 else None,
+                      "band_note": "each rank's own part alone (fused shadow), HIP events on its context stream"})
     return {"value": round(W * H * steps / el / 1e6, 2), "unit": "Mpixels/s", "frames": steps,
             "ms_per_step": round(el / steps * 1e3, 5), "scaling": "strong",
             "format": {0: "RGBA32F", 1: "RGBA8", 2: "RGB8"}[fmt], "bytes_per_pixel": bpp,
-            "root_ingress_bytes_per_frame": int(W * (H - (r01 - r00)) * bpp),
+            "root_ingress_bytes_per_frame": int(W * (H - (shard.stripe_rows_of(H, world, stripe, 0)
+                                                          if stripe > 0 and world > 1 else r01 - r00)) * bpp),
             "gather": gather,
             "shadow": ("fused: each band evaluates the shadow texels it reads" if world > 1 or flags & 4
                        else "two-pass (one band: the whole shadow map)"), **extra}
