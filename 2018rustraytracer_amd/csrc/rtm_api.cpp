@@ -896,7 +896,17 @@ int ensure_tables(rtm_ctx* ctx, int32_t steps, int32_t W, int32_t H, const rtm_c
         const int64_t nd = nt + W + H + nz + nsep;
         const int64_t nok = with_sep ? (int64_t)W + H : 0;
         // the coded shadow tile's records (rtm_kernels.h ZRecK / ColRecK / RowRecK), 32-byte aligned
-        const bool with_rec = with_sep && zmono != 0 && nt >= 1;
+        // (and t strictly rising in k, so the coded tile may compare march codes for t)
+        bool t_rising = true;
+        {
+            double tk = 0.0;  // the t table below: sequential sums of 0.03
+            for (int64_t k = 0; k + 1 < nt && t_rising; ++k) {
+                const double tn = tk + 0.03;
+                t_rising = tn > tk;
+                tk = tn;
+            }
+        }
+        const bool with_rec = with_sep && zmono != 0 && nt >= 1 && t_rising;
         const int64_t rec_at = ((nd + (nok + 1) / 2) + 3) / 4 * 4;
         const int64_t h_pad = ((int64_t)H + 63) / 64 * 64;  // row records padded (RowRecK)
         const int64_t nrec = with_rec ? 4 * (nt + 1) + 4 * (int64_t)n_patches * W + 2 * h_pad : 0;

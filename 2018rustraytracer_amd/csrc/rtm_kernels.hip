@@ -1655,6 +1655,10 @@ __device__ __forceinline__ void shadow_tile_coded(const ShadowPart& a, void* __r
         RTM_PHASE(2)
     };
     if (EB && march) fill_lds();
+    // a sphere covered some texel of this wave (wave-uniform): else every texel's best is
+    // a march code or +INF, and since t_k rises strictly with k (host-checked) the march
+    // compares codes instead of t values
+    bool rasterized = false;
     // shadow viewport rasterize, face BACK (main.rs:1569, 243): as the lean tile
     if (!(a.flags & RTM_FLAG_NO_SHADOW_RASTER) && union_may_cover(a, xb, xb + 127, y0, y0 + NR - 1)) {
         uint32_t live = wave_sphere_mask(a.sph, a.n_spheres, xb, xb + 127, y0, y0 + NR - 1);
@@ -1683,6 +1687,7 @@ __device__ __forceinline__ void shadow_tile_coded(const ShadowPart& a, void* __r
                     in |= s2[c] < 1.0;
                 }
                 if (!__any(in)) continue;  // d < 1 implies s2 < 1 (sqrt monotone, sqrt(1) == 1)
+                rasterized = true;
 #pragma unroll
                 for (int c = 0; c < 2; ++c) {
                     const double d = sqrt(s2[c]);
@@ -1715,8 +1720,12 @@ __device__ __forceinline__ void shadow_tile_coded(const ShadowPart& a, void* __r
             bool sany = false;  // a texel the check cannot decide
             // MASKED: skip rows outside inRange01 or past H (wave-uniform); the
             // common case (every row marches) runs without the row tests
-            auto check = [&](auto masked) {
+            // ZB: the wave holds sphere depths: compare t against the best value (zb);
+            // else compare codes (t_f < t_c <=> f < c; +INF = code -1 -> steps, and the
+            // sentinel guess f = steps never wins), no t read, no zb.
+            auto check = [&](auto masked, auto with_zb) {
                 constexpr bool MASKED = decltype(masked)::value;
+                constexpr bool ZB = decltype(with_zb)::value;
 #pragma unroll
                 for (int r = 0; r < NR; ++r) {
                     if (MASKED && !((rowbits >> r) & 1u)) continue;
@@ -1728,19 +1737,32 @@ __device__ __forceinline__ void shadow_tile_coded(const ShadowPart& a, void* __r
                         // conversion of a value in [1, steps] are exact and defined
                         const int f = (int)ceilf(__builtin_amdgcn_fmed3f(__builtin_fmaf(g1[c], pyf[r], g0[c]), 1.0f,
                                                                          fsteps));
-                        const double zp = T[f].zprev, zf = T[f].z, tf = T[f].t;
+                        const double zp = T[f].zprev, zf = T[f].z;
                         const bool okA = INC ? (zp < Dv) : !(zp < Dv);
                         const bool okB = INC ? !(zf < Dv) : (zf < Dv);
                         const bool entry = INC ? (oz < Dv) : !(oz < Dv);
-                        const bool win = fastD & okA & okB & (tf < zb[r][c]);
-                        zb[r][c] = win ? tf : zb[r][c];
-                        cd[r][c] = win ? f : cd[r][c];
+                        if (ZB) {
+                            const double tf = T[f].t;
+                            const bool win = fastD & okA & okB & (tf < zb[r][c]);
+                            zb[r][c] = win ? tf : zb[r][c];
+                            cd[r][c] = win ? f : cd[r][c];
+                        } else {
+                            const unsigned lim = min((unsigned)cd[r][c], (unsigned)steps);
+                            const bool win = fastD & okA & okB & ((unsigned)f < lim);
+                            cd[r][c] = win ? f : cd[r][c];
+                        }
                         sany |= !fastD | (entry & !(okA & okB));
                     }
                 }
             };
-            if (rowbits == (1u << NR) - 1u) check(std::false_type{});
-            else check(std::true_type{});
+            const bool full = rowbits == (1u << NR) - 1u;
+            if (rasterized) {
+                if (full) check(std::false_type{}, std::true_type{});
+                else check(std::true_type{}, std::true_type{});
+            } else {
+                if (full) check(std::false_type{}, std::false_type{});
+                else check(std::true_type{}, std::false_type{});
+            }
             if (__any(sany)) {
                 // exact per-texel march (march_axis) for the texels the check cannot decide
                 const double sz = a.cam.dir[2] * 0.03;
@@ -1774,7 +1796,9 @@ __device__ __forceinline__ void shadow_tile_coded(const ShadowPart& a, void* __r
                     for (int r = 0; r < NR; ++r)
 #pragma unroll
                         for (int c = 0; c < 2; ++c)
-                            if (q == r * 2 + c && sl && m.hit && m.t < zb[r][c]) {
+                            if (q == r * 2 + c && sl && m.hit &&
+                                (rasterized ? m.t < zb[r][c]
+                                            : (unsigned)m.k < min((unsigned)cd[r][c], (unsigned)steps))) {
                                 zb[r][c] = m.t;
                                 cd[r][c] = m.k;
                             }
