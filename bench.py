@@ -335,7 +335,8 @@ def pmc_fractions(cfg_id: int, kernel: str, frames_per_launch: int, alg_ops: int
     """The counters' view of a kernel next to the algorithmic roofline (VERDICT r02
     item 6): issued f64 lane-ops (SQ_INSTS_VALU_{ADD,MUL,FMA,TRANS}_F64 x 64) over the
     PMC run's own average duration against the non-FMA f64 peak, and the VALU issue
-    fraction: issued wave-instructions x 2 cycles / (1024 SIMDs x 2.4 GHz x duration)."""
+    fraction: issued wave-instructions x 2 cycles / (1024 SIMDs x 2.4 GHz x duration), and
+    the VALU busy fraction with the f64 instructions at 4 cycles."""
     src, k = _latest_pmc(cfg_id, kernel, frames_per_launch)
     if not k or not k.get("avg_duration_ns_profiled"):
         return None
@@ -343,10 +344,13 @@ def pmc_fractions(cfg_id: int, kernel: str, frames_per_launch: int, alg_ops: int
     f64 = 64.0 * sum(k.get(c, 0.0) for c in ("SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64",
                                               "SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_TRANS_F64"))
     valu = k.get("SQ_INSTS_VALU", 0.0)
+    f64_wi = f64 / 64.0
     waves = k.get("SQ_WAVES", 0.0) or 1.0
     return {"source": src, "kernel_name": k.get("kernel_name"), "duration_ns": round(k["avg_duration_ns_profiled"]),
             "issued_f64_lane_ops": int(f64), "issued_f64_frac": round(f64 / dur / 39.3e12, 4),
             "valu_issue_frac": round(valu * 2 / (1024 * 2.4e9 * dur), 4),
+            # f64 wave-instructions hold the SIMD 4 cycles (16 f64 lanes per clock), the rest 2
+            "valu_busy_frac": round((f64_wi * 4 + (valu - f64_wi) * 2) / (1024 * 2.4e9 * dur), 4),
             "valu_insts_per_wave": round(valu / waves, 1), "salu_insts_per_wave": round(k.get("SQ_INSTS_SALU", 0.0) / waves, 1),
             "algorithmic_over_issued_f64": round(alg_ops / f64, 3) if f64 else None,
             "note": "counters from the committed PMC summary of this config (same kernel, same frames per launch)"}
