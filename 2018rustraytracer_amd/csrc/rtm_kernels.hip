@@ -1572,7 +1572,7 @@ __global__ __launch_bounds__(BLOCK) void shadow_lean2_batch_kernel(CBatch* __res
 constexpr int CODED_MAX_STEPS = 1023;  // (steps + 1) * 32 B <= 32 KiB of LDS
 // WL: every wave fills its own copy of the LDS records (no workgroup barrier;
 // steps <= CODED_WL_MAX_STEPS), else the workgroup shares one copy.
-constexpr int CODED_WL_MAX_STEPS = 255;  // 4 copies of (steps + 1) * 32 B <= 32 KiB
+[[maybe_unused]] constexpr int CODED_WL_MAX_STEPS = 255;  // 4 copies of (steps + 1) * 32 B <= 32 KiB
 template <bool INC, int CODE, int NB, bool WL = false, bool EB = false>
 __device__ __forceinline__ void shadow_tile_coded(const ShadowPart& a, void* __restrict__ map, int bx, int by,
                                                   ZRecK* __restrict__ T, int diag) {
@@ -1876,7 +1876,7 @@ __device__ __forceinline__ int eye_row(int row_begin, int S, int stride, int pha
     return S > 0 ? phase + (j / S) * stride + j % S : row_begin + j;
 }
 
-template <bool FUSED, bool COUNT, int RT, int FMT = RTM_FORMAT_RGBA32F>
+template <bool FUSED, bool COUNT, int RT, int FMT = RTM_FORMAT_RGBA32F, bool NOSH = false>
 __device__ __forceinline__ void eye_tile(const EyePart& a, const ShadowPart& sh, const double* __restrict__ smap,
                                          void* __restrict__ out, int bx, int by, StatsK* __restrict__ st,
                                          const DevTabs tabs, int wide = 0) {
@@ -1905,7 +1905,7 @@ __device__ __forceinline__ void eye_tile(const EyePart& a, const ShadowPart& sh,
                          : 0u;
     // the wave's ray-traced primitives (PERSPECTIVE eye; all lanes active here)
     uint32_t rmask = ~0u;
-    if (RTP && tabs.rtmask)
+    if (RTP && tabs.rtmask && a.row_begin + yl < a.row_end)  // (no mask word for rows past the part)
         rmask = ((const __attribute__((address_space(4))) uint32_t*)tabs.rtmask)[yl * ((a.W + TILE_X - 1) / TILE_X) +
                                                                                  (xb / TILE_X)];
     else if (RTB == 1 && rt && a.eye.type == RTM_CAMERA_PERSPECTIVE && !(wide & 4))
@@ -1983,11 +1983,11 @@ __device__ __forceinline__ void eye_tile(const EyePart& a, const ShadowPart& sh,
                     nx = hit.n[0];
                     ny = hit.n[1];
                     nz = hit.n[2];
-                    if (hit.kind == 3) {
+                    if (RT != 2 || hit.kind == 3) {  // (kind 4, an SDF, only with RT 2)
                         cr = rt->cy[hit.id].cr;
                         cg = rt->cy[hit.id].cg;
                         cb = rt->cy[hit.id].cb;
-                    } else if (RT == 2) {
+                    } else {
                         cr = sdf->s[hit.id].cr;
                         cg = sdf->s[hit.id].cg;
                         cb = sdf->s[hit.id].cb;
@@ -2025,8 +2025,8 @@ __device__ __forceinline__ void eye_tile(const EyePart& a, const ShadowPart& sh,
             const int64_t hw = a.Ws / 2, hh = a.Hs / 2;
             const int64_t tx = tex_index(hw, qx * (double)hw);
             const int64_t ty = tex_index(hh, qy * (double)hh);
-            double dsm = INFINITY;
-            if (ty >= 0 && ty < a.Hs && tx >= 0 && tx < a.Ws) {
+            double dsm = INFINITY;  // (NOSH: an all-+INF shadow viewport, no lookup)
+            if (!NOSH && ty >= 0 && ty < a.Hs && tx >= 0 && tx < a.Ws) {
                 if (FUSED)
                     dsm = shadow_texel<COUNT>(sh, (int)tx, (int)ty, (int)tx, (int)tx, (int)ty, sc);
                 else if (sh.smap_fmt == SMAP_F64)
@@ -2153,20 +2153,22 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
     eye_tile<false, false, 2, FMT>(a.ey, a.sh, smap, out, blockIdx.x, blockIdx.y, nullptr, tabs, wide);
 }
 
-template <bool FUSED, int RT, int FMT>
+// NOSH: frames whose shadow viewport is all +INF (no shadow raster, no march): the
+// lookup is skipped (lit = +INF > qz, as the fused texel would give)
+template <bool FUSED, int RT, int FMT, bool NOSH = false>
 __global__ __launch_bounds__(BLOCK) void eye_batch_kernel(CBatch* __restrict__ fr, int wide) {
     CBatch* f = fr + blockIdx.z;
     const DevTabs tabs = *(const DevTabs*)&f->tabs;
-    eye_tile<FUSED, false, RT, FMT>(*(const EyePart*)&f->a.ey, *(const ShadowPart*)&f->a.sh, f->smap, f->out,
+    eye_tile<FUSED, false, RT, FMT, NOSH>(*(const EyePart*)&f->a.ey, *(const ShadowPart*)&f->a.sh, f->smap, f->out,
                                     blockIdx.x, blockIdx.y, nullptr, tabs, wide);
 }
 
-template <int WPE, int FMT>
+template <int WPE, int FMT, bool NOSH = false>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8))) void eye_sdf_batch_kernel(
     CBatch* __restrict__ fr, int wide) {
     CBatch* f = fr + blockIdx.z;
     const DevTabs tabs = *(const DevTabs*)&f->tabs;
-    eye_tile<false, false, 2, FMT>(*(const EyePart*)&f->a.ey, *(const ShadowPart*)&f->a.sh, f->smap, f->out,
+    eye_tile<false, false, 2, FMT, NOSH>(*(const EyePart*)&f->a.ey, *(const ShadowPart*)&f->a.sh, f->smap, f->out,
                                    blockIdx.x, blockIdx.y, nullptr, tabs, wide);
 }
 
@@ -2847,6 +2849,16 @@ bool shadow_batchable(const ShadowPart& sh) {
 
 bool eye_wave_cull_on() { return !(eye_wide() & 4); }
 
+// Eye kernels without the shadow lookup for all-+INF shadow viewports (default;
+// RTM_EYE_NOSH=0: the fused kernels, for A/B runs)
+static bool eye_nosh() {
+    static const bool v = [] {
+        const char* e = getenv("RTM_EYE_NOSH");
+        return !(e && atoi(e) == 0);
+    }();
+    return v;
+}
+
 int launch_eye_batch(const BatchFrame* dev, int n, const FrameArgs& a0, const DevTabs& t0, void* stream) {
     hipStream_t s = (hipStream_t)stream;
     CBatch* fr = (CBatch*)dev;
@@ -2863,10 +2875,18 @@ int launch_eye_batch(const BatchFrame* dev, int n, const FrameArgs& a0, const De
     const bool fused = (a0.ey.flags & RTM_FLAG_FUSED_SHADOW) != 0;
     const int fmt = t0.fmt & FMT_MASK;
     const int rt = t0.sdf ? 2 : (t0.rt && t0.rt_persp) ? 3 : (t0.rt || t0.psp) ? 1 : 0;
+    // an all-+INF shadow viewport (fused, no shadow raster, no march): no lookup at all
+    const int both = RTM_FLAG_NO_MARCH | RTM_FLAG_NO_SHADOW_RASTER;
+    const bool nosh = fused && (a0.sh.flags & both) == both && eye_nosh();
 #define RTM_EB(F, R, M) hipLaunchKernelGGL((eye_batch_kernel<F, R, M>), g, dim3(BLOCK), 0, s, fr, wide)
+#define RTM_EBN(R, M) hipLaunchKernelGGL((eye_batch_kernel<false, R, M, true>), g, dim3(BLOCK), 0, s, fr, wide)
 #define RTM_EBF(M)                                                                           \
     do {                                                                                     \
-        if (rt == 2 && !fused && sdf_wpe5())                                                 \
+        if (rt == 2 && nosh && sdf_wpe5())                                                   \
+            hipLaunchKernelGGL((eye_sdf_batch_kernel<5, M, true>), g, dim3(BLOCK), 0, s, fr, wide); \
+        else if (nosh) { if (rt == 3) RTM_EBN(3, M); else if (rt == 1) RTM_EBN(1, M);          \
+                         else if (rt == 2) RTM_EBN(2, M); else RTM_EBN(0, M); }                \
+        else if (rt == 2 && !fused && sdf_wpe5())                                            \
             hipLaunchKernelGGL((eye_sdf_batch_kernel<5, M>), g, dim3(BLOCK), 0, s, fr, wide); \
         else if (rt == 2) { if (fused) RTM_EB(true, 2, M); else RTM_EB(false, 2, M); }      \
         else if (rt == 3) { if (fused) RTM_EB(true, 3, M); else RTM_EB(false, 3, M); }      \
@@ -2877,6 +2897,7 @@ int launch_eye_batch(const BatchFrame* dev, int n, const FrameArgs& a0, const De
     else if (fmt == RTM_FORMAT_RGB8) RTM_EBF(RTM_FORMAT_RGB8);
     else RTM_EBF(RTM_FORMAT_RGBA32F);
 #undef RTM_EBF
+#undef RTM_EBN
 #undef RTM_EB
     return launched();
 }
