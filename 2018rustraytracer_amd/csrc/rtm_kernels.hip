@@ -2131,11 +2131,11 @@ __global__ __launch_bounds__(BLOCK) void shadow_sep_kernel(const FrameArgs a, do
     shadow_tile_sep<NR, MODE>(a.sh, smap, blockIdx.x, blockIdx.y, diag, lds ? lds_zt : nullptr);
 }
 
-template <bool FUSED, bool COUNT, int RT, int FMT>
+template <bool FUSED, bool COUNT, int RT, int FMT, bool NOSH = false>
 __global__ __launch_bounds__(BLOCK) void eye_pass_kernel(const FrameArgs a, const double* __restrict__ smap,
                                                          void* __restrict__ out, StatsK* __restrict__ st,
                                                          const DevTabs tabs, int wide) {
-    eye_tile<FUSED, COUNT, RT, FMT>(a.ey, a.sh, smap, out, blockIdx.x, blockIdx.y, st, tabs, wide);
+    eye_tile<FUSED, COUNT, RT, FMT, NOSH>(a.ey, a.sh, smap, out, blockIdx.x, blockIdx.y, st, tabs, wide);
 }
 
 // The sphere-only eye pass (RT 0, materialised map) held to 8 waves per SIMD: the
@@ -2147,10 +2147,10 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8))) v
 }
 
 // The SDF eye instantiation (row f-4) with a register cap: WPE waves per SIMD at least.
-template <int WPE, int FMT>
+template <int WPE, int FMT, bool NOSH = false>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8))) void eye_sdf_kernel(
     const FrameArgs a, const double* __restrict__ smap, void* __restrict__ out, const DevTabs tabs, int wide) {
-    eye_tile<false, false, 2, FMT>(a.ey, a.sh, smap, out, blockIdx.x, blockIdx.y, nullptr, tabs, wide);
+    eye_tile<false, false, 2, FMT, NOSH>(a.ey, a.sh, smap, out, blockIdx.x, blockIdx.y, nullptr, tabs, wide);
 }
 
 // NOSH: frames whose shadow viewport is all +INF (no shadow raster, no march): the
@@ -2700,12 +2700,33 @@ static bool eye_wpe8() {
     return v;
 }
 
+// Eye kernels without the shadow lookup for all-+INF shadow viewports (default;
+// RTM_EYE_NOSH=0: the fused kernels, for A/B runs)
+static bool eye_nosh() {
+    static const bool v = [] {
+        const char* e = getenv("RTM_EYE_NOSH");
+        return !(e && atoi(e) == 0);
+    }();
+    return v;
+}
+
 template <int FMT>
 static void launch_eye_fmt(const FrameArgs& a, const double* smap, void* o, hipStream_t s, dim3 g, bool fused,
                            const DevTabs& tabs, int wide) {
 #define RTM_EYE(F, R) \
     hipLaunchKernelGGL((eye_pass_kernel<F, false, R, FMT>), g, dim3(BLOCK), 0, s, a, smap, o, nullptr, tabs, wide)
-    if (tabs.sdf) {
+#define RTM_EYEN(R) \
+    hipLaunchKernelGGL((eye_pass_kernel<false, false, R, FMT, true>), g, dim3(BLOCK), 0, s, a, smap, o, nullptr, tabs, wide)
+    const int both = RTM_FLAG_NO_MARCH | RTM_FLAG_NO_SHADOW_RASTER;
+    const bool nosh = fused && (a.sh.flags & both) == both && eye_nosh();  // (see launch_eye_batch)
+    if (nosh) {
+        if (tabs.sdf) {
+            if (sdf_wpe5()) hipLaunchKernelGGL((eye_sdf_kernel<5, FMT, true>), g, dim3(BLOCK), 0, s, a, smap, o, tabs, wide);
+            else RTM_EYEN(2);
+        } else if (tabs.rt && tabs.rt_persp) RTM_EYEN(3);
+        else if (tabs.rt || tabs.psp) RTM_EYEN(1);
+        else RTM_EYEN(0);
+    } else if (tabs.sdf) {
         if (fused) RTM_EYE(true, 2);
         else if (sdf_wpe5())  // 95 VGPRs, 5 waves/SIMD, no spill: eye 582 -> 565 us at config 8
             hipLaunchKernelGGL((eye_sdf_kernel<5, FMT>), g, dim3(BLOCK), 0, s, a, smap, o, tabs, wide);
@@ -2722,6 +2743,7 @@ static void launch_eye_fmt(const FrameArgs& a, const double* smap, void* o, hipS
             hipLaunchKernelGGL((eye_pass8_kernel<FMT>), g, dim3(BLOCK), 0, s, a, smap, o, tabs, wide);
         else RTM_EYE(false, 0);
     }
+#undef RTM_EYEN
 #undef RTM_EYE
 }
 
@@ -2849,15 +2871,6 @@ bool shadow_batchable(const ShadowPart& sh) {
 
 bool eye_wave_cull_on() { return !(eye_wide() & 4); }
 
-// Eye kernels without the shadow lookup for all-+INF shadow viewports (default;
-// RTM_EYE_NOSH=0: the fused kernels, for A/B runs)
-static bool eye_nosh() {
-    static const bool v = [] {
-        const char* e = getenv("RTM_EYE_NOSH");
-        return !(e && atoi(e) == 0);
-    }();
-    return v;
-}
 
 int launch_eye_batch(const BatchFrame* dev, int n, const FrameArgs& a0, const DevTabs& t0, void* stream) {
     hipStream_t s = (hipStream_t)stream;
