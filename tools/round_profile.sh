@@ -3,7 +3,8 @@
 # lines for configs 3 (headline), 4/5 (8K), 6 (row f-1) and 8 (row f-4), rocprofv3
 # kernel-trace summaries of the same commands, and the PMC passes for config 3.
 # Every GPU step has its own limit; a crash/timeout/abort stops the script.
-# SKIP_TESTS=1: no pytest/smoke; PROF_ONLY=1: no bench lines (rocprof steps only).
+# SKIP_TESTS=1: no pytest/smoke; PROF_ONLY=1: no bench lines (rocprof steps only);
+# BENCH_ONLY=1: stop before the rocprof steps.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 ROOT=$(pwd)
@@ -35,6 +36,7 @@ step() {
 [ "${PROF_ONLY:-0}" = 1 ] || step bench7 300 python bench.py --config 7 --no-alt --no-cpu-baseline
 [ "${PROF_ONLY:-0}" = 1 ] || step bench8 300 python bench.py --config 8 --no-alt
 [ "${PROF_ONLY:-0}" = 1 ] || step bench9 300 python bench.py --config 9 --no-alt
+[ "${BENCH_ONLY:-0}" = 1 ] && { echo done; exit 0; }
 step prof3 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof3" -o run --output-format csv -- python3 "$ROOT/bench.py" --steps 25 --warmup 3 --no-cpu-baseline --no-alt
 RTM_LANES=1 step prof3_one_lane 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof3_one_lane" -o run --output-format csv -- python3 "$ROOT/bench.py" --steps 25 --warmup 3 --no-cpu-baseline --no-alt
 step prof4 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof4" -o run --output-format csv -- python3 "$ROOT/bench.py" --config 4 --steps 13 --warmup 2 --no-cpu-baseline --no-alt
