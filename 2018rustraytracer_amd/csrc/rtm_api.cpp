@@ -1456,7 +1456,17 @@ int enqueue_batch(rtm_ctx* ctx, int lane, FrameArgs* fa, const FrameExtra* ex, v
     TimingSlot* slot = next_slot(ctx);
     if (!fused) {
         if (slot) HIP_TRY(hipEventRecord(slot->ev[0], s));
-        if ((rc = launch_shadow_batch((const BatchFrame*)db, n, fa[0], s))) return fail(rc, "batched shadow pass failed");
+        // the union of the frames' sphere boxes (the split coded launch)
+        int32_t box[4] = {INT32_MAX, INT32_MIN, INT32_MAX, INT32_MIN};
+        for (int k = 0; k < n; ++k) {
+            const ShadowPart& q = fa[k].sh;
+            if (q.cull_x0 > q.cull_x1 || q.cull_y0 > q.cull_y1) continue;
+            box[0] = std::min(box[0], q.cull_x0);
+            box[1] = std::max(box[1], q.cull_x1);
+            box[2] = std::min(box[2], q.cull_y0);
+            box[3] = std::max(box[3], q.cull_y1);
+        }
+        if ((rc = launch_shadow_batch((const BatchFrame*)db, n, fa[0], s, box))) return fail(rc, "batched shadow pass failed");
         if (ctx->stagger_arm) {
             HIP_TRY(hipEventRecord(ctx->stagger, s));
             ctx->stagger_arm = false;

@@ -358,7 +358,8 @@ int launch_eye_pass(const FrameArgs& a, const double* smap, void* out, void* str
 // Batched passes over n frames (gridDim.z = n) whose BatchFrame table is at dev
 // (device memory); a0 / t0: the host copy of frame 0's arguments (every frame of
 // a batch shares the shapes, flags, tables and kernel variant).
-int launch_shadow_batch(const BatchFrame* dev, int n, const FrameArgs& a0, void* stream);
+// box: the union of the batch's sphere pixel boxes (x0, x1, y0, y1) for the split coded launch
+int launch_shadow_batch(const BatchFrame* dev, int n, const FrameArgs& a0, void* stream, const int32_t* box = nullptr);
 int launch_eye_batch(const BatchFrame* dev, int n, const FrameArgs& a0, const DevTabs& t0, void* stream);
 // The eye pass's per-wave primitive cull is on (RTM_EYE_MODE bit 2 clear).
 bool eye_wave_cull_on();

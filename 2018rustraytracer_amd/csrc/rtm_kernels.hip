@@ -1573,7 +1573,10 @@ constexpr int CODED_MAX_STEPS = 1023;  // (steps + 1) * 32 B <= 32 KiB of LDS
 // WL: every wave fills its own copy of the LDS records (no workgroup barrier;
 // steps <= CODED_WL_MAX_STEPS), else the workgroup shares one copy.
 [[maybe_unused]] constexpr int CODED_WL_MAX_STEPS = 255;  // 4 copies of (steps + 1) * 32 B <= 32 KiB
-template <bool INC, int CODE, int NB, bool WL = false, bool EB = false>
+// PART (the split launch, launch_coded): 0 every tile; 1 only workgroup tiles outside
+// the frame's sphere box (no raster code: fewer registers, more waves per SIMD);
+// 2 only tiles meeting the box.
+template <bool INC, int CODE, int NB, bool WL = false, bool EB = false, int PART = 0>
 __device__ __forceinline__ void shadow_tile_coded(const ShadowPart& a, void* __restrict__ map, int bx, int by,
                                                   ZRecK* __restrict__ T, int diag) {
     constexpr int NR = 4 * NB;
@@ -1660,7 +1663,7 @@ __device__ __forceinline__ void shadow_tile_coded(const ShadowPart& a, void* __r
     // compares codes instead of t values
     bool rasterized = false;
     // shadow viewport rasterize, face BACK (main.rs:1569, 243): as the lean tile
-    if (!(a.flags & RTM_FLAG_NO_SHADOW_RASTER) && union_may_cover(a, xb, xb + 127, y0, y0 + NR - 1)) {
+    if (PART != 1 && !(a.flags & RTM_FLAG_NO_SHADOW_RASTER) && union_may_cover(a, xb, xb + 127, y0, y0 + NR - 1)) {
         uint32_t live = wave_sphere_mask(a.sph, a.n_spheres, xb, xb + 127, y0, y0 + NR - 1);
         double xc[2] = {0.0, 0.0};  // the columns' NDC x, only where a sphere may cover
         if (live) {
@@ -1838,29 +1841,43 @@ __device__ __forceinline__ void shadow_tile_coded(const ShadowPart& a, void* __r
     }
 }
 
-template <bool INC, int CODE, int NB, bool WL, bool EB>
+template <bool INC, int CODE, int NB, bool WL, bool EB, int PART = 0>
 __device__ __forceinline__ void shadow_coded_block(const ShadowPart& sh, void* __restrict__ map, ZRecK* __restrict__ lds,
-                                                   int diag) {
+                                                   int diag, int4 org) {
     constexpr int TR = TILE_Y * 4 * NB;
-    const int n = (int)gridDim.y;
-    const int h0 = max(sh.cull_y0, 0) / TR;
-    const int h1 = min(min(sh.cull_y1, sh.H - 1) / TR, n - 1);
-    const bool none = sh.cull_x0 > sh.cull_x1 || sh.cull_y0 > sh.cull_y1 || sh.cull_y1 < 0;
-    const int by = none ? (int)blockIdx.y : hot_rows_first((int)blockIdx.y, n, h0, h1);
-    shadow_tile_coded<INC, CODE, NB, WL, EB>(sh, map, blockIdx.x, by, lds, diag);
+    int bx = (int)blockIdx.x, by;
+    if (PART == 0) {
+        const int n = (int)gridDim.y;
+        const int h0 = max(sh.cull_y0, 0) / TR;
+        const int h1 = min(min(sh.cull_y1, sh.H - 1) / TR, n - 1);
+        const bool none = sh.cull_x0 > sh.cull_x1 || sh.cull_y0 > sh.cull_y1 || sh.cull_y1 < 0;
+        by = none ? (int)blockIdx.y : hot_rows_first((int)blockIdx.y, n, h0, h1);
+    } else {
+        // (workgroup-uniform: the whole workgroup leaves, before its barrier).  org.z: the
+        // row granularity of the box test (PART 1's tile height, so that a PART-1 tile
+        // that leaves has each of its rows taken by PART 2)
+        bx += org.x;
+        by = (int)blockIdx.y + org.y;
+        const int yb = (by * TR) / org.z * org.z;
+        const bool inbox = !(sh.flags & RTM_FLAG_NO_SHADOW_RASTER) &&
+                           union_may_cover(sh, bx * 128, bx * 128 + 127, yb, yb + org.z - 1);
+        if (PART == 1 ? inbox : !inbox) return;
+    }
+    shadow_tile_coded<INC, CODE, NB, WL, EB, PART>(sh, map, bx, by, lds, diag);
 }
 
-template <bool INC, int CODE, int NB, bool WL, bool EB>
-__global__ __launch_bounds__(BLOCK) void shadow_coded_kernel(const FrameArgs a, double* __restrict__ smap, int diag) {
+template <bool INC, int CODE, int NB, bool WL, bool EB, int PART = 0>
+__global__ __launch_bounds__(BLOCK) void shadow_coded_kernel(const FrameArgs a, double* __restrict__ smap, int diag,
+                                                             int4 org) {
     extern __shared__ ZRecK lds_rec[];
-    shadow_coded_block<INC, CODE, NB, WL, EB>(a.sh, smap, lds_rec, diag);
+    shadow_coded_block<INC, CODE, NB, WL, EB, PART>(a.sh, smap, lds_rec, diag, org);
 }
 
-template <bool INC, int CODE, int NB, bool WL, bool EB>
-__global__ __launch_bounds__(BLOCK) void shadow_coded_batch_kernel(CBatch* __restrict__ fr, int diag) {
+template <bool INC, int CODE, int NB, bool WL, bool EB, int PART = 0>
+__global__ __launch_bounds__(BLOCK) void shadow_coded_batch_kernel(CBatch* __restrict__ fr, int diag, int4 org) {
     extern __shared__ ZRecK lds_rec[];
     CBatch* f = fr + blockIdx.z;
-    shadow_coded_block<INC, CODE, NB, WL, EB>(*(const ShadowPart*)&f->a.sh, f->smap, lds_rec, diag);
+    shadow_coded_block<INC, CODE, NB, WL, EB, PART>(*(const ShadowPart*)&f->a.sh, f->smap, lds_rec, diag, org);
 }
 
 
@@ -2567,8 +2584,22 @@ static bool coded_ok(const ShadowPart& sh) {
            (!march || (sh.tab.zrec && sh.tab.col && sh.tab.row && sh.steps <= CODED_MAX_STEPS));
 }
 
+// The split launch (default; RTM_CODED_SPLIT=0: one launch over every tile): the
+// workgroup tiles meeting a frame's sphere box run the full tile, the others a
+// raster-free instantiation with fewer registers (more waves per SIMD).
+static bool coded_split() {
+    static const bool v = [] {
+        const char* e = getenv("RTM_CODED_SPLIT");
+        return !(e && atoi(e) == 0);
+    }();
+    return v;
+}
+
 // Launch the coded tile for one frame (FrameArgs) or a batch (fr != nullptr, n frames).
-static void launch_coded(const ShadowPart& sh, const FrameArgs* a, double* smap, CBatch* fr, int n, hipStream_t s) {
+// box: the union over the frames of their spheres' pixel boxes (x0, x1, y0, y1), for the
+// split launch (nullptr: sh's own).
+static void launch_coded(const ShadowPart& sh, const FrameArgs* a, double* smap, CBatch* fr, int n, hipStream_t s,
+                         const int32_t* box = nullptr) {
     const bool march = !(sh.flags & RTM_FLAG_NO_MARCH) && sh.n_patches > 0 && sh.steps > 0;
     // record fill + barrier before the sphere raster (RTM_CODED_EB=1) or after it (default)
     static const bool eb = [] {
@@ -2576,15 +2607,46 @@ static void launch_coded(const ShadowPart& sh, const FrameArgs* a, double* smap,
         return e && atoi(e) != 0;
     }();
     const size_t lsm = march ? sizeof(ZRecK) * (size_t)(sh.steps + 1) : 0;
-    dim3 g((unsigned)((sh.W + 127) / 128), (unsigned)((sh.H + TILE_Y * 4 - 1) / (TILE_Y * 4)), (unsigned)(fr ? n : 1));
+    constexpr int TR = TILE_Y * 4;
+    // 4-row blocks per wave of the raster-free part: 2 (8 rows, 69 VGPRs, 7 waves per SIMD;
+    // measured faster than 1 block at 52 VGPRs / 8 waves); RTM_CODED_NB1 = 1 or 4 for A/B runs
+    static const int nb1 = [] {
+        const char* e = getenv("RTM_CODED_NB1");
+        const int v = e ? atoi(e) : 2;
+        return v >= 4 ? 4 : v == 1 ? 1 : 2;
+    }();
+    const int gx = (sh.W + 127) / 128, gy = (sh.H + TR - 1) / TR;
+    dim3 g((unsigned)gx, (unsigned)gy, (unsigned)(fr ? n : 1));
     const bool inc = sh.tab.zmono >= 0;  // (no march: either instantiation is exact)
     const int dg = diag_mode() & 8;       // per-wave phase timestamps only (no result change)
-#define RTM_CK(I, M, E)                                                                                     \
-    do {                                                                                                    \
-        if (fr) hipLaunchKernelGGL((shadow_coded_batch_kernel<I, M, 1, false, E>), g, dim3(BLOCK), lsm, s, fr, dg); \
-        else hipLaunchKernelGGL((shadow_coded_kernel<I, M, 1, false, E>), g, dim3(BLOCK), lsm, s, *a, smap, dg);    \
+    const int4 org0 = make_int4(0, 0, TR, 0);
+    // the split: workgroup tiles [bx0, bx1] x [by0, by1] meet some frame's box
+    const int32_t bx_[4] = {sh.cull_x0, sh.cull_x1, sh.cull_y0, sh.cull_y1};
+    const int32_t* b = box ? box : bx_;
+    const bool raster = !(sh.flags & RTM_FLAG_NO_SHADOW_RASTER) && b[0] <= b[1] && b[2] <= b[3];
+    const int tr1 = TR * nb1;  // PART 1's tile height: the box test's granularity in both parts
+    const int bx0 = raster ? std::max(b[0], 0) / 128 : 0, bx1 = raster ? std::min(b[1] / 128, gx - 1) : -1;
+    const int by0 = raster ? std::max(b[2], 0) / tr1 * (tr1 / TR) : 0;
+    const int by1 = raster ? std::min((b[3] / tr1) * (tr1 / TR) + tr1 / TR - 1, gy - 1) : -1;
+    const bool split = coded_split() && !dg && !eb;
+    dim3 gb((unsigned)std::max(bx1 - bx0 + 1, 0), (unsigned)std::max(by1 - by0 + 1, 0), g.z);
+    dim3 g1((unsigned)gx, (unsigned)((sh.H + tr1 - 1) / tr1), g.z);
+    const int4 orgb = make_int4(bx0, by0, tr1, 0), org1 = make_int4(0, 0, tr1, 0);
+#define RTM_CK(I, M, E, P, G, O, NBV)                                                                          \
+    do {                                                                                                       \
+        if (fr) hipLaunchKernelGGL((shadow_coded_batch_kernel<I, M, NBV, false, E, P>), G, dim3(BLOCK), lsm, s, fr, dg, O); \
+        else hipLaunchKernelGGL((shadow_coded_kernel<I, M, NBV, false, E, P>), G, dim3(BLOCK), lsm, s, *a, smap, dg, O);    \
     } while (0)
-#define RTM_CKB(I, M) do { if (eb) RTM_CK(I, M, true); else RTM_CK(I, M, false); } while (0)
+#define RTM_CKB(I, M)                                                          \
+    do {                                                                       \
+        if (split) {                                                           \
+            if (gb.x > 0 && gb.y > 0) RTM_CK(I, M, false, 2, gb, orgb, 1);     \
+            if (nb1 == 4) RTM_CK(I, M, false, 1, g1, org1, 4);                 \
+            else if (nb1 == 2) RTM_CK(I, M, false, 1, g1, org1, 2);                 \
+            else RTM_CK(I, M, false, 1, g1, org1, 1);                          \
+        } else if (eb) RTM_CK(I, M, true, 0, g, org0, 1);                      \
+        else RTM_CK(I, M, false, 0, g, org0, 1);                               \
+    } while (0)
     if (sh.smap_fmt == SMAP_U8) {
         if (inc) RTM_CKB(true, SMAP_U8);
         else RTM_CKB(false, SMAP_U8);
@@ -2796,12 +2858,12 @@ int launch_eye_pass(const FrameArgs& a, const double* smap, void* out, void* str
     return launched();
 }
 
-int launch_shadow_batch(const BatchFrame* dev, int n, const FrameArgs& a0, void* stream) {
+int launch_shadow_batch(const BatchFrame* dev, int n, const FrameArgs& a0, void* stream, const int32_t* box) {
     hipStream_t s = (hipStream_t)stream;
     CBatch* fr = (CBatch*)dev;
     const ShadowPart& sh = a0.sh;
     if (use_sep(sh) && sep_mode(sh) == MARCH_LEAN2 && sep_rows() == 4 && lean_cols() == 2 && coded_ok(sh)) {
-        launch_coded(sh, nullptr, nullptr, fr, n, s);
+        launch_coded(sh, nullptr, nullptr, fr, n, s, box);
         return launched();
     }
     if (use_sep(sh) && sep_mode(sh) == MARCH_LEAN2 && sep_rows() == 4 && lean_cols() == 2) {
