@@ -79,6 +79,27 @@ def main():
                 out["kernels"][prev["kernel_name"]] = prev
             out["kernels"][name] = d
         d["kernel_name"] = k
+    # the split coded launch (two shadow_coded kernels per batch: sphere tiles, raster-free
+    # tiles): the shadow pass is both, so its per-launch counters and duration are the sums
+    parts = {k: d for k, d in out["kernels"].items()
+             if d.get("kernel_name", "").startswith("shadow_coded_batch_kernel<")}
+    if len(parts) > 1:
+        n = max(d["dispatches"] for d in parts.values())
+        if all(d["dispatches"] >= 0.9 * n for d in parts.values()):
+            merged = {"dispatches": n, "kernel_name": " + ".join(sorted(d["kernel_name"] for d in parts.values())),
+                      "note": "split coded launch: the per-launch sums of its two kernels"}
+            for c in set().union(*[set(d) for d in parts.values()]):
+                if c in ("dispatches", "kernel_name", "hbm_bytes_note", "valu_insts_per_wave", "salu_insts_per_wave"):
+                    continue
+                if all(isinstance(d.get(c), (int, float)) for d in parts.values()):
+                    merged[c] = sum(d[c] for d in parts.values())
+            if merged.get("SQ_WAVES"):
+                merged["valu_insts_per_wave"] = merged.get("SQ_INSTS_VALU", 0) / merged["SQ_WAVES"]
+                merged["salu_insts_per_wave"] = merged.get("SQ_INSTS_SALU", 0) / merged["SQ_WAVES"]
+            for k in list(parts):
+                d = out["kernels"].pop(k)
+                out["kernels"][d["kernel_name"]] = d
+            out["kernels"]["shadow_pass"] = merged
     print(json.dumps(out, indent=1, sort_keys=True))
 
 
