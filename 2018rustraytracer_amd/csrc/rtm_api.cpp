@@ -1287,13 +1287,14 @@ int frame_batch(int32_t req, int32_t W, int32_t H) {
     }();
     const int64_t px = (int64_t)W * H;
     // 64 Mpixel worth of frames, at most 64 below 1 Mpixel (512x512: 64 frames per
-    // launch) and 16 above (1920x1080: 16, 3840x2160: 8, 7680x4320: 2).  With the
+    // launch) and 32 above (1920x1080: 32, 3840x2160: 8, 7680x4320: 2; the cap was 16
+    // until r03: 1920x1080 298 -> 304-305 Gpix/s at 32, profiles/r03_ab_batch_split.txt).  With the
     // batch table pulled by the lane's stream (r02_v10) bigger batches pay: 3840x2160
     // 250 -> 262 Gpix/s at 8 frames, 1920x1080 218 -> 248 at 16; with the async copy
     // the larger table went to a copy engine and 8 frames ran at 91-150 Gpix/s
     // (profiles/r02_ab_batch_pull.txt).
     const int64_t target = 64LL << 20;
-    const int64_t cap = px < (1LL << 20) ? 64 : 16;
+    const int64_t cap = px < (1LL << 20) ? 64 : 32;
     int B = req > 0 ? req : env > 0 ? env : (int)std::max<int64_t>(1, std::min<int64_t>(cap, target / px));
     return std::max(1, std::min(B, 64));
 }
