@@ -1573,10 +1573,17 @@ constexpr int CODED_MAX_STEPS = 1023;  // (steps + 1) * 32 B <= 32 KiB of LDS
 // WL: every wave fills its own copy of the LDS records (no workgroup barrier;
 // steps <= CODED_WL_MAX_STEPS), else the workgroup shares one copy.
 [[maybe_unused]] constexpr int CODED_WL_MAX_STEPS = 255;  // 4 copies of (steps + 1) * 32 B <= 32 KiB
+// Two 16-bit codes per register (low: column 0, high: column 1), element-wise min.
+typedef unsigned short ushort2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t pk_min_u16(uint32_t a, uint32_t b) {
+    return __builtin_bit_cast(uint32_t, __builtin_elementwise_min(__builtin_bit_cast(ushort2_t, a),
+                                                                  __builtin_bit_cast(ushort2_t, b)));
+}
+
 // PART (the split launch, launch_coded): 0 every tile; 1 only workgroup tiles outside
 // the frame's sphere box (no raster code: fewer registers, more waves per SIMD);
 // 2 only tiles meeting the box.
-template <bool INC, int CODE, int NB, bool WL = false, bool EB = false, int PART = 0>
+template <bool INC, int CODE, int NB, bool WL = false, bool EB = false, int PART = 0, bool PK_CODES = false>
 __device__ __forceinline__ void shadow_tile_coded(const ShadowPart& a, void* __restrict__ map, int bx, int by,
                                                   ZRecK* __restrict__ T, int diag) {
     constexpr int NR = 4 * NB;
@@ -1624,13 +1631,19 @@ __device__ __forceinline__ void shadow_tile_coded(const ShadowPart& a, void* __r
     RTM_PHASE(0)
     double zb[NR][2];
     int cd[NR][2];
+    // PK (the raster-free part, only march codes < steps or +INF, which fit 16 bits): a
+    // row's two codes packed in one register, +INF = 0xFFFF (half the code registers)
+    constexpr bool PK = PART == 1 && PK_CODES;
+    uint32_t cdp[NR];
 #pragma unroll
-    for (int r = 0; r < NR; ++r)
+    for (int r = 0; r < NR; ++r) {
+        cdp[r] = 0xFFFFFFFFu;
 #pragma unroll
         for (int c = 0; c < 2; ++c) {
             zb[r][c] = INFINITY;
             cd[r][c] = -1;
         }
+    }
     // the records into LDS (all threads) + the barrier: EB = before the sphere raster
     // (waves without spheres then do not wait at the barrier for the raster of waves
     // with spheres), else after it (the record loads in flight during the raster)
@@ -1732,6 +1745,7 @@ __device__ __forceinline__ void shadow_tile_coded(const ShadowPart& a, void* __r
 #pragma unroll
                 for (int r = 0; r < NR; ++r) {
                     if (MASKED && !((rowbits >> r) & 1u)) continue;
+                    unsigned vv[2] = {0xFFFFu, 0xFFFFu};  // (PK: this row's decided codes)
 #pragma unroll
                     for (int c = 0; c < 2; ++c) {
                         const double Dv = d0[c] + dd[c] * py[r];
@@ -1749,6 +1763,9 @@ __device__ __forceinline__ void shadow_tile_coded(const ShadowPart& a, void* __r
                             const bool win = fastD & okA & okB & (tf < zb[r][c]);
                             zb[r][c] = win ? tf : zb[r][c];
                             cd[r][c] = win ? f : cd[r][c];
+                        } else if (PK) {
+                            // a decided crossing below the sentinel; the smaller code wins below
+                            vv[c] = (fastD & okA & okB & ((unsigned)f < (unsigned)steps)) ? (unsigned)f : 0xFFFFu;
                         } else {
                             const unsigned lim = min((unsigned)cd[r][c], (unsigned)steps);
                             const bool win = fastD & okA & okB & ((unsigned)f < lim);
@@ -1756,6 +1773,7 @@ __device__ __forceinline__ void shadow_tile_coded(const ShadowPart& a, void* __r
                         }
                         sany |= !fastD | (entry & !(okA & okB));
                     }
+                    if (PK && !ZB) cdp[r] = pk_min_u16(cdp[r], vv[0] | (vv[1] << 16));
                 }
             };
             const bool full = rowbits == (1u << NR) - 1u;
@@ -1799,9 +1817,13 @@ __device__ __forceinline__ void shadow_tile_coded(const ShadowPart& a, void* __r
                     for (int r = 0; r < NR; ++r)
 #pragma unroll
                         for (int c = 0; c < 2; ++c)
-                            if (q == r * 2 + c && sl && m.hit &&
-                                (rasterized ? m.t < zb[r][c]
-                                            : (unsigned)m.k < min((unsigned)cd[r][c], (unsigned)steps))) {
+                            if (PK) {
+                                const unsigned cur = (cdp[r] >> (16 * c)) & 0xFFFFu;
+                                if (q == r * 2 + c && sl && m.hit && (unsigned)m.k < min(cur, (unsigned)steps))
+                                    cdp[r] = (cdp[r] & ~(0xFFFFu << (16 * c))) | ((unsigned)m.k << (16 * c));
+                            } else if (q == r * 2 + c && sl && m.hit &&
+                                       (rasterized ? m.t < zb[r][c]
+                                                   : (unsigned)m.k < min((unsigned)cd[r][c], (unsigned)steps))) {
                                 zb[r][c] = m.t;
                                 cd[r][c] = m.k;
                             }
@@ -1824,13 +1846,14 @@ __device__ __forceinline__ void shadow_tile_coded(const ShadowPart& a, void* __r
             for (int r = 0; r < 4; ++r)
 #pragma unroll
                 for (int c = 0; c < 2; ++c)
-                    w[r >> 1] |= ((uint32_t)cd[4 * b + r][c] & 0xFFu) << (8 * ((r & 1) * 2 + c));
+                    w[r >> 1] |= ((PK ? cdp[4 * b + r] >> (16 * c) : (uint32_t)cd[4 * b + r][c]) & 0xFFu)
+                                 << (8 * ((r & 1) * 2 + c));
             *reinterpret_cast<uint2*>((uint8_t*)map + blk * 512 + lane * 8) = make_uint2(w[0], w[1]);
         } else {
             uint32_t w[4];
 #pragma unroll
             for (int r = 0; r < 4; ++r)
-                w[r] = ((uint32_t)cd[4 * b + r][0] & 0xFFFFu) | ((uint32_t)cd[4 * b + r][1] << 16);
+                w[r] = PK ? cdp[4 * b + r] : ((uint32_t)cd[4 * b + r][0] & 0xFFFFu) | ((uint32_t)cd[4 * b + r][1] << 16);
             *reinterpret_cast<uint4*>((uint8_t*)map + blk * 1024 + lane * 16) = make_uint4(w[0], w[1], w[2], w[3]);
         }
     }
@@ -1841,7 +1864,7 @@ __device__ __forceinline__ void shadow_tile_coded(const ShadowPart& a, void* __r
     }
 }
 
-template <bool INC, int CODE, int NB, bool WL, bool EB, int PART = 0>
+template <bool INC, int CODE, int NB, bool WL, bool EB, int PART = 0, bool PK = false>
 __device__ __forceinline__ void shadow_coded_block(const ShadowPart& sh, void* __restrict__ map, ZRecK* __restrict__ lds,
                                                    int diag, int4 org) {
     constexpr int TR = TILE_Y * 4 * NB;
@@ -1863,21 +1886,21 @@ __device__ __forceinline__ void shadow_coded_block(const ShadowPart& sh, void* _
                            union_may_cover(sh, bx * 128, bx * 128 + 127, yb, yb + org.z - 1);
         if (PART == 1 ? inbox : !inbox) return;
     }
-    shadow_tile_coded<INC, CODE, NB, WL, EB, PART>(sh, map, bx, by, lds, diag);
+    shadow_tile_coded<INC, CODE, NB, WL, EB, PART, PK>(sh, map, bx, by, lds, diag);
 }
 
-template <bool INC, int CODE, int NB, bool WL, bool EB, int PART = 0>
+template <bool INC, int CODE, int NB, bool WL, bool EB, int PART = 0, bool PK = false>
 __global__ __launch_bounds__(BLOCK) void shadow_coded_kernel(const FrameArgs a, double* __restrict__ smap, int diag,
                                                              int4 org) {
     extern __shared__ ZRecK lds_rec[];
-    shadow_coded_block<INC, CODE, NB, WL, EB, PART>(a.sh, smap, lds_rec, diag, org);
+    shadow_coded_block<INC, CODE, NB, WL, EB, PART, PK>(a.sh, smap, lds_rec, diag, org);
 }
 
-template <bool INC, int CODE, int NB, bool WL, bool EB, int PART = 0>
+template <bool INC, int CODE, int NB, bool WL, bool EB, int PART = 0, bool PK = false>
 __global__ __launch_bounds__(BLOCK) void shadow_coded_batch_kernel(CBatch* __restrict__ fr, int diag, int4 org) {
     extern __shared__ ZRecK lds_rec[];
     CBatch* f = fr + blockIdx.z;
-    shadow_coded_block<INC, CODE, NB, WL, EB, PART>(*(const ShadowPart*)&f->a.sh, f->smap, lds_rec, diag, org);
+    shadow_coded_block<INC, CODE, NB, WL, EB, PART, PK>(*(const ShadowPart*)&f->a.sh, f->smap, lds_rec, diag, org);
 }
 
 
@@ -2608,12 +2631,17 @@ static void launch_coded(const ShadowPart& sh, const FrameArgs* a, double* smap,
     }();
     const size_t lsm = march ? sizeof(ZRecK) * (size_t)(sh.steps + 1) : 0;
     constexpr int TR = TILE_Y * 4;
-    // 4-row blocks per wave of the raster-free part: 2 (8 rows, 69 VGPRs, 7 waves per SIMD;
-    // measured faster than 1 block at 52 VGPRs / 8 waves); RTM_CODED_NB1 = 1 or 4 for A/B runs
+    // 4-row blocks per wave of the raster-free part: 4 (16 rows, codes packed two per
+    // register: 72 VGPRs, 7 waves per SIMD; measured faster than 2 blocks, and than 1 block
+    // at 8 waves); RTM_CODED_NB1 = 1 or 2 for A/B runs
     static const int nb1 = [] {
         const char* e = getenv("RTM_CODED_NB1");
-        const int v = e ? atoi(e) : 2;
+        const int v = e ? atoi(e) : 4;
         return v >= 4 ? 4 : v == 1 ? 1 : 2;
+    }();
+    static const bool pk = [] {  // packed 16-bit codes in the raster-free part (RTM_CODED_PK=0: one per register)
+        const char* e = getenv("RTM_CODED_PK");
+        return !(e && atoi(e) == 0);
     }();
     const int gx = (sh.W + 127) / 128, gy = (sh.H + TR - 1) / TR;
     dim3 g((unsigned)gx, (unsigned)gy, (unsigned)(fr ? n : 1));
@@ -2637,11 +2665,18 @@ static void launch_coded(const ShadowPart& sh, const FrameArgs* a, double* smap,
         if (fr) hipLaunchKernelGGL((shadow_coded_batch_kernel<I, M, NBV, false, E, P>), G, dim3(BLOCK), lsm, s, fr, dg, O); \
         else hipLaunchKernelGGL((shadow_coded_kernel<I, M, NBV, false, E, P>), G, dim3(BLOCK), lsm, s, *a, smap, dg, O);    \
     } while (0)
+#define RTM_CKP(I, M, G, O, NBV)                                                                                \
+    do {                                                                                                       \
+        if (fr) hipLaunchKernelGGL((shadow_coded_batch_kernel<I, M, NBV, false, false, 1, true>), G, dim3(BLOCK), lsm, s, fr, dg, O); \
+        else hipLaunchKernelGGL((shadow_coded_kernel<I, M, NBV, false, false, 1, true>), G, dim3(BLOCK), lsm, s, *a, smap, dg, O);    \
+    } while (0)
 #define RTM_CKB(I, M)                                                          \
     do {                                                                       \
         if (split) {                                                           \
             if (gb.x > 0 && gb.y > 0) RTM_CK(I, M, false, 2, gb, orgb, 1);     \
-            if (nb1 == 4) RTM_CK(I, M, false, 1, g1, org1, 4);                 \
+            if (pk && nb1 == 4) RTM_CKP(I, M, g1, org1, 4);                      \
+            else if (pk && nb1 == 2) RTM_CKP(I, M, g1, org1, 2);                 \
+            else if (nb1 == 4) RTM_CK(I, M, false, 1, g1, org1, 4);            \
             else if (nb1 == 2) RTM_CK(I, M, false, 1, g1, org1, 2);                 \
             else RTM_CK(I, M, false, 1, g1, org1, 1);                          \
         } else if (eb) RTM_CK(I, M, true, 0, g, org0, 1);                      \
@@ -2655,6 +2690,7 @@ static void launch_coded(const ShadowPart& sh, const FrameArgs* a, double* smap,
         else RTM_CKB(false, SMAP_U16);
     }
 #undef RTM_CKB
+#undef RTM_CKP
 #undef RTM_CK
 }
 
