@@ -1716,10 +1716,15 @@ __device__ __forceinline__ void shadow_tile_coded(const ShadowPart& a, void* __r
             }
         }
     }
+    // PART 1: a wave whose rows meet the frame's sphere box leaves its texels to PART 2
+    // (which takes every 16-row tile meeting the box) but still fills the records and
+    // meets the workgroup barrier
+    const bool skipw = PART == 1 && !(a.flags & RTM_FLAG_NO_SHADOW_RASTER) &&
+                       union_may_cover(a, xb, xb + 127, y0, y0 + NR - 1);
     if (march) {
         if (!EB) fill_lds();
         const double oz = a.tab.z0;
-        const int np = a.n_patches;
+        const int np = skipw ? 0 : a.n_patches;
         const float fsteps = (float)steps;
         for (int k = 0; k < np; ++k) {
             if (k > 0) {
@@ -1838,7 +1843,7 @@ __device__ __forceinline__ void shadow_tile_coded(const ShadowPart& a, void* __r
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
         const int yb = y0 + 4 * b;
-        if (yb >= H) break;
+        if (yb >= H || skipw) break;
         const int64_t blk = (int64_t)(yb >> 2) * a.smap_bw + (xb >> 7);
         if (CODE == SMAP_U8) {
             uint32_t w[2] = {0u, 0u};
@@ -1876,15 +1881,18 @@ __device__ __forceinline__ void shadow_coded_block(const ShadowPart& sh, void* _
         const bool none = sh.cull_x0 > sh.cull_x1 || sh.cull_y0 > sh.cull_y1 || sh.cull_y1 < 0;
         by = none ? (int)blockIdx.y : hot_rows_first((int)blockIdx.y, n, h0, h1);
     } else {
-        // (workgroup-uniform: the whole workgroup leaves, before its barrier).  org.z: the
-        // row granularity of the box test (PART 1's tile height, so that a PART-1 tile
-        // that leaves has each of its rows taken by PART 2)
+        // (workgroup-uniform: the whole workgroup leaves, before its barrier).  PART 2 takes
+        // the 16-row tiles (its own tiles) meeting the box; PART 1's waves (16 rows at NB 4)
+        // skip those, and its workgroup leaves when every one of its waves would
         bx += org.x;
         by = (int)blockIdx.y + org.y;
-        const int yb = (by * TR) / org.z * org.z;
-        const bool inbox = !(sh.flags & RTM_FLAG_NO_SHADOW_RASTER) &&
-                           union_may_cover(sh, bx * 128, bx * 128 + 127, yb, yb + org.z - 1);
-        if (PART == 1 ? inbox : !inbox) return;
+        const bool rast = !(sh.flags & RTM_FLAG_NO_SHADOW_RASTER);
+        const int ya = by * TR;
+        const int sub = TR / 4;  // a wave's rows
+        if (PART == 2 ? !(rast && union_may_cover(sh, bx * 128, bx * 128 + 127, ya, ya + TR - 1))
+                      : (rast && union_may_cover(sh, bx * 128, bx * 128 + 127, ya, ya + sub - 1) &&
+                         union_may_cover(sh, bx * 128, bx * 128 + 127, ya + TR - sub, ya + TR - 1)))
+            return;
     }
     shadow_tile_coded<INC, CODE, NB, WL, EB, PART, PK>(sh, map, bx, by, lds, diag);
 }
@@ -2652,11 +2660,21 @@ static void launch_coded(const ShadowPart& sh, const FrameArgs* a, double* smap,
     const int32_t bx_[4] = {sh.cull_x0, sh.cull_x1, sh.cull_y0, sh.cull_y1};
     const int32_t* b = box ? box : bx_;
     const bool raster = !(sh.flags & RTM_FLAG_NO_SHADOW_RASTER) && b[0] <= b[1] && b[2] <= b[3];
-    const int tr1 = TR * nb1;  // PART 1's tile height: the box test's granularity in both parts
+    const int tr1 = TR * nb1;  // PART 1's tile height
     const int bx0 = raster ? std::max(b[0], 0) / 128 : 0, bx1 = raster ? std::min(b[1] / 128, gx - 1) : -1;
-    const int by0 = raster ? std::max(b[2], 0) / tr1 * (tr1 / TR) : 0;
-    const int by1 = raster ? std::min((b[3] / tr1) * (tr1 / TR) + tr1 / TR - 1, gy - 1) : -1;
-    const bool split = coded_split() && !dg && !eb;
+    const int by0 = raster ? std::max(b[2], 0) / TR : 0;
+    const int by1 = raster ? std::min(std::max(b[3], 0) / TR, gy - 1) : -1;
+    // split only when the sphere tiles are a minority of the map (box ≤ 0.3 of the tiles;
+    // configs 2-4 split, config 5's 16 spheres span more: one launch there, measured as fast
+    // in the 4-lane frame and faster one-lane, profiles/r03_ab_coded_split.txt)
+    const double box_frac = raster ? (double)std::max(bx1 - bx0 + 1, 0) * (double)std::max(by1 - by0 + 1, 0) /
+                                         ((double)gx * (double)gy)
+                                   : 0.0;
+    static const double split_max = [] {
+        const char* e = getenv("RTM_CODED_SPLIT_MAX");
+        return e ? atof(e) : 0.3;
+    }();
+    const bool split = coded_split() && !dg && !eb && box_frac <= split_max;
     dim3 gb((unsigned)std::max(bx1 - bx0 + 1, 0), (unsigned)std::max(by1 - by0 + 1, 0), g.z);
     dim3 g1((unsigned)gx, (unsigned)((sh.H + tr1 - 1) / tr1), g.z);
     const int4 orgb = make_int4(bx0, by0, tr1, 0), org1 = make_int4(0, 0, tr1, 0);
