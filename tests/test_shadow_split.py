@@ -1,6 +1,7 @@
-"""The split coded shadow launch: per batch, the workgroup tiles that
-meet a frame's sphere box run the full tile, every other tile a raster-free
-instantiation with 8-row waves; the two decide at the same 32-row granularity, so
+"""The split coded shadow launch: per batch (when the batch's sphere box
+covers at most 0.3 of the map), the 16-row tiles that meet a frame's sphere box run
+the full tile and every other texel is written by a raster-free instantiation with
+16-row waves that skip the rows of the box; both decide on the same 16-row blocks, so
 each texel is written once.  These cases stress the partition: spheres that move
 between the frames of one launch (the sphere grid spans the batch's union box, a
 tile outside its own frame's box leaves), spheres partly or wholly outside the
