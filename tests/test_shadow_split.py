@@ -80,3 +80,32 @@ def test_split_launch_every_frame_and_map(rtm, oracle, scenes, case):
     finally:
         ctx.close()
         torch.cuda.empty_cache()
+
+
+CHILD = r'''
+import importlib, os, sys
+sys.path.insert(0, %(root)r)
+sys.path.insert(0, %(root)r + "/oracle")
+sys.path.insert(0, %(root)r + "/tests")
+import oracle
+rtm = importlib.import_module("2018rustraytracer_amd")
+scenes = importlib.import_module("2018rustraytracer_amd.scenes")
+import test_shadow_split as t
+for case in [("mixed", 517, 299, 240), ("edges", 770, 203, 64)]:
+    t.test_split_launch_every_frame_and_map(rtm, oracle, scenes, case)
+print("CHILD_OK")
+'''
+
+
+@pytest.mark.parametrize("bound", ["1.0", "0"])
+def test_split_forced_on_and_off_in_subprocess(bound):
+    """The same partition checks with the split forced for any box (the 16-sphere frames
+    too; RTM_CODED_SPLIT_MAX=1.0) and with one launch for every batch (0), in child
+    processes (the bound is read once per process)."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, RTM_CODED_SPLIT_MAX=bound)
+    r = subprocess.run([sys.executable, "-c", CHILD % {"root": root}], capture_output=True, text=True, timeout=600,
+                       env=env)
+    assert r.returncode == 0 and "CHILD_OK" in r.stdout, r.stdout[-2000:] + r.stderr[-3000:]
