@@ -6,7 +6,7 @@ march, eye viewport rasterize + shade) at BASELINE config 3 — 3840x2160,
 One process per GPU (torch.distributed.run); prints ONE JSON line on rank 0.
 
 A step is one segment of the animation: --frames-per-step frames (auto: at least 8
-and at least 256 Mpixel worth, so 32 at 3840x2160) enqueued by one
+and at least 512 Mpixel worth, so 64 at 3840x2160) enqueued by one
 rtm_render_frames_async call into a ring of output frames.  `value` is pixels of all
 timed frames / the timed region's wall time; `ms_per_step` is per segment and
 `ms_per_frame` per frame.
@@ -57,7 +57,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--frames-per-step", type=int, default=0,
-                    help="frames of one step (0 = auto: at least 8 and at least 256 Mpixel worth, at most 256)")
+                    help="frames of one step (0 = auto: at least 8 and at least 512 Mpixel worth, at most 256)")
     ap.add_argument("--config", type=int, default=3,
                     help="scenes.CONFIGS id: 1-5 BASELINE, 6-7 row f-1, 8 row f-4, 9 general march (tilted sun)")
     ap.add_argument("--mode", choices=["frames", "tile-gather"], default="frames")
@@ -420,9 +420,11 @@ def main():
     cfg = sc.CONFIGS[a.config]
     W, H, K = cfg["width"], cfg["height"], cfg["steps"]
     # frames per step: a step renders F frames of the sequence (at least 8, and at least
-    # 256 Mpixel, at most 256 frames), so a short --steps run still times many
+    # 512 Mpixel, at most 256 frames), so a short --steps run still times many
     # frames-per-launch batches and the lanes' start and drain stay a small share of it
-    F = a.frames_per_step or min(256, max(8, (1 << 28) // (W * H)))
+    # (r03: 512 instead of 256 Mpixel, the driver's --steps 20 run +1 %,
+    # profiles/r03_ab_frames_per_step.txt)
+    F = a.frames_per_step or min(256, max(8, (1 << 29) // (W * H)))
     nW, nS = a.warmup * F, a.steps * F  # warmup / timed frames
     tile_mode = a.mode == "tile-gather"
     # tile-gather: each band evaluates only the shadow texels it reads (no cross-rank shadow map)
