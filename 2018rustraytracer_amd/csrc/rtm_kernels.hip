@@ -1747,9 +1747,13 @@ __device__ __forceinline__ void shadow_tile_coded(const ShadowPart& a, void* __r
             auto check = [&](auto masked, auto with_zb) {
                 constexpr bool MASKED = decltype(masked)::value;
                 constexpr bool ZB = decltype(with_zb)::value;
+                // (an opaque copy of the row bits per call: the row tests are not hoisted
+                // out of the patch loop as NR live lane masks)
+                uint32_t rb = rowbits;
+                if (MASKED) asm volatile("" : "+s"(rb));
 #pragma unroll
                 for (int r = 0; r < NR; ++r) {
-                    if (MASKED && !((rowbits >> r) & 1u)) continue;
+                    if (MASKED && !((rb >> r) & 1u)) continue;
                     unsigned vv[2] = {0xFFFFu, 0xFFFFu};  // (PK: this row's decided codes)
 #pragma unroll
                     for (int c = 0; c < 2; ++c) {
@@ -1897,15 +1901,21 @@ __device__ __forceinline__ void shadow_coded_block(const ShadowPart& sh, void* _
     shadow_tile_coded<INC, CODE, NB, WL, EB, PART, PK>(sh, map, bx, by, lds, diag);
 }
 
+// waves per SIMD the register allocator must keep: 7 for the packed 16-row raster-free
+// part (72 VGPRs; uncapped, fewer spilled SGPRs cost 90 VGPRs and 5 waves), else free
+template <int PART, bool PK, int NB>
+constexpr int CODED_MIN_WAVES = PART == 1 && PK && NB == 4 ? 7 : 1;
+
 template <bool INC, int CODE, int NB, bool WL, bool EB, int PART = 0, bool PK = false>
-__global__ __launch_bounds__(BLOCK) void shadow_coded_kernel(const FrameArgs a, double* __restrict__ smap, int diag,
-                                                             int4 org) {
+__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(CODED_MIN_WAVES<PART, PK, NB>, 8))) void
+shadow_coded_kernel(const FrameArgs a, double* __restrict__ smap, int diag, int4 org) {
     extern __shared__ ZRecK lds_rec[];
     shadow_coded_block<INC, CODE, NB, WL, EB, PART, PK>(a.sh, smap, lds_rec, diag, org);
 }
 
 template <bool INC, int CODE, int NB, bool WL, bool EB, int PART = 0, bool PK = false>
-__global__ __launch_bounds__(BLOCK) void shadow_coded_batch_kernel(CBatch* __restrict__ fr, int diag, int4 org) {
+__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(CODED_MIN_WAVES<PART, PK, NB>, 8))) void
+shadow_coded_batch_kernel(CBatch* __restrict__ fr, int diag, int4 org) {
     extern __shared__ ZRecK lds_rec[];
     CBatch* f = fr + blockIdx.z;
     shadow_coded_block<INC, CODE, NB, WL, EB, PART, PK>(*(const ShadowPart*)&f->a.sh, f->smap, lds_rec, diag, org);
