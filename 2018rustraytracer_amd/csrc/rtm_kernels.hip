@@ -526,6 +526,17 @@ __device__ __forceinline__ double clamp01_d(double x) {
     const double v = x > 0.0 ? x : 0.0;
     return v < 1.0 ? v : 1.0;
 }
+// clamp01_d(x / d) for an edge parameter, d = |edge|^2 (>= 0, per-SDF constant):
+// the IEEE division only where the quotient can land inside (0, 1).  x <= 0 or NaN
+// gives 0 (x / d is <= 0, -0 or NaN for every d); x > 0 with x >= d, d finite and
+// >= 0 gives a quotient >= 1 (+inf at d = 0), so 1.  Bit-identical to the plain
+// form; a wave whose lanes all clamp skips the division sequence (the points of
+// one wave's rays lie close together, so they usually clamp alike).
+__device__ __forceinline__ double clamp_ratio01_d(double x, double d) {
+    const bool one = (x >= d) & (d >= 0.0) & (d < __builtin_huge_val());
+    if ((x > 0.0) & !one) return clamp01_d(x / d);
+    return x > 0.0 ? 1.0 : 0.0;
+}
 __device__ __forceinline__ int gsign_i(double x) { return (int)(x > 0.0) - (int)(x < 0.0); }
 __device__ __forceinline__ double dot3d(const double a[3], const double b[3]) {
     return a[0] * b[0] + a[1] * b[1] + a[2] * b[2];
@@ -548,9 +559,9 @@ __device__ __forceinline__ double sdf_dist(const SdfK& g, const double p[3]) {
     double d1;
     // (the sum of three signs is a small integer: exact in f64 and in int)
     if (gsign_i(dot3d(g.c1, p1)) + gsign_i(dot3d(g.c2, p2)) + gsign_i(dot3d(g.c3, p3)) < 2) {
-        const double s1 = clamp01_d(dot3d(g.e21, p1) / g.d21);
-        const double s2 = clamp01_d(dot3d(g.e32, p2) / g.d32);
-        const double s3 = clamp01_d(dot3d(g.e13, p3) / g.d13);
+        const double s1 = clamp_ratio01_d(dot3d(g.e21, p1), g.d21);
+        const double s2 = clamp_ratio01_d(dot3d(g.e32, p2), g.d32);
+        const double s3 = clamp_ratio01_d(dot3d(g.e13, p3), g.d13);
         double e1[3], e2[3], e3[3];
         for (int k = 0; k < 3; ++k) {
             e1[k] = g.e21[k] * s1 - p1[k];
