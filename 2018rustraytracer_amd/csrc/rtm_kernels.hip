@@ -571,7 +571,18 @@ __device__ __forceinline__ double sdf_dist(const SdfK& g, const double p[3]) {
         d1 = fmin_d(fmin_d(dot3d(e1, e1), dot3d(e2, e2)), dot3d(e3, e3));
     } else {
         const double dn = dot3d(g.nor, p1);
-        d1 = dn * dn / g.dnor;
+        const double a = dn * dn;
+        // fmin_d(d0, a / dnor) is d0 when d0 < 0 (the quotient is >= +0 or NaN) or when
+        // a > RN(RN(d0 * dnor) * (1 + 2^-40)): then a / dnor > d0 (1 + 2^-41) and the
+        // rounded quotient stays above d0 (d0 > 2^-900 keeps the product normal).
+        // +inf stands in for the quotient there (same fmin_d result, same bits); a
+        // NaN d0 fails both tests.  A wave whose lanes all see the box closer skips
+        // the division sequence.
+        const bool box_wins = (d0 < 0.0) | ((d0 > 0x1p-900) & (a > (d0 * g.dnor) * (1.0 + 0x1p-40)));
+        if (box_wins)
+            d1 = __builtin_huge_val();
+        else
+            d1 = a / g.dnor;
     }
     double d2 = fmin_d(d0, d1);
     d2 -= 0.2;
