@@ -12,7 +12,7 @@ _PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 # RTM_LIB: another build of the same library (A/B timing runs only, tools/ab_bench.py)
 LIB_PATH = os.environ.get("RTM_LIB") or os.path.join(_PKG_DIR, "librtm.so")
 
-RTM_ABI_VERSION = 9
+RTM_ABI_VERSION = 10
 RTM_MAX_SPHERES = 16
 RTM_MAX_PATCHES = 4
 RTM_MAX_CIRCLE_PLANES = 16
@@ -118,6 +118,9 @@ ABI_SYMBOLS = [
     ("rtm_ctx_destroy", None, [_P]),
     ("rtm_ctx_stream", _P, [_P]),
     ("rtm_ctx_synchronize", C.c_int, [_P]),
+    ("rtm_ctx_alloc", C.c_int, [_P, C.c_int64, C.POINTER(_P)]),
+    ("rtm_ctx_free", C.c_int, [_P, _P]),
+    ("rtm_ctx_copy_to_host", C.c_int, [_P, _P, _P, C.c_int64]),
     ("rtm_ctx_last_kernel_ms", C.c_int, [_P, C.POINTER(C.c_float), C.POINTER(C.c_float)]),
     ("rtm_ctx_set_timing_capacity", C.c_int, [_P, _I32]),
     ("rtm_ctx_set_timing_stride", C.c_int, [_P, _I32]),
@@ -214,11 +217,15 @@ def load_library(path: str | None = None) -> C.CDLL:
             f"{p} not built: run `python -c 'import __graft_entry__ as g; g.build()'` "
             "(the HIP library is the only render path)")
     lib = C.CDLL(p)
+    # an A/B build (RTM_LIB) may predate the newest calls: those stay unbound there
+    ab = bool(os.environ.get("RTM_LIB")) and path is None
     for name, res, args in ABI_SYMBOLS:
+        if ab and not hasattr(lib, name):
+            continue
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.rtm_abi_version() != RTM_ABI_VERSION:
+    if lib.rtm_abi_version() != RTM_ABI_VERSION and not ab:
         raise RuntimeError("librtm ABI version mismatch")
     if path is None:
         _lib = lib

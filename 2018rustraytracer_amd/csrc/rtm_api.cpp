@@ -59,48 +59,6 @@ int fail(int code, const char* fmt, ...) {
     return code;
 }
 
-// RTM_HOST_PROF=1 (diagnostic only): host wall time of rtm_render_frames_async by
-// phase, summed over the process and printed to stderr at exit.  Off: one branch
-// on a static per phase.
-struct HostProf {
-    enum { BUILD, SCAN, FILL, SYNC, UPLOAD, LAUNCH, N };
-    const bool on = [] {
-        const char* e = getenv("RTM_HOST_PROF");
-        return e && atoi(e) != 0;
-    }();
-    double s[N] = {};
-    long frames = 0, calls = 0, batches = 0;
-    static double now() {
-        timespec ts;
-        clock_gettime(CLOCK_MONOTONIC, &ts);
-        return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
-    }
-    ~HostProf() {
-        if (!on || !frames) return;
-        static const char* names[N] = {"build", "scan", "fill", "sync", "upload", "launch"};
-        s[SCAN] -= s[FILL] + s[SYNC] + s[UPLOAD] + s[LAUNCH];  // enqueue_batch runs inside the scan phase
-        fprintf(stderr, "RTM_HOST_PROF calls=%ld batches=%ld frames=%ld us/frame:", calls, batches, frames);
-        for (int i = 0; i < N; ++i) fprintf(stderr, " %s=%.3f", names[i], s[i] * 1e6 / (double)frames);
-        fprintf(stderr, "\n");
-    }
-};
-HostProf g_hprof;
-struct HostPhase {  // adds the scope's wall time to one phase when RTM_HOST_PROF is on
-    int ph;
-    double t0;
-    explicit HostPhase(int p) : ph(p), t0(g_hprof.on ? HostProf::now() : 0.0) {}
-    void next(int p) {
-        if (!g_hprof.on) return;
-        const double t = HostProf::now();
-        g_hprof.s[ph] += t - t0;
-        t0 = t;
-        ph = p;
-    }
-    ~HostPhase() {
-        if (g_hprof.on) g_hprof.s[ph] += HostProf::now() - t0;
-    }
-};
-
 #define HIP_TRY(expr)                                                                    \
     do {                                                                                 \
         hipError_t e_ = (expr);                                                          \
@@ -689,26 +647,14 @@ struct TimingSlot {
 // its previous upload has completed (copied[j]), its device side once the
 // kernels that read it have run (used[j]); the upload runs on its own stream, so
 // batch i+1's table crosses PCIe while batch i renders.
-// How a batch's frame table reaches the device (RTM_BATCH_COPY, A/B): "pull" (default)
-// a kernel on the lane's stream reads the pinned slot; "copy" hipMemcpyAsync on a
-// copy stream with event waits both ways (round 2 until r02_v9); "stream"
-// hipMemcpyAsync on the lane's stream.  Past a few tens of KB the async copy goes to a
-// copy engine: 8 frames per launch at 3840x2160 (32 KB) ran at 91 instead of 248
-// Gpix/s with kernels of the same duration (profiles/r02_ab_batch_pull.txt).
-enum { UPLOAD_PULL, UPLOAD_COPY_STREAM, UPLOAD_LANE_STREAM };
-int batch_upload_mode() {
-    static const int m = [] {
-        const char* e = getenv("RTM_BATCH_COPY");
-        if (e && std::string(e) == "copy") return (int)UPLOAD_COPY_STREAM;
-        if (e && std::string(e) == "stream") return (int)UPLOAD_LANE_STREAM;
-        return (int)UPLOAD_PULL;
-    }();
-    return m;
-}
+// A batch's frame table reaches the device by a pull kernel on the lane's stream
+// reading the pinned slot.  (An async copy, on a copy stream or on the lane's stream,
+// went to a copy engine past a few tens of KB: 8 frames per launch at 3840x2160
+// (32 KB) ran at 91 instead of 248 Gpix/s with kernels of the same duration,
+// profiles/r02_ab_batch_pull.txt.)
 
 struct BatchRing {
     static constexpr int R = 4;
-    hipStream_t copy = nullptr;
     void* host[R] = {};
     void* host_dev[R] = {};  // the pinned host slot's device address (the pull kernel reads it)
     size_t host_bytes[R] = {};
@@ -722,14 +668,12 @@ struct BatchRing {
         int cur = 0;
         (void)hipGetDevice(&cur);
         (void)hipSetDevice(device);
-        if (copy) (void)hipStreamSynchronize(copy);
         for (int j = 0; j < R; ++j) {
             if (used[j]) (void)hipEventSynchronize(used[j]);
             if (host[j]) (void)hipHostFree(host[j]);
             if (copied[j]) (void)hipEventDestroy(copied[j]);
             if (used[j]) (void)hipEventDestroy(used[j]);
         }
-        if (copy) (void)hipStreamDestroy(copy);
         (void)hipSetDevice(cur);
     }
 };
@@ -749,11 +693,6 @@ struct rtm_ctx {
     hipStream_t stream = nullptr;
     std::vector<std::unique_ptr<Lane>> lanes;  // extra lanes 1..n (lane 0 is the context itself)
     hipEvent_t fork = nullptr;                 // lanes wait on the context stream's earlier work
-    // lane stagger (rtm_render_frames_async): recorded after the first launch's shadow
-    // pass; the second lane's first launch waits for it, so one lane's shadow pass runs
-    // beside the other's eye pass instead of both lanes running the same pass at once
-    hipEvent_t stagger = nullptr;
-    bool stagger_arm = false;
     int32_t lanes_req = 0;                     // rtm_ctx_set_lanes (0 = auto)
     int32_t lanes_last = 0;                    // lanes of the last frame-sequence call
     int32_t batch_req = 0;                     // rtm_ctx_set_batch (0 = auto)
@@ -764,8 +703,7 @@ struct rtm_ctx {
     int64_t calls = 0;             // renders enqueued (for the stride)
     int32_t stride = 1;
     bool have_shadow_pass = false;
-    DevBuf smap;    // shadow map, W*H f64
-    DevBuf smap2;   // second shadow map for the pipelined frame sequence
+    DevBuf smap;    // shadow map (coded or f64, ShadowPart::smap_fmt)
     const double* last_smap = nullptr;
     bool last_trivial = false;  // the last frame's shadow viewport was all +INF and not materialised
     ShadowPart last_sh{};  // the last shadow pass's arguments (smap_fmt: how last_smap is stored)
@@ -1136,14 +1074,10 @@ int upload_sdf(rtm_ctx* ctx, DevBuf& buf, hipStream_t s, const SdfTabK& k, const
 // main.rs:910-1046) has an all-+INF shadow viewport: it skips the shadow pass and its
 // eye pass takes the fused path, whose on-demand texel is +INF at once -- the same
 // bits, one kernel instead of two.  rtm_ctx_shadow_map then materialises the +INF
-// map on request.  RTM_TRIVIAL_SHADOW=0 keeps the two-pass frame (A/B runs).
+// map on request.
 bool trivial_shadow(int32_t flags) {
-    static const bool on = [] {
-        const char* e = getenv("RTM_TRIVIAL_SHADOW");
-        return !(e && atoi(e) == 0);
-    }();
     const int32_t both = RTM_FLAG_NO_MARCH | RTM_FLAG_NO_SHADOW_RASTER;
-    return on && (flags & both) == both && !(flags & RTM_FLAG_FUSED_SHADOW);
+    return (flags & both) == both && !(flags & RTM_FLAG_FUSED_SHADOW);
 }
 
 void note_trivial(rtm_ctx* ctx, const ShadowPart& sh) {
@@ -1195,10 +1129,6 @@ int enqueue_frame(rtm_ctx* ctx, FrameArgs& a, const FrameExtra* x, void* out_dev
         ctx->smap_h = a.sh.H;
         if (slot) HIP_TRY(hipEventRecord(slot->ev[0], s));
         if ((rc = launch_shadow_pass(a, smap, s, stats))) return fail(rc, "shadow pass launch failed");
-        if (ctx->stagger_arm) {
-            HIP_TRY(hipEventRecord(ctx->stagger, s));
-            ctx->stagger_arm = false;
-        }
         if (slot) HIP_TRY(hipEventRecord(slot->ev[1], s));
         ctx->have_shadow_pass = true;
         ctx->last_trivial = false;
@@ -1278,13 +1208,9 @@ int ensure_lanes(rtm_ctx* ctx, int L) {
 // kernels pay a ramp and a tail each (3840x2160 at 4 frames: each frame's shadow pass
 // 13.4 instead of 16.2 us, its eye pass 21.7 instead of 25.1).  Until r02_v10 the rule
 // was 8 Mpixel worth from 1 to 4 Mpixel and 32 Mpixel worth from 4 to 16: bigger
-// tables went through a copy engine.  rtm_ctx_set_batch / RTM_BATCH override (1 = one
-// frame per launch).
+// tables went through a copy engine.  rtm_ctx_set_batch overrides (1 = one frame per
+// launch).
 int frame_batch(int32_t req, int32_t W, int32_t H) {
-    static const int env = [] {
-        const char* e = getenv("RTM_BATCH");
-        return e ? atoi(e) : 0;
-    }();
     const int64_t px = (int64_t)W * H;
     // 64 Mpixel worth of frames, at most 64 below 1 Mpixel (512x512: 64 frames per
     // launch) and 32 above (1920x1080: 32, 3840x2160: 8, 7680x4320: 2; the cap was 16
@@ -1295,7 +1221,7 @@ int frame_batch(int32_t req, int32_t W, int32_t H) {
     // (profiles/r02_ab_batch_pull.txt).
     const int64_t target = 64LL << 20;
     const int64_t cap = px < (1LL << 20) ? 64 : 32;
-    int B = req > 0 ? req : env > 0 ? env : (int)std::max<int64_t>(1, std::min<int64_t>(cap, target / px));
+    int B = req > 0 ? req : (int)std::max<int64_t>(1, std::min<int64_t>(cap, target / px));
     return std::max(1, std::min(B, 64));
 }
 
@@ -1304,8 +1230,6 @@ int frame_batch(int32_t req, int32_t W, int32_t H) {
 int enqueue_batch(rtm_ctx* ctx, int lane, FrameArgs* fa, const FrameExtra* ex, void* const* outs, int n,
                   int32_t fmt = RTM_FORMAT_RGBA32F) {
     int rc;
-    HostPhase hp(HostProf::FILL);
-    if (g_hprof.on) g_hprof.batches++;
     if ((rc = frame_tables(ctx, fa[0]))) return rc;
     for (int k = 1; k < n; ++k) {
         fa[k].sh.tab = fa[0].sh.tab;
@@ -1318,7 +1242,6 @@ int enqueue_batch(rtm_ctx* ctx, int lane, FrameArgs* fa, const FrameExtra* ex, v
     if (!brp) {
         std::unique_ptr<BatchRing> b(new BatchRing);
         b->device = ctx->device;
-        if (batch_upload_mode() == UPLOAD_COPY_STREAM) HIP_TRY(hipStreamCreateWithFlags(&b->copy, hipStreamNonBlocking));
         for (int j = 0; j < BatchRing::R; ++j) {
             HIP_TRY(hipEventCreateWithFlags(&b->copied[j], hipEventDisableTiming));
             HIP_TRY(hipEventCreateWithFlags(&b->used[j], hipEventDisableTiming));
@@ -1374,9 +1297,7 @@ int enqueue_batch(rtm_ctx* ctx, int lane, FrameArgs* fa, const FrameExtra* ex, v
     const size_t bytes = off;
     const int j = br.next;
     br.next = (br.next + 1) % BatchRing::R;
-    hp.next(HostProf::SYNC);
     HIP_TRY(hipEventSynchronize(br.copied[j]));  // the slot's previous upload has left the host buffer
-    hp.next(HostProf::FILL);
     if (br.host_bytes[j] < bytes) {
         if (br.host[j]) HIP_TRY(hipHostFree(br.host[j]));
         br.host[j] = nullptr;
@@ -1423,7 +1344,7 @@ int enqueue_batch(rtm_ctx* ctx, int lane, FrameArgs* fa, const FrameExtra* ex, v
     }
     // a frame without ray-traced primitives in a RT 3 batch: every frame shares the eye camera
     t0.rt_persp = t0.rt ? t0.rt_persp : 0;
-    if (t0.rt && t0.rt_persp && !t0.sdf && eye_wave_cull_on()) {
+    if (t0.rt && t0.rt_persp && !t0.sdf) {
         // per-wave primitive masks (rt_cull_batch_kernel) for every frame with primitives,
         // ceil(W/64) * rows words each; stream-ordered reuse on this lane
         const size_t nw = (size_t)((fa[0].ey.W + 63) / 64) * (size_t)(fa[0].ey.row_end - fa[0].ey.row_begin);
@@ -1436,24 +1357,11 @@ int enqueue_batch(rtm_ctx* ctx, int lane, FrameArgs* fa, const FrameExtra* ex, v
         t0.rtmask = (uint32_t*)br.rtmask.p;
     }
     t0.fmt = fmt;
-    hp.next(HostProf::UPLOAD);
-    const int mode = batch_upload_mode();
-    if (mode == UPLOAD_PULL) {
-        // the lane's stream pulls the table from the pinned slot: in stream order after the
-        // lane's earlier batches (the previous readers of this device slot), and copied[j]
-        // tells the host when the slot may be refilled
-        if ((rc = launch_pull(br.host_dev[j], bytes, db, s))) return fail(rc, "batch table pull failed");
-        HIP_TRY(hipEventRecord(br.copied[j], s));
-    } else if (mode == UPLOAD_COPY_STREAM) {
-        HIP_TRY(hipStreamWaitEvent(br.copy, br.used[j], 0));  // the device slot is free
-        HIP_TRY(hipMemcpyAsync(db, hb, bytes, hipMemcpyHostToDevice, br.copy));
-        HIP_TRY(hipEventRecord(br.copied[j], br.copy));
-        HIP_TRY(hipStreamWaitEvent(s, br.copied[j], 0));
-    } else {  // in stream order after the lane's earlier batches (which read the older slots)
-        HIP_TRY(hipMemcpyAsync(db, hb, bytes, hipMemcpyHostToDevice, s));
-        HIP_TRY(hipEventRecord(br.copied[j], s));
-    }
-    hp.next(HostProf::LAUNCH);
+    // the lane's stream pulls the table from the pinned slot: in stream order after the
+    // lane's earlier batches (the previous readers of this device slot), and copied[j]
+    // tells the host when the slot may be refilled
+    if ((rc = launch_pull(br.host_dev[j], bytes, db, s))) return fail(rc, "batch table pull failed");
+    HIP_TRY(hipEventRecord(br.copied[j], s));
     TimingSlot* slot = next_slot(ctx);
     if (!fused) {
         if (slot) HIP_TRY(hipEventRecord(slot->ev[0], s));
@@ -1468,10 +1376,6 @@ int enqueue_batch(rtm_ctx* ctx, int lane, FrameArgs* fa, const FrameExtra* ex, v
             box[3] = std::max(box[3], q.cull_y1);
         }
         if ((rc = launch_shadow_batch((const BatchFrame*)db, n, fa[0], s, box))) return fail(rc, "batched shadow pass failed");
-        if (ctx->stagger_arm) {
-            HIP_TRY(hipEventRecord(ctx->stagger, s));
-            ctx->stagger_arm = false;
-        }
         if (slot) HIP_TRY(hipEventRecord(slot->ev[1], s));
         ctx->have_shadow_pass = true;
         ctx->last_trivial = false;
@@ -1566,7 +1470,6 @@ void rtm_ctx_destroy(rtm_ctx* ctx) {
         ctx->lanes.clear();
         ctx->batch.reset();
         if (ctx->fork) (void)hipEventDestroy(ctx->fork);
-        if (ctx->stagger) (void)hipEventDestroy(ctx->stagger);
         for (auto& sl : ctx->ring)
             for (auto& e : sl.ev)
                 if (e) (void)hipEventDestroy(e);
@@ -1580,6 +1483,35 @@ void* rtm_ctx_stream(rtm_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; 
 int rtm_ctx_synchronize(rtm_ctx* ctx) {
     if (!ctx) return fail(RTM_ERR_INVALID, "ctx is NULL");
     DeviceGuard g(ctx->device);
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    return RTM_OK;
+}
+
+int rtm_ctx_alloc(rtm_ctx* ctx, int64_t bytes, void** out_dev) {
+    if (!ctx || !out_dev || bytes <= 0) return fail(RTM_ERR_INVALID, "ctx/out NULL or bytes %lld", (long long)bytes);
+    *out_dev = nullptr;
+    DeviceGuard g(ctx->device);
+    if (hipMalloc(out_dev, (size_t)bytes) != hipSuccess) {
+        *out_dev = nullptr;
+        return fail(RTM_ERR_OOM, "hipMalloc(%lld) failed", (long long)bytes);
+    }
+    return RTM_OK;
+}
+
+int rtm_ctx_free(rtm_ctx* ctx, void* dev) {
+    if (!ctx) return fail(RTM_ERR_INVALID, "ctx is NULL");
+    if (!dev) return RTM_OK;
+    DeviceGuard g(ctx->device);
+    HIP_TRY(hipStreamSynchronize(ctx->stream));  // no enqueued frame still writes it
+    HIP_TRY(hipFree(dev));
+    return RTM_OK;
+}
+
+int rtm_ctx_copy_to_host(rtm_ctx* ctx, const void* dev, void* host, int64_t bytes) {
+    if (!ctx || !dev || !host || bytes < 0) return fail(RTM_ERR_INVALID, "bad arguments");
+    if (bytes == 0) return RTM_OK;
+    DeviceGuard g(ctx->device);
+    HIP_TRY(hipMemcpyAsync(host, dev, (size_t)bytes, hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(hipStreamSynchronize(ctx->stream));
     return RTM_OK;
 }
@@ -1704,199 +1636,79 @@ int rtm_render_frames_async(rtm_ctx* ctx, int32_t n_frames, const rtm_scene* sce
     if (!ctx || !scenes || !out_rgba_dev || n_frames < 1) return fail(RTM_ERR_INVALID, "bad arguments");
     for (int32_t i = 0; i < n_frames; ++i)
         if (!out_rgba_dev[i]) return fail(RTM_ERR_INVALID, "out_rgba_dev[%d] is NULL", i);
-    static const bool pipeline_env = [] {
-        const char* e = getenv("RTM_PIPELINE");
-        return e && atoi(e) != 0;
-    }();
-    if (!pipeline_env) {
-        // two kernels per frame: build each frame's arguments just before its launches,
-        // so the GPU starts on frame 0 while the host prepares frame 1 (building all
-        // frames first left the GPU idle for the whole build)
-        DeviceGuard g(ctx->device);
-        int B = std::min<int32_t>(frame_batch(ctx->batch_req, width, height), n_frames);
-        int L = frame_lanes(ctx->lanes_req, n_frames, width, height, out_rgba_dev, B);
-        int rc = RTM_OK;
-        if (L > 1) {  // fork: the lanes start after the context stream's earlier work
-            if ((rc = ensure_lanes(ctx, L))) return rc;
-            HIP_TRY(hipEventRecord(ctx->fork, ctx->stream));
-            for (int k = 1; k < L; ++k) HIP_TRY(hipStreamWaitEvent(ctx->lanes[(size_t)k - 1]->stream, ctx->fork, 0));
-        }
-        ctx->lanes_last = L;
-        ctx->batch_last = B;
-        const int32_t nb = (n_frames + B - 1) / B;
-        std::vector<FrameArgs> fa((size_t)B);
-        std::vector<FrameExtra> fx((size_t)B);
-        // RTM_STAGGER=1 (A/B only): the second lane starts after the first lane's first
-        // shadow pass, so one lane's shadow pass runs beside the other's eye pass.  Off by
-        // default: the lanes do better in step at 3840x2160 (262 vs 254 Gpix/s: a shadow
-        // pass beside the other lane's eye-pass store stream waits longer on its loads)
-        // and at 512x512 (80 vs 68); +3 % at 1920x1080 (profiles/r02_ab_batch.txt)
-        static const bool stagger_on = [] {
-            const char* e = getenv("RTM_STAGGER");
-            return e && atoi(e) != 0;
-        }();
-        bool stagger = stagger_on && L > 1 && !ctx->stagger_arm;
-        if (stagger && !ctx->stagger) HIP_TRY(hipEventCreateWithFlags(&ctx->stagger, hipEventDisableTiming));
-        HostPhase hp(HostProf::SCAN);
-        if (g_hprof.on) g_hprof.calls++, g_hprof.frames += n_frames;
-        for (int32_t b = 0; b < nb && !rc; ++b) {
-            const int32_t i0 = b * B, nf = std::min(B, n_frames - i0);
-            const int lane = (nb - 1 - b) % L;
-            if (stagger && b == 0) ctx->stagger_arm = true;  // the first launch records it after its shadow pass
-            if (stagger && b == 1) {
-                ctx->stagger_arm = false;
-                hipStream_t ls = lane > 0 ? ctx->lanes[(size_t)lane - 1]->stream : ctx->stream;
-                if (hipStreamWaitEvent(ls, ctx->stagger, 0) != hipSuccess) {
-                    rc = fail(RTM_ERR_HIP, "lane stagger wait failed");
-                    break;
-                }
-            }
-            hp.next(HostProf::BUILD);
-            for (int32_t k = 0; k < nf && !rc; ++k) {
-                rc = build_frame(fa[(size_t)k], &scenes[i0 + k], eye, shadow, width, height, march_steps, flags);
-                if (!rc) build_extra(&scenes[i0 + k], eye, width, height, fx[(size_t)k]);
-            }
-            hp.next(HostProf::SCAN);
-            if (rc) break;
-            // runs of frames with the same march tables (patches) and disjoint outputs share
-            // one launch per pass (frames of one launch run concurrently, so a repeated
-            // output pointer starts a new run: the later frame still lands last); the
-            // A/B-only shadow modes and single frames take the per-frame kernels
-            const uintptr_t frame_bytes = (uintptr_t)width * (uintptr_t)height * 4u * sizeof(float);
-            for (int32_t k = 0; k < nf && !rc;) {
-                int32_t e = k + 1;
-                auto disjoint = [&](int32_t q) {
-                    const uintptr_t o = (uintptr_t)out_rgba_dev[i0 + q];
-                    for (int32_t p = k; p < q; ++p) {
-                        const uintptr_t op = (uintptr_t)out_rgba_dev[i0 + p];
-                        if (o < op + frame_bytes && op < o + frame_bytes) return false;
-                    }
-                    return true;
-                };
-                while (e < nf && fa[(size_t)e].sh.n_patches == fa[(size_t)k].sh.n_patches &&
-                       std::memcmp(fa[(size_t)e].sh.patch, fa[(size_t)k].sh.patch,
-                                   sizeof(PatchK) * (size_t)fa[(size_t)k].sh.n_patches) == 0 &&
-                       disjoint(e))
-                    ++e;
-                if (e - k >= 2 && shadow_batchable(fa[(size_t)k].sh)) {
-                    if (!(rc = frame_tables(ctx, fa[(size_t)k])) && shadow_batchable(fa[(size_t)k].sh))
-                        rc = enqueue_batch(ctx, lane, &fa[(size_t)k], &fx[(size_t)k],
-                                           reinterpret_cast<void* const*>(out_rgba_dev + i0 + k), e - k);
-                    else if (!rc)
-                        for (int32_t q = k; q < e && !rc; ++q)
-                            rc = enqueue_frame(ctx, fa[(size_t)q], &fx[(size_t)q], out_rgba_dev[i0 + q], nullptr, lane);
-                } else {
-                    for (int32_t q = k; q < e && !rc; ++q)
-                        rc = enqueue_frame(ctx, fa[(size_t)q], &fx[(size_t)q], out_rgba_dev[i0 + q], nullptr, lane);
-                }
-                k = e;
-            }
-        }
-        ctx->stagger_arm = false;
-        // join every lane (also after an error, so the context stream still covers what
-        // was enqueued); the first error, of the frames or of a join, is returned
-        const std::string frame_err = rc ? g_last_error : std::string();
-        int join_rc = RTM_OK;
-        for (int k = 1; k < L; ++k) {
-            Lane& l = *ctx->lanes[(size_t)k - 1];
-            hipError_t e = hipEventRecord(l.done, l.stream);
-            if (e == hipSuccess) e = hipStreamWaitEvent(ctx->stream, l.done, 0);
-            if (e != hipSuccess && !join_rc) join_rc = fail(RTM_ERR_HIP, "lane %d join: %s", k, hipGetErrorString(e));
-        }
-        if (rc) {
-            g_last_error = frame_err;
-            return rc;
-        }
-        return join_rc;
-    }
-    ctx->lanes_last = 1;
-    std::vector<FrameArgs> f((size_t)n_frames);
-    std::vector<FrameExtra> ex((size_t)n_frames);
-    bool any_rt = false;
-    for (int32_t i = 0; i < n_frames; ++i) {
-        int rc = build_frame(f[(size_t)i], &scenes[i], eye, shadow, width, height, march_steps, flags);
-        if (rc) return rc;
-        build_extra(&scenes[i], eye, width, height, ex[(size_t)i]);
-        any_rt |= ex[(size_t)i].has_rt || ex[(size_t)i].has_psp || ex[(size_t)i].has_sdf;
-    }
+    // two kernels per frame (or per batch of frames): build each batch's arguments just
+    // before its launches, so the GPU starts on batch 0 while the host prepares batch 1
+    // (building all frames first left the GPU idle for the whole build).  (A software-
+    // pipelined launch -- the shadow pass of frame i with the eye pass of frame i-1 in
+    // one grid -- measured slower than two back-to-back kernels per frame, config 3 99.5
+    // vs 79.1 us/frame, profiles/r01_ab_pipe.txt; a lane stagger lost at 3840x2160 and
+    // 512x512, profiles/r02_ab_batch.txt.  Both are gone.)
     DeviceGuard g(ctx->device);
-    // The pipelined launch (shadow pass of frame i + eye pass of frame i-1) is
-    // opt-in: measured on MI355X it is slower than two back-to-back kernels per
-    // frame (config 3: 99.5 vs 79.1 us/frame, profiles/r01_ab_pipe.txt) — the
-    // latency-bound march slows down beside the eye pass's store stream.
-    static const bool pipeline_on = [] {
-        const char* e = getenv("RTM_PIPELINE");
-        return e && atoi(e) != 0;
-    }();
-    // The pipeline shares one table set: every frame must have the same patches
-    // (the cameras are shared by construction).  Otherwise render frame by frame.
-    // (frames with ray-traced primitives, SDFs or perspective spheres always take the two-kernel path)
-    bool same = pipeline_on && !any_rt && (flags & RTM_FLAG_FUSED_SHADOW) == 0 && n_frames > 1;
-    for (int32_t i = 1; same && i < n_frames; ++i)
-        same = f[(size_t)i].sh.n_patches == f[0].sh.n_patches &&
-               std::memcmp(f[(size_t)i].sh.patch, f[0].sh.patch, sizeof(PatchK) * (size_t)f[0].sh.n_patches) == 0;
-    if (!same) {
-        for (int32_t i = 0; i < n_frames; ++i) {
-            int rc = enqueue_frame(ctx, f[(size_t)i], &ex[(size_t)i], out_rgba_dev[i], nullptr);
-            if (rc) return rc;
+    int B = std::min<int32_t>(frame_batch(ctx->batch_req, width, height), n_frames);
+    int L = frame_lanes(ctx->lanes_req, n_frames, width, height, out_rgba_dev, B);
+    int rc = RTM_OK;
+    if (L > 1) {  // fork: the lanes start after the context stream's earlier work
+        if ((rc = ensure_lanes(ctx, L))) return rc;
+        HIP_TRY(hipEventRecord(ctx->fork, ctx->stream));
+        for (int k = 1; k < L; ++k) HIP_TRY(hipStreamWaitEvent(ctx->lanes[(size_t)k - 1]->stream, ctx->fork, 0));
+    }
+    ctx->lanes_last = L;
+    ctx->batch_last = B;
+    const int32_t nb = (n_frames + B - 1) / B;
+    std::vector<FrameArgs> fa((size_t)B);
+    std::vector<FrameExtra> fx((size_t)B);
+    for (int32_t b = 0; b < nb && !rc; ++b) {
+        const int32_t i0 = b * B, nf = std::min(B, n_frames - i0);
+        const int lane = (nb - 1 - b) % L;
+        for (int32_t k = 0; k < nf && !rc; ++k) {
+            rc = build_frame(fa[(size_t)k], &scenes[i0 + k], eye, shadow, width, height, march_steps, flags);
+            if (!rc) build_extra(&scenes[i0 + k], eye, width, height, fx[(size_t)k]);
         }
-        return RTM_OK;
+        if (rc) break;
+        // runs of frames with the same march tables (patches) and disjoint outputs share
+        // one launch per pass (frames of one launch run concurrently, so a repeated
+        // output pointer starts a new run: the later frame still lands last); single
+        // frames take the per-frame kernels
+        const uintptr_t frame_bytes = (uintptr_t)width * (uintptr_t)height * 4u * sizeof(float);
+        for (int32_t k = 0; k < nf && !rc;) {
+            int32_t e = k + 1;
+            auto disjoint = [&](int32_t q) {
+                const uintptr_t o = (uintptr_t)out_rgba_dev[i0 + q];
+                for (int32_t p = k; p < q; ++p) {
+                    const uintptr_t op = (uintptr_t)out_rgba_dev[i0 + p];
+                    if (o < op + frame_bytes && op < o + frame_bytes) return false;
+                }
+                return true;
+            };
+            while (e < nf && fa[(size_t)e].sh.n_patches == fa[(size_t)k].sh.n_patches &&
+                   std::memcmp(fa[(size_t)e].sh.patch, fa[(size_t)k].sh.patch,
+                               sizeof(PatchK) * (size_t)fa[(size_t)k].sh.n_patches) == 0 &&
+                   disjoint(e))
+                ++e;
+            if (e - k >= 2) {
+                rc = enqueue_batch(ctx, lane, &fa[(size_t)k], &fx[(size_t)k],
+                                   reinterpret_cast<void* const*>(out_rgba_dev + i0 + k), e - k);
+            } else {
+                rc = enqueue_frame(ctx, fa[(size_t)k], &fx[(size_t)k], out_rgba_dev[i0 + k], nullptr, lane);
+            }
+            k = e;
+        }
     }
-    int rc = frame_tables(ctx, f[0]);
-    if (rc) return rc;
-    for (int32_t i = 1; i < n_frames; ++i) {
-        f[(size_t)i].sh.tab = f[0].sh.tab;
-        f[(size_t)i].ey.nx = f[0].ey.nx;
-        f[(size_t)i].ey.ny = f[0].ey.ny;
+    // join every lane (also after an error, so the context stream still covers what
+    // was enqueued); the first error, of the frames or of a join, is returned
+    const std::string frame_err = rc ? g_last_error : std::string();
+    int join_rc = RTM_OK;
+    for (int k = 1; k < L; ++k) {
+        Lane& l = *ctx->lanes[(size_t)k - 1];
+        hipError_t e = hipEventRecord(l.done, l.stream);
+        if (e == hipSuccess) e = hipStreamWaitEvent(ctx->stream, l.done, 0);
+        if (e != hipSuccess && !join_rc) join_rc = fail(RTM_ERR_HIP, "lane %d join: %s", k, hipGetErrorString(e));
     }
-    const size_t smap_bytes = sizeof(double) * (size_t)width * (size_t)height;
-    if ((rc = ctx->smap.ensure(smap_bytes, ctx->device)) || (rc = ctx->smap2.ensure(smap_bytes, ctx->device)))
+    if (rc) {
+        g_last_error = frame_err;
         return rc;
-    double* sm[2] = {(double*)ctx->smap.p, (double*)ctx->smap2.p};
-    hipStream_t s = ctx->stream;
-    // prologue: shadow pass of frame 0
-    TimingSlot* slot = next_slot(ctx);
-    if (slot) HIP_TRY(hipEventRecord(slot->ev[0], s));
-    if ((rc = launch_shadow_pass(f[0], sm[0], s, nullptr))) return fail(rc, "shadow pass launch failed");
-    if (slot) {
-        HIP_TRY(hipEventRecord(slot->ev[1], s));
-        HIP_TRY(hipEventRecord(slot->ev[2], s));
-        HIP_TRY(hipEventRecord(slot->ev[3], s));
-        slot->shadow = true;
-        ctx->renders++;
     }
-    // steady state: shadow pass of frame i + eye pass of frame i-1, one launch
-    for (int32_t i = 1; i < n_frames; ++i) {
-        FrameArgs a;
-        a.sh = f[(size_t)i].sh;
-        a.ey = f[(size_t)(i - 1)].ey;
-        slot = next_slot(ctx);
-        if (slot) HIP_TRY(hipEventRecord(slot->ev[2], s));
-        if ((rc = launch_frame_pipe(a, sm[i & 1], sm[(i - 1) & 1], out_rgba_dev[i - 1], s)))
-            return fail(rc, "pipelined frame launch failed");
-        if (slot) {
-            HIP_TRY(hipEventRecord(slot->ev[3], s));
-            slot->shadow = false;
-            ctx->renders++;
-        }
-    }
-    // epilogue: eye pass of the last frame
-    slot = next_slot(ctx);
-    if (slot) HIP_TRY(hipEventRecord(slot->ev[2], s));
-    const int32_t last = n_frames - 1;
-    if ((rc = launch_eye_pass(f[(size_t)last], sm[last & 1], out_rgba_dev[last], s, nullptr)))
-        return fail(rc, "eye pass launch failed");
-    if (slot) {
-        HIP_TRY(hipEventRecord(slot->ev[3], s));
-        slot->shadow = false;
-        ctx->renders++;
-    }
-    ctx->have_shadow_pass = true;
-    ctx->last_smap = sm[last & 1];
-    ctx->last_sh = f[(size_t)last].sh;  // (f64 map: the pipelined kernel writes 8-byte texels)
-    ctx->smap_w = width;
-    ctx->smap_h = height;
-    return RTM_OK;
+    return join_rc;
 }
 
 int32_t rtm_format_bytes(int32_t format) { return format_bytes(format); }
@@ -2397,12 +2209,6 @@ int enqueue_prepared_batch(rtm_ctx* ctx, const PreparedFrame* const* fs, int n, 
         fa[(size_t)k] = fs[k]->a;
         apply_rows(fa[(size_t)k].ey, row_begin, row_end, map);
         fx[(size_t)k] = fs[k]->x;
-    }
-    if ((rc = frame_tables(ctx, fa[0]))) return rc;
-    if (!(fa[0].ey.flags & RTM_FLAG_FUSED_SHADOW) && !shadow_batchable(fa[0].sh)) {
-        for (int k = 0; k < n; ++k)
-            if ((rc = enqueue_frame(ctx, fa[(size_t)k], &fx[(size_t)k], outs[k], nullptr, 0, format))) return rc;
-        return RTM_OK;
     }
     return enqueue_batch(ctx, 0, fa.data(), fx.data(), outs, n, format);
 }

@@ -136,7 +136,7 @@ struct ShadowPart {
 // all ones = +INF.  The codes are tiled in blocks of 128 columns x 4 rows, one
 // block per shadow wave: texel (x, y) is element
 //   ((y >> 2) * smap_bw + (x >> 7)) * 512 + ((x & 127) >> 1) * 8 + (y & 3) * 2 + (x & 1)
-// (the lean tile's lane holds 4 rows x 2 columns = 8 codes, stored as 8 or 16
+// (the coded tile's lane holds 4 rows x 2 columns = 8 codes, stored as 8 or 16
 // contiguous bytes).  1 or 2 bytes per texel instead of 8.
 constexpr int32_t SMAP_F64 = 0, SMAP_U8 = 1, SMAP_U16 = 2;
 constexpr int64_t smap_code_index(int x, int y, int bw) {
@@ -170,9 +170,8 @@ struct EyePart {
     int32_t stripe_rows, stripe_stride, stripe_phase, out_global;
 };
 
-// One launch's arguments: the shadow pass of frame i and the eye pass of frame
-// i (plain launches, RTM_FLAG_FUSED_SHADOW) or of frame i-1 (the software-
-// pipelined frame kernel).  Kept < 4 KiB (kernarg limit).
+// One launch's arguments: the shadow pass and the eye pass of one frame.  Kept
+// < 4 KiB (kernarg limit).
 struct FrameArgs {
     ShadowPart sh;
     EyePart ey;
@@ -343,9 +342,8 @@ static_assert(sizeof(StatsK) == sizeof(rtm_stats), "StatsK layout");
 // Launchers (rtm_kernels.hip).  All asynchronous on `stream`.
 int launch_shadow_pass(const FrameArgs& a, double* smap, void* stream, StatsK* stats);
 // The map format the (non-counting) shadow pass writes for these arguments: a
-// coded map (SMAP_U8 when steps + n_spheres <= 254, SMAP_U16 up to 65534) for
-// the default lean tile and the generic tile, f64 for the A/B-only modes and
-// when RTM_SMAP=f64.  Set a.sh.smap_fmt / smap_bw before both passes launch.
+// coded map (SMAP_U8 when steps + n_spheres <= 254, SMAP_U16 up to 65534), else
+// f64 (and with RTM_SMAP=f64).  Set a.sh.smap_fmt / smap_bw before both passes launch.
 int32_t shadow_map_format(const ShadowPart& sh);
 // f64 values of a coded map (rtm_ctx_shadow_map's view of it), async on stream.
 int launch_smap_decode(const ShadowPart& sh, const void* codes, double* out, void* stream);
@@ -361,20 +359,12 @@ int launch_eye_pass(const FrameArgs& a, const double* smap, void* out, void* str
 // box: the union of the batch's sphere pixel boxes (x0, x1, y0, y1) for the split coded launch
 int launch_shadow_batch(const BatchFrame* dev, int n, const FrameArgs& a0, void* stream, const int32_t* box = nullptr);
 int launch_eye_batch(const BatchFrame* dev, int n, const FrameArgs& a0, const DevTabs& t0, void* stream);
-// The eye pass's per-wave primitive cull is on (RTM_EYE_MODE bit 2 clear).
-bool eye_wave_cull_on();
-bool shadow_batchable(const ShadowPart& sh);
 // Stream-ordered copy of host bytes into device memory by kernels whose
 // arguments carry the bytes (<= 3968 per launch), so the host copy is consumed
 // at launch: no pinned staging, no host synchronisation.  bytes % 8 == 0.
 int launch_upload(const void* src, size_t bytes, void* dst, void* stream);
 // bytes (a multiple of 16, 16-byte aligned) from pinned, device-accessible host memory
 int launch_pull(const void* src_host, size_t bytes, void* dst, void* stream);
-// Software-pipelined frame step: the shadow pass of a.sh into smap_w and the eye
-// pass of a.ey (the previous frame) from smap_r into out, in ONE launch whose
-// workgroups interleave the two roles (VALU-bound and HBM-store-bound tiles
-// share the CUs).  smap_w != smap_r.
-int launch_frame_pipe(const FrameArgs& a, double* smap_w, const double* smap_r, float* out, void* stream);
 int launch_vp_rasterize(const RasterArgs& a, double* zbuf, double* gh, double* gz, int32_t* gid,
                         void* stream);
 int launch_vp_march(const MarchArgs& a, double* zbuf, void* stream);

@@ -978,555 +978,7 @@ __device__ __forceinline__ void shadow_tile_generic(const ShadowPart& a, double*
     }
 }
 
-// One 8-step chunk of the shared-z march for NR rows: lt[r] += #(z_k < D[r]);
-// returns true when no lane is still marching in any row (wave early-out).
-// March modes of the separable shadow tile (identical results):
-constexpr int MARCH_SIGN = 0;    // 8-step chunks, sign bit of fl(z_k - D)
-constexpr int MARCH_CMP = 1;     // 8-step chunks, compare z_k < D
-constexpr int MARCH_SEARCH = 2;  // first crossing located in the monotone z table
-
-template <int NR, bool CMP>
-__device__ __forceinline__ bool chunk8(const double (&z)[8], const double (&D)[NR], int (&lt)[NR],
-                                       const unsigned (&inrb)[NR], const unsigned (&eposb)[NR]) {
-    unsigned cont = 0u;  // lane still marching in some row: inr & (last ^ epos)
-#pragma unroll
-    for (int r = 0; r < NR; ++r) {
-        unsigned last = 0u;
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            // [z_k < D]: a compare, or the sign bit of fl(z_k - D) (equal for finite nonzero D)
-            last = CMP ? (z[u] < D[r] ? 1u : 0u) : (unsigned)__double2hiint(z[u] - D[r]) >> 31;
-            lt[r] += (int)last;
-        }
-        cont |= inrb[r] & (last ^ eposb[r]);
-    }
-    return !__any(cont != 0u);
-}
-
-// first_crossing over the workgroup's LDS copy of the table: T[k] = (z_k, t_k)
-// for k <= steps, so one 16-byte read at the guessed index yields both the
-// verification value and the hit's t (main.rs:2264).
-constexpr int SEARCH_LDS_MAX_STEPS = 2048;  // 32 KiB of LDS at most
-__device__ __forceinline__ int first_crossing_lds(const double2* T, double D, double oz, double inv_sz, bool inc,
-                                                  int steps, double& t) {
-    if ((oz < D) != inc) return steps;
-    double g = (D - oz) * inv_sz;
-    g = fmin(fmax(g, 0.0), (double)steps);  // NaN -> 0
-    int f = (int)ceil(g);
-    const double2 e = T[f];
-    const double zp = T[f > 0 ? f - 1 : 0].x;
-    const bool ok = (f == 0 || ((zp < D) == inc)) && (f == steps || ((e.x < D) != inc));
-    if (ok) {
-        t = e.y;
-        return f;
-    }
-    int lo = 0, hi = steps;
-    while (lo < hi) {
-        const int mid = (lo + hi) >> 1;
-        if ((T[mid].x < D) != inc) hi = mid;
-        else lo = mid + 1;
-    }
-    t = T[lo].y;
-    return lo;
-}
-
-// Shadow tile for the separable axis-aligned shadow camera with a shared z
-// sequence (the BASELINE scenes): 64 x (TILE_Y*NR) texels, NR rows per wave, so
-// every lane runs NR independent march chains (ILP against VALU and load
-// latency).  MARCH_SEARCH (default when the host proved the z table monotone)
-// locates each chain's first crossing directly (first_crossing); the chunk
-// modes walk the table in 8-step chunks, prefetched one chunk ahead, each step
-// the sign bit of fl(z_k - D) or the compare z_k < D (D finite and nonzero on
-// this path, so both are exactly the class test, see march_axis).  If any
-// lane's D is not finite/nonzero the wave takes the exact per-texel loop instead.
-template <int NR, int MODE>
-__device__ __forceinline__ void shadow_tile_sep(const ShadowPart& a, double* __restrict__ smap, int bx, int by,
-                                                int diag, double2* lds_zt = nullptr) {
-    constexpr bool CMP = MODE == MARCH_CMP;
-    // MARCH_SEARCH with lds_zt: stage (z_k, t_k), k <= steps, in LDS once per workgroup
-    const bool use_lds = MODE == MARCH_SEARCH && lds_zt != nullptr;
-    if (use_lds) {
-        for (int k = threadIdx.x; k <= a.steps; k += BLOCK)
-            lds_zt[k] = make_double2(a.tab.z[k], k < a.steps ? a.tab.t[k] : 0.0);
-        __syncthreads();
-    }
-    const int lane = threadIdx.x & (TILE_X - 1);
-    const int xb = bx * TILE_X;
-    const int xi = xb + lane;
-    const int y0 = __builtin_amdgcn_readfirstlane(by * (TILE_Y * NR) + (threadIdx.x >> 6) * NR);
-    const bool colv = xi < a.W;
-    const int xs = colv ? xi : a.W - 1;  // clamped column for table reads
-    double zb[NR];
-    bool rowv[NR];
-#pragma unroll
-    for (int r = 0; r < NR; ++r) {
-        zb[r] = INFINITY;
-        rowv[r] = y0 + r < a.H;
-    }
-    // shadow viewport rasterize, face BACK (main.rs:1569, 243)
-    if (!(a.flags & RTM_FLAG_NO_SHADOW_RASTER) && !(diag & 1) &&
-        union_may_cover(a, xb, xb + TILE_X - 1, y0, y0 + NR - 1)) {
-        const double x = a.tab.nx[xs];
-        for (int i = 0; i < a.n_spheres; ++i) {
-            const RasterSphereK& sp = a.sph[i];
-            if (y0 + NR - 1 < sp.iy0 || y0 > sp.iy1 || xb + TILE_X - 1 < sp.ix0 || xb > sp.ix1) continue;
-#pragma unroll 1
-            for (int r = 0; r < NR; ++r) {  // rows are wave-uniform: scalar loop, one copy of cover()
-                if (y0 + r >= a.H || !may_cover(a.sph[i], xb, xb + TILE_X - 1, y0 + r)) continue;
-                double h;
-                if (cover(a.sph[i], x, a.tab.ny[y0 + r], h)) {
-                    const double depth = a.sph[i].z + h * a.sph[i].r;
-#pragma unroll
-                    for (int q = 0; q < NR; ++q)
-                        if (q == r && depth < zb[q]) zb[q] = depth;
-                }
-            }
-        }
-    }
-    if (!(a.flags & RTM_FLAG_NO_MARCH) && !(diag & 2)) {
-        const double oz = a.tab.z[0];
-        const double sz = a.cam.dir[2] * 0.03;
-        const int steps = a.steps;
-        const bool colok = a.tab.ok[xs] != 0;
-        for (int k = 0; k < a.n_patches; ++k) {
-            double D[NR];
-            bool inr[NR], fast = true;
-            const double d0 = a.tab.d0[k * a.W + xs];
-            const double dd = a.tab.dd[k * a.W + xs];
-#pragma unroll
-            for (int r = 0; r < NR; ++r) {
-                const int yr = rowv[r] ? y0 + r : y0;  // wave-uniform: scalar loads
-                D[r] = d0 + dd * ((cdouble*)a.tab.py)[yr];
-                inr[r] = colv && rowv[r] && colok && ((cint*)a.tab.ok)[a.W + yr] != 0;
-                fast = fast && (!inr[r] || (fabs(D[r]) < INFINITY && D[r] != 0.0));
-            }
-            int cnt[NR];
-            double tl[NR];  // t of the hit step (LDS search only)
-            if (MODE == MARCH_SEARCH && use_lds && __all(fast)) {
-                const bool inc = a.tab.zmono > 0;
-                const double inv_sz = 1.0 / sz;
-#pragma unroll
-                for (int r = 0; r < NR; ++r)
-                    cnt[r] = inr[r] ? first_crossing_lds(lds_zt, D[r], oz, inv_sz, inc, steps, tl[r]) : steps;
-            } else if (MODE == MARCH_SEARCH && __all(fast)) {
-                cdouble* zt = (cdouble*)a.tab.z;
-                const bool inc = a.tab.zmono > 0;
-                const double inv_sz = 1.0 / sz;
-#pragma unroll
-                for (int r = 0; r < NR; ++r) cnt[r] = inr[r] ? first_crossing(zt, D[r], oz, inv_sz, inc, steps) : steps;
-            } else if (MODE != MARCH_SEARCH && __all(fast)) {
-                cdouble* zt = (cdouble*)a.tab.z;  // padded by 8 entries past `steps`
-                unsigned eposb[NR], inrb[NR];
-                bool epos[NR];
-                int lt[NR];
-                bool any_inr = false;
-#pragma unroll
-                for (int r = 0; r < NR; ++r) {
-                    epos[r] = !(oz < D[r]);  // entry class POS <=> z0 >= D
-                    eposb[r] = epos[r] ? 1u : 0u;
-                    inrb[r] = inr[r] ? 1u : 0u;
-                    lt[r] = 0;
-                    any_inr = any_inr || inr[r];
-                }
-                int kk = 0;
-                if (__any(any_inr)) {
-                    // 8-step chunks, two per iteration with ping-pong table buffers (A, B):
-                    // the next chunk's 8 values are in flight while the current 8 are compared
-                    double zA[8], zB[8];
-#pragma unroll
-                    for (int u = 0; u < 8; ++u) zA[u] = zt[u];
-                    bool stopped = false;
-                    while (kk + 8 <= steps) {
-#pragma unroll
-                        for (int u = 0; u < 8; ++u) zB[u] = zt[kk + 8 + u];
-                        if (chunk8<NR, CMP>(zA, D, lt, inrb, eposb)) {
-                            kk += 8;
-                            stopped = true;
-                            break;
-                        }
-                        kk += 8;
-                        if (kk + 8 > steps) {
-#pragma unroll
-                            for (int u = 0; u < 8; ++u) zA[u] = zB[u];
-                            break;
-                        }
-#pragma unroll
-                        for (int u = 0; u < 8; ++u) zA[u] = zt[kk + 8 + u];
-                        if (chunk8<NR, CMP>(zB, D, lt, inrb, eposb)) {
-                            kk += 8;
-                            stopped = true;
-                            break;
-                        }
-                        kk += 8;
-                    }
-                    if (!stopped) {
-                        for (; kk < steps; ++kk) {
-                            const double z = zt[kk];
-#pragma unroll
-                            for (int r = 0; r < NR; ++r) lt[r] += (z < D[r]) ? 1 : 0;
-                        }
-                    }
-                }
-#pragma unroll
-                for (int r = 0; r < NR; ++r) cnt[r] = inr[r] ? (epos[r] ? kk - lt[r] : lt[r]) : steps;
-            } else {
-                // exact per-texel path (march_axis returns t itself);
-                // one (not unrolled) copy of the exact loop: keeps the fast path's registers low
-#pragma unroll 1
-                for (int r = 0; r < NR; ++r) {
-                    double Dr = D[0];
-                    bool ir = inr[0];
-#pragma unroll
-                    for (int q = 1; q < NR; ++q) {
-                        Dr = r == q ? D[q] : Dr;
-                        ir = r == q ? inr[q] : ir;
-                    }
-                    MarchResult m = march_axis<false>(Dr, ir, oz, sz, steps, a.tab);
-#pragma unroll
-                    for (int q = 0; q < NR; ++q)
-                        if (q == r && m.hit && m.t < zb[q]) zb[q] = m.t;
-                }
-#pragma unroll
-                for (int r = 0; r < NR; ++r) cnt[r] = steps;
-            }
-            if (MODE == MARCH_SEARCH && use_lds && __all(fast)) {
-#pragma unroll
-                for (int r = 0; r < NR; ++r) {
-                    const bool hit = cnt[r] < steps;
-                    zb[r] = (hit && tl[r] < zb[r]) ? tl[r] : zb[r];
-                }
-            } else if (steps > 0) {
-                // t of the first hit step (branch-free: clamped table index + select)
-#pragma unroll
-                for (int r = 0; r < NR; ++r) {
-                    const bool hit = cnt[r] < steps;
-                    const double t = a.tab.t[hit ? cnt[r] : 0];
-                    zb[r] = (hit && t < zb[r]) ? t : zb[r];
-                }
-            }
-        }
-    }
-    if (colv) {
-#pragma unroll
-        for (int r = 0; r < NR; ++r)
-            if (rowv[r]) smap[(int64_t)(y0 + r) * a.W + xi] = zb[r];
-    }
-}
-
 typedef float f32x4 __attribute__((ext_vector_type(4)));
-
-__device__ __forceinline__ double readlane_f64(double v, int l) {
-    const uint64_t b = __double_as_longlong(v);
-    const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)b, l);
-    const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(b >> 32), l);
-    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
-}
-
-// Phase timestamps of the lean tile (timing diagnostic, RTM_DIAG_SHADOW bit 8):
-// s_memtime of lane 0 of every wave at 6 program points; read by
-// rtm_diag_shadow_phases (not part of include/rtm.h).
-__device__ unsigned long long g_phase[1 << 18];
-#define RTM_PHASE(k)                                                                                         \
-    if (diag & 8) {                                                                                          \
-        const unsigned long long t_ = __builtin_amdgcn_s_memtime();                                         \
-        const unsigned wid_ = ((blockIdx.y * gridDim.x + blockIdx.x) * (BLOCK / 64) + (threadIdx.x >> 6)); \
-        if ((threadIdx.x & 63) == 0 && wid_ * 8u + 8u <= (1u << 18)) g_phase[wid_ * 8u + (k)] = t_;        \
-    }
-
-// The lean separable shadow tile (the default for every BASELINE scene): the
-// texels and bits of shadow_tile_sep<NR, MARCH_SEARCH>, with the common path
-// free of divergent control flow.  Sphere coverage computes h = sqrt(1 - d*d)
-// unconditionally and selects on d < 1; the first-crossing guess is clamped to
-// [1, steps] and both table entries are read from LDS unconditionally; lanes the
-// fast path cannot decide take the exact march_axis behind a wave ballot.
-// CW columns per lane (a wave covers 64*CW columns, so a row's texels leave as
-// one 16-byte store per lane when CW == 2), NR rows per wave, the table
-// direction as a template parameter.  Needs 1 <= steps <= SEARCH_LDS_MAX_STEPS
-// and a monotone z table (host-checked).  Per texel the search is: D (exact, 2
-// ops), "D finite and nonzero" (one class test), the index guess
-// fma(dd', py, d0') from per-column pre-scaled terms (a guess only: the
-// verification below decides), clamp/ceil/convert, two LDS reads, and with
-// P(z) = INC ? !(z < D) : (z < D):
-//   okA = !P(z_{f-1}), okB = P(z_f), entry = !P(z_0)   (monotone P)
-//   hit  = inr & fastD & okA & okB & f < steps      -> t = t_f
-//   slow = inr & (!fastD | (entry & !(okA & (f == steps | okB))))  -> exact march_axis
-// CODE: the map's storage (SMAP_F64, or a coded map, rtm_kernels.h): the tile
-// tracks which source won each texel beside its value.
-template <int NR, int CW, bool INC, int FILLN = 4, int CODE = SMAP_F64>
-__device__ __forceinline__ void shadow_tile_lean2(const ShadowPart& a, double* __restrict__ smap, int bx, int by,
-                                                  double2* __restrict__ T, int diag) {
-    static_assert(CODE == SMAP_F64 || (NR == 4 && CW == 2), "coded maps use the 4 x 128 texel block layout");
-    constexpr int TW = TILE_X * CW;
-    const int lane = threadIdx.x & (TILE_X - 1);
-    const int xb = bx * TW;
-    const int x0 = xb + lane * CW;
-    const int y0 = __builtin_amdgcn_readfirstlane(by * (TILE_Y * NR) + (threadIdx.x >> 6) * NR);
-    bool colv[CW];
-    int xs[CW];
-#pragma unroll
-    for (int c = 0; c < CW; ++c) {
-        colv[c] = x0 + c < a.W;
-        xs[c] = colv[c] ? x0 + c : a.W - 1;
-    }
-    const int steps = a.steps;
-    const bool march = !(a.flags & RTM_FLAG_NO_MARCH) && !(diag & 2) && a.n_patches > 0 && steps > 0;
-    RTM_PHASE(0)
-    // LDS table fill, split so its global loads are in flight during the sphere
-    // raster below (which does not read it); written + barrier afterwards
-    constexpr int FILL = FILLN;  // entries per thread held in registers (steps + 1 <= FILL * BLOCK)
-    double2 fv[FILL];
-    const bool fill_regs = march && steps + 1 <= FILL * BLOCK;
-    if (fill_regs) {
-#pragma unroll
-        for (int u = 0; u < FILL; ++u) {
-            const int k = threadIdx.x + u * BLOCK;
-            if (k <= steps) fv[u] = make_double2(a.tab.z[k], k < steps ? a.tab.t[k] : 0.0);
-        }
-    }
-    // Every vector global load of the tile is issued here, before any store:
-    // loads and stores share vmcnt, so a load after a store would wait for that
-    // store's (long, under a full write stream) completion.
-    bool colok[CW];
-    double xcol[CW];       // shadow-camera NDC x of the columns (raster)
-    double h_d0[CW], h_dd[CW];  // patch 0's column terms
-    float h_g0[CW], h_g1[CW];
-    const double oz = a.tab.z0;
-    const double inv_sz = 1.0 / (a.cam.dir[2] * 0.03);
-#pragma unroll
-    for (int c = 0; c < CW; ++c) xcol[c] = a.tab.nx[xs[c]];
-    // the wave's row terms as one vector load (lane l: row yw + l), read back per
-    // row with readlane: no serial chain of scalar loads in the march
-    static_assert(NR <= TILE_X, "rows per wave");
-    double py_l = 0.0;
-    int ok_l = 0;
-    if (march) {
-        const int yl = min(y0 + (lane < NR ? lane : 0), a.H - 1);
-        py_l = a.tab.py[yl];
-        ok_l = a.tab.ok[a.W + yl];
-    }
-    if (march) {
-#pragma unroll
-        for (int c = 0; c < CW; ++c) {
-            colok[c] = colv[c] & (a.tab.ok[xs[c]] != 0);  // xs clamped: no branch
-            h_d0[c] = a.tab.d0[xs[c]];
-            h_dd[c] = a.tab.dd[xs[c]];
-            // guess terms, f32: (D - z0)/sz ~ g0 + g1*py.  A guess only (the table
-            // verification below decides), so f32's ~1e-5-step error just sends
-            // the rare texel within it of a step boundary to the exact path.
-            h_g0[c] = (float)((h_d0[c] - oz) * inv_sz);
-            h_g1[c] = (float)(h_dd[c] * inv_sz);
-        }
-    }
-    double zb[NR][CW];
-    int cd[NR][CW];  // CODE: the winning source (-1: +INF)
-#pragma unroll
-    for (int r = 0; r < NR; ++r)
-#pragma unroll
-        for (int c = 0; c < CW; ++c) {
-            zb[r][c] = INFINITY;
-            cd[r][c] = -1;
-        }
-    // shadow viewport rasterize, face BACK (main.rs:1569, 243)
-    if (!(a.flags & RTM_FLAG_NO_SHADOW_RASTER) && !(diag & 1) &&
-        union_may_cover(a, xb, xb + TW - 1, y0, y0 + NR - 1)) {
-        // the wave's sphere set first (one ballot), so a tile no sphere reaches
-        // skips the raster
-        uint32_t live = wave_sphere_mask(a.sph, a.n_spheres, xb, xb + TW - 1, y0, y0 + NR - 1);
-        const double* x = xcol;
-        while (live) {
-            const int i = __builtin_ctz(live);
-            live &= live - 1u;
-            const RasterSphereK& sp = a.sph[i];
-            double pa[CW];
-#pragma unroll
-            for (int c = 0; c < CW; ++c) pa[c] = ((x[c] - sp.cx) * sp.n) / sp.m;
-#pragma unroll
-            for (int r = 0; r < NR; ++r) {
-                const int y = y0 + r;
-                if (y >= a.H || y < sp.iy0 || y > sp.iy1) continue;  // wave-uniform
-                const double pb = ((((cdouble*)a.tab.ny)[y] - sp.cy) * sp.n) / sp.m;
-                double s2[CW];
-                bool in = false;
-#pragma unroll
-                for (int c = 0; c < CW; ++c) {
-                    s2[c] = pa[c] * pa[c] + pb * pb;
-                    in |= s2[c] < 1.0;
-                }
-                // sqrt is monotone with sqrt(1) == 1, so d < 1 implies s2 < 1: a wave
-                // with no s2 < 1 has no covered texel in this row and skips both sqrts
-                if (!__any(in)) continue;
-#pragma unroll
-                for (int c = 0; c < CW; ++c) {
-                    const double d = sqrt(s2[c]);
-                    const double h = sqrt(1.0 - d * d);
-                    const double depth = sp.z + h * sp.r;
-                    const bool win = (d < 1.0) & (depth < zb[r][c]);
-                    zb[r][c] = win ? depth : zb[r][c];
-                    if (CODE) cd[r][c] = win ? a.steps + i : cd[r][c];
-                }
-            }
-        }
-    }
-    RTM_PHASE(1)
-    if (march) {
-        if (fill_regs) {
-#pragma unroll
-            for (int u = 0; u < FILL; ++u) {
-                const int k = threadIdx.x + u * BLOCK;
-                if (k <= steps) T[k] = fv[u];
-            }
-        } else {
-            for (int k = threadIdx.x; k <= steps; k += BLOCK)
-                T[k] = make_double2(a.tab.z[k], k < steps ? a.tab.t[k] : 0.0);
-        }
-        __syncthreads();
-    }
-    RTM_PHASE(2)
-    if (march) {
-        const double sz = a.cam.dir[2] * 0.03;
-        const float fsteps = (float)steps;
-        // per-row terms, patch-invariant (rows past H: row H-1's, masked by rowv)
-        double pyr[NR];
-        bool rowok[NR];
-#pragma unroll
-        for (int r = 0; r < NR; ++r) {
-            pyr[r] = readlane_f64(py_l, r);
-            rowok[r] = (y0 + r < a.H) & (__builtin_amdgcn_readlane(ok_l, r) != 0);
-        }
-        for (int k = 0; k < a.n_patches; ++k) {
-            double d0[CW], dd[CW];
-            float g0[CW], g1[CW];
-            if (k == 0) {
-#pragma unroll
-                for (int c = 0; c < CW; ++c) {
-                    d0[c] = h_d0[c];
-                    dd[c] = h_dd[c];
-                    g0[c] = h_g0[c];
-                    g1[c] = h_g1[c];
-                }
-            } else {
-#pragma unroll
-                for (int c = 0; c < CW; ++c) {
-                    d0[c] = a.tab.d0[k * a.W + xs[c]];
-                    dd[c] = a.tab.dd[k * a.W + xs[c]];
-                    g0[c] = (float)((d0[c] - oz) * inv_sz);
-                    g1[c] = (float)(dd[c] * inv_sz);
-                }
-            }
-            unsigned slow = 0u;
-#pragma unroll
-            for (int r = 0; r < NR; ++r) {
-                const double py = pyr[r];
-                const float pyf = (float)py;
-#pragma unroll
-                for (int c = 0; c < CW; ++c) {
-                    const double Dv = d0[c] + dd[c] * py;
-                    const bool inr = rowok[r] & colok[c];
-                    const bool fastD = __builtin_amdgcn_class(Dv, 0x198);  // finite, nonzero
-                    const float g = fminf(fmaxf(__builtin_fmaf(g1[c], pyf, g0[c]), 1.0f), fsteps);  // NaN -> 1
-                    const int f = (int)ceilf(g);
-                    const double2 e = T[f];
-                    const double zp = T[f - 1].x;
-                    // bitwise & | on the predicates: no short-circuit, so no divergent
-                    // branches (and the t read is not sunk into one)
-                    const bool okA = INC ? (zp < Dv) : !(zp < Dv);
-                    const bool okB = INC ? !(e.x < Dv) : (e.x < Dv);
-                    const bool entry = INC ? (oz < Dv) : !(oz < Dv);
-                    const bool hit = inr & fastD & okA & okB & (f < steps);
-                    const double ty = e.y;
-                    const bool win = hit & (ty < zb[r][c]);
-                    zb[r][c] = win ? ty : zb[r][c];
-                    if (CODE) cd[r][c] = win ? f : cd[r][c];
-                    const bool sl = inr & (!fastD | (entry & !(okA & ((f == steps) | okB))));
-                    slow |= sl ? (1u << (r * CW + c)) : 0u;
-                }
-            }
-            if (__any(slow != 0u)) {
-                // exact per-texel march for the lanes the fast path cannot decide
-#pragma unroll 1
-                for (int q = 0; q < NR * CW; ++q) {
-                    if (!((slow >> q) & 1u)) continue;
-                    // D recomputed (same two ops, same bits) rather than held live
-                    // across the fast path: NR*CW*2 fewer VGPRs there
-                    const int qr = q / CW, qc = q % CW;
-                    double d0q = d0[0], ddq = dd[0], pyq = pyr[0];
-#pragma unroll
-                    for (int c = 1; c < CW; ++c) {
-                        d0q = qc == c ? d0[c] : d0q;
-                        ddq = qc == c ? dd[c] : ddq;
-                    }
-#pragma unroll
-                    for (int r = 1; r < NR; ++r) pyq = qr == r ? pyr[r] : pyq;
-                    const double Dq = d0q + ddq * pyq;
-                    MarchResult m = march_axis<false>(Dq, true, oz, sz, steps, a.tab);
-#pragma unroll
-                    for (int r = 0; r < NR; ++r)
-#pragma unroll
-                        for (int c = 0; c < CW; ++c)
-                            if (q == r * CW + c && m.hit && m.t < zb[r][c]) {
-                                zb[r][c] = m.t;
-                                if (CODE) cd[r][c] = m.k;
-                            }
-                }
-            }
-        }
-    }
-    RTM_PHASE(3)
-    const bool vec = CW == 2 && (a.W % 2) == 0 && colv[CW - 1];  // x0 even: 16-byte aligned row pairs
-    if (diag & 4) {  // timing diagnostic: compute everything, store (almost) nothing
-        bool any = false;
-#pragma unroll
-        for (int r = 0; r < NR; ++r)
-#pragma unroll
-            for (int c = 0; c < CW; ++c) any |= zb[r][c] == -12345.0;
-        if (any) smap[0] = 0.0;
-        return;
-    }
-    if (CODE != SMAP_F64) {
-        // the lane's 4 rows x 2 columns as one 8- (U8) or 16-byte (U16) store into
-        // the wave's block: element lane*8 + r*2 + c (rows past H and columns past
-        // W hold codes no reader looks up; a wave whose rows all lie past H has no
-        // block: the map holds ceil(H/4) block rows)
-        const int64_t blk = (int64_t)(y0 >> 2) * a.smap_bw + (xb >> 7);
-        if (y0 >= a.H) {
-        } else if (CODE == SMAP_U8) {
-            uint32_t w[2] = {0u, 0u};
-#pragma unroll
-            for (int r = 0; r < NR; ++r)
-#pragma unroll
-                for (int c = 0; c < CW; ++c) w[r >> 1] |= ((uint32_t)cd[r][c] & 0xFFu) << (8 * ((r & 1) * 2 + c));
-            *reinterpret_cast<uint2*>((uint8_t*)smap + blk * 512 + lane * 8) = make_uint2(w[0], w[1]);
-        } else {
-            uint32_t w[NR];
-#pragma unroll
-            for (int r = 0; r < NR; ++r) w[r] = ((uint32_t)cd[r][0] & 0xFFFFu) | ((uint32_t)cd[r][1] << 16);
-            *reinterpret_cast<uint4*>((uint8_t*)smap + blk * 1024 + lane * 16) = make_uint4(w[0], w[1], w[2], w[3]);
-        }
-        RTM_PHASE(4)
-        if (diag & 8) {
-            __builtin_amdgcn_s_waitcnt(0);
-            RTM_PHASE(5)
-        }
-        return;
-    }
-#pragma unroll
-    for (int r = 0; r < NR; ++r) {
-        if (y0 + r >= a.H) continue;
-        double* row = smap + (int64_t)(y0 + r) * a.W;
-        if (CW == 2 && vec) {
-            *reinterpret_cast<double2*>(row + x0) = make_double2(zb[r][0], zb[r][CW - 1]);
-        } else {
-#pragma unroll
-            for (int c = 0; c < CW; ++c)
-                if (colv[c]) row[x0 + c] = zb[r][c];
-        }
-    }
-    RTM_PHASE(4)
-    if (diag & 8) {
-        __builtin_amdgcn_s_waitcnt(0);  // (diagnostic only: when this wave's stores have left)
-        RTM_PHASE(5)
-    }
-}
 
 // Tile row of workgroup row b (of n) with the rows [h0, h1] that the spheres'
 // pixel-range union reaches dispatched first: their waves carry the raster work,
@@ -1539,62 +991,51 @@ __device__ __forceinline__ int hot_rows_first(int b, int n, int h0, int h1) {
     return r < h0 ? r : r + nh;
 }
 
-template <int NR, int CW, bool INC, int FILLN, int CODE>
-__device__ __forceinline__ void shadow_lean2_block(const ShadowPart& sh, double* __restrict__ smap, int diag, int hot,
-                                                   double2* __restrict__ lds) {
-    int by = blockIdx.y;
-    if (hot) {
-        constexpr int TR = TILE_Y * NR;
-        const int n = (int)gridDim.y;
-        const int h0 = max(sh.cull_y0, 0) / TR;
-        const int h1 = min(min(sh.cull_y1, sh.H - 1) / TR, n - 1);
-        const bool none = sh.cull_x0 > sh.cull_x1 || sh.cull_y0 > sh.cull_y1 || sh.cull_y1 < 0;
-        by = none ? by : hot_rows_first(by, n, h0, h1);
-    }
-    shadow_tile_lean2<NR, CW, INC, FILLN, CODE>(sh, smap, blockIdx.x, by, lds, diag);
-}
-
-template <int NR, int CW, bool INC, int FILLN = 4, int CODE = SMAP_F64>
-__global__ __launch_bounds__(BLOCK) void shadow_lean2_kernel(const FrameArgs a, double* __restrict__ smap, int diag,
-                                                             int hot) {
-    extern __shared__ double2 lds_zt[];
-    shadow_lean2_block<NR, CW, INC, FILLN, CODE>(a.sh, smap, diag, hot, lds_zt);
-}
-
 // Batched forms: frame blockIdx.z of a BatchFrame table in device memory.  The
 // table is read through the constant address space, so its fields become scalar
 // loads exactly like kernel arguments.
 using CBatch = const __attribute__((address_space(4))) BatchFrame;
 
-template <int NR, int CW, bool INC, int FILLN, int CODE>
-__global__ __launch_bounds__(BLOCK) void shadow_lean2_batch_kernel(CBatch* __restrict__ fr, int diag, int hot) {
-    extern __shared__ double2 lds_zt[];
-    CBatch* f = fr + blockIdx.z;
-    shadow_lean2_block<NR, CW, INC, FILLN, CODE>(*(const ShadowPart*)&f->a.sh, f->smap, diag, hot, lds_zt);
-}
-
-// The coded shadow tile (the default for every coded map, rtm_kernels.h): the
-// texels and codes of shadow_tile_lean2<4, 2, INC, *, CODE> with NB 4-row blocks
-// per wave (a wave covers 128 columns x 4*NB rows, lane l columns xb + 2l, +1),
-// rebuilt around host-built records (ZRecK / ColRecK / RowRecK) so that the
-// per-texel work is only what the first-crossing check needs:
+// The coded shadow tile (every coded map whose march has host-built records,
+// rtm_kernels.h; launch_coded): a wave owns a strip of 128 columns x 16 rows (lane l:
+// columns xb + 2l, +1), stored as four 128 x 4 blocks of the coded map.
+//
+// The first-crossing check of one texel (code_check): with the host's records
+// (ZRecK / ColRecK / RowRecK),
 //   D = d0 + dd*py (exact, 2 f64 ops); "D finite and nonzero" (one class test);
 //   f = ceil(clamp(g0 + g1*py, 1, steps)) (an f32 index guess, checked below; ceil,
 //     not trunc(x) + 1: an x that rounds to an integer in f32 is common and would be
-//     mis-guessed by one, sending its wave down the slow path);
+//     mis-guessed by one);
 //   one LDS record T[f] = (z_{f-1}, z_f, t_f), and with P(z) = INC ? !(z < D) : (z < D)
 //   okA = !P(z_{f-1}), okB = P(z_f), entry = !P(z_0)   (P monotone over the table)
-//   hit  = inr & fastD & okA & okB          (T[steps] = (z_{steps-1}, past, +INF):
-//                                            a guess of `steps` never wins)
-//   slow = inr & (!fastD | (entry & !(okA & okB)))  -> the exact march_axis
-// The slow texels are rare (a guess within f32 error of a step boundary, or a
-// non-finite/zero D): the wave only records THAT one exists, and its slow path
-// re-derives which.  The last patch updates only the codes (zb is dead after it).
+//   hit  = fastD & okA & okB & f < steps   -> code f (t_f), else NONE (+INF)
+//   slow = !fastD | (entry & !(okA & okB))  -> the check cannot decide: exact march_axis
+//
+// Monotone codes (the per-strip shortcut).  Down a column, py rises (or falls) with
+// the row and D = fl(d0 + fl(dd*py)) is monotone in py (rounding is monotone), so D is
+// monotone down the strip.  For a fixed D the reference's answer is: NONE when the
+// entry test fails, else the first k with P(z_k) (NONE if there is none before
+// `steps`) -- a monotone function of D on each side of the entry threshold.  So when
+// both ends of a column's strip are decided by the check, lie on the same side of the
+// entry threshold and have D of the same sign (every D between is then finite and
+// nonzero), the column's 16 codes are a monotone sequence from the top code to the
+// bottom code: equal end codes fill the column; different ones are located by a
+// binary search over the rows (4 checks) for the first row whose code differs, and
+// when that row's code is the bottom code the column has one boundary (the usual
+// case: a code changes every ~100 rows at 3840x2160).  A wave takes the shortcut when
+// every lane's columns qualify and every search check decides; otherwise the wave
+// checks every texel (the fallback, which is also the path for strips with rows that
+// do not march).  Per 16 x 2 texels of a lane: 4 checks, + 4 per column with a boundary.
+//
+// Spheres (PART 0 / 2, strips meeting the frame's sphere box) are rasterized after the
+// march codes, block by block (4 rows): the strict minimum over the spheres in scene
+// order, then the march wins only where its t is strictly below it (main.rs:559) --
+// the reference's rasterize-then-march order.
 // Needs 1 <= steps <= CODED_MAX_STEPS (LDS) when marching, and a coded map.
 constexpr int CODED_MAX_STEPS = 1023;  // (steps + 1) * 32 B <= 32 KiB of LDS
-// WL: every wave fills its own copy of the LDS records (no workgroup barrier;
-// steps <= CODED_WL_MAX_STEPS), else the workgroup shares one copy.
-[[maybe_unused]] constexpr int CODED_WL_MAX_STEPS = 255;  // 4 copies of (steps + 1) * 32 B <= 32 KiB
+constexpr int CODED_ROWS = 16;          // rows per wave
+constexpr int CODED_TILE_ROWS = CODED_ROWS * TILE_Y;
+constexpr uint32_t CODE_NONE = 0xFFFFu;  // packed-code +INF (also the U8 map's 0xFF)
 // Two 16-bit codes per register (low: column 0, high: column 1), element-wise min.
 typedef unsigned short ushort2_t __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint32_t pk_min_u16(uint32_t a, uint32_t b) {
@@ -1602,153 +1043,91 @@ __device__ __forceinline__ uint32_t pk_min_u16(uint32_t a, uint32_t b) {
                                                                   __builtin_bit_cast(ushort2_t, b)));
 }
 
-// PART (the split launch, launch_coded): 0 every tile; 1 only workgroup tiles outside
-// the frame's sphere box (no raster code: fewer registers, more waves per SIMD);
-// 2 only tiles meeting the box.
-template <bool INC, int CODE, int NB, bool WL = false, bool EB = false, int PART = 0, bool PK_CODES = false>
+// A wave's row record in LDS (the binary search's per-lane row lookups).
+struct RowLdsK {
+    double py;
+    float pyf;
+    int32_t pad;
+};
+// Dynamic LDS of the coded tile: the 4 waves' row records, then the ZRecK table.
+constexpr size_t CODED_ROW_LDS = sizeof(RowLdsK) * CODED_TILE_ROWS;
+
+template <bool INC>
+__device__ __forceinline__ uint32_t code_check(const ZRecK* __restrict__ T, double D, float pyf, float g0, float g1,
+                                               float fsteps, double oz, int steps, bool& slow, bool& entry) {
+    const bool fastD = __builtin_amdgcn_class(D, 0x198);  // finite, nonzero
+    // g0, g1, pyf are host-bounded finite values: the median and the conversion of a
+    // value in [1, steps] are exact and defined
+    const int f = (int)ceilf(__builtin_amdgcn_fmed3f(__builtin_fmaf(g1, pyf, g0), 1.0f, fsteps));
+    const double zp = T[f].zprev, zf = T[f].z;
+    // bitwise & | on the predicates: no short-circuit, so no divergent branches
+    const bool okA = INC ? (zp < D) : !(zp < D);
+    const bool okB = INC ? !(zf < D) : (zf < D);
+    entry = INC ? (oz < D) : !(oz < D);
+    slow = !fastD | (entry & !(okA & okB));
+    return (fastD & okA & okB & (f < steps)) ? (uint32_t)f : CODE_NONE;
+}
+
+// PART (the split launch, launch_coded): 0 every strip; 1 only strips outside the
+// frame's sphere box (no raster code); 2 only strips meeting it.
+template <bool INC, int CODE, int PART>
 __device__ __forceinline__ void shadow_tile_coded(const ShadowPart& a, void* __restrict__ map, int bx, int by,
-                                                  ZRecK* __restrict__ T, int diag) {
-    constexpr int NR = 4 * NB;
+                                                  ZRecK* __restrict__ T, RowLdsK* __restrict__ RL) {
+    constexpr int NR = CODED_ROWS;
     const int lane = threadIdx.x & (TILE_X - 1);
+    const int wv = threadIdx.x >> 6;
     const int xb = bx * 128;
     const int x0 = xb + lane * 2;
-    const int y0 = __builtin_amdgcn_readfirstlane(by * (TILE_Y * NR) + (threadIdx.x >> 6) * NR);
+    const int y0 = __builtin_amdgcn_readfirstlane(by * CODED_TILE_ROWS + wv * NR);
     const int W = a.W, H = a.H, steps = a.steps;
     const bool march = !(a.flags & RTM_FLAG_NO_MARCH) && a.n_patches > 0 && steps > 0;
-    // the LDS records: one per thread, loaded now, written after the raster
+    // the LDS records: one per thread, loaded now, written before the barrier
     // (as double2 halves: a ZRecK value would be kept in scratch)
     const double2* zsrc = reinterpret_cast<const double2*>(a.tab.zrec);
     double2 rec0 = make_double2(0.0, 0.0), rec1 = rec0;
-    const int fid = WL ? lane : (int)threadIdx.x;  // this thread's first record
-    const bool fill1 = march && steps + 1 <= (WL ? TILE_X : BLOCK);
+    const int fid = (int)threadIdx.x;  // this thread's first record
     if (march && fid <= steps) {
         rec0 = zsrc[2 * fid];
         rec1 = zsrc[2 * fid + 1];
     }
-    if (WL) T += (threadIdx.x >> 6) * (steps + 1);  // the wave's copy
     const int xs0 = min(x0, W - 1), xs1 = min(x0 + 1, W - 1);
     ColRecK c0{}, c1{};
+    RowRecK rl{};  // lane < 16: row y0 + lane's record (the wave's LDS row table)
     if (march) {
         c0 = a.tab.col[xs0];
         c1 = a.tab.col[xs1];
+        // (the host pads the row table with non-marching rows to a multiple of 64 rows:
+        // y0 + 15 is inside it, no clamp)
+        if (lane < NR) rl = a.tab.row[y0 + lane];
     }
-    // the wave's row records: 4 rows per 64-byte scalar load, issued now (the host pads
-    // the table with non-marching rows to a multiple of 64 rows: no clamp, no H test)
-    using CRow4 = const __attribute__((address_space(4))) RowRec4K;
-    double py[NR];
-    float pyf[NR];
-    uint32_t rowbits = 0;  // (wave-uniform: bit r = row r marches: inRange01 and < H)
-    if (march) {
-#pragma unroll
-        for (int b = 0; b < NB; ++b) {
-            CRow4& r4 = ((CRow4*)a.tab.row)[(y0 >> 2) + b];
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                py[4 * b + r] = r4.r[r].py;
-                pyf[4 * b + r] = r4.r[r].pyf;
-                rowbits |= r4.r[r].ok != 0 ? 1u << (4 * b + r) : 0u;
-            }
-        }
-    }
-    RTM_PHASE(0)
-    double zb[NR][2];
-    int cd[NR][2];
-    // PK (the raster-free part, only march codes < steps or +INF, which fit 16 bits): a
-    // row's two codes packed in one register, +INF = 0xFFFF (half the code registers)
-    constexpr bool PK = PART == 1 && PK_CODES;
+    // this wave's strip is left to the other part of a split launch (wave-uniform); a
+    // skipping wave still fills its records and meets the workgroup barrier
+    const bool strip_box = !(a.flags & RTM_FLAG_NO_SHADOW_RASTER) && union_may_cover(a, xb, xb + 127, y0, y0 + NR - 1);
+    const bool skipw = (PART == 1 && strip_box) || (PART == 2 && !strip_box);
+    // a row's two codes packed in one register (low: column 0), NONE = 0xFFFF
     uint32_t cdp[NR];
 #pragma unroll
-    for (int r = 0; r < NR; ++r) {
-        cdp[r] = 0xFFFFFFFFu;
-#pragma unroll
-        for (int c = 0; c < 2; ++c) {
-            zb[r][c] = INFINITY;
-            cd[r][c] = -1;
-        }
-    }
-    // the records into LDS (all threads) + the barrier: EB = before the sphere raster
-    // (waves without spheres then do not wait at the barrier for the raster of waves
-    // with spheres), else after it (the record loads in flight during the raster)
-    auto fill_lds = [&]() {
+    for (int r = 0; r < NR; ++r) cdp[r] = 0xFFFFFFFFu;
+    if (march) {
         double2* T2 = reinterpret_cast<double2*>(T);
         if (fid <= steps) {
             T2[2 * fid] = rec0;
             T2[2 * fid + 1] = rec1;
         }
-        if (!fill1) {
-            const int stride = WL ? TILE_X : BLOCK;
-            for (int k = fid + stride; k <= steps; k += stride) {
-                T2[2 * k] = zsrc[2 * k];
-                T2[2 * k + 1] = zsrc[2 * k + 1];
-            }
+        for (int k = fid + BLOCK; k <= steps; k += BLOCK) {
+            T2[2 * k] = zsrc[2 * k];
+            T2[2 * k + 1] = zsrc[2 * k + 1];
         }
-        RTM_PHASE(1)
-        if (WL) {
-            // the wave's own copy: its LDS writes complete before its reads (in order per
-            // wave); the fence keeps the compiler from moving reads above the writes
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        } else {
-            __syncthreads();
-        }
-        RTM_PHASE(2)
-    };
-    if (EB && march) fill_lds();
-    // a sphere covered some texel of this wave (wave-uniform): else every texel's best is
-    // a march code or +INF, and since t_k rises strictly with k (host-checked) the march
-    // compares codes instead of t values
-    bool rasterized = false;
-    // shadow viewport rasterize, face BACK (main.rs:1569, 243): as the lean tile
-    if (PART != 1 && !(a.flags & RTM_FLAG_NO_SHADOW_RASTER) && union_may_cover(a, xb, xb + 127, y0, y0 + NR - 1)) {
-        uint32_t live = wave_sphere_mask(a.sph, a.n_spheres, xb, xb + 127, y0, y0 + NR - 1);
-        double xc[2] = {0.0, 0.0};  // the columns' NDC x, only where a sphere may cover
-        if (live) {
-            xc[0] = a.tab.nx[xs0];
-            xc[1] = a.tab.nx[xs1];
-        }
-        while (live) {
-            const int i = __builtin_ctz(live);
-            live &= live - 1u;
-            const RasterSphereK& sp = a.sph[i];
-            double pa[2];
-#pragma unroll
-            for (int c = 0; c < 2; ++c) pa[c] = ((xc[c] - sp.cx) * sp.n) / sp.m;
-#pragma unroll
-            for (int r = 0; r < NR; ++r) {
-                const int y = y0 + r;
-                if (y >= H || y < sp.iy0 || y > sp.iy1) continue;  // wave-uniform
-                const double pb = ((((cdouble*)a.tab.ny)[y] - sp.cy) * sp.n) / sp.m;
-                double s2[2];
-                bool in = false;
-#pragma unroll
-                for (int c = 0; c < 2; ++c) {
-                    s2[c] = pa[c] * pa[c] + pb * pb;
-                    in |= s2[c] < 1.0;
-                }
-                if (!__any(in)) continue;  // d < 1 implies s2 < 1 (sqrt monotone, sqrt(1) == 1)
-                rasterized = true;
-#pragma unroll
-                for (int c = 0; c < 2; ++c) {
-                    const double d = sqrt(s2[c]);
-                    const double h = sqrt(1.0 - d * d);
-                    const double depth = sp.z + h * sp.r;
-                    const bool win = (d < 1.0) & (depth < zb[r][c]);
-                    zb[r][c] = win ? depth : zb[r][c];
-                    cd[r][c] = win ? steps + i : cd[r][c];
-                }
-            }
-        }
+        if (lane < NR) RL[wv * NR + lane] = RowLdsK{rl.py, rl.pyf, 0};
+        __syncthreads();
     }
-    // PART 1: a wave whose rows meet the frame's sphere box leaves its texels to PART 2
-    // (which takes every 16-row tile meeting the box) but still fills the records and
-    // meets the workgroup barrier
-    const bool skipw = PART == 1 && !(a.flags & RTM_FLAG_NO_SHADOW_RASTER) &&
-                       union_may_cover(a, xb, xb + 127, y0, y0 + NR - 1);
-    if (march) {
-        if (!EB) fill_lds();
+    if (march && !skipw) {
         const double oz = a.tab.z0;
-        const int np = skipw ? 0 : a.n_patches;
         const float fsteps = (float)steps;
-        for (int k = 0; k < np; ++k) {
+        const RowLdsK* RW = RL + wv * NR;  // the wave's rows (uniform reads are broadcasts)
+        // wave-uniform: bit r = row r marches (inRange01 and < H)
+        const uint32_t rowbits = (uint32_t)__ballot((lane < NR) & (rl.ok != 0)) & ((1u << NR) - 1u);
+        for (int k = 0; k < a.n_patches; ++k) {
             if (k > 0) {
                 c0 = a.tab.col[k * W + xs0];
                 c1 = a.tab.col[k * W + xs1];
@@ -1759,16 +1138,73 @@ __device__ __forceinline__ void shadow_tile_coded(const ShadowPart& a, void* __r
             const float g1[2] = {c0.g1, c1.g1};
             // A column outside inRange01 has the host record d0 = "before the start"
             // (finite), dd = 0: entry and okA are false there, so it neither hits nor
-            // goes slow -- no per-texel in-range test.  Rows are wave-uniform.
+            // goes slow -- no per-texel in-range test.
+            // -- the shortcut: both ends of each column's strip
+            bool sc = rowbits == (1u << NR) - 1u;  // every row marches (wave-uniform)
+            uint32_t top[2] = {CODE_NONE, CODE_NONE}, bot[2] = {CODE_NONE, CODE_NONE};
+            int bnd[2] = {NR, NR};  // first row with the bottom code (NR: none)
+            if (sc) {
+                bool ok = true;
+#pragma unroll
+                for (int c = 0; c < 2; ++c) {
+                    const RowLdsK rt = RW[0], rb = RW[NR - 1];
+                    const double Dt = d0[c] + dd[c] * rt.py;
+                    const double Db = d0[c] + dd[c] * rb.py;
+                    bool st, et, sb, eb;
+                    top[c] = code_check<INC>(T, Dt, rt.pyf, g0[c], g1[c], fsteps, oz, steps, st, et);
+                    bot[c] = code_check<INC>(T, Db, rb.pyf, g0[c], g1[c], fsteps, oz, steps, sb, eb);
+                    ok = ok & !st & !sb & (et == eb) & (__builtin_signbit(Dt) == __builtin_signbit(Db));
+                }
+                sc = __all(ok);
+            }
+            if (sc) {
+                const bool need0 = top[0] != bot[0], need1 = top[1] != bot[1];
+                if (__any(need0 | need1)) {
+                    // binary search, both columns side by side: code(lo) == top, code(hi) != top
+                    int lo[2] = {0, 0}, hi[2] = {NR - 1, NR - 1};
+                    uint32_t chi[2] = {bot[0], bot[1]};
+                    const bool need[2] = {need0, need1};
+                    bool bad = false;
+#pragma unroll
+                    for (int it = 0; it < 4; ++it) {  // 15 rows: 4 halvings
+#pragma unroll
+                        for (int c = 0; c < 2; ++c) {
+                            const bool act = need[c] & (hi[c] - lo[c] > 1);
+                            const int mid = (lo[c] + hi[c]) >> 1;
+                            const RowLdsK rr = RW[act ? mid : 0];
+                            const double Dm = d0[c] + dd[c] * rr.py;
+                            bool sm, em;
+                            const uint32_t cm = code_check<INC>(T, Dm, rr.pyf, g0[c], g1[c], fsteps, oz, steps, sm, em);
+                            bad |= act & sm;
+                            const bool same = cm == top[c];
+                            lo[c] = (act & same) ? mid : lo[c];
+                            hi[c] = (act & !same) ? mid : hi[c];
+                            chi[c] = (act & !same) ? cm : chi[c];
+                        }
+                    }
+                    // one boundary per column: the first differing row already has the bottom code
+#pragma unroll
+                    for (int c = 0; c < 2; ++c) {
+                        bad |= need[c] & (chi[c] != bot[c]);
+                        bnd[c] = need[c] ? hi[c] : NR;
+                    }
+                    sc = !__any(bad);
+                }
+            }
+            if (sc) {
+                // rows [0, bnd) hold the top code, [bnd, NR) the bottom one
+#pragma unroll
+                for (int r = 0; r < NR; ++r) {
+                    const uint32_t v = (r < bnd[0] ? top[0] : bot[0]) | ((r < bnd[1] ? top[1] : bot[1]) << 16);
+                    cdp[r] = k == 0 ? v : pk_min_u16(cdp[r], v);
+                }
+                continue;
+            }
+            // -- the fallback: every texel's check (MASKED: skip rows outside inRange01 or
+            // past H, wave-uniform; the common case runs without the row tests)
             bool sany = false;  // a texel the check cannot decide
-            // MASKED: skip rows outside inRange01 or past H (wave-uniform); the
-            // common case (every row marches) runs without the row tests
-            // ZB: the wave holds sphere depths: compare t against the best value (zb);
-            // else compare codes (t_f < t_c <=> f < c; +INF = code -1 -> steps, and the
-            // sentinel guess f = steps never wins), no t read, no zb.
-            auto check = [&](auto masked, auto with_zb) {
+            auto check = [&](auto masked) {
                 constexpr bool MASKED = decltype(masked)::value;
-                constexpr bool ZB = decltype(with_zb)::value;
                 // (an opaque copy of the row bits per call: the row tests are not hoisted
                 // out of the patch loop as NR live lane masks)
                 uint32_t rb = rowbits;
@@ -1776,129 +1212,149 @@ __device__ __forceinline__ void shadow_tile_coded(const ShadowPart& a, void* __r
 #pragma unroll
                 for (int r = 0; r < NR; ++r) {
                     if (MASKED && !((rb >> r) & 1u)) continue;
-                    unsigned vv[2] = {0xFFFFu, 0xFFFFu};  // (PK: this row's decided codes)
+                    const RowLdsK rr = RW[r];
+                    uint32_t vv[2];
 #pragma unroll
                     for (int c = 0; c < 2; ++c) {
-                        const double Dv = d0[c] + dd[c] * py[r];
-                        const bool fastD = __builtin_amdgcn_class(Dv, 0x198);  // finite, nonzero
-                        // g0, g1, pyf are host-bounded finite values: the median and the
-                        // conversion of a value in [1, steps] are exact and defined
-                        const int f = (int)ceilf(__builtin_amdgcn_fmed3f(__builtin_fmaf(g1[c], pyf[r], g0[c]), 1.0f,
-                                                                         fsteps));
-                        const double zp = T[f].zprev, zf = T[f].z;
-                        const bool okA = INC ? (zp < Dv) : !(zp < Dv);
-                        const bool okB = INC ? !(zf < Dv) : (zf < Dv);
-                        const bool entry = INC ? (oz < Dv) : !(oz < Dv);
-                        if (ZB) {
-                            const double tf = T[f].t;
-                            const bool win = fastD & okA & okB & (tf < zb[r][c]);
-                            zb[r][c] = win ? tf : zb[r][c];
-                            cd[r][c] = win ? f : cd[r][c];
-                        } else if (PK) {
-                            // a decided crossing below the sentinel; the smaller code wins below
-                            vv[c] = (fastD & okA & okB & ((unsigned)f < (unsigned)steps)) ? (unsigned)f : 0xFFFFu;
-                        } else {
-                            const unsigned lim = min((unsigned)cd[r][c], (unsigned)steps);
-                            const bool win = fastD & okA & okB & ((unsigned)f < lim);
-                            cd[r][c] = win ? f : cd[r][c];
-                        }
-                        sany |= !fastD | (entry & !(okA & okB));
+                        bool sl, en;
+                        vv[c] = code_check<INC>(T, d0[c] + dd[c] * rr.py, rr.pyf, g0[c], g1[c], fsteps, oz, steps, sl,
+                                                en);
+                        sany |= sl;
                     }
-                    if (PK && !ZB) cdp[r] = pk_min_u16(cdp[r], vv[0] | (vv[1] << 16));
+                    cdp[r] = pk_min_u16(cdp[r], vv[0] | (vv[1] << 16));
                 }
             };
-            const bool full = rowbits == (1u << NR) - 1u;
-            if (rasterized) {
-                if (full) check(std::false_type{}, std::true_type{});
-                else check(std::true_type{}, std::true_type{});
-            } else {
-                if (full) check(std::false_type{}, std::false_type{});
-                else check(std::true_type{}, std::false_type{});
-            }
+            if (rowbits == (1u << NR) - 1u) check(std::false_type{});
+            else check(std::true_type{});
             if (__any(sany)) {
                 // exact per-texel march (march_axis) for the texels the check cannot decide
                 const double sz = a.cam.dir[2] * 0.03;
 #pragma unroll 1
                 for (int q = 0; q < NR * 2; ++q) {
                     const int qr = q >> 1, qc = q & 1;
-                    double pyq = py[0];
-                    float pyfq = pyf[0];
-                    const bool rokq = (rowbits >> qr) & 1u;
-#pragma unroll
-                    for (int r = 1; r < NR; ++r) {
-                        pyq = qr == r ? py[r] : pyq;
-                        pyfq = qr == r ? pyf[r] : pyfq;
-                    }
+                    const RowLdsK rq = RW[qr];
+                    const double pyq = rq.py;
+                    const float pyfq = rq.pyf;
                     // (selects, not indexing: a dynamically indexed array would live in scratch)
                     const double d0q = qc ? d0[1] : d0[0], ddq = qc ? dd[1] : dd[0];
                     const float g0q = qc ? g0[1] : g0[0], g1q = qc ? g1[1] : g1[0];
                     const double Dv = d0q + ddq * pyq;
-                    const bool inr = rokq;
-                    const bool fastD = __builtin_amdgcn_class(Dv, 0x198);
-                    const int f = (int)ceilf(__builtin_amdgcn_fmed3f(__builtin_fmaf(g1q, pyfq, g0q), 1.0f, fsteps));
-                    const double zp = T[f].zprev, zf = T[f].z;
-                    const bool okA = INC ? (zp < Dv) : !(zp < Dv);
-                    const bool okB = INC ? !(zf < Dv) : (zf < Dv);
-                    const bool entry = INC ? (oz < Dv) : !(oz < Dv);
-                    const bool sl = inr & (!fastD | (entry & !(okA & okB)));
+                    bool sl, en;
+                    (void)code_check<INC>(T, Dv, pyfq, g0q, g1q, fsteps, oz, steps, sl, en);
+                    sl = sl & (((rowbits >> qr) & 1u) != 0u);
                     if (!__any(sl)) continue;
                     MarchResult m{false, 0.0, 0, 0};
                     if (sl) m = march_axis<false>(Dv, true, oz, sz, steps, a.tab);
 #pragma unroll
                     for (int r = 0; r < NR; ++r)
 #pragma unroll
-                        for (int c = 0; c < 2; ++c)
-                            if (PK) {
-                                const unsigned cur = (cdp[r] >> (16 * c)) & 0xFFFFu;
-                                if (q == r * 2 + c && sl && m.hit && (unsigned)m.k < min(cur, (unsigned)steps))
-                                    cdp[r] = (cdp[r] & ~(0xFFFFu << (16 * c))) | ((unsigned)m.k << (16 * c));
-                            } else if (q == r * 2 + c && sl && m.hit &&
-                                       (rasterized ? m.t < zb[r][c]
-                                                   : (unsigned)m.k < min((unsigned)cd[r][c], (unsigned)steps))) {
-                                zb[r][c] = m.t;
-                                cd[r][c] = m.k;
-                            }
+                        for (int c = 0; c < 2; ++c) {
+                            const unsigned cur = (cdp[r] >> (16 * c)) & 0xFFFFu;
+                            if (q == r * 2 + c && sl && m.hit && (unsigned)m.k < min(cur, (unsigned)steps))
+                                cdp[r] = (cdp[r] & ~(0xFFFFu << (16 * c))) | ((unsigned)m.k << (16 * c));
+                        }
                 }
             }
         }
     }
-    RTM_PHASE(3)
+    // shadow viewport rasterize, face BACK (main.rs:1569, 243), 4 rows at a time: the
+    // strict minimum over the spheres in scene order (zs, cs), then the march code only
+    // where its t is strictly below that minimum (main.rs:559)
+    if (PART != 1 && strip_box && !skipw) {
+        const uint32_t live0 = wave_sphere_mask(a.sph, a.n_spheres, xb, xb + 127, y0, y0 + NR - 1);
+        if (live0) {
+            const double xc[2] = {a.tab.nx[xs0], a.tab.nx[xs1]};
+#pragma unroll
+            for (int b = 0; b < NR / 4; ++b) {
+                const int yb = y0 + 4 * b;
+                if (yb >= H) break;  // (wave-uniform)
+                double zs[4][2];
+                uint32_t cs[4];  // packed sphere codes, NONE = no sphere covers
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    cs[r] = 0xFFFFFFFFu;
+                    zs[r][0] = zs[r][1] = INFINITY;
+                }
+                bool any = false;
+                uint32_t live = live0;
+                while (live) {
+                    const int i = __builtin_ctz(live);
+                    live &= live - 1u;
+                    const RasterSphereK& sp = a.sph[i];
+                    if (yb + 3 < sp.iy0 || yb > sp.iy1) continue;  // wave-uniform
+                    double pa[2];
+#pragma unroll
+                    for (int c = 0; c < 2; ++c) pa[c] = ((xc[c] - sp.cx) * sp.n) / sp.m;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const int y = yb + r;
+                        if (y >= H || y < sp.iy0 || y > sp.iy1) continue;  // wave-uniform
+                        const double pb = ((((cdouble*)a.tab.ny)[y] - sp.cy) * sp.n) / sp.m;
+                        double s2[2];
+                        bool in = false;
+#pragma unroll
+                        for (int c = 0; c < 2; ++c) {
+                            s2[c] = pa[c] * pa[c] + pb * pb;
+                            in |= s2[c] < 1.0;
+                        }
+                        // sqrt is monotone with sqrt(1) == 1, so d < 1 implies s2 < 1: a wave
+                        // with no s2 < 1 has no covered texel in this row and skips both sqrts
+                        if (!__any(in)) continue;
+                        any = true;
+#pragma unroll
+                        for (int c = 0; c < 2; ++c) {
+                            const double d = sqrt(s2[c]);
+                            const double h = sqrt(1.0 - d * d);
+                            const double depth = sp.z + h * sp.r;
+                            const bool win = (d < 1.0) & (depth < zs[r][c]);
+                            zs[r][c] = win ? depth : zs[r][c];
+                            const uint32_t sh16 = 16u * (uint32_t)c;
+                            cs[r] = win ? (cs[r] & ~(0xFFFFu << sh16)) | ((uint32_t)(steps + i) << sh16) : cs[r];
+                        }
+                    }
+                }
+                if (!any) continue;
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+#pragma unroll
+                    for (int c = 0; c < 2; ++c) {
+                        const uint32_t sh16 = 16u * (uint32_t)c;
+                        const uint32_t sc16 = (cs[r] >> sh16) & 0xFFFFu;
+                        if (sc16 == CODE_NONE) continue;
+                        const uint32_t mc = (cdp[4 * b + r] >> sh16) & 0xFFFFu;
+                        // t of the march code (NONE: T[steps].t = +INF); no march: +INF
+                        const double tm = march ? T[min(mc, (uint32_t)steps)].t : INFINITY;
+                        if (!(tm < zs[r][c]))
+                            cdp[4 * b + r] = (cdp[4 * b + r] & ~(0xFFFFu << sh16)) | (sc16 << sh16);
+                    }
+            }
+        }
+    }
+    if (skipw) return;
     // the lane's 4 rows x 2 columns of each block as one 8- (U8) or 16-byte (U16)
     // store: element lane*8 + r*2 + c of block (y >> 2, xb >> 7) (rows past H hold
     // codes no reader looks up; a block wholly past H does not exist)
 #pragma unroll
-    for (int b = 0; b < NB; ++b) {
+    for (int b = 0; b < NR / 4; ++b) {
         const int yb = y0 + 4 * b;
-        if (yb >= H || skipw) break;
+        if (yb >= H) break;
         const int64_t blk = (int64_t)(yb >> 2) * a.smap_bw + (xb >> 7);
         if (CODE == SMAP_U8) {
-            uint32_t w[2] = {0u, 0u};
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-#pragma unroll
-                for (int c = 0; c < 2; ++c)
-                    w[r >> 1] |= ((PK ? cdp[4 * b + r] >> (16 * c) : (uint32_t)cd[4 * b + r][c]) & 0xFFu)
-                                 << (8 * ((r & 1) * 2 + c));
-            *reinterpret_cast<uint2*>((uint8_t*)map + blk * 512 + lane * 8) = make_uint2(w[0], w[1]);
+            // bytes (r, c) at 8*((r & 1)*2 + c) of word r >> 1: the low bytes of two rows' codes
+            const uint32_t w0 = __builtin_amdgcn_perm(cdp[4 * b + 1], cdp[4 * b], 0x06040200u);
+            const uint32_t w1 = __builtin_amdgcn_perm(cdp[4 * b + 3], cdp[4 * b + 2], 0x06040200u);
+            *reinterpret_cast<uint2*>((uint8_t*)map + blk * 512 + lane * 8) = make_uint2(w0, w1);
         } else {
-            uint32_t w[4];
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-                w[r] = PK ? cdp[4 * b + r] : ((uint32_t)cd[4 * b + r][0] & 0xFFFFu) | ((uint32_t)cd[4 * b + r][1] << 16);
-            *reinterpret_cast<uint4*>((uint8_t*)map + blk * 1024 + lane * 16) = make_uint4(w[0], w[1], w[2], w[3]);
+            *reinterpret_cast<uint4*>((uint8_t*)map + blk * 1024 + lane * 16) =
+                make_uint4(cdp[4 * b], cdp[4 * b + 1], cdp[4 * b + 2], cdp[4 * b + 3]);
         }
-    }
-    RTM_PHASE(4)
-    if (diag & 8) {
-        __builtin_amdgcn_s_waitcnt(0);  // (diagnostic only: when this wave's stores have left)
-        RTM_PHASE(5)
     }
 }
 
-template <bool INC, int CODE, int NB, bool WL, bool EB, int PART = 0, bool PK = false>
-__device__ __forceinline__ void shadow_coded_block(const ShadowPart& sh, void* __restrict__ map, ZRecK* __restrict__ lds,
-                                                   int diag, int4 org) {
-    constexpr int TR = TILE_Y * 4 * NB;
+template <bool INC, int CODE, int PART>
+__device__ __forceinline__ void shadow_coded_block(const ShadowPart& sh, void* __restrict__ map, char* __restrict__ lds,
+                                                   int4 org) {
+    constexpr int TR = CODED_TILE_ROWS;
     int bx = (int)blockIdx.x, by;
     if (PART == 0) {
         const int n = (int)gridDim.y;
@@ -1907,40 +1363,41 @@ __device__ __forceinline__ void shadow_coded_block(const ShadowPart& sh, void* _
         const bool none = sh.cull_x0 > sh.cull_x1 || sh.cull_y0 > sh.cull_y1 || sh.cull_y1 < 0;
         by = none ? (int)blockIdx.y : hot_rows_first((int)blockIdx.y, n, h0, h1);
     } else {
-        // (workgroup-uniform: the whole workgroup leaves, before its barrier).  PART 2 takes
-        // the 16-row tiles (its own tiles) meeting the box; PART 1's waves (16 rows at NB 4)
-        // skip those, and its workgroup leaves when every one of its waves would
+        // (workgroup-uniform: the whole workgroup leaves, before its barrier, when none of
+        // its 4 strips is this part's; the box is a rectangle, so its strips are a run)
         bx += org.x;
         by = (int)blockIdx.y + org.y;
         const bool rast = !(sh.flags & RTM_FLAG_NO_SHADOW_RASTER);
         const int ya = by * TR;
-        const int sub = TR / 4;  // a wave's rows
-        if (PART == 2 ? !(rast && union_may_cover(sh, bx * 128, bx * 128 + 127, ya, ya + TR - 1))
-                      : (rast && union_may_cover(sh, bx * 128, bx * 128 + 127, ya, ya + sub - 1) &&
-                         union_may_cover(sh, bx * 128, bx * 128 + 127, ya + TR - sub, ya + TR - 1)))
+        const int sub = CODED_ROWS;
+        const int xa = bx * 128, xe = xa + 127;
+        if (PART == 2 ? !(rast && union_may_cover(sh, xa, xe, ya, ya + TR - 1))
+                      : (rast && union_may_cover(sh, xa, xe, ya, ya + sub - 1) &&
+                         union_may_cover(sh, xa, xe, ya + TR - sub, ya + TR - 1)))
             return;
     }
-    shadow_tile_coded<INC, CODE, NB, WL, EB, PART, PK>(sh, map, bx, by, lds, diag);
+    shadow_tile_coded<INC, CODE, PART>(sh, map, bx, by, reinterpret_cast<ZRecK*>(lds + CODED_ROW_LDS),
+                                       reinterpret_cast<RowLdsK*>(lds));
 }
 
-// waves per SIMD the register allocator must keep: 7 for the packed 16-row raster-free
-// part (72 VGPRs; uncapped, fewer spilled SGPRs cost 90 VGPRs and 5 waves), else free
-template <int PART, bool PK, int NB>
-constexpr int CODED_MIN_WAVES = PART == 1 && PK && NB == 4 ? 7 : 1;
+// waves per SIMD the register allocator must keep: 7 for the raster-free part (round 3:
+// uncapped, fewer spilled SGPRs cost 90 VGPRs and 5 waves), else free
+template <int PART>
+constexpr int CODED_MIN_WAVES = PART == 1 ? 7 : 1;
 
-template <bool INC, int CODE, int NB, bool WL, bool EB, int PART = 0, bool PK = false>
-__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(CODED_MIN_WAVES<PART, PK, NB>, 8))) void
-shadow_coded_kernel(const FrameArgs a, double* __restrict__ smap, int diag, int4 org) {
-    extern __shared__ ZRecK lds_rec[];
-    shadow_coded_block<INC, CODE, NB, WL, EB, PART, PK>(a.sh, smap, lds_rec, diag, org);
+template <bool INC, int CODE, int PART>
+__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(CODED_MIN_WAVES<PART>, 8))) void
+shadow_coded_kernel(const FrameArgs a, double* __restrict__ smap, int4 org) {
+    extern __shared__ char lds_coded[];
+    shadow_coded_block<INC, CODE, PART>(a.sh, smap, lds_coded, org);
 }
 
-template <bool INC, int CODE, int NB, bool WL, bool EB, int PART = 0, bool PK = false>
-__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(CODED_MIN_WAVES<PART, PK, NB>, 8))) void
-shadow_coded_batch_kernel(CBatch* __restrict__ fr, int diag, int4 org) {
-    extern __shared__ ZRecK lds_rec[];
+template <bool INC, int CODE, int PART>
+__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(CODED_MIN_WAVES<PART>, 8))) void
+shadow_coded_batch_kernel(CBatch* __restrict__ fr, int4 org) {
+    extern __shared__ char lds_coded[];
     CBatch* f = fr + blockIdx.z;
-    shadow_coded_block<INC, CODE, NB, WL, EB, PART, PK>(*(const ShadowPart*)&f->a.sh, f->smap, lds_rec, diag, org);
+    shadow_coded_block<INC, CODE, PART>(*(const ShadowPart*)&f->a.sh, f->smap, lds_coded, org);
 }
 
 
@@ -1959,7 +1416,7 @@ __device__ __forceinline__ int eye_row(int row_begin, int S, int stride, int pha
 template <bool FUSED, bool COUNT, int RT, int FMT = RTM_FORMAT_RGBA32F, bool NOSH = false>
 __device__ __forceinline__ void eye_tile(const EyePart& a, const ShadowPart& sh, const double* __restrict__ smap,
                                          void* __restrict__ out, int bx, int by, StatsK* __restrict__ st,
-                                         const DevTabs tabs, int wide = 0) {
+                                         const DevTabs tabs) {
     // RT 3: RT 1 under a PERSPECTIVE eye, with the host's origin-only primitive
     // constants (RtK::persp) and the per-wave primitive masks of rt_cull_kernel
     constexpr bool RTP = RT == 3;
@@ -1967,11 +1424,10 @@ __device__ __forceinline__ void eye_tile(const EyePart& a, const ShadowPart& sh,
     const RtK* __restrict__ rt = tabs.rt;
     const PerspK* __restrict__ psp = tabs.psp;
     const SdfTabK* __restrict__ sdf = tabs.sdf;
-    // wide: the workgroup's 4 waves side by side in one row (256 x 1), else stacked (64 x 4)
-    const int wv = threadIdx.x >> 6;
-    const int xb = __builtin_amdgcn_readfirstlane((wide & 1) ? (bx * TILE_Y + wv) * TILE_X : bx * TILE_X);
+    // the workgroup's 4 waves stacked (64 x 4 pixels)
+    const int xb = __builtin_amdgcn_readfirstlane(bx * TILE_X);
     const int xi = xb + (threadIdx.x & (TILE_X - 1));
-    const int yl = __builtin_amdgcn_readfirstlane((wide & 1) ? by : by * TILE_Y + wv);
+    const int yl = __builtin_amdgcn_readfirstlane(by * TILE_Y + (int)(threadIdx.x >> 6));
     const int yi = __builtin_amdgcn_readfirstlane(eye_row(a.row_begin, a.stripe_rows, a.stripe_stride, a.stripe_phase, yl));
     const int yo = a.out_global ? yi : yl;  // the output row
     const bool live = xi < a.W && a.row_begin + yl < a.row_end && yi < a.H;
@@ -1988,7 +1444,7 @@ __device__ __forceinline__ void eye_tile(const EyePart& a, const ShadowPart& sh,
     if (RTP && tabs.rtmask && a.row_begin + yl < a.row_end)  // (no mask word for rows past the part)
         rmask = ((const __attribute__((address_space(4))) uint32_t*)tabs.rtmask)[yl * ((a.W + TILE_X - 1) / TILE_X) +
                                                                                  (xb / TILE_X)];
-    else if (RTB == 1 && rt && a.eye.type == RTM_CAMERA_PERSPECTIVE && !(wide & 4))
+    else if (RTB == 1 && rt && a.eye.type == RTM_CAMERA_PERSPECTIVE)
         rmask = rt_wave_mask(rt, a.eye, min(xb, a.W - 1), min(xb + TILE_X - 1, a.W - 1), min(yi, a.H - 1), a.W, a.H);
     float4 c = make_float4(0.0f, 0.2f, 0.2f, 1.0f);  // (0.0, 0.2, 0.2) as f32 (main.rs:718-720)
     bool shaded = false;
@@ -2131,13 +1587,10 @@ __device__ __forceinline__ void eye_tile(const EyePart& a, const ShadowPart& sh,
     // the frame store (all lanes converged): RGBA f32, or writeColorImage's bytes
     if (FMT == RTM_FORMAT_RGBA32F) {
         float4* o = reinterpret_cast<float4*>(out);
-        if (live) {
-            if (wide & 2)  // non-temporal: the frame's stores do not allocate in the caches
-                __builtin_nontemporal_store(f32x4{c.x, c.y, c.z, c.w},
-                                            reinterpret_cast<f32x4*>(&o[(int64_t)yo * a.W + xi]));
-            else
-                o[(int64_t)yo * a.W + xi] = c;
-        }
+        // non-temporal: the frame is not re-read, and at 7680x4320 its 531 MB would
+        // otherwise evict the shadow map the pass gathers from (eye 120 -> 85 us)
+        if (live)
+            __builtin_nontemporal_store(f32x4{c.x, c.y, c.z, c.w}, reinterpret_cast<f32x4*>(&o[(int64_t)yo * a.W + xi]));
     } else {
         uint32_t e = tabs.bg;  // background: one host-encoded constant
         if (shaded) {
@@ -2204,52 +1657,45 @@ __global__ __launch_bounds__(BLOCK) void shadow_pass_batch_kernel(CBatch* __rest
     shadow_tile_generic<false>(*(const ShadowPart*)&f->a.sh, f->smap, blockIdx.x, blockIdx.y, nullptr);
 }
 
-template <int NR, int MODE>
-__global__ __launch_bounds__(BLOCK) void shadow_sep_kernel(const FrameArgs a, double* __restrict__ smap, int diag,
-                                                           int lds) {
-    extern __shared__ double2 lds_zt[];
-    shadow_tile_sep<NR, MODE>(a.sh, smap, blockIdx.x, blockIdx.y, diag, lds ? lds_zt : nullptr);
-}
-
 template <bool FUSED, bool COUNT, int RT, int FMT, bool NOSH = false>
 __global__ __launch_bounds__(BLOCK) void eye_pass_kernel(const FrameArgs a, const double* __restrict__ smap,
                                                          void* __restrict__ out, StatsK* __restrict__ st,
-                                                         const DevTabs tabs, int wide) {
-    eye_tile<FUSED, COUNT, RT, FMT, NOSH>(a.ey, a.sh, smap, out, blockIdx.x, blockIdx.y, st, tabs, wide);
+                                                         const DevTabs tabs) {
+    eye_tile<FUSED, COUNT, RT, FMT, NOSH>(a.ey, a.sh, smap, out, blockIdx.x, blockIdx.y, st, tabs);
 }
 
 // The sphere-only eye pass (RT 0, materialised map) held to 8 waves per SIMD: the
 // coded map's decode (smap_decode_wave) would otherwise take it to 66 VGPRs, 7 waves.
 template <int FMT>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8))) void eye_pass8_kernel(
-    const FrameArgs a, const double* __restrict__ smap, void* __restrict__ out, const DevTabs tabs, int wide) {
-    eye_tile<false, false, 0, FMT>(a.ey, a.sh, smap, out, blockIdx.x, blockIdx.y, nullptr, tabs, wide);
+    const FrameArgs a, const double* __restrict__ smap, void* __restrict__ out, const DevTabs tabs) {
+    eye_tile<false, false, 0, FMT>(a.ey, a.sh, smap, out, blockIdx.x, blockIdx.y, nullptr, tabs);
 }
 
 // The SDF eye instantiation (row f-4) with a register cap: WPE waves per SIMD at least.
 template <int WPE, int FMT, bool NOSH = false>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8))) void eye_sdf_kernel(
-    const FrameArgs a, const double* __restrict__ smap, void* __restrict__ out, const DevTabs tabs, int wide) {
-    eye_tile<false, false, 2, FMT, NOSH>(a.ey, a.sh, smap, out, blockIdx.x, blockIdx.y, nullptr, tabs, wide);
+    const FrameArgs a, const double* __restrict__ smap, void* __restrict__ out, const DevTabs tabs) {
+    eye_tile<false, false, 2, FMT, NOSH>(a.ey, a.sh, smap, out, blockIdx.x, blockIdx.y, nullptr, tabs);
 }
 
 // NOSH: frames whose shadow viewport is all +INF (no shadow raster, no march): the
 // lookup is skipped (lit = +INF > qz, as the fused texel would give)
 template <bool FUSED, int RT, int FMT, bool NOSH = false>
-__global__ __launch_bounds__(BLOCK) void eye_batch_kernel(CBatch* __restrict__ fr, int wide) {
+__global__ __launch_bounds__(BLOCK) void eye_batch_kernel(CBatch* __restrict__ fr) {
     CBatch* f = fr + blockIdx.z;
     const DevTabs tabs = *(const DevTabs*)&f->tabs;
     eye_tile<FUSED, false, RT, FMT, NOSH>(*(const EyePart*)&f->a.ey, *(const ShadowPart*)&f->a.sh, f->smap, f->out,
-                                    blockIdx.x, blockIdx.y, nullptr, tabs, wide);
+                                    blockIdx.x, blockIdx.y, nullptr, tabs);
 }
 
 template <int WPE, int FMT, bool NOSH = false>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8))) void eye_sdf_batch_kernel(
-    CBatch* __restrict__ fr, int wide) {
+    CBatch* __restrict__ fr) {
     CBatch* f = fr + blockIdx.z;
     const DevTabs tabs = *(const DevTabs*)&f->tabs;
     eye_tile<false, false, 2, FMT, NOSH>(*(const EyePart*)&f->a.ey, *(const ShadowPart*)&f->a.sh, f->smap, f->out,
-                                   blockIdx.x, blockIdx.y, nullptr, tabs, wide);
+                                   blockIdx.x, blockIdx.y, nullptr, tabs);
 }
 
 // launch_upload: one 8-byte word per thread from the kernarg copy.
@@ -2308,46 +1754,6 @@ __global__ __launch_bounds__(BLOCK) void rt_cull_batch_kernel(CBatch* __restrict
     const EyePart& e = *(const EyePart*)&f->a.ey;
     rt_cull_wave(e.eye, rt, e.W, e.H, e.row_begin, e.row_end - e.row_begin,
                  make_int4(e.stripe_rows, e.stripe_stride, e.stripe_phase, 0), masks, blockIdx.x * BLOCK + threadIdx.x);
-}
-
-// Timing diagnostic only (RTM_DIAG_EYE=1): the eye pass's stores without its work.
-__global__ __launch_bounds__(BLOCK) void eye_store_only_kernel(const FrameArgs a, float4* __restrict__ out, int wide) {
-    const int wv = threadIdx.x >> 6;
-    const int xi = ((wide & 1) ? (blockIdx.x * TILE_Y + wv) * TILE_X : blockIdx.x * TILE_X) + (threadIdx.x & (TILE_X - 1));
-    const int yl = (wide & 1) ? blockIdx.y : blockIdx.y * TILE_Y + wv;
-    if (xi < a.ey.W && a.ey.row_begin + yl < a.ey.row_end)
-        out[(int64_t)yl * a.ey.W + xi] = make_float4(0.0f, 0.2f, 0.2f, 1.0f);
-}
-
-// Software-pipelined frame step (launch_frame_pipe): a 1-D grid of
-// n_sh shadow tiles (frame i) and n_eye eye tiles (frame i-1) merged in
-// proportion (Bresenham), so both roles are resident on every CU through the
-// whole launch.  SEP: shadow tiles use shadow_tile_sep<NR>, else the generic one.
-// KIND: 0 generic shadow tiles, 1 separable chunked (MARCH_CMP), 2 lean2 (2
-// columns per lane, LDS table in the dynamic shared memory; INC = table direction).
-template <int KIND, int NR, bool INC>
-__global__ __launch_bounds__(BLOCK) void frame_pipe_kernel(const FrameArgs a, double* __restrict__ smap_w,
-                                                           const double* __restrict__ smap_r,
-                                                           float4* __restrict__ out, int sh_gx, int n_sh,
-                                                           int eye_gx, int n_eye) {
-    extern __shared__ double2 lds_zt[];
-    const int64_t b = blockIdx.x;
-    const int64_t total = (int64_t)n_sh + n_eye;
-    const int64_t s_before = (b * n_sh) / total;         // shadow tiles among blocks [0, b)
-    const int64_t s_after = ((b + 1) * n_sh) / total;    // ... among [0, b]
-    if (s_after > s_before) {
-        const int t = (int)s_before;
-        if (KIND == 2)
-            shadow_tile_lean2<NR, 2, INC>(a.sh, smap_w, t % sh_gx, t / sh_gx, lds_zt, 0);
-        else if (KIND == 1)
-            shadow_tile_sep<NR, MARCH_CMP>(a.sh, smap_w, t % sh_gx, t / sh_gx, 0);
-        else
-            shadow_tile_generic<false>(a.sh, smap_w, t % sh_gx, t / sh_gx, nullptr);
-    } else {
-        const int t = (int)(b - s_before);
-        eye_tile<false, false, 0>(a.ey, a.sh, smap_r, out, t % eye_gx, t / eye_gx, nullptr,
-                                      DevTabs{nullptr, nullptr, nullptr});
-    }
 }
 
 // ---- reference-seam kernels ----
@@ -2545,160 +1951,39 @@ inline int launched() { return hipGetLastError() == hipSuccess ? 0 : RTM_ERR_HIP
 
 }  // namespace
 
-// Rows per wave of the separable shadow kernel (0 = generic kernel).  Default
-// chosen by measurement (profiles/); RTM_SEP_ROWS overrides it for A/B runs.
-// Timing diagnostics only (RTM_DIAG_SHADOW: 1 = skip rasterize, 2 = skip march,
-// 3 = store only; RTM_DIAG_EYE=1: store-only eye pass); results are wrong under
-// them and no test sets them.
-static int diag_mode() {
-    static int v = [] {
-        const char* e = getenv("RTM_DIAG_SHADOW");
-        return e ? atoi(e) : 0;
-    }();
-    return v;
-}
-static int diag_eye() {
-    static int v = [] {
-        const char* e = getenv("RTM_DIAG_EYE");
-        return e ? atoi(e) : 0;
-    }();
-    return v;
-}
-
-// Rows per wave of the separable shadow tile (0 = generic tile).  Default chosen
-// by measurement (profiles/); RTM_SEP_ROWS overrides it for A/B runs.
-static int sep_rows() {
-    static int v = [] {
-        const char* e = getenv("RTM_SEP_ROWS");
-        int r = e ? atoi(e) : 4;
-        return (r == 0 || r == 1 || r == 2 || r == 4 || r == 8) ? r : 4;
-    }();
-    return v;
-}
-
-static bool use_sep(const ShadowPart& s) { return sep_rows() > 0 && s.tab.d0 && s.tab.z && s.tab.t; }
-
-// March mode of the separable shadow tile: the first-crossing search when the
-// z table is monotone (default), else 8-step chunks with a compare per step
-// (47.1 vs 52.9 us for the sign bit at config 3, profiles/r01_ab_cmp.txt).
-// RTM_SEP_MODE=0/1/2 forces sign/compare/search for A/B runs (search only when
-// the table allows it) — identical results.
-constexpr int MARCH_LEAN2 = 4;  // shadow_lean2_kernel (the default when it applies)
-static int sep_mode(const ShadowPart& sh) {
-    static int v = [] {
-        const char* e = getenv("RTM_SEP_MODE");
-        return e ? atoi(e) : -1;
-    }();
-    const bool march = !(sh.flags & RTM_FLAG_NO_MARCH) && sh.n_patches > 0 && sh.steps > 0;
-    const bool lean_ok = sh.tab.zmono != 0 && sh.steps >= 1 && sh.steps <= SEARCH_LDS_MAX_STEPS;
-    int want = v < 0 ? MARCH_LEAN2 : v;
-    if (want == MARCH_LEAN2 && !(lean_ok || !march)) want = MARCH_SEARCH;
-    if (want != MARCH_LEAN2 && want != MARCH_CMP && want != MARCH_SIGN) want = MARCH_SEARCH;
-    return (want == MARCH_SEARCH && sh.tab.zmono == 0) ? MARCH_CMP : want;
-}
-
-
-// Columns per lane of shadow_lean2_kernel (RTM_LEAN_COLS=1|2, default 2).
-static int lean_cols() {
-    static int v = [] {
-        const char* e = getenv("RTM_LEAN_COLS");
-        return (e && atoi(e) == 1) ? 1 : 2;
-    }();
-    return v;
-}
-
-// Register-held LDS table entries of the lean tile: 1 per thread when the table
-// fits (RTM_LEAN_FILL=4 forces the 4-entry form for A/B runs).
-static bool lean_fill1() {
-    static bool v = [] {
-        const char* e = getenv("RTM_LEAN_FILL");
-        return !(e && atoi(e) == 4);
-    }();
-    return v;
-}
-
-
-// Sphere rows dispatched first (default; RTM_HOT=0 keeps the plain row order
-// for A/B runs).
-static bool lean_hot() {
-    static bool v = [] {
-        const char* e = getenv("RTM_HOT");
-        return !(e && atoi(e) == 0);
-    }();
-    return v;
-}
-
-// The coded shadow tile (shadow_tile_coded), default; RTM_CODED=0 keeps the lean tile
-// for coded maps (A/B runs).  (Measured and dropped from the dispatch: 2 blocks per
-// wave, 281.9 vs 305.5 Gpix/s, and per-wave record copies without the workgroup
-// barrier, 295.7: profiles/r03_ab_coded_variants.txt.)
-static int coded_blocks() {
-    static int v = [] {
-        const char* e = getenv("RTM_CODED");
-        return (e && atoi(e) == 0) ? 0 : 1;
-    }();
-    return v;
-}
-
-// Does this frame's (lean, coded) shadow pass take shadow_tile_coded?
+// Can the coded shadow tile render this frame's shadow pass?  It needs a coded map
+// and, when the frame marches, the host-built records (a separable march camera with
+// a monotone shared z table, rtm_api.cpp ensure_tables) and at most CODED_MAX_STEPS
+// steps (its LDS table).  Everything else takes the generic tile.
 static bool coded_ok(const ShadowPart& sh) {
     const bool march = !(sh.flags & RTM_FLAG_NO_MARCH) && sh.n_patches > 0 && sh.steps > 0;
-    return coded_blocks() > 0 && sh.smap_fmt != SMAP_F64 &&
+    return sh.smap_fmt != SMAP_F64 &&
            (!march || (sh.tab.zrec && sh.tab.col && sh.tab.row && sh.steps <= CODED_MAX_STEPS));
-}
-
-// The split launch (default; RTM_CODED_SPLIT=0: one launch over every tile): the
-// workgroup tiles meeting a frame's sphere box run the full tile, the others a
-// raster-free instantiation with fewer registers (more waves per SIMD).
-static bool coded_split() {
-    static const bool v = [] {
-        const char* e = getenv("RTM_CODED_SPLIT");
-        return !(e && atoi(e) == 0);
-    }();
-    return v;
 }
 
 // Launch the coded tile for one frame (FrameArgs) or a batch (fr != nullptr, n frames).
 // box: the union over the frames of their spheres' pixel boxes (x0, x1, y0, y1), for the
-// split launch (nullptr: sh's own).
+// split launch (nullptr: sh's own).  The split: the workgroup tiles meeting the box run
+// the full tile (PART 2), the others a raster-free instantiation with fewer registers
+// (PART 1), when the box covers at most RTM_CODED_SPLIT_MAX (default 0.3) of the tiles
+// (configs 2-4 split; config 5's 16 spheres span more: one launch there, measured as
+// fast in the 4-lane frame and faster one-lane, profiles/r03_ab_coded_split.txt).
 static void launch_coded(const ShadowPart& sh, const FrameArgs* a, double* smap, CBatch* fr, int n, hipStream_t s,
                          const int32_t* box = nullptr) {
     const bool march = !(sh.flags & RTM_FLAG_NO_MARCH) && sh.n_patches > 0 && sh.steps > 0;
-    // record fill + barrier before the sphere raster (RTM_CODED_EB=1) or after it (default)
-    static const bool eb = [] {
-        const char* e = getenv("RTM_CODED_EB");
-        return e && atoi(e) != 0;
-    }();
-    const size_t lsm = march ? sizeof(ZRecK) * (size_t)(sh.steps + 1) : 0;
-    constexpr int TR = TILE_Y * 4;
-    // 4-row blocks per wave of the raster-free part: 4 (16 rows, codes packed two per
-    // register: 72 VGPRs, 7 waves per SIMD; measured faster than 2 blocks, and than 1 block
-    // at 8 waves); RTM_CODED_NB1 = 1 or 2 for A/B runs
-    static const int nb1 = [] {
-        const char* e = getenv("RTM_CODED_NB1");
-        const int v = e ? atoi(e) : 4;
-        return v >= 4 ? 4 : v == 1 ? 1 : 2;
-    }();
-    static const bool pk = [] {  // packed 16-bit codes in the raster-free part (RTM_CODED_PK=0: one per register)
-        const char* e = getenv("RTM_CODED_PK");
-        return !(e && atoi(e) == 0);
-    }();
+    const size_t lsm = march ? CODED_ROW_LDS + sizeof(ZRecK) * (size_t)(sh.steps + 1) : 0;
+    constexpr int TR = CODED_TILE_ROWS;
     const int gx = (sh.W + 127) / 128, gy = (sh.H + TR - 1) / TR;
     dim3 g((unsigned)gx, (unsigned)gy, (unsigned)(fr ? n : 1));
     const bool inc = sh.tab.zmono >= 0;  // (no march: either instantiation is exact)
-    const int dg = diag_mode() & 8;       // per-wave phase timestamps only (no result change)
     const int4 org0 = make_int4(0, 0, TR, 0);
     // the split: workgroup tiles [bx0, bx1] x [by0, by1] meet some frame's box
     const int32_t bx_[4] = {sh.cull_x0, sh.cull_x1, sh.cull_y0, sh.cull_y1};
     const int32_t* b = box ? box : bx_;
     const bool raster = !(sh.flags & RTM_FLAG_NO_SHADOW_RASTER) && b[0] <= b[1] && b[2] <= b[3];
-    const int tr1 = TR * nb1;  // PART 1's tile height
     const int bx0 = raster ? std::max(b[0], 0) / 128 : 0, bx1 = raster ? std::min(b[1] / 128, gx - 1) : -1;
     const int by0 = raster ? std::max(b[2], 0) / TR : 0;
     const int by1 = raster ? std::min(std::max(b[3], 0) / TR, gy - 1) : -1;
-    // split only when the sphere tiles are a minority of the map (box ≤ 0.3 of the tiles;
-    // configs 2-4 split, config 5's 16 spheres span more: one launch there, measured as fast
-    // in the 4-lane frame and faster one-lane, profiles/r03_ab_coded_split.txt)
     const double box_frac = raster ? (double)std::max(bx1 - bx0 + 1, 0) * (double)std::max(by1 - by0 + 1, 0) /
                                          ((double)gx * (double)gy)
                                    : 0.0;
@@ -2706,31 +1991,22 @@ static void launch_coded(const ShadowPart& sh, const FrameArgs* a, double* smap,
         const char* e = getenv("RTM_CODED_SPLIT_MAX");
         return e ? atof(e) : 0.3;
     }();
-    const bool split = coded_split() && !dg && !eb && box_frac <= split_max;
+    const bool split = box_frac <= split_max;
     dim3 gb((unsigned)std::max(bx1 - bx0 + 1, 0), (unsigned)std::max(by1 - by0 + 1, 0), g.z);
-    dim3 g1((unsigned)gx, (unsigned)((sh.H + tr1 - 1) / tr1), g.z);
-    const int4 orgb = make_int4(bx0, by0, tr1, 0), org1 = make_int4(0, 0, tr1, 0);
-#define RTM_CK(I, M, E, P, G, O, NBV)                                                                          \
-    do {                                                                                                       \
-        if (fr) hipLaunchKernelGGL((shadow_coded_batch_kernel<I, M, NBV, false, E, P>), G, dim3(BLOCK), lsm, s, fr, dg, O); \
-        else hipLaunchKernelGGL((shadow_coded_kernel<I, M, NBV, false, E, P>), G, dim3(BLOCK), lsm, s, *a, smap, dg, O);    \
+    const int4 orgb = make_int4(bx0, by0, TR, 0);
+#define RTM_CK(I, M, P, G, O)                                                                                     \
+    do {                                                                                                        \
+        if (fr) hipLaunchKernelGGL((shadow_coded_batch_kernel<I, M, P>), G, dim3(BLOCK), lsm, s, fr, O);          \
+        else hipLaunchKernelGGL((shadow_coded_kernel<I, M, P>), G, dim3(BLOCK), lsm, s, *a, smap, O);            \
     } while (0)
-#define RTM_CKP(I, M, G, O, NBV)                                                                                \
-    do {                                                                                                       \
-        if (fr) hipLaunchKernelGGL((shadow_coded_batch_kernel<I, M, NBV, false, false, 1, true>), G, dim3(BLOCK), lsm, s, fr, dg, O); \
-        else hipLaunchKernelGGL((shadow_coded_kernel<I, M, NBV, false, false, 1, true>), G, dim3(BLOCK), lsm, s, *a, smap, dg, O);    \
-    } while (0)
-#define RTM_CKB(I, M)                                                          \
-    do {                                                                       \
-        if (split) {                                                           \
-            if (gb.x > 0 && gb.y > 0) RTM_CK(I, M, false, 2, gb, orgb, 1);     \
-            if (pk && nb1 == 4) RTM_CKP(I, M, g1, org1, 4);                      \
-            else if (pk && nb1 == 2) RTM_CKP(I, M, g1, org1, 2);                 \
-            else if (nb1 == 4) RTM_CK(I, M, false, 1, g1, org1, 4);            \
-            else if (nb1 == 2) RTM_CK(I, M, false, 1, g1, org1, 2);                 \
-            else RTM_CK(I, M, false, 1, g1, org1, 1);                          \
-        } else if (eb) RTM_CK(I, M, true, 0, g, org0, 1);                      \
-        else RTM_CK(I, M, false, 0, g, org0, 1);                               \
+#define RTM_CKB(I, M)                                           \
+    do {                                                        \
+        if (split) {                                            \
+            if (gb.x > 0 && gb.y > 0) RTM_CK(I, M, 2, gb, orgb); \
+            RTM_CK(I, M, 1, g, org0);                           \
+        } else {                                                \
+            RTM_CK(I, M, 0, g, org0);                           \
+        }                                                       \
     } while (0)
     if (sh.smap_fmt == SMAP_U8) {
         if (inc) RTM_CKB(true, SMAP_U8);
@@ -2740,74 +2016,13 @@ static void launch_coded(const ShadowPart& sh, const FrameArgs* a, double* smap,
         else RTM_CKB(false, SMAP_U16);
     }
 #undef RTM_CKB
-#undef RTM_CKP
 #undef RTM_CK
-}
-
-template <int NR>
-static void launch_sep(const FrameArgs& a, double* smap, hipStream_t s) {
-    dim3 g((unsigned)((a.sh.W + TILE_X - 1) / TILE_X), (unsigned)((a.sh.H + TILE_Y * NR - 1) / (TILE_Y * NR)));
-    const int mode = sep_mode(a.sh);
-    // LDS-staged table for the search (RTM_SEP_LDS=0 disables it for A/B runs)
-    static const bool lds_on = [] {
-        const char* e = getenv("RTM_SEP_LDS");
-        return !e || atoi(e) != 0;
-    }();
-    const bool march = !(a.sh.flags & RTM_FLAG_NO_MARCH) && a.sh.n_patches > 0 && a.sh.steps > 0;
-    const int lds = (mode == MARCH_SEARCH && lds_on && march && a.sh.steps <= SEARCH_LDS_MAX_STEPS) ? 1 : 0;
-    const size_t smem = lds ? sizeof(double2) * (size_t)(a.sh.steps + 1) : 0;
-    if (mode == MARCH_LEAN2) {
-        const size_t lsm = march ? sizeof(double2) * (size_t)(a.sh.steps + 1) : 0;
-        const int cw = lean_cols();
-        const int tw = TILE_X * cw;
-        dim3 g2((unsigned)((a.sh.W + tw - 1) / tw), g.y);
-        const bool inc = a.sh.tab.zmono >= 0;  // (no march: either instantiation is exact)
-        // one register-held table entry per thread when the table fits one per thread
-        const bool fill1 = lean_fill1() && a.sh.steps + 1 <= BLOCK;
-        const int hot = lean_hot() ? 1 : 0;
-#define RTM_L2(C, I, F) \
-    hipLaunchKernelGGL((shadow_lean2_kernel<NR, C, I, F>), g2, dim3(BLOCK), lsm, s, a, smap, diag_mode(), hot)
-#define RTM_L2C(I, F, M) \
-    hipLaunchKernelGGL((shadow_lean2_kernel<4, 2, I, F, M>), g2, dim3(BLOCK), lsm, s, a, smap, diag_mode(), hot)
-        const int code = a.sh.smap_fmt;
-        if (NR == 4 && cw == 2 && code != SMAP_F64 && coded_ok(a.sh)) {
-            launch_coded(a.sh, &a, smap, nullptr, 1, s);
-        } else if (NR == 4 && cw == 2 && code != SMAP_F64) {  // coded map (shadow_map_format)
-            if (code == SMAP_U8) {
-                if (fill1) { if (inc) RTM_L2C(true, 1, SMAP_U8); else RTM_L2C(false, 1, SMAP_U8); }
-                else { if (inc) RTM_L2C(true, 4, SMAP_U8); else RTM_L2C(false, 4, SMAP_U8); }
-            } else {
-                if (fill1) { if (inc) RTM_L2C(true, 1, SMAP_U16); else RTM_L2C(false, 1, SMAP_U16); }
-                else { if (inc) RTM_L2C(true, 4, SMAP_U16); else RTM_L2C(false, 4, SMAP_U16); }
-            }
-        } else if (cw == 2 && fill1) {
-            if (inc) RTM_L2(2, true, 1);
-            else RTM_L2(2, false, 1);
-        } else if (cw == 2) {
-            if (inc) RTM_L2(2, true, 4);
-            else RTM_L2(2, false, 4);
-        } else {
-            if (inc) RTM_L2(1, true, 4);
-            else RTM_L2(1, false, 4);
-        }
-#undef RTM_L2
-#undef RTM_L2C
-    } else if (mode == MARCH_SEARCH)
-        hipLaunchKernelGGL((shadow_sep_kernel<NR, MARCH_SEARCH>), g, dim3(BLOCK), smem, s, a, smap, diag_mode(), lds);
-    else if (mode == MARCH_CMP)
-        hipLaunchKernelGGL((shadow_sep_kernel<NR, MARCH_CMP>), g, dim3(BLOCK), 0, s, a, smap, diag_mode(), 0);
-    else
-        hipLaunchKernelGGL((shadow_sep_kernel<NR, MARCH_SIGN>), g, dim3(BLOCK), 0, s, a, smap, diag_mode(), 0);
 }
 
 int launch_shadow_pass(const FrameArgs& a, double* smap, void* stream, StatsK* stats) {
     hipStream_t s = (hipStream_t)stream;
-    if (!stats && use_sep(a.sh)) {
-        const int nr = sep_rows();
-        if (nr == 1) launch_sep<1>(a, smap, s);
-        else if (nr == 2) launch_sep<2>(a, smap, s);
-        else if (nr == 8) launch_sep<8>(a, smap, s);
-        else launch_sep<4>(a, smap, s);
+    if (!stats && coded_ok(a.sh)) {
+        launch_coded(a.sh, &a, smap, nullptr, 1, s);
         return launched();
     }
     if (stats)
@@ -2817,81 +2032,55 @@ int launch_shadow_pass(const FrameArgs& a, double* smap, void* stream, StatsK* s
     return launched();
 }
 
-// Eye pass store/shape mode (RTM_EYE_MODE, for A/B runs): bit 0 = 256 x 1
-// workgroups instead of 64 x 4 (measured neutral), bit 1 = non-temporal frame
-// stores (default: the frame is not re-read, and at 7680x4320 its 531 MB would
-// otherwise evict the shadow map the pass gathers from: eye 120 -> 85 us).
-static int eye_wide() {
-    static int v = [] {
-        const char* e = getenv("RTM_EYE_MODE");
-        return e ? atoi(e) : 2;
-    }();
-    return v;
-}
-
-// The SDF eye kernel at >= 5 waves per SIMD (default; RTM_SDF_WPE=0 for the
-// compiler's 99-VGPR, 4-wave allocation in A/B runs; 6 spills 44 VGPRs, 8 runs 1.6x slower).
-static bool sdf_wpe5() {
-    static bool v = [] {
-        const char* e = getenv("RTM_SDF_WPE");
-        return !(e && atoi(e) == 0);
-    }();
-    return v;
-}
-
-// The sphere-only eye pass at 8 waves/SIMD (default; RTM_EYE_WPE8=0: the compiler's allocation)
-static bool eye_wpe8() {
-    static bool v = [] {
-        const char* e = getenv("RTM_EYE_WPE8");
-        return !(e && atoi(e) == 0);
-    }();
-    return v;
-}
-
-// Eye kernels without the shadow lookup for all-+INF shadow viewports (default;
-// RTM_EYE_NOSH=0: the fused kernels, for A/B runs)
-static bool eye_nosh() {
-    static const bool v = [] {
-        const char* e = getenv("RTM_EYE_NOSH");
-        return !(e && atoi(e) == 0);
-    }();
-    return v;
-}
-
+// Eye kernel of one frame (or of a batch: FR != nullptr, n frames, every frame with
+// frame 0's shapes, flags, tables and variant):
+//   * an all-+INF shadow viewport (fused, no shadow raster, no march; rtm_api.cpp
+//     trivial_shadow): NOSH, no lookup at all (lit = +INF > qz, the fused texel's value);
+//   * SDFs (row f-4) on the materialised map or NOSH: the SDF kernel held to 5 waves
+//     per SIMD (95 VGPRs, no spill: eye 582 -> 565 us at config 8); fused: RT 2;
+//   * ray-traced primitives under a PERSPECTIVE eye (row f-1): RT 3 (host-hoisted
+//     origin terms, per-wave primitive masks); other ray-traced frames and PERSPECTIVE
+//     spheres (row f-3): RT 1;
+//   * spheres only on the materialised map: one frame held to 8 waves per SIMD
+//     (eye_pass8_kernel); batched, the compiler's allocation (the headline kernel).
 template <int FMT>
 static void launch_eye_fmt(const FrameArgs& a, const double* smap, void* o, hipStream_t s, dim3 g, bool fused,
-                           const DevTabs& tabs, int wide) {
-#define RTM_EYE(F, R) \
-    hipLaunchKernelGGL((eye_pass_kernel<F, false, R, FMT>), g, dim3(BLOCK), 0, s, a, smap, o, nullptr, tabs, wide)
-#define RTM_EYEN(R) \
-    hipLaunchKernelGGL((eye_pass_kernel<false, false, R, FMT, true>), g, dim3(BLOCK), 0, s, a, smap, o, nullptr, tabs, wide)
+                           const DevTabs& tabs, CBatch* fr) {
+#define RTM_EYE(F, R, N)                                                                                           \
+    do {                                                                                                        \
+        if (fr) hipLaunchKernelGGL((eye_batch_kernel<F, R, FMT, N>), g, dim3(BLOCK), 0, s, fr);                  \
+        else hipLaunchKernelGGL((eye_pass_kernel<F, false, R, FMT, N>), g, dim3(BLOCK), 0, s, a, smap, o, nullptr, tabs); \
+    } while (0)
+#define RTM_EYE_SDF(N)                                                                                              \
+    do {                                                                                                        \
+        if (fr) hipLaunchKernelGGL((eye_sdf_batch_kernel<5, FMT, N>), g, dim3(BLOCK), 0, s, fr);                 \
+        else hipLaunchKernelGGL((eye_sdf_kernel<5, FMT, N>), g, dim3(BLOCK), 0, s, a, smap, o, tabs);            \
+    } while (0)
     const int both = RTM_FLAG_NO_MARCH | RTM_FLAG_NO_SHADOW_RASTER;
-    const bool nosh = fused && (a.sh.flags & both) == both && eye_nosh();  // (see launch_eye_batch)
+    const bool nosh = fused && (a.sh.flags & both) == both;
+    const int rt = tabs.sdf ? 2 : (tabs.rt && tabs.rt_persp) ? 3 : (tabs.rt || tabs.psp) ? 1 : 0;
     if (nosh) {
-        if (tabs.sdf) {
-            if (sdf_wpe5()) hipLaunchKernelGGL((eye_sdf_kernel<5, FMT, true>), g, dim3(BLOCK), 0, s, a, smap, o, tabs, wide);
-            else RTM_EYEN(2);
-        } else if (tabs.rt && tabs.rt_persp) RTM_EYEN(3);
-        else if (tabs.rt || tabs.psp) RTM_EYEN(1);
-        else RTM_EYEN(0);
-    } else if (tabs.sdf) {
-        if (fused) RTM_EYE(true, 2);
-        else if (sdf_wpe5())  // 95 VGPRs, 5 waves/SIMD, no spill: eye 582 -> 565 us at config 8
-            hipLaunchKernelGGL((eye_sdf_kernel<5, FMT>), g, dim3(BLOCK), 0, s, a, smap, o, tabs, wide);
-        else RTM_EYE(false, 2);
-    } else if (tabs.rt && tabs.rt_persp) {
-        if (fused) RTM_EYE(true, 3);
-        else RTM_EYE(false, 3);
-    } else if (tabs.rt || tabs.psp) {
-        if (fused) RTM_EYE(true, 1);
-        else RTM_EYE(false, 1);
+        if (rt == 2) RTM_EYE_SDF(true);
+        else if (rt == 3) RTM_EYE(false, 3, true);
+        else if (rt == 1) RTM_EYE(false, 1, true);
+        else RTM_EYE(false, 0, true);
+    } else if (rt == 2) {
+        if (fused) RTM_EYE(true, 2, false);
+        else RTM_EYE_SDF(false);
+    } else if (rt == 3) {
+        if (fused) RTM_EYE(true, 3, false);
+        else RTM_EYE(false, 3, false);
+    } else if (rt == 1) {
+        if (fused) RTM_EYE(true, 1, false);
+        else RTM_EYE(false, 1, false);
+    } else if (fused) {
+        RTM_EYE(true, 0, false);
+    } else if (fr) {
+        RTM_EYE(false, 0, false);
     } else {
-        if (fused) RTM_EYE(true, 0);
-        else if (eye_wpe8())
-            hipLaunchKernelGGL((eye_pass8_kernel<FMT>), g, dim3(BLOCK), 0, s, a, smap, o, tabs, wide);
-        else RTM_EYE(false, 0);
+        hipLaunchKernelGGL((eye_pass8_kernel<FMT>), g, dim3(BLOCK), 0, s, a, smap, o, tabs);
     }
-#undef RTM_EYEN
+#undef RTM_EYE_SDF
 #undef RTM_EYE
 }
 
@@ -2899,19 +2088,13 @@ int launch_eye_pass(const FrameArgs& a, const double* smap, void* out, void* str
                     const DevTabs& tabs) {
     hipStream_t s = (hipStream_t)stream;
     const int rows = a.ey.row_end - a.ey.row_begin;
-    const int wide = eye_wide();
-    dim3 g = (wide & 1) ? dim3((unsigned)((a.ey.W + BLOCK - 1) / BLOCK), (unsigned)rows) : grid_for(a.ey.W, rows);
+    dim3 g = grid_for(a.ey.W, rows);
     const bool fused = (a.ey.flags & RTM_FLAG_FUSED_SHADOW) != 0;
     const int fmt = tabs.fmt & FMT_MASK;
-    if (diag_eye() && fmt == RTM_FORMAT_RGBA32F) {
-        hipLaunchKernelGGL(eye_store_only_kernel, g, dim3(BLOCK), 0, s, a, reinterpret_cast<float4*>(out), wide);
-        return launched();
-    }
     if (stats) {  // counting kernels: RGBA f32 output only
         if (fmt != RTM_FORMAT_RGBA32F) return RTM_ERR_INVALID;
 #define RTM_EYE(F, R) \
-    hipLaunchKernelGGL((eye_pass_kernel<F, true, R, RTM_FORMAT_RGBA32F>), g, dim3(BLOCK), 0, s, a, smap, out, stats, \
-                       tabs, wide)
+    hipLaunchKernelGGL((eye_pass_kernel<F, true, R, RTM_FORMAT_RGBA32F>), g, dim3(BLOCK), 0, s, a, smap, out, stats, tabs)
         const int rt = tabs.sdf ? 2 : (tabs.rt || tabs.psp) ? 1 : 0;
         if (rt == 2) {
             if (fused) RTM_EYE(true, 2);
@@ -2927,20 +2110,18 @@ int launch_eye_pass(const FrameArgs& a, const double* smap, void* out, void* str
         return launched();
     }
     DevTabs t = tabs;
-    if (t.rt && t.rt_persp && !t.sdf) {
+    if (t.rt && t.rt_persp && !t.sdf && t.rtmask) {
         // the per-wave primitive masks (RT 3): one thread per wave of the eye pass
-        if (t.rtmask && !(wide & 4)) {
-            const int n = ((a.ey.W + TILE_X - 1) / TILE_X) * rows;
-            hipLaunchKernelGGL(rt_cull_kernel, dim3((unsigned)((n + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, s, a.ey.eye,
-                               t.rt, a.ey.W, a.ey.H, a.ey.row_begin, rows,
-                               make_int4(a.ey.stripe_rows, a.ey.stripe_stride, a.ey.stripe_phase, 0), t.rtmask);
-        } else {
-            t.rtmask = nullptr;
-        }
+        const int n = ((a.ey.W + TILE_X - 1) / TILE_X) * rows;
+        hipLaunchKernelGGL(rt_cull_kernel, dim3((unsigned)((n + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, s, a.ey.eye,
+                           t.rt, a.ey.W, a.ey.H, a.ey.row_begin, rows,
+                           make_int4(a.ey.stripe_rows, a.ey.stripe_stride, a.ey.stripe_phase, 0), t.rtmask);
+    } else {
+        t.rtmask = nullptr;
     }
-    if (fmt == RTM_FORMAT_RGBA8) launch_eye_fmt<RTM_FORMAT_RGBA8>(a, smap, out, s, g, fused, t, wide);
-    else if (fmt == RTM_FORMAT_RGB8) launch_eye_fmt<RTM_FORMAT_RGB8>(a, smap, out, s, g, fused, t, wide);
-    else launch_eye_fmt<RTM_FORMAT_RGBA32F>(a, smap, out, s, g, fused, t, wide);
+    if (fmt == RTM_FORMAT_RGBA8) launch_eye_fmt<RTM_FORMAT_RGBA8>(a, smap, out, s, g, fused, t, nullptr);
+    else if (fmt == RTM_FORMAT_RGB8) launch_eye_fmt<RTM_FORMAT_RGB8>(a, smap, out, s, g, fused, t, nullptr);
+    else launch_eye_fmt<RTM_FORMAT_RGBA32F>(a, smap, out, s, g, fused, t, nullptr);
     return launched();
 }
 
@@ -2948,50 +2129,26 @@ int launch_shadow_batch(const BatchFrame* dev, int n, const FrameArgs& a0, void*
     hipStream_t s = (hipStream_t)stream;
     CBatch* fr = (CBatch*)dev;
     const ShadowPart& sh = a0.sh;
-    if (use_sep(sh) && sep_mode(sh) == MARCH_LEAN2 && sep_rows() == 4 && lean_cols() == 2 && coded_ok(sh)) {
+    if (coded_ok(sh)) {
         launch_coded(sh, nullptr, nullptr, fr, n, s, box);
         return launched();
     }
-    if (use_sep(sh) && sep_mode(sh) == MARCH_LEAN2 && sep_rows() == 4 && lean_cols() == 2) {
-        const bool march = !(sh.flags & RTM_FLAG_NO_MARCH) && sh.n_patches > 0 && sh.steps > 0;
-        const size_t lsm = march ? sizeof(double2) * (size_t)(sh.steps + 1) : 0;
-        dim3 g((unsigned)((sh.W + 2 * TILE_X - 1) / (2 * TILE_X)), (unsigned)((sh.H + TILE_Y * 4 - 1) / (TILE_Y * 4)),
-               (unsigned)n);
-        const bool inc = sh.tab.zmono >= 0;
-        const bool fill1 = lean_fill1() && sh.steps + 1 <= BLOCK;
-        const int hot = lean_hot() ? 1 : 0;
-#define RTM_LB(I, F, M) \
-    hipLaunchKernelGGL((shadow_lean2_batch_kernel<4, 2, I, F, M>), g, dim3(BLOCK), lsm, s, fr, diag_mode(), hot)
-#define RTM_LBM(M)                                              \
-    do {                                                        \
-        if (fill1) { if (inc) RTM_LB(true, 1, M); else RTM_LB(false, 1, M); } \
-        else { if (inc) RTM_LB(true, 4, M); else RTM_LB(false, 4, M); }       \
-    } while (0)
-        if (sh.smap_fmt == SMAP_U8) RTM_LBM(SMAP_U8);
-        else if (sh.smap_fmt == SMAP_U16) RTM_LBM(SMAP_U16);
-        else RTM_LBM(SMAP_F64);
-#undef RTM_LBM
-#undef RTM_LB
-        return launched();
-    }
-    if (use_sep(sh)) return RTM_ERR_UNSUPPORTED;  // A/B-only shadow modes: the caller renders frame by frame
     dim3 g = grid_for(sh.W, sh.H);
     g.z = (unsigned)n;
     hipLaunchKernelGGL(shadow_pass_batch_kernel, g, dim3(BLOCK), 0, s, fr);
     return launched();
 }
 
-// The shadow map's storage for these arguments (rtm_kernels.h): coded when the
-// default lean tile (4 rows x 2 columns per lane) or the generic tile writes it and
-// every code fits (steps + n_spheres codes plus +INF); f64 for the A/B-only
-// separable modes, and with RTM_SMAP=f64 (A/B runs: the 8-byte map).
+// The shadow map's storage for these arguments (rtm_kernels.h): coded when every code
+// fits (steps + n_spheres codes plus +INF) -- the coded tile and the generic tile both
+// write codes -- else f64; RTM_SMAP=f64 forces the 8-byte map (tests/test_smap_codes.py:
+// the generic tile's f64 map must give the same image).
 int32_t shadow_map_format(const ShadowPart& sh) {
     static const bool f64_env = [] {
         const char* e = getenv("RTM_SMAP");
         return e && (std::string(e) == "f64" || std::string(e) == "0");
     }();
     if (f64_env) return SMAP_F64;
-    if (use_sep(sh) && !(sep_mode(sh) == MARCH_LEAN2 && sep_rows() == 4 && lean_cols() == 2)) return SMAP_F64;
     const int64_t codes = (int64_t)sh.steps + sh.n_spheres;  // + the all-ones +INF code
     if (codes <= 254) return SMAP_U8;
     if (codes <= 65534 && sh.tab.t) return SMAP_U16;
@@ -3012,54 +2169,23 @@ int launch_smap_decode(const ShadowPart& sh, const void* codes, double* out, voi
     return launched();
 }
 
-// Can a batch take the batched shadow kernels (the lean tile or the generic one)?
-bool shadow_batchable(const ShadowPart& sh) {
-    return !use_sep(sh) || (sep_mode(sh) == MARCH_LEAN2 && sep_rows() == 4 && lean_cols() == 2);
-}
-
-bool eye_wave_cull_on() { return !(eye_wide() & 4); }
-
-
 int launch_eye_batch(const BatchFrame* dev, int n, const FrameArgs& a0, const DevTabs& t0, void* stream) {
     hipStream_t s = (hipStream_t)stream;
     CBatch* fr = (CBatch*)dev;
     const int rows = a0.ey.row_end - a0.ey.row_begin;
-    const int wide = eye_wide();
     if (t0.rtmask) {  // the batch's per-wave primitive masks first (RT 3)
         const int nw = ((a0.ey.W + TILE_X - 1) / TILE_X) * rows;
         hipLaunchKernelGGL(rt_cull_batch_kernel, dim3((unsigned)((nw + BLOCK - 1) / BLOCK), 1, (unsigned)n),
                            dim3(BLOCK), 0, s, fr);
         if (launched()) return RTM_ERR_HIP;
     }
-    dim3 g = (wide & 1) ? dim3((unsigned)((a0.ey.W + BLOCK - 1) / BLOCK), (unsigned)rows) : grid_for(a0.ey.W, rows);
+    dim3 g = grid_for(a0.ey.W, rows);
     g.z = (unsigned)n;
     const bool fused = (a0.ey.flags & RTM_FLAG_FUSED_SHADOW) != 0;
     const int fmt = t0.fmt & FMT_MASK;
-    const int rt = t0.sdf ? 2 : (t0.rt && t0.rt_persp) ? 3 : (t0.rt || t0.psp) ? 1 : 0;
-    // an all-+INF shadow viewport (fused, no shadow raster, no march): no lookup at all
-    const int both = RTM_FLAG_NO_MARCH | RTM_FLAG_NO_SHADOW_RASTER;
-    const bool nosh = fused && (a0.sh.flags & both) == both && eye_nosh();
-#define RTM_EB(F, R, M) hipLaunchKernelGGL((eye_batch_kernel<F, R, M>), g, dim3(BLOCK), 0, s, fr, wide)
-#define RTM_EBN(R, M) hipLaunchKernelGGL((eye_batch_kernel<false, R, M, true>), g, dim3(BLOCK), 0, s, fr, wide)
-#define RTM_EBF(M)                                                                           \
-    do {                                                                                     \
-        if (rt == 2 && nosh && sdf_wpe5())                                                   \
-            hipLaunchKernelGGL((eye_sdf_batch_kernel<5, M, true>), g, dim3(BLOCK), 0, s, fr, wide); \
-        else if (nosh) { if (rt == 3) RTM_EBN(3, M); else if (rt == 1) RTM_EBN(1, M);          \
-                         else if (rt == 2) RTM_EBN(2, M); else RTM_EBN(0, M); }                \
-        else if (rt == 2 && !fused && sdf_wpe5())                                            \
-            hipLaunchKernelGGL((eye_sdf_batch_kernel<5, M>), g, dim3(BLOCK), 0, s, fr, wide); \
-        else if (rt == 2) { if (fused) RTM_EB(true, 2, M); else RTM_EB(false, 2, M); }      \
-        else if (rt == 3) { if (fused) RTM_EB(true, 3, M); else RTM_EB(false, 3, M); }      \
-        else if (rt == 1) { if (fused) RTM_EB(true, 1, M); else RTM_EB(false, 1, M); }      \
-        else { if (fused) RTM_EB(true, 0, M); else RTM_EB(false, 0, M); }                   \
-    } while (0)
-    if (fmt == RTM_FORMAT_RGBA8) RTM_EBF(RTM_FORMAT_RGBA8);
-    else if (fmt == RTM_FORMAT_RGB8) RTM_EBF(RTM_FORMAT_RGB8);
-    else RTM_EBF(RTM_FORMAT_RGBA32F);
-#undef RTM_EBF
-#undef RTM_EBN
-#undef RTM_EB
+    if (fmt == RTM_FORMAT_RGBA8) launch_eye_fmt<RTM_FORMAT_RGBA8>(a0, nullptr, nullptr, s, g, fused, t0, fr);
+    else if (fmt == RTM_FORMAT_RGB8) launch_eye_fmt<RTM_FORMAT_RGB8>(a0, nullptr, nullptr, s, g, fused, t0, fr);
+    else launch_eye_fmt<RTM_FORMAT_RGBA32F>(a0, nullptr, nullptr, s, g, fused, t0, fr);
     return launched();
 }
 
@@ -3087,48 +2213,6 @@ int launch_upload(const void* src, size_t bytes, void* dst, void* stream) {
     return 0;
 }
 
-}  // namespace rtm
-
-extern "C" int rtm_diag_shadow_phases(unsigned long long* out, int n) {
-    if (n > (1 << 18)) n = 1 << 18;
-    return hipMemcpyFromSymbol(out, HIP_SYMBOL(rtm::g_phase), sizeof(unsigned long long) * (size_t)n) == hipSuccess
-               ? 0
-               : -1;
-}
-
-namespace rtm {
-
-
-template <int KIND, int NR, bool INC>
-static void launch_pipe(const FrameArgs& a, double* smap_w, const double* smap_r, float4* out, hipStream_t s) {
-    const int tw = TILE_X * (KIND == 2 ? 2 : 1);
-    const int sh_gx = (a.sh.W + tw - 1) / tw;
-    const int sh_gy = (a.sh.H + TILE_Y * NR - 1) / (TILE_Y * NR);
-    const int eye_gx = (a.ey.W + TILE_X - 1) / TILE_X;
-    const int eye_gy = (a.ey.row_end - a.ey.row_begin + TILE_Y - 1) / TILE_Y;
-    const int n_sh = sh_gx * sh_gy, n_eye = eye_gx * eye_gy;
-    const bool march = !(a.sh.flags & RTM_FLAG_NO_MARCH) && a.sh.n_patches > 0 && a.sh.steps > 0;
-    const size_t smem = (KIND == 2 && march) ? sizeof(double2) * (size_t)(a.sh.steps + 1) : 0;
-    hipLaunchKernelGGL((frame_pipe_kernel<KIND, NR, INC>), dim3((unsigned)(n_sh + n_eye)), dim3(BLOCK), smem, s, a,
-                       smap_w, smap_r, out, sh_gx, n_sh, eye_gx, n_eye);
-}
-
-int launch_frame_pipe(const FrameArgs& a, double* smap_w, const double* smap_r, float* out, void* stream) {
-    hipStream_t s = (hipStream_t)stream;
-    float4* o = reinterpret_cast<float4*>(out);
-    if (use_sep(a.sh)) {
-        const int mode = sep_mode(a.sh);
-        if (mode == MARCH_LEAN2) {
-            if (a.sh.tab.zmono >= 0) launch_pipe<2, 4, true>(a, smap_w, smap_r, o, s);
-            else launch_pipe<2, 4, false>(a, smap_w, smap_r, o, s);
-        } else {
-            launch_pipe<1, 4, true>(a, smap_w, smap_r, o, s);
-        }
-    } else {
-        launch_pipe<0, 1, true>(a, smap_w, smap_r, o, s);
-    }
-    return launched();
-}
 
 int launch_vp_rasterize(const RasterArgs& a, double* zbuf, double* gh, double* gz, int32_t* gid, void* stream) {
     hipLaunchKernelGGL(vp_rasterize_kernel, grid_for(a.W, a.H), dim3(BLOCK), 0, (hipStream_t)stream, a, zbuf, gh,

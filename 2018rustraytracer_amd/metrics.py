@@ -134,9 +134,7 @@ def frame_work(stats: dict, width: int, height: int, n_spheres: int, n_patches: 
     sh_bytes = 0 if fused else map_texel_bytes * px
     eye_bytes = 16 * px + (0 if fused else map_texel_bytes * stats["eye_hit_pixels"])
     return dict(shadow_pass=dict(ops=sh_ops, bytes=sh_bytes),
-                eye_pass=dict(ops=eye_ops + (sh_ops if fused else 0), bytes=eye_bytes),
-                # software-pipelined launch: shadow pass of frame i + eye pass of frame i-1
-                frame_pipe=dict(ops=sh_ops + eye_ops, bytes=sh_bytes + eye_bytes))
+                eye_pass=dict(ops=eye_ops + (sh_ops if fused else 0), bytes=eye_bytes))
 
 
 def roofline(kernel: str, work: dict, ms: float, traffic_bytes=None) -> dict:

@@ -145,7 +145,7 @@ class Context:
 
     def render_frames_async(self, scenes, eye: Camera, shadow: Camera, width: int, height: int, steps: int,
                             flags: int, out_ptrs, prepared=None):
-        """Enqueue len(scenes) frames (software-pipelined when the patches agree);
+        """Enqueue len(scenes) frames (batched and spread over the context's lanes);
         frame i goes to device pointer out_ptrs[i]."""
         arr, keep = prepared if prepared is not None else self.prepare_frames(scenes)  # scenes unused if prepared
         n = len(arr)

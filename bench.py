@@ -480,17 +480,15 @@ def main():
     # batches of 2-8 frames on 2-3 lanes; 25 GB at 7680x4320, of 288 GB), 128 below
     # (batches of up to 64 frames on 2 lanes)
     lanes_env = int(os.environ.get("RTM_LANES", "0") or 0)
-    batch_env = int(os.environ.get("RTM_BATCH", "0") or 0)
     n_ring = 48 if W * H >= (4 << 20) else 128
     # the library's auto rules (rtm_api.cpp frame_lanes / frame_batch), for overrides of one
     lanes_auto = 3 if W * H >= (16 << 20) else 4
-    batch_auto = max(1, min(64 if W * H < (1 << 20) else 16, (64 << 20) // (W * H)))
-    m = (lanes_env if lanes_env > 0 else lanes_auto) * (batch_env if batch_env > 0 else batch_auto)
+    batch_auto = max(1, min(64 if W * H < (1 << 20) else 32, (64 << 20) // (W * H)))
+    m = (lanes_env if lanes_env > 0 else lanes_auto) * batch_auto
     n_ring = n_ring if n_ring % m == 0 else m * ((n_ring + m - 1) // m)
     ring = ([torch.empty((H, W, 4), dtype=torch.float32, device=f"cuda:{local}") for _ in range(n_ring)]
             if not tile_mode else [])
     sequence = not tile_mode and not a.per_frame_calls
-    pipelined = sequence and os.environ.get("RTM_PIPELINE", "0") not in ("", "0")
 
     import ctypes as C
     e_c, s_c = eye.to_c(), shadow.to_c()
@@ -502,7 +500,7 @@ def main():
 
     if sequence:
         # the whole timed region is ONE rtm_render_frames_async call over the animation
-        # frames (two kernels per frame; with RTM_PIPELINE=1 the software-pipelined launch)
+        # frames (two kernels per frame or per batch of frames)
         warm = ctx.prepare_frames(scenes[:nW])
         timed = ctx.prepare_frames(scenes[nW:])
         outp = [ring[i % n_ring].data_ptr() for i in range(max(nW, nS, 1))]
@@ -560,10 +558,10 @@ def main():
     # A frame without shadow raster and march (config 7, main()'s scene) has an all-+INF
     # shadow viewport: the library runs no shadow pass and its eye pass evaluates the
     # +INF texels on demand (rtm_api.cpp trivial_shadow), i.e. the fused frame's work
-    trivial = (flags & 3) == 3 and not fused and os.environ.get("RTM_TRIVIAL_SHADOW", "1") != "0"
+    trivial = (flags & 3) == 3 and not fused
     map_bytes = ctx.shadow_map_texel_bytes() or 8
     # per-kernel HIP-event durations over the timed region (ctx stream)
-    n_launches = nS + 1 if pipelined else nS
+    n_launches = nS
     sh_ms, eye_ms = ctx.kernel_ms_history((n_launches + timing_stride - 1) // timing_stride)
     if tile_mode:  # the group's own contexts ran the bands: one timed pass of rank 0's band on ctx
         ctx.set_timing_capacity(1)
@@ -625,7 +623,7 @@ def main():
     # texels the eye pass looks up instead of materialising the whole shadow map.
     # Bit-identical image (tests/test_gpu_parity.py::test_fused_shadow_identical).
     alt_fused = None
-    if sequence and not pipelined and not a.no_alt and not fused and not trivial:
+    if sequence and not a.no_alt and not fused and not trivial:
         fflags = flags | rtm.abi.RTM_FLAG_FUSED_SHADOW
         ctx.set_timing_capacity(max(1, nS // timing_stride))
         ctx.render_frames_async([0] * min(nW, F), eye, shadow, W, H, K, fflags, outp[:min(nW, F)],
@@ -645,16 +643,8 @@ def main():
                      "note": "RTM_FLAG_FUSED_SHADOW (shadow texels evaluated on demand in the eye pass, "
                              "bit-identical image); secondary measurement, not the headline value"}
 
-    pipe_ms = None
-    if pipelined:
-        # sampled launches j = 0, stride, 2*stride, ...: j = 0 is the prologue shadow pass,
-        # j = steps (if sampled) the epilogue eye pass; the rest are pipelined frame launches
-        pipe = eye_ms[1:-1] if nS % timing_stride == 0 else eye_ms[1:]
-        pipe_ms = sum(pipe) / max(len(pipe), 1)
-        avg_sh, avg_eye = sh_ms[0], 0.0
-    else:
-        avg_sh = sum(sh_ms) / max(len(sh_ms), 1)
-        avg_eye = sum(eye_ms) / max(len(eye_ms), 1)
+    avg_sh = sum(sh_ms) / max(len(sh_ms), 1)
+    avg_eye = sum(eye_ms) / max(len(eye_ms), 1)
 
     res = None
     if rank == 0:
@@ -670,7 +660,7 @@ def main():
                                       sep=sep, n_planes=len(s0.circlePlanePrimitives),
                                       n_cyls=len(s0.cappedCylinderPrimitives),
                                       perspective=eye.type_ == sc.PERSPECTIVE,
-                                      search=sep and os.environ.get("RTM_SEP_MODE", "2") == "2",
+                                      search=sep,
                                       n_sdfs=len(s0.sdfPrimitives), map_texel_bytes=map_bytes,
                                       moving=(shadow.dirNormalized[0] * 0.03 != 0.0
                                               or shadow.dirNormalized[1] * 0.03 != 0.0))
@@ -709,17 +699,12 @@ def main():
             r["pmc"] = pmc_fractions(a.config, kernel, fpl, work_l[kernel]["ops"])
             return r
 
-        if pipelined:
-            dom, dom_ms = "frame_pipe", pipe_ms
-            roof = metrics.roofline(dom, work, dom_ms, _latest_traffic(a.config, dom))
-            roof_other = None
-        else:
-            dom = "eye_pass" if (fused or trivial or avg_eye >= avg_sh) else "shadow_pass"
-            dom_ms = avg_eye if dom == "eye_pass" else avg_sh
-            roof = kroof(dom, dom_ms)
-            other = "shadow_pass" if dom == "eye_pass" else "eye_pass"
-            other_ms = avg_sh if other == "shadow_pass" else avg_eye
-            roof_other = kroof(other, other_ms) if other_ms > 0 and not trivial else None
+        dom = "eye_pass" if (fused or trivial or avg_eye >= avg_sh) else "shadow_pass"
+        dom_ms = avg_eye if dom == "eye_pass" else avg_sh
+        roof = kroof(dom, dom_ms)
+        other = "shadow_pass" if dom == "eye_pass" else "eye_pass"
+        other_ms = avg_sh if other == "shadow_pass" else avg_eye
+        roof_other = kroof(other, other_ms) if other_ms > 0 and not trivial else None
         res = {
             "metric": cfg.get("metric", METRIC if a.config <= 5 else METRIC_F1 if a.config <= 7 else METRIC_F4),
             "value": round(value, 2),
@@ -742,15 +727,11 @@ def main():
             "config": {"workload": cfg["desc"], "config_id": a.config, "width": W, "height": H,
                        "march_steps": K, "mode": a.mode, "shadow": ("fused" if fused else "none: all-+INF viewport (no shadow raster or march), "
                                  "eye pass only" if trivial else "two-pass"),
-                       "pipelined": pipelined,
                        "parallelism": (f"frame-parallel x{world}" if not tile_mode
                                        else f"row-bands x{world} + one gather ({a.format})"),
                        "rows_rank0": band_h},
-            "kernels": ({"frame_pipe_ms": round(pipe_ms, 5), "prologue_shadow_pass_ms": round(avg_sh, 5),
-                         "note": "launch j = shadow pass of frame j + eye pass of frame j-1"}
-                        if pipelined else
-                        {"shadow_pass_ms": round(avg_sh, 5), "eye_pass_ms": round(avg_eye, 5),
-                         "frame_kernel_ms": round(avg_sh + avg_eye, 5)}),
+            "kernels": {"shadow_pass_ms": round(avg_sh, 5), "eye_pass_ms": round(avg_eye, 5),
+                        "frame_kernel_ms": round(avg_sh + avg_eye, 5)},
             "roofline": roof,
             "roofline_other_kernel": roof_other,
             "roofline_frame": roof_frame,

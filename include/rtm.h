@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define RTM_ABI_VERSION 9
+#define RTM_ABI_VERSION 10
 
 /* ---- limits: scene constants travel as kernel arguments (SGPR path) ---- */
 #define RTM_MAX_SPHERES 16
@@ -212,6 +212,14 @@ void rtm_ctx_destroy(rtm_ctx* ctx);
 /* hipStream_t the context enqueues on (as void*) */
 void* rtm_ctx_stream(rtm_ctx* ctx);
 int rtm_ctx_synchronize(rtm_ctx* ctx);
+/* ABI v10: device memory on the context's device for a host that has no HIP
+ * binding of its own (the Rust crate's swap chain of output frames for
+ * rtm_render_frames_async).  rtm_ctx_free first waits for the context's stream.
+ * rtm_ctx_copy_to_host: `bytes` from device memory into host memory in the
+ * context's stream order, blocking (after the frames enqueued before it). */
+int rtm_ctx_alloc(rtm_ctx* ctx, int64_t bytes, void** out_dev);
+int rtm_ctx_free(rtm_ctx* ctx, void* dev);
+int rtm_ctx_copy_to_host(rtm_ctx* ctx, const void* dev, void* host, int64_t bytes);
 /* Durations in ms of the last render's two kernels, from HIP events recorded on
  * the context stream around each launch (valid after rtm_ctx_synchronize). */
 int rtm_ctx_last_kernel_ms(rtm_ctx* ctx, float* shadow_pass_ms, float* eye_pass_ms);
@@ -238,10 +246,9 @@ int rtm_ctx_last_lanes(rtm_ctx* ctx, int32_t* lanes);
 /* Frames per launch of rtm_render_frames_async (ABI v6): consecutive frames with
  * the same patches share ONE launch per pass (the frame index is the grid's z
  * dimension; each frame's constants come from a table uploaded per batch), so
- * small frames stop paying a launch per pass per frame.  0 = auto (RTM_BATCH
- * from the environment, else as many frames as make 64 Mpixel, at most 64 below
- * 1 Mpixel (64 at 512x512) and 16 from 1 Mpixel up (16 at 1920x1080, 8 at
- * 3840x2160, 2 at 7680x4320));
+ * small frames stop paying a launch per pass per frame.  0 = auto (as many
+ * frames as make 64 Mpixel, at most 64 below 1 Mpixel (64 at 512x512) and 32
+ * from 1 Mpixel up (32 at 1920x1080, 8 at 3840x2160, 2 at 7680x4320));
  * 1 = one frame per launch; at most 64.  Frames with overlapping outputs never share a launch (a repeated output
  * pointer still ends with the later frame).  Batches are spread over the lanes.  Kernel durations of
  * rtm_ctx_kernel_ms_history are then per launch, i.e. per batch;
@@ -310,11 +317,8 @@ int rtm_render_rows_async(rtm_ctx* ctx, const rtm_scene* scene, const rtm_camera
  * into out_rgba_dev[i] (full frames; pointers may repeat), two kernels per
  * frame, spread over the context's lanes (rtm_ctx_set_lanes) when no two frames
  * of different lanes share output memory; the context's shadow map ends up
- * holding the last frame's shadow pass either way.  With RTM_PIPELINE=1 in the environment and equal patches in every
- * frame the sequence is software-pipelined instead: the shadow pass of frame i
- * and the eye pass of frame i-1 run in ONE launch (double-buffered shadow
- * maps) — correct, but measured slower on MI355X.  Each frame's
- * output is bit-identical to rtm_render.  Frames are validated as they are
+ * holding the last frame's shadow pass either way.  Each frame's output is
+ * bit-identical to rtm_render.  Frames are validated as they are
  * enqueued: on an error return, the frames before the failing one may already
  * be on the stream.  The march tables (built from the patches, the shadow camera
  * and march_steps) are shared by all lanes: when a frame's tables differ from the

@@ -317,14 +317,14 @@ def _frames_vs_single(rtm, scenes, gpu_ctx, frames, eye, shadow, w, h, k, flags=
 
 
 @pytest.mark.parametrize("n", [1, 2, 5])
-def test_pipelined_frames_match_single_frames(rtm, scenes, gpu_ctx, n):
-    """rtm_render_frames_async (shadow pass of frame i + eye pass of frame i-1 in
-    one launch, double-buffered shadow maps) == frame-by-frame rtm_render."""
+def test_frame_sequence_matches_single_frames(rtm, scenes, gpu_ctx, n):
+    """rtm_render_frames_async (batched launches over the context's lanes) ==
+    frame-by-frame rtm_render."""
     frames = [scenes.scene_a_bench(100 + 7 * i) for i in range(n)]
     _frames_vs_single(rtm, scenes, gpu_ctx, frames, scenes.eye_camera(), scenes.shadow_camera(), 1920, 1080, 32)
 
 
-def test_pipelined_frames_reference_scene_and_oracle(rtm, oracle, scenes, gpu_ctx):
+def test_frame_sequence_reference_scene_and_oracle(rtm, oracle, scenes, gpu_ctx):
     import torch
     frames = [scenes.closely_orbiting_sphere(f) for f in (0, 1, 2, 100)]
     outs = [torch.empty((512, 512, 4), dtype=torch.float32, device="cuda") for _ in frames]
@@ -337,15 +337,15 @@ def test_pipelined_frames_reference_scene_and_oracle(rtm, oracle, scenes, gpu_ct
         assert bits_equal(o.cpu().numpy(), want)
 
 
-def test_pipelined_frames_generic_shadow_tiles(rtm, scenes, gpu_ctx):
-    """Rotated shadow camera: the pipelined launch uses the generic shadow tile."""
+def test_frame_sequence_generic_shadow_tiles(rtm, scenes, gpu_ctx):
+    """Rotated shadow camera: the sequence's batched launches use the generic shadow tile."""
     rng = np.random.default_rng(7)
     shadow = _random_camera(scenes, rng, False)
     frames = [_random_scene(scenes, np.random.default_rng(11), 6, 2) for _ in range(3)]
     _frames_vs_single(rtm, scenes, gpu_ctx, frames, scenes.eye_camera(), shadow, 333, 217, 80)
 
 
-def test_pipelined_frames_differing_patches_fallback(rtm, scenes, gpu_ctx):
+def test_frame_sequence_differing_patches(rtm, scenes, gpu_ctx):
     frames = [scenes.scene_a_bench(100), scenes.scene_b(), scenes.closely_orbiting_sphere(3)]
     _frames_vs_single(rtm, scenes, gpu_ctx, frames, scenes.eye_camera(), scenes.shadow_camera(), 640, 360, 64)
 
@@ -441,8 +441,8 @@ def test_set_lanes_api(rtm, scenes, gpu_ctx):
         gpu_ctx.set_batch(0)
 
 
-def test_pipelined_frames_scene_b_8k(rtm, oracle, scenes, gpu_ctx):
-    """BASELINE config 5 geometry through the pipelined path, against the oracle."""
+def test_frame_sequence_scene_b_8k(rtm, oracle, scenes, gpu_ctx):
+    """BASELINE config 5 geometry through a frame sequence, against the oracle."""
     import torch
     w, h, k = 7680, 4320, 128
     frames = [scenes.scene_b(), scenes.scene_b()]
@@ -454,36 +454,6 @@ def test_pipelined_frames_scene_b_8k(rtm, oracle, scenes, gpu_ctx):
     want = oracle.render(frames[0], scenes.eye_camera(), scenes.shadow_camera(), w, h, k, 0, nthreads=NT)["rgba"]
     for o in outs:
         assert bits_equal(o.cpu().numpy(), want)
-
-
-def test_pipelined_launch_in_subprocess(rtm, scenes):
-    """RTM_PIPELINE=1 (read once per process): the software-pipelined launch
-    (shadow pass of frame i + eye pass of frame i-1 in one grid) is opt-in, so
-    it runs in a child process here, against frame-by-frame rtm_render."""
-    import subprocess
-    import sys
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    code = r'''
-import importlib, sys
-import numpy as np, torch
-sys.path.insert(0, %r)
-rtm = importlib.import_module("2018rustraytracer_amd")
-sc = importlib.import_module("2018rustraytracer_amd.scenes")
-ctx = rtm.Context(0)
-for frames, w, h, k in (([sc.scene_a_bench(100 + 3 * i) for i in range(4)], 1920, 1080, 64),
-                        ([sc.scene_b(), sc.scene_b()], 640, 480, 128)):
-    outs = [torch.empty((h, w, 4), dtype=torch.float32, device="cuda") for _ in frames]
-    torch.cuda.synchronize()
-    ctx.render_frames_async(frames, sc.eye_camera(), sc.shadow_camera(), w, h, k, 0, [o.data_ptr() for o in outs])
-    ctx.synchronize()
-    for s, o in zip(frames, outs):
-        want = rtm.render_frame(s, sc.eye_camera(), sc.shadow_camera(), w, h, k, 0)
-        assert np.array_equal(o.cpu().numpy().view(np.uint32), want.view(np.uint32))
-print("pipelined ok")
-''' % root
-    env = dict(os.environ, RTM_PIPELINE="1")
-    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=600)
-    assert r.returncode == 0 and "pipelined ok" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
 
 
 def test_render_multi(rtm, oracle, scenes):
