@@ -121,6 +121,7 @@ ABI_SYMBOLS = [
     ("rtm_ctx_alloc", C.c_int, [_P, C.c_int64, C.POINTER(_P)]),
     ("rtm_ctx_free", C.c_int, [_P, _P]),
     ("rtm_ctx_copy_to_host", C.c_int, [_P, _P, _P, C.c_int64]),
+    ("rtm_ctx_oob_reads", C.c_int, [_P, C.POINTER(C.c_int64)]),
     ("rtm_ctx_last_kernel_ms", C.c_int, [_P, C.POINTER(C.c_float), C.POINTER(C.c_float)]),
     ("rtm_ctx_set_timing_capacity", C.c_int, [_P, _I32]),
     ("rtm_ctx_set_timing_stride", C.c_int, [_P, _I32]),

@@ -958,6 +958,7 @@ int ensure_tables(rtm_ctx* ctx, int32_t steps, int32_t W, int32_t H, const rtm_c
         out->py = out->d0 = out->dd = nullptr;
         out->ok = nullptr;
     }
+    out->row_recs = ctx->tab_rec >= 0 ? (int32_t)(((int64_t)H + 63) / 64 * 64) : 0;
     if (ctx->tab_rec >= 0) {
         out->zrec = reinterpret_cast<const ZRecK*>(base + ctx->tab_rec);
         out->col = reinterpret_cast<const ColRecK*>(out->zrec + nt2 + 1);
@@ -1112,6 +1113,7 @@ int enqueue_frame(rtm_ctx* ctx, FrameArgs& a, const FrameExtra* x, void* out_dev
         const size_t words = (size_t)((a.ey.W + 63) / 64) * (size_t)(a.ey.row_end - a.ey.row_begin);
         if ((rc = mb.ensure(words * sizeof(uint32_t), ctx->device))) return rc;
         tabs.rtmask = (uint32_t*)mb.p;
+        tabs.rtmask_words = (int32_t)words;
     }
     const bool trivial = !stats && trivial_shadow(a.ey.flags);
     if (trivial) a.ey.flags |= RTM_FLAG_FUSED_SHADOW;
@@ -1323,6 +1325,7 @@ int enqueue_batch(rtm_ctx* ctx, int lane, FrameArgs* fa, const FrameExtra* ex, v
         bf.tabs.psp = nullptr;
         bf.tabs.sdf = nullptr;
         bf.tabs.rtmask = nullptr;
+        bf.tabs.rtmask_words = 0;
         bf.tabs.rt_persp = 0;
         if (ex[k].has_rt) {
             if (fresh_rt[(size_t)k]) std::memcpy(hb + o_rt[(size_t)k], &ex[k].rt, sizeof(RtK));
@@ -1353,8 +1356,10 @@ int enqueue_batch(rtm_ctx* ctx, int lane, FrameArgs* fa, const FrameExtra* ex, v
             if (ex[k].has_rt) {
                 BatchFrame& bf = *(BatchFrame*)(hb + sizeof(BatchFrame) * (size_t)k);
                 bf.tabs.rtmask = (uint32_t*)br.rtmask.p + nw * (size_t)k;
+                bf.tabs.rtmask_words = (int32_t)nw;
             }
         t0.rtmask = (uint32_t*)br.rtmask.p;
+        t0.rtmask_words = (int32_t)nw;
     }
     t0.fmt = fmt;
     // the lane's stream pulls the table from the pinned slot: in stream order after the
@@ -1513,6 +1518,17 @@ int rtm_ctx_copy_to_host(rtm_ctx* ctx, const void* dev, void* host, int64_t byte
     DeviceGuard g(ctx->device);
     HIP_TRY(hipMemcpyAsync(host, dev, (size_t)bytes, hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(hipStreamSynchronize(ctx->stream));
+    return RTM_OK;
+}
+
+int rtm_ctx_oob_reads(rtm_ctx* ctx, int64_t* count) {
+    if (!ctx || !count) return fail(RTM_ERR_INVALID, "ctx/count is NULL");
+    DeviceGuard g(ctx->device);
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    for (auto& l : ctx->lanes) HIP_TRY(hipStreamSynchronize(l->stream));
+    unsigned long long c = 0;
+    if (read_oob_reads(&c, ctx->stream)) return fail(RTM_ERR_HIP, "reading the out-of-range count failed");
+    *count = (int64_t)c;
     return RTM_OK;
 }
 
@@ -2165,7 +2181,7 @@ int check_rows(const FrameArgs& a, int32_t row_begin, int32_t row_end, const Row
 }
 
 int enqueue_prepared(rtm_ctx* ctx, const PreparedFrame* f, int32_t format, int32_t row_begin, int32_t row_end,
-                     void* out_dev, const RowMap* map) {
+                     void* out_dev, const RowMap* map, int lane) {
     if (!ctx || !f || !out_dev) return fail(RTM_ERR_INVALID, "bad arguments");
     int rc = validate_format(format, out_dev);
     if (rc) return rc;
@@ -2173,13 +2189,14 @@ int enqueue_prepared(rtm_ctx* ctx, const PreparedFrame* f, int32_t format, int32
     FrameArgs a = f->a;
     apply_rows(a.ey, row_begin, row_end, map);
     DeviceGuard g(ctx->device);
-    return enqueue_frame(ctx, a, &f->x, out_dev, nullptr, 0, format);
+    return enqueue_frame(ctx, a, &f->x, out_dev, nullptr, lane, format);
 }
 
 int enqueue_prepared_batch(rtm_ctx* ctx, const PreparedFrame* const* fs, int n, int32_t format, int32_t row_begin,
-                           int32_t row_end, void* const* outs, const RowMap* map) {
+                           int32_t row_end, void* const* outs, const RowMap* map, int lane) {
     if (!ctx || !fs || !outs || n < 1) return fail(RTM_ERR_INVALID, "bad arguments");
-    if (n == 1) return enqueue_prepared(ctx, fs[0], format, row_begin, row_end, outs[0], map);
+    if (lane < 0 || lane > (int)ctx->lanes.size()) return fail(RTM_ERR_INVALID, "lane %d of %zu", lane, ctx->lanes.size() + 1);
+    if (n == 1) return enqueue_prepared(ctx, fs[0], format, row_begin, row_end, outs[0], map, lane);
     int rc;
     for (int k = 0; k < n; ++k) {
         if (!fs[k] || !outs[k]) return fail(RTM_ERR_INVALID, "bad arguments");
@@ -2200,7 +2217,7 @@ int enqueue_prepared_batch(rtm_ctx* ctx, const PreparedFrame* const* fs, int n, 
     DeviceGuard g(ctx->device);
     if (!same) {
         for (int k = 0; k < n; ++k)
-            if ((rc = enqueue_prepared(ctx, fs[k], format, row_begin, row_end, outs[k], map))) return rc;
+            if ((rc = enqueue_prepared(ctx, fs[k], format, row_begin, row_end, outs[k], map, lane))) return rc;
         return RTM_OK;
     }
     std::vector<FrameArgs> fa((size_t)n);
@@ -2210,7 +2227,36 @@ int enqueue_prepared_batch(rtm_ctx* ctx, const PreparedFrame* const* fs, int n, 
         apply_rows(fa[(size_t)k].ey, row_begin, row_end, map);
         fx[(size_t)k] = fs[k]->x;
     }
-    return enqueue_batch(ctx, 0, fa.data(), fx.data(), outs, n, format);
+    return enqueue_batch(ctx, lane, fa.data(), fx.data(), outs, n, format);
+}
+
+int lanes_begin(rtm_ctx* ctx, int32_t width, int32_t rows, int32_t n_batches) {
+    if (!ctx || n_batches < 1) return fail(RTM_ERR_INVALID, "bad arguments");
+    // frame_lanes' rule with disjoint outputs (the caller's batches never share one)
+    int L = ctx->lanes_req > 0 ? ctx->lanes_req : ((int64_t)width * rows >= (16LL << 20) ? 3 : 4);
+    L = std::min<int>(std::min(L, 8), n_batches);
+    ctx->lanes_last = std::max(L, 1);  // (rtm_ctx_last_lanes)
+    if (L <= 1) return 1;
+    DeviceGuard g(ctx->device);
+    int rc = ensure_lanes(ctx, L);
+    if (rc) return rc;
+    HIP_TRY(hipEventRecord(ctx->fork, ctx->stream));
+    for (int k = 1; k < L; ++k) HIP_TRY(hipStreamWaitEvent(ctx->lanes[(size_t)k - 1]->stream, ctx->fork, 0));
+    return L;
+}
+
+int lanes_end(rtm_ctx* ctx, int L) {
+    DeviceGuard g(ctx->device);
+    for (int k = 1; k < L && k <= (int)ctx->lanes.size(); ++k) {
+        Lane& l = *ctx->lanes[(size_t)k - 1];
+        HIP_TRY(hipEventRecord(l.done, l.stream));
+        HIP_TRY(hipStreamWaitEvent(ctx->stream, l.done, 0));
+    }
+    return RTM_OK;
+}
+
+hipStream_t lane_stream(const rtm_ctx* ctx, int lane) {
+    return lane > 0 && lane <= (int)ctx->lanes.size() ? ctx->lanes[(size_t)lane - 1]->stream : ctx->stream;
 }
 
 int auto_frames_per_launch(int32_t width, int32_t rows) { return frame_batch(0, width, rows); }

@@ -124,19 +124,13 @@ inline void band_rows(int32_t H, int32_t n, int32_t r, int32_t* r0, int32_t* r1)
     *r1 = std::min<int64_t>(H, (int64_t)(r + 1) * band);
 }
 
-// The partition's stripe height: RTM_GROUP_STRIPE=S overrides (0: contiguous bands);
-// default 8-row cyclic stripes once there are several ranks.  Contiguous bands of
+// The partition's default stripe height: 8-row cyclic stripes once there are several
+// ranks (a function of the rank count only, so every rank of a one-process-per-GPU
+// group picks the same; rtm_group_set_partition is collective).  Contiguous bands of
 // ceil(H/N) rows were measured 1.26-1.56x max/mean band time at N = 4-8 (the spheres
 // sit mid-frame, and a band's cost follows its hit pixels); 8-row stripes model at
 // 1.01-1.06 (tools/band_balance.py, profiles/r03_band_balance.json).
-int32_t default_stripe(int32_t n) {
-    static const int env = [] {
-        const char* e = getenv("RTM_GROUP_STRIPE");
-        return e ? atoi(e) : -1;
-    }();
-    if (env >= 0) return env;
-    return n > 1 ? 8 : 0;
-}
+int32_t default_stripe(int32_t n) { return n > 1 ? 8 : 0; }
 
 // Rank r's rows of an H-row frame: contiguous [r0, r0 + rows) or S-row cyclic stripes
 // (local row j = image row r*S + (j / S)*N*S + j % S).
@@ -182,7 +176,10 @@ hipError_t place_rows(void* dst, const void* src, const Part& p, size_t row_byte
 
 }  // namespace
 
-// One local device of the group.
+// One local device of the group.  A chunk of frames renders into one of NSLOT
+// staging slots (chunks spread over the context's lanes, so up to NSLOT chunks are
+// in flight); a slot is reused once its sends have read it.
+constexpr int NSLOT = 4;
 struct Member {
     rtm_ctx* ctx = nullptr;
     int device = 0;
@@ -190,12 +187,12 @@ struct Member {
     ncclComm_t comm = nullptr;
     hipStream_t xfer = nullptr;      // the member's RCCL transfers
     hipEvent_t start = nullptr;      // frame start on the render stream (the root's receives wait for it)
-    hipEvent_t ready[2] = {nullptr, nullptr};  // band rendered into stage[s]
-    hipEvent_t sent[2] = {nullptr, nullptr};   // stage[s] read by its send
+    hipEvent_t ready[NSLOT] = {};    // band rendered into stage[s]
+    hipEvent_t sent[NSLOT] = {};     // stage[s] read by its send
     hipEvent_t done = nullptr;       // the frame's transfers on this member are finished
     hipEvent_t lb_sent = nullptr;    // loopback transport: this member's send is posted
     hipEvent_t lb_recv = nullptr;    // loopback transport: the root's copy of it has run
-    void* stage[2] = {nullptr, nullptr};
+    void* stage[NSLOT] = {};
     size_t stage_bytes = 0;
     int slot = 0;
 };
@@ -221,15 +218,22 @@ void release(rtm_group* g, bool destroy_comms) {
     const Rccl& R = rccl();
     for (Member& mb : g->m) {
         Guard d(mb.device);
+        // renders (which write the staging slots) and transfers (which read them) first
+        if (mb.ctx) (void)rtm_ctx_synchronize(mb.ctx);
         if (mb.xfer) (void)hipStreamSynchronize(mb.xfer);
         if (mb.comm && destroy_comms && R.CommDestroy) (void)R.CommDestroy(mb.comm);
         mb.comm = nullptr;
-        for (hipEvent_t* e : {&mb.start, &mb.ready[0], &mb.ready[1], &mb.sent[0], &mb.sent[1], &mb.done,
-                              &mb.lb_sent, &mb.lb_recv})
+        for (hipEvent_t* e : {&mb.start, &mb.done, &mb.lb_sent, &mb.lb_recv})
             if (*e) {
                 (void)hipEventDestroy(*e);
                 *e = nullptr;
             }
+        for (int k = 0; k < NSLOT; ++k)
+            for (hipEvent_t* e : {&mb.ready[k], &mb.sent[k]})
+                if (*e) {
+                    (void)hipEventDestroy(*e);
+                    *e = nullptr;
+                }
         for (void*& p : mb.stage)
             if (p) {
                 (void)hipFree(p);
@@ -264,9 +268,10 @@ int setup_members(rtm_group* g) {
         if (rc) return rc;
         Guard d(mb.device);
         GHIP_TRY(hipStreamCreateWithFlags(&mb.xfer, hipStreamNonBlocking));
-        for (hipEvent_t* e : {&mb.start, &mb.ready[0], &mb.ready[1], &mb.sent[0], &mb.sent[1], &mb.done,
-                              &mb.lb_sent, &mb.lb_recv})
+        for (hipEvent_t* e : {&mb.start, &mb.done, &mb.lb_sent, &mb.lb_recv})
             GHIP_TRY(hipEventCreateWithFlags(e, hipEventDisableTiming));
+        for (int k = 0; k < NSLOT; ++k)
+            for (hipEvent_t* e : {&mb.ready[k], &mb.sent[k]}) GHIP_TRY(hipEventCreateWithFlags(e, hipEventDisableTiming));
     }
     return RTM_OK;
 }
@@ -274,7 +279,8 @@ int setup_members(rtm_group* g) {
 int ensure_stage(Member& mb, size_t bytes) {
     if (bytes <= mb.stage_bytes) return RTM_OK;
     Guard d(mb.device);
-    // both staging buffers are idle once their last sends are done
+    // the staging buffers are idle once their renders and their last sends are done
+    GHIP_TRY(hipStreamSynchronize(rtm::internal::ctx_stream(mb.ctx)));
     GHIP_TRY(hipStreamSynchronize(mb.xfer));
     for (void*& p : mb.stage) {
         if (p) (void)hipFree(p);
@@ -403,12 +409,13 @@ int rtm_group_create_rank(int32_t device, int32_t n_ranks, int32_t rank, const u
 
 void rtm_group_destroy(rtm_group* g) {
     if (!g) return;
-    // bounded: a peer that never posts its matching transfer would otherwise hang
-    // the caller (and interpreter shutdown); past the limit the communicators are
-    // aborted (RTM_GROUP_DESTROY_TIMEOUT_MS, default 120 s; <= 0 waits indefinitely)
+    // waits for the group's queued work without a limit (a long 8K sequence may be
+    // in flight); a caller that must not hang on a lost peer bounds it itself with
+    // rtm_group_synchronize(g, timeout_ms) first, which aborts the communicators past
+    // the limit (RTM_GROUP_DESTROY_TIMEOUT_MS > 0: the same bound here, opt-in)
     static const int32_t limit_ms = [] {
         const char* e = getenv("RTM_GROUP_DESTROY_TIMEOUT_MS");
-        return e ? (int32_t)atoi(e) : 120000;
+        return e ? (int32_t)atoi(e) : 0;
     }();
     if (!g->aborted) (void)rtm_group_synchronize(g, limit_ms);
     release(g, !g->aborted);
@@ -449,20 +456,30 @@ int group_stripe(const rtm_group* g) { return g->stripe >= 0 ? g->stripe : defau
 // The root's receive staging for striped RCCL gathers: one part per rank (its compact
 // rows land here, then place_rows scatters them), on the root's device.
 int ensure_recv(rtm_group* g, Member& rm, size_t bytes) {
-    if (bytes <= g->recv_bytes) return RTM_OK;
-    Guard d(rm.device);
-    GHIP_TRY(hipStreamSynchronize(rm.xfer));
-    if (g->recv) (void)hipFree(g->recv);
+    if (g->recv && bytes <= g->recv_bytes && g->recv_device == rm.device) return RTM_OK;
+    // a bigger buffer, or the root moved to another device: the old buffer's last
+    // receives and placements ran on the previous root's transfer stream
+    for (Member& mb : g->m) {
+        Guard d(mb.device);
+        GHIP_TRY(hipStreamSynchronize(mb.xfer));
+    }
+    if (g->recv) {
+        Guard d(g->recv_device);
+        (void)hipFree(g->recv);
+    }
     g->recv = nullptr;
     g->recv_bytes = 0;
+    Guard d(rm.device);
     if (hipMalloc(&g->recv, bytes) != hipSuccess) return set_error(RTM_ERR_OOM, "receive staging allocation failed");
     g->recv_bytes = bytes;
     g->recv_device = rm.device;
     return RTM_OK;
 }
 
+// lanes[i]: the lane of member i that renders this chunk (its context's streams,
+// rtm::internal::lanes_begin)
 int group_chunk(rtm_group* g, const rtm::internal::PreparedFrame* const* pf, int nf, int32_t width, int32_t height,
-                int32_t format, int32_t root, void* const* out_dev) {
+                int32_t format, int32_t root, void* const* out_dev, const int* lanes) {
     const int32_t n = g->n_ranks;
     const int32_t S = group_stripe(g);
     const size_t row_bytes = (size_t)rtm::internal::bytes_per_pixel(format) * (size_t)width;
@@ -470,10 +487,11 @@ int group_chunk(rtm_group* g, const rtm::internal::PreparedFrame* const* pf, int
     int rc;
     std::vector<void*> outs((size_t)nf);
     // 1. every local member renders its rows of the chunk's frames
-    for (Member& mb : g->m) {
+    for (size_t mi = 0; mi < g->m.size(); ++mi) {
+        Member& mb = g->m[mi];
         Part pt = part_of(height, n, S, mb.rank);
         Guard d(mb.device);
-        hipStream_t rs = rtm::internal::ctx_stream(mb.ctx);
+        hipStream_t rs = rtm::internal::lane_stream(mb.ctx, lanes[mi]);
         const bool staged = mb.rank != root || g->root_staging;
         if (pt.rows > 0) {
             const int sl = mb.slot;
@@ -486,9 +504,9 @@ int group_chunk(rtm_group* g, const rtm::internal::PreparedFrame* const* pf, int
                                          : stripes ? out_dev[j]
                                                    : (void*)((char*)out_dev[j] + row_bytes * (size_t)pt.r0);
             rc = stripes ? rtm::internal::enqueue_prepared_batch(mb.ctx, pf, nf, format, 0, pt.rows, outs.data(),
-                                                                 &pt.map)
+                                                                 &pt.map, lanes[mi])
                          : rtm::internal::enqueue_prepared_batch(mb.ctx, pf, nf, format, pt.r0, pt.r0 + pt.rows,
-                                                                 outs.data());
+                                                                 outs.data(), nullptr, lanes[mi]);
             if (rc) return rc;
             if (staged) {
                 GHIP_TRY(hipEventRecord(mb.ready[sl], rs));
@@ -501,62 +519,66 @@ int group_chunk(rtm_group* g, const rtm::internal::PreparedFrame* const* pf, int
         }
     }
     // 2. ONE gather per frame: the root receives every other part, the others send
-    //    theirs (nothing to move for a one-rank group rendering in place)
+    //    theirs (nothing to move for a one-rank group rendering in place).  A part lands
+    //    in place (a contiguous band) or compact in the root's receive staging (stripes),
+    //    and after the frame's transfers the root places the staged parts at their image
+    //    rows.  The transfers are RCCL's matched sends and receives, or with the loopback
+    //    transport device copies of the same bytes to the same places, in RCCL's
+    //    completion order for a pair (the copy runs once the sender's transfer stream
+    //    reached its send; the sender's stream moves past its send once the copy read it).
     Member* rm = nullptr;
     for (Member& mb : g->m)
         if (mb.rank == root) rm = &mb;
-    if ((n > 1 || g->root_staging) && g->loopback) {
-        // the same matched pairs with device copies on the root's transfer stream:
-        // the copy runs after the sender's transfer stream reached its send (part
-        // rendered), and the sender's stream moves past its send only once the copy
-        // has read the part -- RCCL's completion order for a send/receive pair
-        for (int j = 0; j < nf; ++j)
-            for (Member& mb : g->m) {
-                const bool staged = mb.rank != root || g->root_staging;
-                const Part pt = part_of(height, n, S, mb.rank);
-                if (!staged || pt.rows <= 0) continue;
-                GHIP_TRY(hipEventRecord(mb.lb_sent, mb.xfer));
-                GHIP_TRY(hipStreamWaitEvent(rm->xfer, mb.lb_sent, 0));
-                GHIP_TRY(place_rows(out_dev[j], (char*)mb.stage[mb.slot] + part_bytes * (size_t)j, pt, row_bytes,
-                                    hipMemcpyDeviceToDevice, rm->xfer));
-                GHIP_TRY(hipEventRecord(mb.lb_recv, rm->xfer));
-                GHIP_TRY(hipStreamWaitEvent(mb.xfer, mb.lb_recv, 0));
-            }
-    } else if (n > 1 || g->root_staging) {
+    if (n > 1 || g->root_staging) {
         const Rccl& R = rccl();
         const bool stripes = S > 0 && n > 1;
         if (stripes && rm && (rc = ensure_recv(g, *rm, part_bytes * (size_t)n))) return rc;
+        auto dst_of = [&](int j, int32_t p) -> void* {
+            return stripes ? (void*)((char*)g->recv + part_bytes * (size_t)p)
+                           : (void*)((char*)out_dev[j] + row_bytes * (size_t)part_of(height, n, S, p).r0);
+        };
         for (int j = 0; j < nf; ++j) {
-            NCCL_TRY(R.GroupStart());
-            for (Member& mb : g->m) {
-                if (mb.rank == root) {
-                    for (int32_t p = 0; p < n; ++p) {
-                        if (p == root && !g->root_staging) continue;
-                        const Part pt = part_of(height, n, S, p);
-                        if (pt.rows <= 0) continue;
-                        // a contiguous band lands in place; stripes land compact in the
-                        // receive staging and are placed after the group
-                        void* dst = stripes ? (void*)((char*)g->recv + part_bytes * (size_t)p)
-                                            : (void*)((char*)out_dev[j] + row_bytes * (size_t)pt.r0);
-                        ncclResult_t r = R.Recv(dst, row_bytes * (size_t)pt.rows, ncclUint8, p, mb.comm, mb.xfer);
+            if (g->loopback) {
+                for (Member& mb : g->m) {
+                    const bool staged = mb.rank != root || g->root_staging;
+                    const Part pt = part_of(height, n, S, mb.rank);
+                    if (!staged || pt.rows <= 0) continue;
+                    GHIP_TRY(hipEventRecord(mb.lb_sent, mb.xfer));
+                    GHIP_TRY(hipStreamWaitEvent(rm->xfer, mb.lb_sent, 0));
+                    GHIP_TRY(hipMemcpyAsync(dst_of(j, mb.rank), (char*)mb.stage[mb.slot] + part_bytes * (size_t)j,
+                                            row_bytes * (size_t)pt.rows, hipMemcpyDeviceToDevice, rm->xfer));
+                    GHIP_TRY(hipEventRecord(mb.lb_recv, rm->xfer));
+                    GHIP_TRY(hipStreamWaitEvent(mb.xfer, mb.lb_recv, 0));
+                }
+            } else {
+                NCCL_TRY(R.GroupStart());
+                for (Member& mb : g->m) {
+                    if (mb.rank == root) {
+                        for (int32_t p = 0; p < n; ++p) {
+                            if (p == root && !g->root_staging) continue;
+                            const Part pt = part_of(height, n, S, p);
+                            if (pt.rows <= 0) continue;
+                            ncclResult_t r = R.Recv(dst_of(j, p), row_bytes * (size_t)pt.rows, ncclUint8, p, mb.comm,
+                                                    mb.xfer);
+                            if (r != ncclSuccess) {
+                                (void)R.GroupEnd();
+                                return comm_fail("ncclRecv", r);
+                            }
+                        }
+                    }
+                    const Part pt = part_of(height, n, S, mb.rank);
+                    const bool staged = mb.rank != root || g->root_staging;
+                    if (staged && pt.rows > 0) {
+                        ncclResult_t r = R.Send((char*)mb.stage[mb.slot] + part_bytes * (size_t)j,
+                                                row_bytes * (size_t)pt.rows, ncclUint8, root, mb.comm, mb.xfer);
                         if (r != ncclSuccess) {
                             (void)R.GroupEnd();
-                            return comm_fail("ncclRecv", r);
+                            return comm_fail("ncclSend", r);
                         }
                     }
                 }
-                const Part pt = part_of(height, n, S, mb.rank);
-                const bool staged = mb.rank != root || g->root_staging;
-                if (staged && pt.rows > 0) {
-                    ncclResult_t r = R.Send((char*)mb.stage[mb.slot] + part_bytes * (size_t)j,
-                                            row_bytes * (size_t)pt.rows, ncclUint8, root, mb.comm, mb.xfer);
-                    if (r != ncclSuccess) {
-                        (void)R.GroupEnd();
-                        return comm_fail("ncclSend", r);
-                    }
-                }
+                NCCL_TRY(R.GroupEnd());
             }
-            NCCL_TRY(R.GroupEnd());
             if (stripes && rm) {  // the received parts to their image rows, in the root's transfer order
                 Guard d(rm->device);
                 for (int32_t p = 0; p < n; ++p) {
@@ -574,7 +596,7 @@ int group_chunk(rtm_group* g, const rtm::internal::PreparedFrame* const* pf, int
         if (staged && pt.rows > 0) {
             Guard d(mb.device);
             GHIP_TRY(hipEventRecord(mb.sent[mb.slot], mb.xfer));
-            mb.slot ^= 1;
+            mb.slot = (mb.slot + 1) % NSLOT;
         }
     }
     return RTM_OK;
@@ -655,7 +677,32 @@ int rtm_group_render_frames_async(rtm_group* g, int32_t n_frames, const rtm_scen
     bool holds_root = false;
     for (const Member& mb : g->m) holds_root |= mb.rank == root;
     const uintptr_t frame_bytes = (uintptr_t)rtm::internal::bytes_per_pixel(format) * (uintptr_t)width * height;
-    for (int32_t i0 = 0; i0 < n_frames;) {
+    // every member spreads the call's chunks over its context's lanes, as
+    // rtm_render_frames_async spreads batches (chunk c on lane c % L); the lanes join
+    // the context stream at the end (rtm_group_synchronize waits on it)
+    const int32_t n_chunks = (n_frames + B - 1) / B;
+    std::vector<int> L(g->m.size(), 1), lane(g->m.size(), 0);
+    for (size_t mi = 0; mi < g->m.size(); ++mi) {
+        const int32_t rows = part_of(height, g->n_ranks, group_stripe(g), g->m[mi].rank).rows;
+        if (rows <= 0) continue;
+        Guard d(g->m[mi].device);
+        const int l = rtm::internal::lanes_begin(g->m[mi].ctx, width, rows, n_chunks);
+        if (l < 0) {
+            for (size_t q = 0; q < mi; ++q) (void)rtm::internal::lanes_end(g->m[q].ctx, L[q]);
+            return l;
+        }
+        L[mi] = l;
+    }
+    auto join = [&]() {
+        int jr = RTM_OK;
+        for (size_t mi = 0; mi < g->m.size(); ++mi) {
+            Guard d(g->m[mi].device);
+            const int r = rtm::internal::lanes_end(g->m[mi].ctx, L[mi]);
+            if (r && !jr) jr = r;
+        }
+        return jr;
+    };
+    for (int32_t i0 = 0, c = 0; i0 < n_frames; ++c) {
         int nf = std::min<int32_t>(B, n_frames - i0);
         // on the root, a chunk's frames need disjoint outputs (they render side by side);
         // a repeated output starts the next chunk, so the later frame still lands last
@@ -672,14 +719,18 @@ int rtm_group_render_frames_async(rtm_group* g, int32_t n_frames, const rtm_scen
                     break;
                 }
             }
-        for (int k = 0; k < nf; ++k)
-            if ((rc = rtm::internal::prepare_frame(pf[(size_t)k].get(), &scenes[i0 + k], eye, shadow, width, height,
-                                                   march_steps, f)))
-                return rc;
-        if ((rc = group_chunk(g, pp.data(), nf, width, height, format, root, out_dev + i0))) return rc;
+        for (int k = 0; k < nf && !rc; ++k)
+            rc = rtm::internal::prepare_frame(pf[(size_t)k].get(), &scenes[i0 + k], eye, shadow, width, height,
+                                              march_steps, f);
+        for (size_t mi = 0; mi < g->m.size(); ++mi) lane[mi] = c % L[mi];
+        if (!rc) rc = group_chunk(g, pp.data(), nf, width, height, format, root, out_dev + i0, lane.data());
+        if (rc) {
+            (void)join();  // the context streams still cover what was enqueued
+            return rc;
+        }
         i0 += nf;
     }
-    return RTM_OK;
+    return join();
 }
 
 namespace {
@@ -750,6 +801,8 @@ int group_render_direct(rtm_group* g, const rtm_scene* scene, const rtm_camera* 
 int rtm_group_set_partition(rtm_group* g, int32_t stripe_rows) {
     if (!g) return set_error(RTM_ERR_INVALID, "group is NULL");
     if (stripe_rows < -1 || stripe_rows > RTM_MAX_DIM) return set_error(RTM_ERR_INVALID, "stripe_rows outside [-1, RTM_MAX_DIM]");
+    if ((int64_t)stripe_rows * g->n_ranks > (int64_t)RTM_MAX_DIM * 8)  // the stripe period stays an int32 row count
+        return set_error(RTM_ERR_INVALID, "stripe period stripe_rows * n_ranks too large");
     const int rc = rtm_group_synchronize(g, 0);  // frames in flight keep the partition they were issued with
     if (rc) return rc;
     g->stripe = stripe_rows;

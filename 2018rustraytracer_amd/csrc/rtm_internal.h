@@ -32,12 +32,21 @@ int32_t stripe_rows_of(int32_t H, int32_t n, int32_t S, int32_t r);
 // rows [row_begin, row_end) in `format` into out_dev, on ctx's stream (map: stripes,
 // row_begin = 0 and row_end = the local row count then)
 int enqueue_prepared(rtm_ctx* ctx, const PreparedFrame* f, int32_t format, int32_t row_begin, int32_t row_end,
-                     void* out_dev, const RowMap* map = nullptr);
-// n frames' rows [row_begin, row_end) in `format`, frame k into outs[k], on ctx's
-// stream: one launch per pass when the frames share their march tables
-// (rtm_ctx_set_batch's batched kernels), else frame by frame
+                     void* out_dev, const RowMap* map = nullptr, int lane = 0);
+// n frames' rows [row_begin, row_end) in `format`, frame k into outs[k], on the stream
+// of ctx's lane `lane` (0: ctx's own stream; lanes_begin forks the others): one launch
+// per pass when the frames share their march tables (rtm_ctx_set_batch's batched
+// kernels), else frame by frame
 int enqueue_prepared_batch(rtm_ctx* ctx, const PreparedFrame* const* fs, int n, int32_t format, int32_t row_begin,
-                           int32_t row_end, void* const* outs, const RowMap* map = nullptr);
+                           int32_t row_end, void* const* outs, const RowMap* map = nullptr, int lane = 0);
+// Lanes for n_batches batches of width x rows frames (the rtm_render_frames_async
+// rule, rtm_ctx_set_lanes honoured): creates them and makes them start after ctx's
+// stream; returns the count (1: ctx's stream only) or a negative error.
+int lanes_begin(rtm_ctx* ctx, int32_t width, int32_t rows, int32_t n_batches);
+// ctx's stream waits for lanes 1..L-1 (every batch enqueued on them is then in its order)
+int lanes_end(rtm_ctx* ctx, int L);
+// the stream of ctx's lane (0: ctx's own)
+hipStream_t lane_stream(const rtm_ctx* ctx, int lane);
 // frames per launch the library's auto rule picks for width x rows frames
 int auto_frames_per_launch(int32_t width, int32_t rows);
 // bytes per pixel of an RTM_FORMAT_* (0: unknown)

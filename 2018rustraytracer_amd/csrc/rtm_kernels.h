@@ -109,7 +109,7 @@ struct Tables {
     const double* dd;  // n_patches*W
     const int32_t* ok; // W + H
     int32_t zmono;     // z table (first `steps` entries) is non-decreasing (+1) / non-increasing (-1)
-    int32_t pad;
+    int32_t row_recs;  // RowRecK entries (H rounded up to 64; every read is bounds-checked against it)
     double z0;         // z[0] when z != nullptr (a kernarg copy: no dependent global load for it)
     double inv_sz;     // 1.0 / step.z when z != nullptr (the first-crossing guess's scale)
 };
@@ -273,9 +273,10 @@ struct DevTabs {
     uint32_t bg;          // the encoded background pixel (0.0, 0.2, 0.2) (main.rs:718-720), R | G<<8 | B<<16
     // PERSPECTIVE eye with ray-traced primitives: rt holds the origin-only constants
     // (rt_persp) and rtmask is scratch for the per-wave primitive masks,
-    // ceil(W/64) * rows words (launch_eye_pass fills it first; nullptr: in-kernel cull)
+    // rtmask_words = ceil(W/64) * rows words (launch_eye_pass fills it first; nullptr:
+    // in-kernel cull); every read of it is bounds-checked against rtmask_words
     uint32_t* rtmask;
-    int32_t rt_persp, pad;
+    int32_t rt_persp, rtmask_words;
 };
 constexpr int32_t FMT_MASK = 0xff;
 constexpr int32_t FMT_RGB8_DWORDS = 0x100;
@@ -372,5 +373,8 @@ int launch_vp_shade(const ShadeArgs& a, const double* szbuf, const double* gh, c
                     const int32_t* gid, float* out, void* stream);
 int launch_vp_trace(const TraceArgs& a, double* zbuf, double* gh, int32_t* gid, double* gn, void* stream);
 int launch_fill(double* p, int64_t n, double v, int32_t* ip, int32_t iv, void* stream);
+// The device's count of out-of-range side-table reads (skipped, not performed), then
+// cleared; blocking on `stream`.
+int read_oob_reads(unsigned long long* count, void* stream);
 
 }  // namespace rtm

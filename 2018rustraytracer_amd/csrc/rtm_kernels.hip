@@ -48,6 +48,17 @@ __device__ __forceinline__ uint32_t enc_byte(float c, const float* __restrict__ 
 }
 
 
+// Out-of-range reads of the host-built side tables (the per-wave primitive masks,
+// the coded tile's row records): every read of them is checked against the table's
+// length; an index past it is counted here and not performed (the lanes that would
+// make it are dead: rows past the launch's part).  rtm_ctx_oob_reads reads and
+// clears the count; tests/test_bounds.py requires 0.
+__device__ unsigned long long g_oob_reads;
+
+__device__ __forceinline__ void note_oob() {
+    if ((threadIdx.x & 63) == __builtin_ctzll(__ballot(1))) atomicAdd(&g_oob_reads, 1ull);
+}
+
 // main.rs:306-307 / 1903-1907: ((i as f64) / (res as f64)) * 2.0 - 1.0
 __device__ __forceinline__ double ndc(int i, int res) { return ((double)i / (double)res) * 2.0 - 1.0; }
 
@@ -1033,8 +1044,16 @@ using CBatch = const __attribute__((address_space(4))) BatchFrame;
 // the reference's rasterize-then-march order.
 // Needs 1 <= steps <= CODED_MAX_STEPS (LDS) when marching, and a coded map.
 constexpr int CODED_MAX_STEPS = 1023;  // (steps + 1) * 32 B <= 32 KiB of LDS
-constexpr int CODED_ROWS = 16;          // rows per wave
+constexpr int CODED_ROWS = 16;          // rows per strip (a wave's rows in PART 0 / 1)
 constexpr int CODED_TILE_ROWS = CODED_ROWS * TILE_Y;
+// PART 2 (the sphere strips of a split launch) runs 4-row waves, a strip per
+// workgroup: the sphere raster is most of its work and 16-row waves left it with too
+// few waves to hide its latency (2,800 per 8-frame launch at config 3: 37.9 instead of
+// 24 us, profiles/r04_v3_*); its march codes take the per-texel check.
+template <int PART>
+constexpr int coded_wave_rows = PART == 2 ? 4 : CODED_ROWS;
+template <int PART>
+constexpr int coded_tile_rows = coded_wave_rows<PART> * TILE_Y;
 constexpr uint32_t CODE_NONE = 0xFFFFu;  // packed-code +INF (also the U8 map's 0xFF)
 // Two 16-bit codes per register (low: column 0, high: column 1), element-wise min.
 typedef unsigned short ushort2_t __attribute__((ext_vector_type(2)));
@@ -1073,12 +1092,12 @@ __device__ __forceinline__ uint32_t code_check(const ZRecK* __restrict__ T, doub
 template <bool INC, int CODE, int PART>
 __device__ __forceinline__ void shadow_tile_coded(const ShadowPart& a, void* __restrict__ map, int bx, int by,
                                                   ZRecK* __restrict__ T, RowLdsK* __restrict__ RL) {
-    constexpr int NR = CODED_ROWS;
+    constexpr int NR = coded_wave_rows<PART>;
     const int lane = threadIdx.x & (TILE_X - 1);
     const int wv = threadIdx.x >> 6;
     const int xb = bx * 128;
     const int x0 = xb + lane * 2;
-    const int y0 = __builtin_amdgcn_readfirstlane(by * CODED_TILE_ROWS + wv * NR);
+    const int y0 = __builtin_amdgcn_readfirstlane(by * coded_tile_rows<PART> + wv * NR);
     const int W = a.W, H = a.H, steps = a.steps;
     const bool march = !(a.flags & RTM_FLAG_NO_MARCH) && a.n_patches > 0 && steps > 0;
     // the LDS records: one per thread, loaded now, written before the barrier
@@ -1097,12 +1116,18 @@ __device__ __forceinline__ void shadow_tile_coded(const ShadowPart& a, void* __r
         c0 = a.tab.col[xs0];
         c1 = a.tab.col[xs1];
         // (the host pads the row table with non-marching rows to a multiple of 64 rows:
-        // y0 + 15 is inside it, no clamp)
-        if (lane < NR) rl = a.tab.row[y0 + lane];
+        // y0 + 15 is inside it; checked all the same)
+        if (lane < NR) {
+            if (y0 + NR <= a.tab.row_recs) rl = a.tab.row[y0 + lane];
+            else note_oob();
+        }
     }
     // this wave's strip is left to the other part of a split launch (wave-uniform); a
-    // skipping wave still fills its records and meets the workgroup barrier
-    const bool strip_box = !(a.flags & RTM_FLAG_NO_SHADOW_RASTER) && union_may_cover(a, xb, xb + 127, y0, y0 + NR - 1);
+    // skipping wave still fills its records and meets the workgroup barrier.  The
+    // split is decided per 16-row strip (a PART 2 wave's 4 rows lie in one)
+    const int s0 = y0 & ~(CODED_ROWS - 1);
+    const bool strip_box =
+        !(a.flags & RTM_FLAG_NO_SHADOW_RASTER) && union_may_cover(a, xb, xb + 127, s0, s0 + CODED_ROWS - 1);
     const bool skipw = (PART == 1 && strip_box) || (PART == 2 && !strip_box);
     // a row's two codes packed in one register (low: column 0), NONE = 0xFFFF
     uint32_t cdp[NR];
@@ -1140,7 +1165,7 @@ __device__ __forceinline__ void shadow_tile_coded(const ShadowPart& a, void* __r
             // (finite), dd = 0: entry and okA are false there, so it neither hits nor
             // goes slow -- no per-texel in-range test.
             // -- the shortcut: both ends of each column's strip
-            bool sc = rowbits == (1u << NR) - 1u;  // every row marches (wave-uniform)
+            bool sc = NR == CODED_ROWS && rowbits == (1u << NR) - 1u;  // every row marches (wave-uniform)
             uint32_t top[2] = {CODE_NONE, CODE_NONE}, bot[2] = {CODE_NONE, CODE_NONE};
             int bnd[2] = {NR, NR};  // first row with the bottom code (NR: none)
             if (sc) {
@@ -1166,7 +1191,7 @@ __device__ __forceinline__ void shadow_tile_coded(const ShadowPart& a, void* __r
                     const bool need[2] = {need0, need1};
                     bool bad = false;
 #pragma unroll
-                    for (int it = 0; it < 4; ++it) {  // 15 rows: 4 halvings
+                    for (int it = 0; it < 4; ++it) {  // 15 rows: 4 halvings (NR == 16 here)
 #pragma unroll
                         for (int c = 0; c < 2; ++c) {
                             const bool act = need[c] & (hi[c] - lo[c] > 1);
@@ -1354,7 +1379,7 @@ __device__ __forceinline__ void shadow_tile_coded(const ShadowPart& a, void* __r
 template <bool INC, int CODE, int PART>
 __device__ __forceinline__ void shadow_coded_block(const ShadowPart& sh, void* __restrict__ map, char* __restrict__ lds,
                                                    int4 org) {
-    constexpr int TR = CODED_TILE_ROWS;
+    constexpr int TR = coded_tile_rows<PART>;
     int bx = (int)blockIdx.x, by;
     if (PART == 0) {
         const int n = (int)gridDim.y;
@@ -1369,7 +1394,7 @@ __device__ __forceinline__ void shadow_coded_block(const ShadowPart& sh, void* _
         by = (int)blockIdx.y + org.y;
         const bool rast = !(sh.flags & RTM_FLAG_NO_SHADOW_RASTER);
         const int ya = by * TR;
-        const int sub = CODED_ROWS;
+        const int sub = CODED_ROWS;  // (PART 1's waves; a PART 2 workgroup is one 16-row strip)
         const int xa = bx * 128, xe = xa + 127;
         if (PART == 2 ? !(rast && union_may_cover(sh, xa, xe, ya, ya + TR - 1))
                       : (rast && union_may_cover(sh, xa, xe, ya, ya + sub - 1) &&
@@ -1441,10 +1466,15 @@ __device__ __forceinline__ void eye_tile(const EyePart& a, const ShadowPart& sh,
                          : 0u;
     // the wave's ray-traced primitives (PERSPECTIVE eye; all lanes active here)
     uint32_t rmask = ~0u;
-    if (RTP && tabs.rtmask && a.row_begin + yl < a.row_end)  // (no mask word for rows past the part)
-        rmask = ((const __attribute__((address_space(4))) uint32_t*)tabs.rtmask)[yl * ((a.W + TILE_X - 1) / TILE_X) +
-                                                                                 (xb / TILE_X)];
-    else if (RTB == 1 && rt && a.eye.type == RTM_CAMERA_PERSPECTIVE)
+#ifndef RTM_TEST_REVERT_MASK_GUARD
+    if (RTP && tabs.rtmask && a.row_begin + yl < a.row_end) {  // (no mask word for rows past the part)
+#else  // (tools/bounds_demo.sh only: the round-3 over-read, to show tests/test_bounds.py catches it)
+    if (RTP && tabs.rtmask) {
+#endif
+        const int widx = yl * ((a.W + TILE_X - 1) / TILE_X) + (xb / TILE_X);  // (wave-uniform)
+        if (widx < tabs.rtmask_words) rmask = ((const __attribute__((address_space(4))) uint32_t*)tabs.rtmask)[widx];
+        else note_oob();
+    } else if (RTB == 1 && rt && a.eye.type == RTM_CAMERA_PERSPECTIVE)
         rmask = rt_wave_mask(rt, a.eye, min(xb, a.W - 1), min(xb + TILE_X - 1, a.W - 1), min(yi, a.H - 1), a.W, a.H);
     float4 c = make_float4(0.0f, 0.2f, 0.2f, 1.0f);  // (0.0, 0.2, 0.2) as f32 (main.rs:718-720)
     bool shaded = false;
@@ -1987,13 +2017,18 @@ static void launch_coded(const ShadowPart& sh, const FrameArgs* a, double* smap,
     const double box_frac = raster ? (double)std::max(bx1 - bx0 + 1, 0) * (double)std::max(by1 - by0 + 1, 0) /
                                          ((double)gx * (double)gy)
                                    : 0.0;
+    // PART 2's workgroup tiles (one 16-row strip each) over the box's rows
+    constexpr int TR2 = coded_tile_rows<2>;
+    const int gy2 = (sh.H + TR2 - 1) / TR2;
+    const int c0 = raster ? std::max(b[2], 0) / TR2 : 0;
+    const int c1 = raster ? std::min(std::max(b[3], 0) / TR2, gy2 - 1) : -1;
     static const double split_max = [] {
         const char* e = getenv("RTM_CODED_SPLIT_MAX");
         return e ? atof(e) : 0.3;
     }();
     const bool split = box_frac <= split_max;
-    dim3 gb((unsigned)std::max(bx1 - bx0 + 1, 0), (unsigned)std::max(by1 - by0 + 1, 0), g.z);
-    const int4 orgb = make_int4(bx0, by0, TR, 0);
+    dim3 gb((unsigned)std::max(bx1 - bx0 + 1, 0), (unsigned)std::max(c1 - c0 + 1, 0), g.z);
+    const int4 orgb = make_int4(bx0, c0, TR2, 0);
 #define RTM_CK(I, M, P, G, O)                                                                                     \
     do {                                                                                                        \
         if (fr) hipLaunchKernelGGL((shadow_coded_batch_kernel<I, M, P>), G, dim3(BLOCK), lsm, s, fr, O);          \
@@ -2187,6 +2222,17 @@ int launch_eye_batch(const BatchFrame* dev, int n, const FrameArgs& a0, const De
     else if (fmt == RTM_FORMAT_RGB8) launch_eye_fmt<RTM_FORMAT_RGB8>(a0, nullptr, nullptr, s, g, fused, t0, fr);
     else launch_eye_fmt<RTM_FORMAT_RGBA32F>(a0, nullptr, nullptr, s, g, fused, t0, fr);
     return launched();
+}
+
+int read_oob_reads(unsigned long long* count, void* stream) {
+    const unsigned long long zero = 0ull;
+    if (hipMemcpyFromSymbolAsync(count, HIP_SYMBOL(g_oob_reads), sizeof zero, 0, hipMemcpyDeviceToHost,
+                                 (hipStream_t)stream) != hipSuccess ||
+        hipMemcpyToSymbolAsync(HIP_SYMBOL(g_oob_reads), &zero, sizeof zero, 0, hipMemcpyHostToDevice,
+                               (hipStream_t)stream) != hipSuccess ||
+        hipStreamSynchronize((hipStream_t)stream) != hipSuccess)
+        return RTM_ERR_HIP;
+    return 0;
 }
 
 int launch_pull(const void* src_host, size_t bytes, void* dst, void* stream) {

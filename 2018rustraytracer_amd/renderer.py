@@ -350,6 +350,13 @@ class Group:
         abi.check(lib, lib.rtm_group_info(self._h, C.byref(n), C.byref(loc), C.byref(first)), "rtm_group_info")
         return int(n.value), int(loc.value), int(first.value)
 
+    def member_lanes(self, local: int = 0) -> int:
+        """Lanes local member `local`'s context used for the last frame call."""
+        lib = _lib()
+        n = C.c_int32()
+        abi.check(lib, lib.rtm_ctx_last_lanes(lib.rtm_group_ctx(self._h, local), C.byref(n)), "rtm_ctx_last_lanes")
+        return int(n.value)
+
     def ctx_stream(self, local: int = 0) -> int:
         lib = _lib()
         c = lib.rtm_group_ctx(self._h, local)

@@ -220,6 +220,12 @@ int rtm_ctx_synchronize(rtm_ctx* ctx);
 int rtm_ctx_alloc(rtm_ctx* ctx, int64_t bytes, void** out_dev);
 int rtm_ctx_free(rtm_ctx* ctx, void* dev);
 int rtm_ctx_copy_to_host(rtm_ctx* ctx, const void* dev, void* host, int64_t bytes);
+/* ABI v10, diagnostic: the kernels check every read of their host-built side tables
+ * (per-wave primitive masks, row records) against the table's length and skip an
+ * out-of-range one.  *count receives how many were skipped on the context's device
+ * since the last call (every kernel enqueued before it included), and the count is
+ * cleared.  0 on a correct library; tests/test_bounds.py requires it. */
+int rtm_ctx_oob_reads(rtm_ctx* ctx, int64_t* count);
 /* Durations in ms of the last render's two kernels, from HIP events recorded on
  * the context stream around each launch (valid after rtm_ctx_synchronize). */
 int rtm_ctx_last_kernel_ms(rtm_ctx* ctx, float* shadow_pass_ms, float* eye_pass_ms);
@@ -391,7 +397,9 @@ int rtm_group_render_async(rtm_group* g, const rtm_scene* scene, const rtm_camer
                            const rtm_camera* shadow, int32_t width, int32_t height, int32_t march_steps,
                            int32_t flags, int32_t format, int32_t root, void* out_dev);
 /* A sequence of frames, frame i into out_dev[i] (entries ignored off the root);
- * every frame's inputs are validated before the first is enqueued. */
+ * every frame's inputs are validated before the first is enqueued.  Each member
+ * renders its parts in chunks of frames (one launch per pass per chunk), spread over
+ * its context's lanes as rtm_render_frames_async spreads its batches. */
 int rtm_group_render_frames_async(rtm_group* g, int32_t n_frames, const rtm_scene* scenes,
                                   const rtm_camera* eye, const rtm_camera* shadow, int32_t width, int32_t height,
                                   int32_t march_steps, int32_t flags, int32_t format, int32_t root,
@@ -422,8 +430,10 @@ int rtm_group_set_root_staging(rtm_group* g, int32_t on);
  * its stripes compact and the root places them: a 2-D copy per part); 0: contiguous
  * bands of ceil(H/N) rows (SURVEY.md §8e's first form); -1: the default, 8-row
  * stripes for N > 1 (bands measured 1.26-1.56x max/mean band time at N = 4-8, the
- * spheres sit mid-frame; stripes even it out).  RTM_GROUP_STRIPE overrides the
- * default.  Waits for the group's work first.  rtm_group_partition: the S in use. */
+ * spheres sit mid-frame; stripes even it out).  Collective: in a one-process-per-GPU
+ * group every rank must set the same value before its next frame (the default
+ * depends on the rank count only).  stripe_rows * n_ranks <= 8 * RTM_MAX_DIM.  Waits
+ * for the group's work first.  rtm_group_partition: the S in use. */
 int rtm_group_set_partition(rtm_group* g, int32_t stripe_rows);
 int32_t rtm_group_partition(rtm_group* g);
 /* ABI v9: part `part` of n_parts of the frame under stripe_rows-row cyclic stripes

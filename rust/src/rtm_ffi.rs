@@ -176,6 +176,7 @@ extern "C" {
     pub fn rtm_ctx_alloc(ctx: *mut rtm_ctx, bytes: i64, out_dev: *mut *mut c_void) -> i32;
     pub fn rtm_ctx_free(ctx: *mut rtm_ctx, dev: *mut c_void) -> i32;
     pub fn rtm_ctx_copy_to_host(ctx: *mut rtm_ctx, dev: *const c_void, host: *mut c_void, bytes: i64) -> i32;
+    pub fn rtm_ctx_oob_reads(ctx: *mut rtm_ctx, count: *mut i64) -> i32;
     pub fn rtm_ctx_last_kernel_ms(ctx: *mut rtm_ctx, shadow_pass_ms: *mut f32, eye_pass_ms: *mut f32) -> i32;
     pub fn rtm_ctx_set_timing_capacity(ctx: *mut rtm_ctx, capacity: i32) -> i32;
     pub fn rtm_ctx_set_timing_stride(ctx: *mut rtm_ctx, stride: i32) -> i32;

@@ -225,3 +225,58 @@ def test_render_stripes_matches_oracle_rows(rtm, oracle, scenes, gpu_ctx, S, n):
             gpu_ctx.synchronize()
             got = to_host(out, rows, w, f, rtm.abi)
             assert np.array_equal(got.view(np.uint8), want[f][shard.stripe_image_rows(h, n, S, r)].view(np.uint8)), (f, r)
+
+
+def test_loopback_root_moves_between_calls(rtm, oracle, scenes):
+    """The root changes from call to call on one group (8-row stripes: the parts land in
+    the root's receive staging, the same buffer and placement code as over RCCL, which
+    is reallocated when the root moves): every frame == the oracle's."""
+    import torch
+    c = scenes.CONFIGS[2]
+    w, h, k = c["width"], c["height"], c["steps"]
+    s = scenes.scene_a_bench(100)
+    g = rtm.Group(n_devices=5, loopback=True)
+    try:
+        assert g.partition == 8
+        want = want_cached(oracle, rtm, scenes, 2, 100, 0)
+        for root in (0, 3, 4, 1, 0):
+            out = device_out(torch, rtm, h, w, 0)
+            out.fill_(7.0)
+            torch.cuda.synchronize()
+            g.render_async(s, scenes.eye_camera(), scenes.shadow_camera(), w, h, k, c["flags"], 0, root,
+                           out.data_ptr())
+            g.synchronize(120000)
+            got = to_host(out, h, w, 0, rtm.abi)
+            assert np.array_equal(got.view(np.uint32), want.view(np.uint32)), root
+    finally:
+        g.close()
+
+
+@pytest.mark.parametrize("n", [1, 3])
+def test_group_sequence_spreads_chunks_over_lanes(rtm, oracle, scenes, n):
+    """A long sequence: every member's chunks (frames per launch of its part) go to its
+    context's lanes (4 below 16 Mpixel), as rtm_render_frames_async's batches do; frames
+    sampled across the chunks == the oracle's (N = 1: the RCCL group, rendered in place)."""
+    import torch
+    w, h, k = 1920, 1080, 32
+    eye, sh = scenes.eye_camera(), scenes.shadow_camera()
+    frames = [scenes.scene_a_bench(100 + i) for i in range(96)]
+    g = rtm.Group(n_devices=1) if n == 1 else rtm.Group(n_devices=n, loopback=True)
+    try:
+        bufs = [device_out(torch, rtm, h, w, 0) for _ in frames]
+        torch.cuda.synchronize()
+        g.render_frames_async(frames, eye, sh, w, h, k, 0, 0, 0, [b.data_ptr() for b in bufs])
+        g.synchronize(120000)
+        # chunks of the library's auto frames per launch for member 0's part; lanes: 4 at most
+        shard = __import__("importlib").import_module("2018rustraytracer_amd.shard")
+        px = w * (shard.stripe_rows_of(h, n, 8, 0) if n > 1 else h)
+        per = max(1, min(len(frames), 64 if px < (1 << 20) else 32, (64 << 20) // px))
+        assert g.member_lanes(0) == min(4, -(-len(frames) // per))  # n = 1: 3 chunks of 32; n = 3: 2 of 64
+        for i in (0, 31, 32, 63, 64, 95):
+            fl = rtm.abi.RTM_FLAG_FUSED_SHADOW if n > 1 else 0
+            want = oracle.render(frames[i], eye, sh, w, h, k, fl, nthreads=NT)["rgba"]
+            got = to_host(bufs[i], h, w, 0, rtm.abi)
+            assert np.array_equal(got.view(np.uint32), want.view(np.uint32)), i
+    finally:
+        g.close()
+        torch.cuda.empty_cache()
