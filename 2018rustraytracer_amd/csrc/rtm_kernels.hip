@@ -516,26 +516,29 @@ __device__ __forceinline__ void icapped_normal(const CylK& c, const double ro[3]
 }
 
 // ---- row f-4: the GL preview's SDF, the f64 restatement of oracle/rtm_oracle.c ----
-// min/max: NaN-ignoring with +0 > -0 (a NaN a gives b, a NaN b gives a; a tie
-// gives a unless the signs of zero decide); sign: GLSL (0 for 0 and NaN).  All
-// branch-free: the predicates combine with bitwise ops into one select, so the
-// march loop stays straight-line code (nested ternaries compiled to exec-mask
-// branches, ~4x the instructions).
+// min/max: NaN-ignoring with +0 > -0 (a NaN a gives b, a NaN b gives a; a tie gives
+// a unless the signs of zero decide): IEEE 754-2019 minimumNumber / maximumNumber,
+// which v_min_f64 / v_max_f64 implement (one instruction each; the oracle's
+// compare-and-select form gives the same value, NaN payloads aside, which never
+// reach the output: a NaN distance never hits).  sign: GLSL (0 for 0 and NaN).
+// (inline asm: the builtins' sNaN canonicalisation is not needed -- every operand is an
+// arithmetic result -- and with them the allocator spilled 74 VGPRs in the SDF kernel)
 __device__ __forceinline__ double fmax_d(double a, double b) {
-    const bool take_a = !(a != a) & ((a > b) | (b != b) | ((a == b) & !__builtin_signbit(a)));
-    return take_a ? a : b;
+    double r;
+    asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
 }
 __device__ __forceinline__ double fmin_d(double a, double b) {
-    const bool take_a = !(a != a) & ((a < b) | (b != b) | ((a == b) & __builtin_signbit(a)));
-    return take_a ? a : b;
+    double r;
+    asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
 }
 // fmax_d(x, +0.0) and fmin_d(x, +0.0)
-__device__ __forceinline__ double fmax0_d(double x) { return x > 0.0 ? x : 0.0; }
-__device__ __forceinline__ double fmin0_d(double x) { return (__builtin_signbit(x) & !(x != x)) ? x : 0.0; }
+__device__ __forceinline__ double fmax0_d(double x) { return __builtin_fmaximum_num(x, 0.0); }
+__device__ __forceinline__ double fmin0_d(double x) { return __builtin_fminimum_num(x, 0.0); }
 // fmin_d(fmax_d(x, 0.0), 1.0)
 __device__ __forceinline__ double clamp01_d(double x) {
-    const double v = x > 0.0 ? x : 0.0;
-    return v < 1.0 ? v : 1.0;
+    return __builtin_fminimum_num(__builtin_fmaximum_num(x, 0.0), 1.0);
 }
 // clamp01_d(x / d) for an edge parameter, d = |edge|^2 (>= 0, per-SDF constant):
 // the IEEE division only where the quotient can land inside (0, 1).  x <= 0 or NaN
@@ -625,13 +628,21 @@ __device__ __forceinline__ bool sdf_slabs(const double ro[3], const double m[3],
 
 // The implicit-surface branch of bvhProcessLeafHit (entry.frag:842-905):
 // t of the hit or -1, and the sdNormalFast normal.  m = 1/rd, am = |m|.
+// NEAR (the render kernels): zb is the pixel's nearest surface so far, and the
+// caller accepts a hit only at t < zb (entry.frag:908-917).  t starts at the AABB
+// entry tIn and only grows (a step adds a distance >= 0.03), so once t >= zb neither
+// a later hit nor a miss can change the pixel: the trace stops there and reports a
+// miss -- the same pixel, without the steps (and the normal) that could not count.
+// The counting kernel (rtm_render_stats) keeps every step the shader takes.
+template <bool NEAR = false>
 __device__ __forceinline__ double sdf_trace(const SdfK& g, const double ro[3], const double rd[3], const double m[3],
-                                            const double am[3], double n[3], uint32_t& evals) {
+                                            const double am[3], double n[3], uint32_t& evals, double zb = 0.0) {
     double tIn, tOut;
     if (!sdf_slabs(ro, m, am, g, tIn, tOut)) return -1.0;
     double t = tIn;
     bool hit = false;
     for (int step = 0; step < g.steps; ++step) {
+        if (NEAR && !(t < zb)) break;  // (a NaN t never hits either)
         const double p[3] = {ro[0] + rd[0] * t, ro[1] + rd[1] * t, ro[2] + rd[2] * t};
         const double dist = sdf_dist(g, p);
         ++evals;
@@ -669,6 +680,7 @@ struct RtHit {
     double n[3];
 };
 
+template <bool NEAR = false>
 __device__ __forceinline__ void trace_sdfs(const SdfTabK* __restrict__ sdf, const double o[3], const double d[3],
                                            double zb, RtHit& hit, uint32_t& evals) {
     const int ns = sdf->n;
@@ -676,7 +688,7 @@ __device__ __forceinline__ void trace_sdfs(const SdfTabK* __restrict__ sdf, cons
     const double am[3] = {fabs(m[0]), fabs(m[1]), fabs(m[2])};
     for (int i = 0; i < ns; ++i) {
         double n[3];
-        const double t = sdf_trace(sdf->s[i], o, d, m, am, n, evals);
+        const double t = sdf_trace<NEAR>(sdf->s[i], o, d, m, am, n, evals, zb);
         if (!(t > 0.0) || !(t < zb)) continue;  // the shader's acceptance (entry.frag:908-917)
         hit.kind = 4;
         hit.id = sdf->s[i].id;
@@ -1055,6 +1067,12 @@ constexpr int coded_wave_rows = PART == 2 ? 4 : CODED_ROWS;
 template <int PART>
 constexpr int coded_tile_rows = coded_wave_rows<PART> * TILE_Y;
 constexpr uint32_t CODE_NONE = 0xFFFFu;  // packed-code +INF (also the U8 map's 0xFF)
+// The BACK-face depth range of a sphere's covered texels: fl(z + fl(h*r)), h in (0, 1].
+__device__ __forceinline__ void sphere_range(const RasterSphereK& s, double& lo, double& hi) {
+    const double e = s.z + s.r;
+    lo = s.r >= 0.0 ? s.z : e;
+    hi = s.r >= 0.0 ? e : s.z;
+}
 // Two 16-bit codes per register (low: column 0, high: column 1), element-wise min.
 typedef unsigned short ushort2_t __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint32_t pk_min_u16(uint32_t a, uint32_t b) {
@@ -1283,16 +1301,135 @@ __device__ __forceinline__ void shadow_tile_coded(const ShadowPart& a, void* __r
         }
     }
     // shadow viewport rasterize, face BACK (main.rs:1569, 243), 4 rows at a time: the
-    // strict minimum over the spheres in scene order (zs, cs), then the march code only
-    // where its t is strictly below that minimum (main.rs:559)
+    // strict minimum over the spheres in scene order, then the march code only where its
+    // t is strictly below that minimum (main.rs:559).
+    //
+    // A covered texel's BACK-face depth is fl(z + fl(h*r)) with h = sqrt(1 - d*d) in
+    // (0, 1], so it lies in the sphere's range [z, fl(z + r)] (rounding is monotone; the
+    // ends swap for r < 0), and coverage d < 1 is exactly s2 < 1 (sqrt is monotone and
+    // the square root of the double below 1 is below 1).  When the ranges of a wave's
+    // spheres are pairwise disjoint (wave-uniform), the nearest covering sphere is the
+    // one with the lowest range -- the strict minimum in scene order picks it too -- and
+    // the march beats it exactly when its t is below the range, loses when t is at or
+    // above the range's top: no square root is taken.  Only a texel whose t falls inside
+    // its winner's range, and waves with overlapping ranges, evaluate the depths.
     if (PART != 1 && strip_box && !skipw) {
         const uint32_t live0 = wave_sphere_mask(a.sph, a.n_spheres, xb, xb + 127, y0, y0 + NR - 1);
         if (live0) {
             const double xc[2] = {a.tab.nx[xs0], a.tab.nx[xs1]};
+            bool disjoint = true;  // (wave-uniform)
+            for (uint32_t li = live0; li && disjoint; li &= li - 1u) {
+                double loi, hii;
+                sphere_range(a.sph[__builtin_ctz(li)], loi, hii);
+                disjoint = __builtin_isfinite(loi) & __builtin_isfinite(hii);
+                for (uint32_t lj = li & (li - 1u); lj && disjoint; lj &= lj - 1u) {
+                    double loj, hij;
+                    sphere_range(a.sph[__builtin_ctz(lj)], loj, hij);
+                    disjoint = (hii < loj) | (hij < loi);
+                }
+            }
 #pragma unroll
             for (int b = 0; b < NR / 4; ++b) {
                 const int yb = y0 + 4 * b;
                 if (yb >= H) break;  // (wave-uniform)
+                if (disjoint) {
+                    // t of each texel's march code (NONE: T[steps].t = +INF; no march: +INF)
+                    double tm[4][2];
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+#pragma unroll
+                        for (int c = 0; c < 2; ++c) {
+                            const uint32_t mc = (cdp[4 * b + r] >> (16 * c)) & 0xFFFFu;
+                            tm[r][c] = march ? T[min(mc, (uint32_t)steps)].t : INFINITY;
+                        }
+                    uint32_t wc[4];     // packed winner codes (NONE: not covered)
+                    uint32_t dec = 0u;  // 2 bits per texel (r, c) at 4r + 2c: 0 march, 1 sphere, 2 undecided
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) wc[r] = 0xFFFFFFFFu;
+                    bool any = false;
+                    // farthest range first: a nearer covering sphere overwrites
+                    for (uint32_t rem = live0; rem;) {
+                        int i = __builtin_ctz(rem);
+                        double best = -INFINITY;
+                        for (uint32_t l = rem; l; l &= l - 1u) {
+                            double lo, hi;
+                            sphere_range(a.sph[__builtin_ctz(l)], lo, hi);
+                            if (lo > best) {
+                                best = lo;
+                                i = __builtin_ctz(l);
+                            }
+                        }
+                        rem &= ~(1u << i);
+                        const RasterSphereK& sp = a.sph[i];
+                        if (yb + 3 < sp.iy0 || yb > sp.iy1) continue;  // wave-uniform
+                        double lo, hi;
+                        sphere_range(sp, lo, hi);
+                        double pa2[2];
+#pragma unroll
+                        for (int c = 0; c < 2; ++c) {
+                            const double pa = ((xc[c] - sp.cx) * sp.n) / sp.m;
+                            pa2[c] = pa * pa;
+                        }
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            const int y = yb + r;
+                            if (y >= H || y < sp.iy0 || y > sp.iy1) continue;  // wave-uniform
+                            const double pb = ((((cdouble*)a.tab.ny)[y] - sp.cy) * sp.n) / sp.m;
+                            const double pb2 = pb * pb;
+#pragma unroll
+                            for (int c = 0; c < 2; ++c) {
+                                const bool in = pa2[c] + pb2 < 1.0;  // d = sqrt(pa*pa + pb*pb) < 1
+                                any |= in;
+                                const uint32_t sh16 = 16u * (uint32_t)c, sh2 = 4u * (uint32_t)r + 2u * (uint32_t)c;
+                                const uint32_t v = tm[r][c] < lo ? 0u : tm[r][c] >= hi ? 1u : 2u;
+                                wc[r] = in ? (wc[r] & ~(0xFFFFu << sh16)) | ((uint32_t)(steps + i) << sh16) : wc[r];
+                                dec = in ? (dec & ~(3u << sh2)) | (v << sh2) : dec;
+                            }
+                        }
+                    }
+                    if (!__any(any)) continue;
+                    // texels whose t lies inside their winner's range: that sphere's depth
+                    uint32_t amb = 0u;
+#pragma unroll
+                    for (int q = 0; q < 8; ++q) amb |= ((dec >> (2 * q)) & 3u) == 2u ? 1u << q : 0u;
+                    if (__any(amb != 0u)) {
+                        for (uint32_t l = live0; l; l &= l - 1u) {
+                            const int j = __builtin_ctz(l);
+                            const RasterSphereK& sp = a.sph[j];
+                            double pa[2];
+#pragma unroll
+                            for (int c = 0; c < 2; ++c) pa[c] = ((xc[c] - sp.cx) * sp.n) / sp.m;
+#pragma unroll
+                            for (int r = 0; r < 4; ++r)
+#pragma unroll
+                                for (int c = 0; c < 2; ++c) {
+                                    const uint32_t sh16 = 16u * (uint32_t)c;
+                                    const bool mine = ((amb >> (2 * r + c)) & 1u) &&
+                                                      ((wc[r] >> sh16) & 0xFFFFu) == (uint32_t)(steps + j);
+                                    if (!__any(mine)) continue;
+                                    const double pb = ((((cdouble*)a.tab.ny)[yb + r] - sp.cy) * sp.n) / sp.m;
+                                    const double d = sqrt(pa[c] * pa[c] + pb * pb);
+                                    const double h = sqrt(1.0 - d * d);
+                                    const double depth = sp.z + h * sp.r;
+                                    const uint32_t sh2 = 4u * (uint32_t)r + 2u * (uint32_t)c;
+                                    const uint32_t v = tm[r][c] < depth ? 0u : 1u;
+                                    dec = mine ? (dec & ~(3u << sh2)) | (v << sh2) : dec;
+                                }
+                        }
+                    }
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+#pragma unroll
+                        for (int c = 0; c < 2; ++c) {
+                            const uint32_t sh16 = 16u * (uint32_t)c;
+                            const bool sph = ((wc[r] >> sh16) & 0xFFFFu) != CODE_NONE &&
+                                             ((dec >> (4 * r + 2 * c)) & 3u) == 1u;
+                            cdp[4 * b + r] = sph ? (cdp[4 * b + r] & ~(0xFFFFu << sh16)) | (wc[r] & (0xFFFFu << sh16))
+                                                 : cdp[4 * b + r];
+                        }
+                    continue;
+                }
+                // overlapping ranges: every covering sphere's depth, the strict minimum (zs, cs)
                 double zs[4][2];
                 uint32_t cs[4];  // packed sphere codes, NONE = no sphere covers
 #pragma unroll
@@ -1322,9 +1459,7 @@ __device__ __forceinline__ void shadow_tile_coded(const ShadowPart& a, void* __r
                             s2[c] = pa[c] * pa[c] + pb * pb;
                             in |= s2[c] < 1.0;
                         }
-                        // sqrt is monotone with sqrt(1) == 1, so d < 1 implies s2 < 1: a wave
-                        // with no s2 < 1 has no covered texel in this row and skips both sqrts
-                        if (!__any(in)) continue;
+                        if (!__any(in)) continue;  // (d < 1 <=> s2 < 1: no covered texel in this row)
                         any = true;
 #pragma unroll
                         for (int c = 0; c < 2; ++c) {
@@ -1514,7 +1649,8 @@ __device__ __forceinline__ void eye_tile(const EyePart& a, const ShadowPart& sh,
                     n_cy_tests = __builtin_popcount((rmask >> 16) & ((1u << rt->n_cy) - 1u));
                 }
             }
-            if (RT == 2 && sdf) trace_sdfs(sdf, o, d, zb, hit, n_evals);  // (a batch mixes frames with and without SDFs)
+            // (a batch mixes frames with and without SDFs)
+            if (RT == 2 && sdf) trace_sdfs<!COUNT>(sdf, o, d, zb, hit, n_evals);
         }
         if (hit.kind) {
             shaded = true;

@@ -57,7 +57,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--frames-per-step", type=int, default=0,
-                    help="frames of one step (0 = auto: at least 8 and at least 512 Mpixel worth, at most 256)")
+                    help="frames of one step (0 = auto: at least 8 and at least 8 Gpixel worth, at most 4096)")
     ap.add_argument("--config", type=int, default=3,
                     help="scenes.CONFIGS id: 1-5 BASELINE, 6-7 row f-1, 8 row f-4, 9 general march (tilted sun)")
     ap.add_argument("--mode", choices=["frames", "tile-gather"], default="frames")
@@ -72,7 +72,7 @@ def parse():
                          "with several ranks on one GPU (timing tensors and tile-gather bands on the CPU)")
     ap.add_argument("--format", choices=["rgba32f", "rgba8"], default="rgba32f",
                     help="tile-gather mode: what is rendered and gathered")
-    ap.add_argument("--tile-gather-steps", type=int, default=200,
+    ap.add_argument("--tile-gather-steps", type=int, default=512,
                     help="frames of the secondary tile-gather measurement (0 = skip it)")
     ap.add_argument("--tile-gather-timeout-s", type=float, default=240.0,
                     help="watchdog of the secondary tile-gather measurement (group set-up included)")
@@ -166,24 +166,22 @@ def tile_gather(rtm, lib, ctx, group, world, rank, dist, tdev, c_scenes, eye, sh
     r0, r1 = shard.row_band(H, world, rank)
     e_c, s_c = eye.to_c(), shadow.to_c()
     if group is not None:
-        # a swap chain of output frames on the root: the library renders a band of up to
-        # 16 frames per launch (distinct outputs), frame i+1.. render while frame i is
-        # gathered
+        # a swap chain of output frames on the root: every member renders its part of a
+        # chunk of frames per launch (distinct outputs), chunks spread over its lanes, and
+        # frame i+1.. render while frame i is gathered
         n_out = 32
         outs = ([torch.empty(W * H * bpp, dtype=torch.uint8, device=dev) for _ in range(n_out)] if rank == 0
                 else [None] * n_out)
-        arr = (rtm.abi.rtm_scene * len(c_scenes))(*[c[0] for c in c_scenes])
-        ptrs = (C.c_void_p * n_out)(*[C.c_void_p(o.data_ptr() if o is not None else 0) for o in outs])
+        ptrs = [C.c_void_p(o.data_ptr() if o is not None else 0) for o in outs]
 
-        def run(first, n):  # one rtm_group_render_frames_async call per <= len(c_scenes) frames
-            done = 0
-            while done < n:
-                k = min(n - done, len(c_scenes))
-                ov = (C.c_void_p * k)(*[ptrs[(first + done + j) % n_out] for j in range(k)])
-                rc = lib.rtm_group_render_frames_async(group.handle, k, arr, C.byref(e_c), C.byref(s_c), W, H, K,
-                                                       flags, fmt, 0, ov)
-                rtm.abi.check(lib, rc, "rtm_group_render_frames_async")
-                done += k
+        def run(first, n):  # ONE rtm_group_render_frames_async call over the n frames, like frames mode
+            if n <= 0:
+                return
+            arr = (rtm.abi.rtm_scene * n)(*[c_scenes[(first + j) % len(c_scenes)][0] for j in range(n)])
+            ov = (C.c_void_p * n)(*[ptrs[(first + j) % n_out] for j in range(n)])
+            rc = lib.rtm_group_render_frames_async(group.handle, n, arr, C.byref(e_c), C.byref(s_c), W, H, K,
+                                                   flags, fmt, 0, ov)
+            rtm.abi.check(lib, rc, "rtm_group_render_frames_async")
 
         def drain():
             group.synchronize(timeout_ms)
@@ -420,11 +418,11 @@ def main():
     cfg = sc.CONFIGS[a.config]
     W, H, K = cfg["width"], cfg["height"], cfg["steps"]
     # frames per step: a step renders F frames of the sequence (at least 8, and at least
-    # 512 Mpixel, at most 256 frames), so a short --steps run still times many
-    # frames-per-launch batches and the lanes' start and drain stay a small share of it
-    # (r03: 512 instead of 256 Mpixel, the driver's --steps 20 run +1 %,
-    # profiles/r03_ab_frames_per_step.txt)
-    F = a.frames_per_step or min(256, max(8, (1 << 29) // (W * H)))
+    # 8 Gpixel, at most 4096 frames: 1035 at 3840x2160, ~25 ms), so the driver's
+    # --steps 20 run times >= 0.5 s of frames, the lanes' start and drain are a small
+    # share of it, and a box's clock and noise average out over it (r03: 512 Mpixel,
+    # a 33 ms timed region)
+    F = a.frames_per_step or min(4096, max(8, (8 << 30) // (W * H)))
     nW, nS = a.warmup * F, a.steps * F  # warmup / timed frames
     tile_mode = a.mode == "tile-gather"
     # tile-gather: each band evaluates only the shadow texels it reads (no cross-rank shadow map)
@@ -435,7 +433,7 @@ def main():
     lib = rtm.load_library()
     # kernel durations: HIP events on every TIMING_STRIDE-th frame of the timed region
     # (an event is a barrier packet; timing every frame would cost ~15% throughput)
-    timing_stride = 10
+    timing_stride = max(10, nS // 1000)  # (at most ~1000 sampled launches: events cost host time to create)
     ctx.set_timing_capacity(max(1, nS // timing_stride))
 
     def scene_for(frame_index: int):
@@ -599,16 +597,16 @@ def main():
         ctx.set_lanes(1)
         ctx.render_frames_async([0] * min(nW, F), eye, shadow, W, H, K, flags, outp[:min(nW, F)],
                                 ctx.prepare_frames(scenes[:min(nW, F)]))
-        ctx.set_timing_capacity(max(1, n1 // timing_stride))
+        ctx.set_timing_capacity(n1)  # every launch of this short pass timed
         one = ctx.prepare_frames(scenes[nW:nW + n1])
         outs_one = ctx.out_array(outp[:n1])
         barrier()
-        ctx.set_timing_stride(timing_stride)
+        ctx.set_timing_stride(1)
         t1 = time.perf_counter()
         ctx.render_frames_async([0] * n1, eye, shadow, W, H, K, flags, outs_one, one)
         barrier()
         el1 = time.perf_counter() - t1
-        sh_ms, eye_ms = ctx.kernel_ms_history((n1 + timing_stride - 1) // timing_stride)
+        sh_ms, eye_ms = ctx.kernel_ms_history(n1)
         b1 = ctx.last_batch()
         launch_batch = b1
         sh_ms, eye_ms = [v / b1 for v in sh_ms], [v / b1 for v in eye_ms]

@@ -117,10 +117,10 @@ def test_bench_tile_gather_gloo_rehearsal_world2(fmt):
 def test_bench_frames_gloo_rehearsal_world2_carries_tile_gather():
     """The default (frames) mode with two ranks also reports the tile-gather figures."""
     res = _run_bench(["--gpus", "2", "--dist-backend", "gloo", "--config", "2", "--steps", "20", "--warmup", "5",
-                      "--preroll-ms", "20", "--tile-gather-steps", "4", "--no-cpu-baseline", "--no-alt"], 2)
+                      "--frames-per-step", "64", "--preroll-ms", "20", "--tile-gather-steps", "4", "--no-cpu-baseline",
+                      "--no-alt"], 2)
     assert res["scaling"] == "weak" and res["n_gpus"] == 2
-    # the auto frame count is a tuning choice: check what it must satisfy (the bench's
-    # minimum; value = both ranks' frames of a step over the step time), not its value
+    # value = both ranks' frames of a step over the step time
     F = res["frames_per_step"]
     assert F >= 8 and res["value"] == pytest.approx(2 * F * 1920 * 1080 / (res["ms_per_step"] * 1e-3) / 1e6, rel=1e-2)
     assert set(res["tile_gather"]) == {"rgba32f", "rgba8"}
