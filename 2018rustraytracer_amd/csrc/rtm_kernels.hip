@@ -791,24 +791,32 @@ __device__ __forceinline__ uint32_t rt_wave_mask(const RtK* __restrict__ rt, con
     const RayCone k = ray_cone(c, xb, xe, yi, W, H);
     double C[3], R;
     bool cullable;
-    rt_bound(rt, threadIdx.x & 63, C, R, cullable);
-    return ~(uint32_t)__ballot(cone_culls(k, c, C, R, cullable));  // lane i < 16: plane i; lane 16 + i: cylinder i
+    const int l = threadIdx.x & 63;
+    rt_bound(rt, l, C, R, cullable);
+    const bool exists = l < 16 ? l < rt->n_pl : l - 16 < rt->n_cy;
+    return (uint32_t)__ballot(exists & !cone_culls(k, c, C, R, cullable));  // lane i < 16: plane i; 16 + i: cylinder i
 }
 
-// rt_wave_mask culls whole primitives per wave: bits 0-15 planes, 16-31
-// cylinders.  A skipped primitive is one no ray of the wave can hit, so zb and
-// the hit are what the full loop would leave.
+// The slot bits of a frame's existing primitives (bits 0-15 planes, 16-31 cylinders).
+__device__ __forceinline__ uint32_t rt_slots(int n_pl, int n_cy) {
+    return ((1u << n_pl) - 1u) | (((1u << n_cy) - 1u) << 16);
+}
+
+// The primitives of `mask` (wave-uniform; bits 0-15 planes, 16-31 cylinders, set only
+// for existing slots: rt_slots, or rt_wave_mask / rt_cull_wave, which also clear the
+// primitives no ray of the wave can hit), in the reference's order (main.rs:575-642):
+// planes by index, then cylinders by index.  A skipped primitive is one no ray of the
+// wave can hit, so zb and the hit are what the full loop would leave.
 // PERSP: the rays start at the PERSPECTIVE camera position and rt holds its
 // origin-only constants (RtK::persp; a compile-time choice, so the kernel carries
 // one path).
 template <bool PERSP>
 __device__ __forceinline__ void trace_pixel(const RtK* __restrict__ rt, const double o[3], const double d[3],
-                                            double& zb_io, RtHit& hit, uint32_t mask = ~0u) {
+                                            double& zb_io, RtHit& hit, uint32_t mask) {
     double zb = zb_io;
-    const int npl = rt->n_pl, ncy = rt->n_cy;
     constexpr bool persp = PERSP;
-    for (int i = 0; i < npl; ++i) {
-        if (!((mask >> i) & 1u)) continue;  // wave-uniform
+    for (uint32_t m = mask & 0xFFFFu; m; m &= m - 1u) {
+        const int i = __builtin_ctz(m);
         double t;
         if (persp ? plane_hit_persp(rt->pl[i], o, d, zb, t) : plane_hit(rt->pl[i], o, d, zb, t)) {
             hit.kind = 2;
@@ -818,8 +826,8 @@ __device__ __forceinline__ void trace_pixel(const RtK* __restrict__ rt, const do
         }
     }
     int cyi = -1, cypart = 0;  // the cylinder that takes the pixel: its normal afterwards
-    for (int i = 0; i < ncy; ++i) {
-        if (!((mask >> (16 + i)) & 1u)) continue;  // wave-uniform
+    for (uint32_t m = mask >> 16; m; m &= m - 1u) {
+        const int i = __builtin_ctz(m);
         int part = 0;
         const double t = persp ? icapped_persp_t(rt->cy[i], d, part) : icapped_t(rt->cy[i], o, d, part);
         if (t < 0.0) continue;  // behind the camera (and misses)
@@ -1588,32 +1596,70 @@ __device__ __forceinline__ void eye_tile(const EyePart& a, const ShadowPart& sh,
     const int xb = __builtin_amdgcn_readfirstlane(bx * TILE_X);
     const int xi = xb + (threadIdx.x & (TILE_X - 1));
     const int yl = __builtin_amdgcn_readfirstlane(by * TILE_Y + (int)(threadIdx.x >> 6));
+#ifdef RTM_AB_HDR
+    // the header fields the prologue needs, read before any branch so their scalar
+    // loads issue as one group (one wait instead of a chain of dependent round trips)
+    const int W_ = a.W, H_ = a.H, rb_ = a.row_begin, re_ = a.row_end, og_ = a.out_global;
+    const int S_ = a.stripe_rows, ss_ = a.stripe_stride, sp_ = a.stripe_phase;
+    const uint32_t* const rtm_ = tabs.rtmask;
+    const int ns_ = a.n_spheres, cx0_ = a.cull_x0, cx1_ = a.cull_x1, cy0_ = a.cull_y0, cy1_ = a.cull_y1;
+    const double* const nx_ = a.nx;
+    const double* const ny_ = a.ny;
+    const int rtw_ = tabs.rtmask_words;
+    // (an empty asm that reads them: the loads issue here, together, and one wait covers them)
+    asm volatile("" ::"s"(W_), "s"(H_), "s"(rb_), "s"(re_), "s"(og_), "s"(S_), "s"(ss_), "s"(sp_), "s"(rtm_), "s"(ns_),
+                 "s"(cx0_), "s"(cx1_), "s"(cy0_), "s"(cy1_), "s"(nx_), "s"(ny_), "s"(rtw_));
+    const int yi = __builtin_amdgcn_readfirstlane(eye_row(rb_, S_, ss_, sp_, yl));
+    const int yo = og_ ? yi : yl;  // the output row
+    const bool live = (xi < W_) & (rb_ + yl < re_) & (yi < H_);
+    const bool um_ = (yi >= cy0_) & (yi <= cy1_) & (xb + TILE_X - 1 >= cx0_) & (xb <= cx1_);
+#else
     const int yi = __builtin_amdgcn_readfirstlane(eye_row(a.row_begin, a.stripe_rows, a.stripe_stride, a.stripe_phase, yl));
     const int yo = a.out_global ? yi : yl;  // the output row
     const bool live = xi < a.W && a.row_begin + yl < a.row_end && yi < a.H;
+#endif
     unsigned long long n_tests = 0, n_hit = 0, n_lit = 0, n_pl_tests = 0, n_cy_tests = 0;
     ShadowCounts sc;
     int hit_kind = 0, hit_id = -1;
     uint32_t n_evals = 0;
     // the wave's spheres (all lanes active here); ascending bit order = scene order
+#ifdef RTM_AB_HDR
+    uint32_t smask = um_ ? wave_sphere_mask(a.sph, ns_, xb, xb + TILE_X - 1, yi, yi) : 0u;
+#else
     uint32_t smask = union_may_cover(a, xb, xb + TILE_X - 1, yi, yi)
                          ? wave_sphere_mask(a.sph, a.n_spheres, xb, xb + TILE_X - 1, yi, yi)
                          : 0u;
+#endif
     // the wave's ray-traced primitives (PERSPECTIVE eye; all lanes active here)
-    uint32_t rmask = ~0u;
-#ifndef RTM_TEST_REVERT_MASK_GUARD
-    if (RTP && tabs.rtmask && a.row_begin + yl < a.row_end) {  // (no mask word for rows past the part)
-#else  // (tools/bounds_demo.sh only: the round-3 over-read, to show tests/test_bounds.py catches it)
+    uint32_t rmask = 0u;
+#if defined(RTM_TEST_REVERT_MASK_GUARD)  // (tools/bounds_demo.sh only: the round-3 over-read, to show tests/test_bounds.py catches it)
     if (RTP && tabs.rtmask) {
+#elif defined(RTM_AB_HDR)
+    if (RTP && rtm_ && rb_ + yl < re_) {
+#else
+    if (RTP && tabs.rtmask && a.row_begin + yl < a.row_end) {  // (no mask word for rows past the part)
 #endif
         const int widx = yl * ((a.W + TILE_X - 1) / TILE_X) + (xb / TILE_X);  // (wave-uniform)
-        if (widx < tabs.rtmask_words) rmask = ((const __attribute__((address_space(4))) uint32_t*)tabs.rtmask)[widx];
-        else note_oob();
-    } else if (RTB == 1 && rt && a.eye.type == RTM_CAMERA_PERSPECTIVE)
+        if (widx < tabs.rtmask_words) {
+            rmask = ((const __attribute__((address_space(4))) uint32_t*)tabs.rtmask)[widx];
+        } else {
+            note_oob();
+            rmask = rt_slots(rt->n_pl, rt->n_cy);  // (every primitive: the result stays exact)
+        }
+    } else if (RTB == 1 && rt && a.eye.type == RTM_CAMERA_PERSPECTIVE) {
         rmask = rt_wave_mask(rt, a.eye, min(xb, a.W - 1), min(xb + TILE_X - 1, a.W - 1), min(yi, a.H - 1), a.W, a.H);
+    } else if (RTB && rt) {
+        rmask = rt_slots(rt->n_pl, rt->n_cy);
+    }
     float4 c = make_float4(0.0f, 0.2f, 0.2f, 1.0f);  // (0.0, 0.2, 0.2) as f32 (main.rs:718-720)
     bool shaded = false;
+#ifdef RTM_AB_BG
+    // a wave no sphere, primitive or SDF can reach is background: no NDC loads, no rays
+    const bool reach = smask != 0u || (RTB && rt && rmask != 0u) || (RT == 2 && sdf);
+    if (live && reach) {
+#else
     if (live) {
+#endif
         const double x = a.nx[xi];
         const double y = a.ny[yi];
         // z-test over spheres in scene order, strict '<' against +INF init (main.rs:318)
@@ -1892,9 +1938,9 @@ __device__ __forceinline__ void rt_cull_wave(const CamK& c, const RtK* __restric
     if (t >= gx * rows) return;
     const int xb = (t % gx) * TILE_X, yi = eye_row(row_begin, stripes.x, stripes.y, stripes.z, t / gx);
     const RayCone k = ray_cone(c, min(xb, W - 1), min(xb + TILE_X - 1, W - 1), min(yi, H - 1), W, H);
-    uint32_t m = ~0u;
+    uint32_t m = rt_slots(rt->n_pl, rt->n_cy);
     for (int l = 0; l < 32; ++l) {
-        if (l < 16 ? l >= rt->n_pl : l - 16 >= rt->n_cy) continue;
+        if (!((m >> l) & 1u)) continue;
         double C[3], R;
         bool cullable;
         rt_bound(rt, l, C, R, cullable);
@@ -1995,8 +2041,9 @@ __global__ __launch_bounds__(BLOCK) void vp_trace_kernel(const TraceArgs a, doub
     hit.id = 0;
     double zb = zbuf[idx];
     if (a.rt) {
-        if (a.rt->persp) trace_pixel<true>(a.rt, o, d, zb, hit);
-        else trace_pixel<false>(a.rt, o, d, zb, hit);
+        const uint32_t slots = rt_slots(a.rt->n_pl, a.rt->n_cy);
+        if (a.rt->persp) trace_pixel<true>(a.rt, o, d, zb, hit, slots);
+        else trace_pixel<false>(a.rt, o, d, zb, hit, slots);
     }
     uint32_t evals = 0;
     if (a.sdf) trace_sdfs(a.sdf, o, d, zb, hit, evals);

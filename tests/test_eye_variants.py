@@ -64,7 +64,12 @@ def test_eye_variant_single_and_batched(rtm, oracle, scenes, gpu_ctx, kind, shad
         torch.cuda.synchronize()
         g.render_frames_async([s] * 3, eye, scenes.shadow_camera(), w, h, k, flags, fmt, 0, [o.data_ptr() for o in outs])
         g.synchronize(60000)
-        for o in outs:
-            assert np.array_equal(o.cpu().numpy(), want.view(np.uint8).reshape(-1)), "batched"
+        wb = want.view(np.uint8).reshape(h, w, -1)
+        for i, o in enumerate(outs):
+            gb = o.cpu().numpy().reshape(h, w, -1)
+            bad = np.argwhere(np.any(gb != wb, axis=-1))
+            assert bad.size == 0, (f"batched frame {i}: {len(bad)} pixels differ, first (y, x) {tuple(bad[0])}, "
+                                   f"rows {bad[:, 0].min()}..{bad[:, 0].max()}: got {gb[tuple(bad[0])]} "
+                                   f"want {wb[tuple(bad[0])]}")
     finally:
         g.close()
