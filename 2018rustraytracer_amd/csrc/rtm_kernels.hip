@@ -106,9 +106,13 @@ __device__ __forceinline__ uint32_t wave_sphere_mask(const RasterSphereK* __rest
 }
 
 // Does the union of a viewport's sphere pixel ranges reach columns [xb, xe] of rows [ya, ye]?
+// An empty union (no sphere covers anything: x0 > x1, the host's (1, 0, 1, 0)) reaches
+// nothing -- without the emptiness test a range spanning row 0 and column 0 would
+// "meet" it, and the split shadow launch would leave that strip to a part it never runs.
 template <typename P>
 __device__ __forceinline__ bool union_may_cover(const P& a, int xb, int xe, int ya, int ye) {
-    return ye >= a.cull_y0 && ya <= a.cull_y1 && xe >= a.cull_x0 && xb <= a.cull_x1;
+    return (a.cull_x0 <= a.cull_x1) & (a.cull_y0 <= a.cull_y1) & (ye >= a.cull_y0) & (ya <= a.cull_y1) &
+           (xe >= a.cull_x0) & (xb <= a.cull_x1);
 }
 
 // Coverage under a PERSPECTIVE camera (row f-3): the same test with the general
@@ -943,6 +947,10 @@ __device__ __forceinline__ double smap_decode(const ShadowPart& sh, const void* 
     const uint32_t inf = sh.smap_fmt == SMAP_U8 ? 0xFFu : 0xFFFFu;
     if (code == inf) return INFINITY;
     if ((int)code < sh.steps) return t_after(sh.tab, (int)code);
+    if ((int)code - sh.steps >= sh.n_spheres) {  // (no writer stores such a code: counted, read as +INF)
+        note_oob();
+        return INFINITY;
+    }
     const RasterSphereK& sp = sh.sph[(int)code - sh.steps];
     const double pa = ((sh.tab.nx[tx] - sp.cx) * sp.n) / sp.m;
     const double pb = ((sh.tab.ny[ty] - sp.cy) * sp.n) / sp.m;
@@ -967,6 +975,10 @@ __device__ __forceinline__ double smap_decode_wave(const ShadowPart& sh, const v
     double v = INFINITY;
     if (code != inf && (int)code < steps) v = t_after(sh.tab, (int)code);
     int si = (code != inf && (int)code >= steps) ? (int)code - steps : -1;
+    if (si >= sh.n_spheres) {  // (no writer stores such a code: counted, read as +INF)
+        note_oob();
+        si = -1;
+    }
     while (__any(si >= 0)) {
         const unsigned long long b = __ballot(si >= 0);
         const int i = __builtin_amdgcn_readfirstlane(__shfl(si, __builtin_ctzll(b)));
