@@ -524,8 +524,11 @@ int validate_dims(int32_t w, int32_t h) {
     return RTM_OK;
 }
 
-int build_frame(FrameArgs& a, const rtm_scene* scene, const rtm_camera* eye, const rtm_camera* shadow, int32_t W,
-                int32_t H, int32_t steps, int32_t flags) {
+// Everything build_frame can reject, without building anything (the group's up-front
+// check of a whole call's frames: a full build per frame there cost the group path a
+// second build of every frame before its first launch).
+int validate_frame(const rtm_scene* scene, const rtm_camera* eye, const rtm_camera* shadow, int32_t W, int32_t H,
+                   int32_t steps, int32_t flags) {
     int rc;
     if ((rc = validate_scene(scene)) || (rc = validate_camera(eye, "eye")) || (rc = validate_camera(shadow, "shadow")) ||
         (rc = validate_dims(W, H)))
@@ -537,6 +540,13 @@ int build_frame(FrameArgs& a, const rtm_scene* scene, const rtm_camera* eye, con
     // shadow lookup; the eye may be PERSPECTIVE (spheres via project_sphere_persp, row f-3).
     if (shadow->type != RTM_CAMERA_ORTHOGONAL)
         return fail(RTM_ERR_UNSUPPORTED, "frame path needs an ORTHOGONAL shadow camera");
+    return RTM_OK;
+}
+
+int build_frame(FrameArgs& a, const rtm_scene* scene, const rtm_camera* eye, const rtm_camera* shadow, int32_t W,
+                int32_t H, int32_t steps, int32_t flags) {
+    int rc;
+    if ((rc = validate_frame(scene, eye, shadow, W, H, steps, flags))) return rc;
     std::memset(&a, 0, sizeof a);
     ShadowPart& sh = a.sh;
     EyePart& ey = a.ey;
@@ -2142,8 +2152,7 @@ namespace internal {
 
 int check_frame(const rtm_scene* scene, const rtm_camera* eye, const rtm_camera* shadow, int32_t width,
                 int32_t height, int32_t march_steps, int32_t flags) {
-    FrameArgs a;
-    return build_frame(a, scene, eye, shadow, width, height, march_steps, flags);
+    return validate_frame(scene, eye, shadow, width, height, march_steps, flags);
 }
 
 PreparedFrame* new_prepared() { return new (std::nothrow) PreparedFrame; }

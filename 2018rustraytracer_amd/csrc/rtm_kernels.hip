@@ -1608,9 +1608,9 @@ __device__ __forceinline__ void eye_tile(const EyePart& a, const ShadowPart& sh,
     const int xb = __builtin_amdgcn_readfirstlane(bx * TILE_X);
     const int xi = xb + (threadIdx.x & (TILE_X - 1));
     const int yl = __builtin_amdgcn_readfirstlane(by * TILE_Y + (int)(threadIdx.x >> 6));
-#ifdef RTM_AB_HDR
-    // the header fields the prologue needs, read before any branch so their scalar
-    // loads issue as one group (one wait instead of a chain of dependent round trips)
+    // the header fields the prologue needs, read before any branch so their scalar loads
+    // issue as one group: one wait instead of a chain of dependent round trips (the
+    // short waves of small frames are latency-bound: config 7 +6 %, profiles/r04_ab_eye_prologue.txt)
     const int W_ = a.W, H_ = a.H, rb_ = a.row_begin, re_ = a.row_end, og_ = a.out_global;
     const int S_ = a.stripe_rows, ss_ = a.stripe_stride, sp_ = a.stripe_phase;
     const uint32_t* const rtm_ = tabs.rtmask;
@@ -1624,32 +1624,20 @@ __device__ __forceinline__ void eye_tile(const EyePart& a, const ShadowPart& sh,
     const int yi = __builtin_amdgcn_readfirstlane(eye_row(rb_, S_, ss_, sp_, yl));
     const int yo = og_ ? yi : yl;  // the output row
     const bool live = (xi < W_) & (rb_ + yl < re_) & (yi < H_);
-    const bool um_ = (yi >= cy0_) & (yi <= cy1_) & (xb + TILE_X - 1 >= cx0_) & (xb <= cx1_);
-#else
-    const int yi = __builtin_amdgcn_readfirstlane(eye_row(a.row_begin, a.stripe_rows, a.stripe_stride, a.stripe_phase, yl));
-    const int yo = a.out_global ? yi : yl;  // the output row
-    const bool live = xi < a.W && a.row_begin + yl < a.row_end && yi < a.H;
-#endif
+    // (union_may_cover on the loaded fields; an empty union (x0 > x1) meets nothing)
+    const bool um_ = (cx0_ <= cx1_) & (yi >= cy0_) & (yi <= cy1_) & (xb + TILE_X - 1 >= cx0_) & (xb <= cx1_);
     unsigned long long n_tests = 0, n_hit = 0, n_lit = 0, n_pl_tests = 0, n_cy_tests = 0;
     ShadowCounts sc;
     int hit_kind = 0, hit_id = -1;
     uint32_t n_evals = 0;
     // the wave's spheres (all lanes active here); ascending bit order = scene order
-#ifdef RTM_AB_HDR
     uint32_t smask = um_ ? wave_sphere_mask(a.sph, ns_, xb, xb + TILE_X - 1, yi, yi) : 0u;
-#else
-    uint32_t smask = union_may_cover(a, xb, xb + TILE_X - 1, yi, yi)
-                         ? wave_sphere_mask(a.sph, a.n_spheres, xb, xb + TILE_X - 1, yi, yi)
-                         : 0u;
-#endif
     // the wave's ray-traced primitives (PERSPECTIVE eye; all lanes active here)
     uint32_t rmask = 0u;
 #if defined(RTM_TEST_REVERT_MASK_GUARD)  // (tools/bounds_demo.sh only: the round-3 over-read, to show tests/test_bounds.py catches it)
-    if (RTP && tabs.rtmask) {
-#elif defined(RTM_AB_HDR)
-    if (RTP && rtm_ && rb_ + yl < re_) {
+    if (RTP && rtm_) {
 #else
-    if (RTP && tabs.rtmask && a.row_begin + yl < a.row_end) {  // (no mask word for rows past the part)
+    if (RTP && rtm_ && rb_ + yl < re_) {  // (no mask word for rows past the part)
 #endif
         const int widx = yl * ((a.W + TILE_X - 1) / TILE_X) + (xb / TILE_X);  // (wave-uniform)
         if (widx < tabs.rtmask_words) {
@@ -1665,13 +1653,10 @@ __device__ __forceinline__ void eye_tile(const EyePart& a, const ShadowPart& sh,
     }
     float4 c = make_float4(0.0f, 0.2f, 0.2f, 1.0f);  // (0.0, 0.2, 0.2) as f32 (main.rs:718-720)
     bool shaded = false;
-#ifdef RTM_AB_BG
     // a wave no sphere, primitive or SDF can reach is background: no NDC loads, no rays
+    // (its pixels keep the background colour, as the full loop would leave them)
     const bool reach = smask != 0u || (RTB && rt && rmask != 0u) || (RT == 2 && sdf);
     if (live && reach) {
-#else
-    if (live) {
-#endif
         const double x = a.nx[xi];
         const double y = a.ny[yi];
         // z-test over spheres in scene order, strict '<' against +INF init (main.rs:318)

@@ -15,6 +15,7 @@ import numpy as np
 import pytest
 
 from conftest import bits_equal, first_mismatch
+from test_bounds import oob
 
 pytestmark = pytest.mark.gpu
 
@@ -52,6 +53,7 @@ def test_sphere_free_frame_writes_every_texel(rtm, oracle, scenes, w, h, batched
     outs = [torch.empty((h, w, 4), dtype=torch.float32, device="cuda") for _ in range(n)]
     try:
         torch.cuda.synchronize()
+        assert oob(rtm, ctx) >= 0  # (clears the device-wide count)
         for s in (big, empty):
             if batched:
                 ctx.render_frames_async([s] * n, eye, sh, w, h, k, 0, [o.data_ptr() for o in outs])
@@ -62,6 +64,7 @@ def test_sphere_free_frame_writes_every_texel(rtm, oracle, scenes, w, h, batched
             assert ctx.last_batch() == n, ctx.last_batch()
         got = _smap(ctx, w, h)
         assert bits_equal(got, want["shadow"]), first_mismatch(got, want["shadow"])
+        assert oob(rtm, ctx) == 0  # no decode met a code outside the frame's spheres
         for o in outs:
             g = o.cpu().numpy()
             assert bits_equal(g, want["rgba"]), first_mismatch(g, want["rgba"])
