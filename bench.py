@@ -219,6 +219,7 @@ def tile_gather(rtm, lib, ctx, group, world, rank, dist, tdev, c_scenes, eye, sh
     barrier()
     t0 = time.perf_counter()
     run(warmup, steps)
+    t_enq = time.perf_counter() - t0  # the host's enqueue of the frames (the calls returned)
     drain()
     barrier()
     el = time.perf_counter() - t0
@@ -245,6 +246,7 @@ def tile_gather(rtm, lib, ctx, group, world, rank, dist, tdev, c_scenes, eye, sh
                       "band_note": "each rank's own part alone (fused shadow), HIP events on its context stream"})
     return {"value": round(W * H * steps / el / 1e6, 2), "unit": "Mpixels/s", "frames": steps,
             "ms_per_step": round(el / steps * 1e3, 5), "scaling": "strong",
+            "host_enqueue_ms_per_frame": round(t_enq / max(steps, 1) * 1e3, 5),
             "format": {0: "RGBA32F", 1: "RGBA8", 2: "RGB8"}[fmt], "bytes_per_pixel": bpp,
             "root_ingress_bytes_per_frame": int(W * (H - (shard.stripe_rows_of(H, world, stripe, 0)
                                                           if stripe > 0 and world > 1 else r01 - r00)) * bpp),
