@@ -1228,36 +1228,6 @@ __device__ __forceinline__ void shadow_tile_coded(const ShadowPart& a, void* __r
                     uint32_t chi[2] = {bot[0], bot[1]};
                     const bool need[2] = {need0, need1};
                     bool bad = false;
-#ifdef RTM_AB_GUESS
-                    // first a guess: a settled texel's code is the f32 guess ceil(g1*pyf + g0)
-                    // (code_check), so the boundary is where g1*pyf + g0 crosses top (codes
-                    // growing down the column) or top - 1 (shrinking); pyf is near-linear in the
-                    // row, so interpolating between the strip's end rows lands on it or next to
-                    // it.  Two independent checks verify a guess g (code(g-1) == top,
-                    // code(g) == bot, both settled: by monotonicity every row before g has top
-                    // and every row from g on has bot); an unverified column searches.
-                    bool srch = false;
-#pragma unroll
-                    for (int c = 0; c < 2; ++c) {
-                        const bool grow = bot[c] > top[c];
-                        const float X = grow ? (float)top[c] : (float)top[c] - 1.0f;
-                        const float p0 = RW[0].pyf, p1 = RW[NR - 1].pyf;
-                        const float t = ((X - g0[c]) / g1[c] - p0) / (p1 - p0) * (float)(NR - 1);
-                        const int gr = (int)ceilf(fminf(fmaxf(t, 1.0f), (float)(NR - 1)));  // (NaN: 1)
-                        const bool tr = need[c] & (top[c] != CODE_NONE) & (bot[c] != CODE_NONE);
-                        const RowLdsK ra = RW[tr ? gr - 1 : 0], rz = RW[tr ? gr : 0];
-                        bool s1, e1, s2, e2;
-                        const uint32_t ca = code_check<INC>(T, d0[c] + dd[c] * ra.py, ra.pyf, g0[c], g1[c], fsteps, oz,
-                                                            steps, s1, e1);
-                        const uint32_t cz = code_check<INC>(T, d0[c] + dd[c] * rz.py, rz.pyf, g0[c], g1[c], fsteps, oz,
-                                                            steps, s2, e2);
-                        const bool v = tr & !s1 & !s2 & (ca == top[c]) & (cz == bot[c]);
-                        lo[c] = v ? gr - 1 : 0;
-                        hi[c] = v ? gr : NR - 1;
-                        srch |= need[c] & !v;
-                    }
-                    if (__any(srch))
-#endif
 #pragma unroll
                     for (int it = 0; it < 4; ++it) {  // 15 rows: 4 halvings (NR == 16 here)
 #pragma unroll
@@ -1648,9 +1618,11 @@ __device__ __forceinline__ void eye_tile(const EyePart& a, const ShadowPart& sh,
     const double* const nx_ = a.nx;
     const double* const ny_ = a.ny;
     const int rtw_ = tabs.rtmask_words;
-    // (an empty asm that reads them: the loads issue here, together, and one wait covers them)
-    asm volatile("" ::"s"(W_), "s"(H_), "s"(rb_), "s"(re_), "s"(og_), "s"(S_), "s"(ss_), "s"(sp_), "s"(rtm_), "s"(ns_),
-                 "s"(cx0_), "s"(cx1_), "s"(cy0_), "s"(cy1_), "s"(nx_), "s"(ny_), "s"(rtw_));
+    // (an empty asm that reads them: the loads issue here, together, and one wait covers
+    // them; not in the SDF instantiation, whose allocation it pushes to 155 spilled VGPRs)
+    if (RT != 2)
+        asm volatile("" ::"s"(W_), "s"(H_), "s"(rb_), "s"(re_), "s"(og_), "s"(S_), "s"(ss_), "s"(sp_), "s"(rtm_), "s"(ns_),
+                     "s"(cx0_), "s"(cx1_), "s"(cy0_), "s"(cy1_), "s"(nx_), "s"(ny_), "s"(rtw_));
     const int yi = __builtin_amdgcn_readfirstlane(eye_row(rb_, S_, ss_, sp_, yl));
     const int yo = og_ ? yi : yl;  // the output row
     const bool live = (xi < W_) & (rb_ + yl < re_) & (yi < H_);
