@@ -1314,13 +1314,10 @@ int enqueue_batch(rtm_ctx* ctx, int lane, FrameArgs* fa, const FrameExtra* ex, v
         if (br.host[j]) HIP_TRY(hipHostFree(br.host[j]));
         br.host[j] = nullptr;
         br.host_bytes[j] = 0;
-#ifdef RTM_AB_COHERENT_RING
-        HIP_TRY(hipHostMalloc(&br.host[j], bytes, hipHostMallocCoherent | hipHostMallocMapped));
-#else
         // (coarse-grained pinned memory: coherent at the pull kernel's dispatch, after the
-        // host filled the slot; copied[j] keeps the host from refilling it earlier)
+        // host filled the slot; copied[j] keeps the host from refilling it earlier.  A
+        // fine-grained ring measured the same, profiles/r04_ab_eye_prologue.txt)
         HIP_TRY(hipHostMalloc(&br.host[j], bytes, hipHostMallocDefault));
-#endif
         br.host_bytes[j] = bytes;
         HIP_TRY(hipHostGetDevicePointer(&br.host_dev[j], br.host[j], 0));
     }

@@ -1619,8 +1619,10 @@ __device__ __forceinline__ void eye_tile(const EyePart& a, const ShadowPart& sh,
     const double* const ny_ = a.ny;
     const int rtw_ = tabs.rtmask_words;
     // (an empty asm that reads them: the loads issue here, together, and one wait covers
-    // them; not in the SDF instantiation, whose allocation it pushes to 155 spilled VGPRs)
-    if (RT != 2)
+    // them -- for the ray-traced instantiations only: it pushes the SDF one to 155 spilled
+    // VGPRs and the sphere-only one from 60 to 66 VGPRs, 7 waves, -3 % at configs 2 / 3,
+    // profiles/r04_ab_eye_prologue.txt)
+    if (RT == 1 || RT == 3)
         asm volatile("" ::"s"(W_), "s"(H_), "s"(rb_), "s"(re_), "s"(og_), "s"(S_), "s"(ss_), "s"(sp_), "s"(rtm_), "s"(ns_),
                      "s"(cx0_), "s"(cx1_), "s"(cy0_), "s"(cy1_), "s"(nx_), "s"(ny_), "s"(rtw_));
     const int yi = __builtin_amdgcn_readfirstlane(eye_row(rb_, S_, ss_, sp_, yl));
