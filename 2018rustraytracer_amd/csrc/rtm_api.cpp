@@ -1239,7 +1239,7 @@ int frame_batch(int32_t req, int32_t W, int32_t H) {
 
 // Enqueue frames [0, n) of `fa` (same tables, flags and sizes) as ONE batched
 // launch per pass on `lane`; a frame's output is outs[k] (RGBA f32).
-int enqueue_batch(rtm_ctx* ctx, int lane, FrameArgs* fa, const FrameExtra* ex, void* const* outs, int n,
+int enqueue_batch(rtm_ctx* ctx, int lane, FrameArgs* fa, const FrameExtra* const* exs, void* const* outs, int n,
                   int32_t fmt = RTM_FORMAT_RGBA32F) {
     int rc;
     if ((rc = frame_tables(ctx, fa[0]))) return rc;
@@ -1286,21 +1286,21 @@ int enqueue_batch(rtm_ctx* ctx, int lane, FrameArgs* fa, const FrameExtra* ex, v
     // move) is uploaded once and shared: same bytes, so the same bits
     std::vector<char> fresh_rt((size_t)n, 1), fresh_psp((size_t)n, 1), fresh_sdf((size_t)n, 1);
     for (int k = 0; k < n; ++k) {
-        const FrameExtra* pv = k > 0 ? &ex[k - 1] : nullptr;
-        if (ex[k].has_rt) {
-            if (pv && pv->has_rt && std::memcmp(&pv->rt, &ex[k].rt, sizeof(RtK)) == 0) {
+        const FrameExtra* pv = k > 0 ? exs[k - 1] : nullptr;
+        if (exs[k]->has_rt) {
+            if (pv && pv->has_rt && std::memcmp(&pv->rt, &exs[k]->rt, sizeof(RtK)) == 0) {
                 o_rt[(size_t)k] = o_rt[(size_t)k - 1];
                 fresh_rt[(size_t)k] = 0;
             } else { o_rt[(size_t)k] = off; off = up(off + sizeof(RtK)); }
         }
-        if (ex[k].has_psp) {
-            if (pv && pv->has_psp && std::memcmp(&pv->psp, &ex[k].psp, sizeof(PerspK)) == 0) {
+        if (exs[k]->has_psp) {
+            if (pv && pv->has_psp && std::memcmp(&pv->psp, &exs[k]->psp, sizeof(PerspK)) == 0) {
                 o_psp[(size_t)k] = o_psp[(size_t)k - 1];
                 fresh_psp[(size_t)k] = 0;
             } else { o_psp[(size_t)k] = off; off = up(off + sizeof(PerspK)); }
         }
-        if (ex[k].has_sdf) {
-            if (pv && pv->has_sdf && std::memcmp(&pv->sdf, &ex[k].sdf, sizeof(SdfTabK)) == 0) {
+        if (exs[k]->has_sdf) {
+            if (pv && pv->has_sdf && std::memcmp(&pv->sdf, &exs[k]->sdf, sizeof(SdfTabK)) == 0) {
                 o_sdf[(size_t)k] = o_sdf[(size_t)k - 1];
                 fresh_sdf[(size_t)k] = 0;
             } else { o_sdf[(size_t)k] = off; off = up(off + sizeof(SdfTabK)); }
@@ -1340,20 +1340,20 @@ int enqueue_batch(rtm_ctx* ctx, int lane, FrameArgs* fa, const FrameExtra* ex, v
         bf.tabs.rtmask = nullptr;
         bf.tabs.rtmask_words = 0;
         bf.tabs.rt_persp = 0;
-        if (ex[k].has_rt) {
-            if (fresh_rt[(size_t)k]) std::memcpy(hb + o_rt[(size_t)k], &ex[k].rt, sizeof(RtK));
+        if (exs[k]->has_rt) {
+            if (fresh_rt[(size_t)k]) std::memcpy(hb + o_rt[(size_t)k], &exs[k]->rt, sizeof(RtK));
             bf.tabs.rt = (const RtK*)(db + o_rt[(size_t)k]);
-            bf.tabs.rt_persp = ex[k].rt.persp;
+            bf.tabs.rt_persp = exs[k]->rt.persp;
             t0.rt = bf.tabs.rt;
-            t0.rt_persp = ex[k].rt.persp;
+            t0.rt_persp = exs[k]->rt.persp;
         }
-        if (ex[k].has_psp) {
-            if (fresh_psp[(size_t)k]) std::memcpy(hb + o_psp[(size_t)k], &ex[k].psp, sizeof(PerspK));
+        if (exs[k]->has_psp) {
+            if (fresh_psp[(size_t)k]) std::memcpy(hb + o_psp[(size_t)k], &exs[k]->psp, sizeof(PerspK));
             bf.tabs.psp = (const PerspK*)(db + o_psp[(size_t)k]);
             t0.psp = bf.tabs.psp;
         }
-        if (ex[k].has_sdf) {
-            if (fresh_sdf[(size_t)k]) std::memcpy(hb + o_sdf[(size_t)k], &ex[k].sdf, sizeof(SdfTabK));
+        if (exs[k]->has_sdf) {
+            if (fresh_sdf[(size_t)k]) std::memcpy(hb + o_sdf[(size_t)k], &exs[k]->sdf, sizeof(SdfTabK));
             bf.tabs.sdf = (const SdfTabK*)(db + o_sdf[(size_t)k]);
             t0.sdf = bf.tabs.sdf;
         }
@@ -1366,7 +1366,7 @@ int enqueue_batch(rtm_ctx* ctx, int lane, FrameArgs* fa, const FrameExtra* ex, v
         const size_t nw = (size_t)((fa[0].ey.W + 63) / 64) * (size_t)(fa[0].ey.row_end - fa[0].ey.row_begin);
         if ((rc = br.rtmask.ensure(sizeof(uint32_t) * nw * (size_t)n, ctx->device))) return rc;
         for (int k = 0; k < n; ++k)
-            if (ex[k].has_rt) {
+            if (exs[k]->has_rt) {
                 BatchFrame& bf = *(BatchFrame*)(hb + sizeof(BatchFrame) * (size_t)k);
                 bf.tabs.rtmask = (uint32_t*)br.rtmask.p + nw * (size_t)k;
                 bf.tabs.rtmask_words = (int32_t)nw;
@@ -1715,7 +1715,9 @@ int rtm_render_frames_async(rtm_ctx* ctx, int32_t n_frames, const rtm_scene* sce
                    disjoint(e))
                 ++e;
             if (e - k >= 2) {
-                rc = enqueue_batch(ctx, lane, &fa[(size_t)k], &fx[(size_t)k],
+                std::vector<const FrameExtra*> xp((size_t)(e - k));
+                for (int32_t q = k; q < e; ++q) xp[(size_t)(q - k)] = &fx[(size_t)q];
+                rc = enqueue_batch(ctx, lane, &fa[(size_t)k], xp.data(),
                                    reinterpret_cast<void* const*>(out_rgba_dev + i0 + k), e - k);
             } else {
                 rc = enqueue_frame(ctx, fa[(size_t)k], &fx[(size_t)k], out_rgba_dev[i0 + k], nullptr, lane);
@@ -2232,14 +2234,16 @@ int enqueue_prepared_batch(rtm_ctx* ctx, const PreparedFrame* const* fs, int n, 
             if ((rc = enqueue_prepared(ctx, fs[k], format, row_begin, row_end, outs[k], map, lane))) return rc;
         return RTM_OK;
     }
+    // the frames' arguments are copied (the rows and tables are set per launch); their
+    // extras (13 KB of primitive tables each) are only read
     std::vector<FrameArgs> fa((size_t)n);
-    std::vector<FrameExtra> fx((size_t)n);
+    std::vector<const FrameExtra*> xp((size_t)n);
     for (int k = 0; k < n; ++k) {
         fa[(size_t)k] = fs[k]->a;
         apply_rows(fa[(size_t)k].ey, row_begin, row_end, map);
-        fx[(size_t)k] = fs[k]->x;
+        xp[(size_t)k] = &fs[k]->x;
     }
-    return enqueue_batch(ctx, lane, fa.data(), fx.data(), outs, n, format);
+    return enqueue_batch(ctx, lane, fa.data(), xp.data(), outs, n, format);
 }
 
 int lanes_begin(rtm_ctx* ctx, int32_t width, int32_t rows, int32_t n_batches) {

