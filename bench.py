@@ -72,8 +72,9 @@ def parse():
                          "with several ranks on one GPU (timing tensors and tile-gather bands on the CPU)")
     ap.add_argument("--format", choices=["rgba32f", "rgba8"], default="rgba32f",
                     help="tile-gather mode: what is rendered and gathered")
-    ap.add_argument("--tile-gather-steps", type=int, default=512,
-                    help="frames of the secondary tile-gather measurement (0 = skip it)")
+    ap.add_argument("--tile-gather-steps", type=int, default=-1,
+                    help="frames of the secondary tile-gather measurement (0 = skip it; -1 = auto: "
+                         "at least 512 and at least 2 Gpixel, at most 8192)")
     ap.add_argument("--tile-gather-timeout-s", type=float, default=240.0,
                     help="watchdog of the secondary tile-gather measurement (group set-up included)")
     # The clocks ramp for tens of ms after an idle GPU: a time-based pre-roll before the
@@ -760,7 +761,7 @@ def main():
 
     # Secondary: the tile-partitioned, gathered frame (strong scaling) in RGBA f32 and RGBA8
     tile = None
-    if not tile_mode and a.tile_gather_steps > 0:
+    if not tile_mode and a.tile_gather_steps != 0:
         tile = {}
         # a watchdog for the secondary measurement: RCCL over several ranks is exercised
         # here for the first time in a run; if it stalls, rank 0 still prints the line
@@ -774,12 +775,16 @@ def main():
         # every band count renders the same algorithm: each band evaluates the shadow
         # texels it reads (N = 1 included, so the N = 1 figure is the strong-scaling base)
         tflags = cfg["flags"] | rtm.abi.RTM_FLAG_FUSED_SHADOW
+        tg_steps = (a.tile_gather_steps if a.tile_gather_steps >= 0
+                    else min(8192, max(512, (2 << 30) // (W * H))))
         for name, fmt in FORMATS.items():
             if "error" in tile:
                 break
             try:
+                # (warmup: one call of the same shape, so every lane's table slots and
+                # pinned buffers are allocated before the clock, as in frames mode)
                 tile[name] = tile_gather(rtm, lib, ctx, group, world, rank, dist, tdev, tg_c, eye, shadow, W, H, K,
-                                         tflags, fmt, a.tile_gather_steps, min(20, a.tile_gather_steps),
+                                         tflags, fmt, tg_steps, tg_steps,
                                          bands=name == "rgba32f")
             except Exception as ex:  # a failed secondary measurement must not lose the headline line
                 tile[name] = {"error": str(ex)[:300]}
