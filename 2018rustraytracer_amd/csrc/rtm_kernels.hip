@@ -964,7 +964,10 @@ __device__ __forceinline__ double smap_decode(const ShadowPart& sh, const void* 
 // (no chain of dependent loads), and sphere codes are resolved one sphere at a
 // time with that sphere's constants as wave-uniform (scalar) values instead of a
 // per-lane indexed load of them.  Same operations as smap_decode: same bits.
-__device__ __forceinline__ double smap_decode_wave(const ShadowPart& sh, const void* __restrict__ map, int tx, int ty) {
+// oob: set when the code names no sphere of the frame (reported by the caller after its
+// last load, see eye_tile).
+__device__ __forceinline__ double smap_decode_wave(const ShadowPart& sh, const void* __restrict__ map, int tx, int ty,
+                                                   bool& oob) {
     const int64_t e = smap_code_index(tx, ty, sh.smap_bw);
     const bool u8 = sh.smap_fmt == SMAP_U8;
     const uint32_t code = u8 ? (uint32_t)((const uint8_t*)map)[e] : (uint32_t)((const uint16_t*)map)[e];
@@ -976,7 +979,7 @@ __device__ __forceinline__ double smap_decode_wave(const ShadowPart& sh, const v
     if (code != inf && (int)code < steps) v = t_after(sh.tab, (int)code);
     int si = (code != inf && (int)code >= steps) ? (int)code - steps : -1;
     if (si >= sh.n_spheres) {  // (no writer stores such a code: counted, read as +INF)
-        note_oob();
+        oob = true;
         si = -1;
     }
     while (__any(si >= 0)) {
@@ -1611,25 +1614,31 @@ __device__ __forceinline__ void eye_tile(const EyePart& a, const ShadowPart& sh,
     // the header fields the prologue needs, read before any branch so their scalar loads
     // issue as one group: one wait instead of a chain of dependent round trips (the
     // short waves of small frames are latency-bound: config 7 +6 %, profiles/r04_ab_eye_prologue.txt)
-    const int W_ = a.W, H_ = a.H, rb_ = a.row_begin, re_ = a.row_end, og_ = a.out_global;
-    const int S_ = a.stripe_rows, ss_ = a.stripe_stride, sp_ = a.stripe_phase;
-    const uint32_t* const rtm_ = tabs.rtmask;
-    const int ns_ = a.n_spheres, cx0_ = a.cull_x0, cx1_ = a.cull_x1, cy0_ = a.cull_y0, cy1_ = a.cull_y1;
-    const double* const nx_ = a.nx;
-    const double* const ny_ = a.ny;
-    const int rtw_ = tabs.rtmask_words;
-    // (an empty asm that reads them: the loads issue here, together, and one wait covers
-    // them -- for the ray-traced instantiations only: it pushes the SDF one to 155 spilled
-    // VGPRs and the sphere-only one from 60 to 66 VGPRs, 7 waves, -3 % at configs 2 / 3,
-    // profiles/r04_ab_eye_prologue.txt)
+    int W_ = a.W, H_ = a.H, rb_ = a.row_begin, re_ = a.row_end, og_ = a.out_global;
+    int S_ = a.stripe_rows, ss_ = a.stripe_stride, sp_ = a.stripe_phase;
+    const uint32_t* rtm_ = tabs.rtmask;
+    int ns_ = a.n_spheres, cx0_ = a.cull_x0, cx1_ = a.cull_x1, cy0_ = a.cull_y0, cy1_ = a.cull_y1;
+    const double* nx_ = a.nx;
+    const double* ny_ = a.ny;
+    int rtw_ = tabs.rtmask_words;
+    // (an empty asm that passes them through -- not volatile, no memory operand, so it
+    // does not count as a write that would turn the later table loads into vector loads
+    // -- makes every load complete here, together, under one wait; for the ray-traced
+    // instantiations only: it pushes the SDF one to 155 spilled VGPRs and the sphere-only
+    // one from 60 to 66 VGPRs, profiles/r04_ab_eye_prologue.txt)
     if (RT == 1 || RT == 3)
-        asm volatile("" ::"s"(W_), "s"(H_), "s"(rb_), "s"(re_), "s"(og_), "s"(S_), "s"(ss_), "s"(sp_), "s"(rtm_), "s"(ns_),
-                     "s"(cx0_), "s"(cx1_), "s"(cy0_), "s"(cy1_), "s"(nx_), "s"(ny_), "s"(rtw_));
+        asm("" : "+s"(W_), "+s"(H_), "+s"(rb_), "+s"(re_), "+s"(og_), "+s"(S_), "+s"(ss_), "+s"(sp_), "+s"(rtm_),
+            "+s"(ns_), "+s"(cx0_), "+s"(cx1_), "+s"(cy0_), "+s"(cy1_), "+s"(nx_), "+s"(ny_), "+s"(rtw_));
     const int yi = __builtin_amdgcn_readfirstlane(eye_row(rb_, S_, ss_, sp_, yl));
     const int yo = og_ ? yi : yl;  // the output row
     const bool live = (xi < W_) & (rb_ + yl < re_) & (yi < H_);
     // (union_may_cover on the loaded fields; an empty union (x0 > x1) meets nothing)
     const bool um_ = (cx0_ <= cx1_) & (yi >= cy0_) & (yi <= cy1_) & (xb + TILE_X - 1 >= cx0_) & (xb <= cx1_);
+    // An out-of-range side-table read is counted once the tile's last load is done: the
+    // counter's atomic is a global write, and one ahead of a load makes the compiler treat
+    // the load as clobbered -- the primitive tables would go through vector instead of
+    // scalar loads (config 6 eye pass 77 -> 96 us per frame before this was noticed).
+    bool oob = false;
     unsigned long long n_tests = 0, n_hit = 0, n_lit = 0, n_pl_tests = 0, n_cy_tests = 0;
     ShadowCounts sc;
     int hit_kind = 0, hit_id = -1;
@@ -1647,7 +1656,7 @@ __device__ __forceinline__ void eye_tile(const EyePart& a, const ShadowPart& sh,
         if (widx < tabs.rtmask_words) {
             rmask = ((const __attribute__((address_space(4))) uint32_t*)tabs.rtmask)[widx];
         } else {
-            note_oob();
+            oob = true;
             rmask = rt_slots(rt->n_pl, rt->n_cy);  // (every primitive: the result stays exact)
         }
     } else if (RTB == 1 && rt && a.eye.type == RTM_CAMERA_PERSPECTIVE) {
@@ -1781,7 +1790,7 @@ __device__ __forceinline__ void eye_tile(const EyePart& a, const ShadowPart& sh,
                 else if (sh.smap_fmt == SMAP_F64)
                     dsm = smap[ty * a.Ws + tx];
                 else
-                    dsm = smap_decode_wave(sh, smap, (int)tx, (int)ty);
+                    dsm = smap_decode_wave(sh, smap, (int)tx, (int)ty, oob);
             }
             const bool lit = dsm > qz - 0.0;
             const double lm = lit ? 1.0 : 0.25;
@@ -1835,6 +1844,7 @@ __device__ __forceinline__ void eye_tile(const EyePart& a, const ShadowPart& sh,
             }
         }
     }
+    if (__builtin_expect(oob, 0)) note_oob();  // (after the tile's last load, see above)
     if (COUNT) {
         stat_add(&st->eye_sphere_tests, n_tests);
         stat_add(&st->eye_hit_pixels, n_hit);
