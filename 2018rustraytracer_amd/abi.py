@@ -13,6 +13,8 @@ _PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("RTM_LIB") or os.path.join(_PKG_DIR, "librtm.so")
 
 RTM_ABI_VERSION = 10
+# library versions whose public structs share this layout (an RTM_LIB A/B build may be one)
+RTM_ABI_LAYOUT_COMPATIBLE = frozenset({9, 10})
 RTM_MAX_SPHERES = 16
 RTM_MAX_PATCHES = 4
 RTM_MAX_CIRCLE_PLANES = 16
@@ -218,16 +220,25 @@ def load_library(path: str | None = None) -> C.CDLL:
             f"{p} not built: run `python -c 'import __graft_entry__ as g; g.build()'` "
             "(the HIP library is the only render path)")
     lib = C.CDLL(p)
-    # an A/B build (RTM_LIB) may predate the newest calls: those stay unbound there
+    # An A/B build (RTM_LIB) may predate the newest calls: those stay unbound there (and
+    # are named on stderr).  Its public struct layouts must still be this package's: only
+    # the versions listed as layout-compatible are accepted.
     ab = bool(os.environ.get("RTM_LIB")) and path is None
+    ver = lib.rtm_abi_version()
+    if ver != RTM_ABI_VERSION and not (ab and ver in RTM_ABI_LAYOUT_COMPATIBLE):
+        raise RuntimeError(f"librtm ABI version {ver} at {p}, this package needs {RTM_ABI_VERSION}"
+                           + (f" (an RTM_LIB build may be one of {sorted(RTM_ABI_LAYOUT_COMPATIBLE)})" if ab else ""))
+    unbound = []
     for name, res, args in ABI_SYMBOLS:
         if ab and not hasattr(lib, name):
+            unbound.append(name)
             continue
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.rtm_abi_version() != RTM_ABI_VERSION and not ab:
-        raise RuntimeError("librtm ABI version mismatch")
+    if unbound:
+        import sys
+        sys.stderr.write(f"librtm ({p}, RTM_LIB A/B build, ABI {ver}): unbound {', '.join(unbound)}\n")
     if path is None:
         _lib = lib
     return lib

@@ -2246,11 +2246,17 @@ int enqueue_prepared_batch(rtm_ctx* ctx, const PreparedFrame* const* fs, int n, 
     return enqueue_batch(ctx, lane, fa.data(), xp.data(), outs, n, format);
 }
 
-int lanes_begin(rtm_ctx* ctx, int32_t width, int32_t rows, int32_t n_batches) {
-    if (!ctx || n_batches < 1) return fail(RTM_ERR_INVALID, "bad arguments");
-    // frame_lanes' rule with disjoint outputs (the caller's batches never share one)
+int lanes_plan(const rtm_ctx* ctx, int32_t width, int32_t rows, int32_t n_batches) {
+    // frame_lanes' rule for batches with disjoint outputs (the caller checks overlaps
+    // and caps the count, lanes_begin's max_lanes)
     int L = ctx->lanes_req > 0 ? ctx->lanes_req : ((int64_t)width * rows >= (16LL << 20) ? 3 : 4);
-    L = std::min<int>(std::min(L, 8), n_batches);
+    return std::max(1, std::min<int>(std::min(L, 8), n_batches));
+}
+
+int lanes_begin(rtm_ctx* ctx, int32_t width, int32_t rows, int32_t n_batches, int32_t max_lanes) {
+    if (!ctx || n_batches < 1) return fail(RTM_ERR_INVALID, "bad arguments");
+    int L = lanes_plan(ctx, width, rows, n_batches);
+    if (max_lanes > 0) L = std::min<int>(L, max_lanes);
     ctx->lanes_last = std::max(L, 1);  // (rtm_ctx_last_lanes)
     if (L <= 1) return 1;
     DeviceGuard g(ctx->device);

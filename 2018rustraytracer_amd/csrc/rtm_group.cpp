@@ -176,9 +176,10 @@ hipError_t place_rows(void* dst, const void* src, const Part& p, size_t row_byte
 
 }  // namespace
 
-// One local device of the group.  A chunk of frames renders into one of NSLOT
-// staging slots (chunks spread over the context's lanes, so up to NSLOT chunks are
-// in flight); a slot is reused once its sends have read it.
+// One local device of the group.  A chunk of frames renders into one of its staging
+// slots (chunks spread over the context's L lanes: L + 1 slots, at most NSLOT, keep
+// every lane busy while a chunk is in transfer); a slot is reused once its sends have
+// read it.
 constexpr int NSLOT = 4;
 struct Member {
     rtm_ctx* ctx = nullptr;
@@ -194,6 +195,7 @@ struct Member {
     hipEvent_t lb_recv = nullptr;    // loopback transport: the root's copy of it has run
     void* stage[NSLOT] = {};
     size_t stage_bytes = 0;
+    int nstage = 0;  // staging slots allocated (stage[0 .. nstage))
     int slot = 0;
 };
 
@@ -276,8 +278,14 @@ int setup_members(rtm_group* g) {
     return RTM_OK;
 }
 
-int ensure_stage(Member& mb, size_t bytes) {
-    if (bytes <= mb.stage_bytes) return RTM_OK;
+// At least `nslot` staging slots of at least `bytes` each (slots only grow: a slot in
+// the rotation stays valid).  At 7680x4320 RGBA f32 and N = 2 a slot of 2 frames'
+// parts is 0.53 GB, so a one-lane member keeps 2 slots, not NSLOT.
+int ensure_stage(Member& mb, size_t bytes, int nslot) {
+    nslot = std::max(1, std::min(nslot, NSLOT));
+    if (bytes <= mb.stage_bytes && nslot <= mb.nstage) return RTM_OK;
+    bytes = std::max(bytes, mb.stage_bytes);
+    nslot = std::max(nslot, mb.nstage);
     Guard d(mb.device);
     // the staging buffers are idle once their renders and their last sends are done
     GHIP_TRY(hipStreamSynchronize(rtm::internal::ctx_stream(mb.ctx)));
@@ -287,9 +295,12 @@ int ensure_stage(Member& mb, size_t bytes) {
         p = nullptr;
     }
     mb.stage_bytes = 0;
-    for (void*& p : mb.stage)
-        if (hipMalloc(&p, bytes) != hipSuccess) return set_error(RTM_ERR_OOM, "band staging allocation failed");
+    mb.nstage = 0;
+    mb.slot = 0;
+    for (int k = 0; k < nslot; ++k)
+        if (hipMalloc(&mb.stage[k], bytes) != hipSuccess) return set_error(RTM_ERR_OOM, "band staging allocation failed");
     mb.stage_bytes = bytes;
+    mb.nstage = nslot;
     return RTM_OK;
 }
 
@@ -409,13 +420,15 @@ int rtm_group_create_rank(int32_t device, int32_t n_ranks, int32_t rank, const u
 
 void rtm_group_destroy(rtm_group* g) {
     if (!g) return;
-    // waits for the group's queued work without a limit (a long 8K sequence may be
-    // in flight); a caller that must not hang on a lost peer bounds it itself with
-    // rtm_group_synchronize(g, timeout_ms) first, which aborts the communicators past
-    // the limit (RTM_GROUP_DESTROY_TIMEOUT_MS > 0: the same bound here, opt-in)
+    // waits for the group's queued work, at most 600 s by default (far above any
+    // queued sequence: 8192 frames at 7680x4320 drain in seconds), then aborts the
+    // communicators, so a peer lost with a transfer unmatched cannot hang the caller
+    // for ever.  A caller bounds it tighter with rtm_group_synchronize(g, timeout_ms)
+    // first (the Python Group.close does); RTM_GROUP_DESTROY_TIMEOUT_MS sets the
+    // bound (0: no limit)
     static const int32_t limit_ms = [] {
         const char* e = getenv("RTM_GROUP_DESTROY_TIMEOUT_MS");
-        return e ? (int32_t)atoi(e) : 0;
+        return e ? (int32_t)atoi(e) : 600000;
     }();
     if (!g->aborted) (void)rtm_group_synchronize(g, limit_ms);
     release(g, !g->aborted);
@@ -596,7 +609,7 @@ int group_chunk(rtm_group* g, const rtm::internal::PreparedFrame* const* pf, int
         if (staged && pt.rows > 0) {
             Guard d(mb.device);
             GHIP_TRY(hipEventRecord(mb.sent[mb.slot], mb.xfer));
-            mb.slot = (mb.slot + 1) % NSLOT;
+            mb.slot = (mb.slot + 1) % mb.nstage;
         }
     }
     return RTM_OK;
@@ -606,9 +619,10 @@ struct PreparedDeleter {
     void operator()(rtm::internal::PreparedFrame* f) const { rtm::internal::delete_prepared(f); }
 };
 
-// Shared checks of the frame calls; allocates the staging buffers (two slots of
-// `frames` bands each).
-int group_begin(rtm_group* g, int32_t width, int32_t height, int32_t format, int32_t root, int32_t frames) {
+// Shared checks of the frame calls; allocates the staging buffers (slots[mi] slots of
+// `frames` parts each on local member mi; nullptr: one slot).
+int group_begin(rtm_group* g, int32_t width, int32_t height, int32_t format, int32_t root, int32_t frames,
+                const int* slots = nullptr) {
     if (!g) return set_error(RTM_ERR_INVALID, "group is NULL");
     if (g->aborted) return set_error(RTM_ERR_COMM, "group was aborted");
     if (root < 0 || root >= g->n_ranks) return set_error(RTM_ERR_INVALID, "root outside [0, n_ranks)");
@@ -617,13 +631,33 @@ int group_begin(rtm_group* g, int32_t width, int32_t height, int32_t format, int
     if (width <= 0 || height <= 0 || width > RTM_MAX_DIM || height > RTM_MAX_DIM)
         return set_error(RTM_ERR_INVALID, "image size outside [1, RTM_MAX_DIM]");
     const int32_t rows0 = part_of(height, g->n_ranks, group_stripe(g), 0).rows;  // the largest part
-    for (Member& mb : g->m) {
+    for (size_t mi = 0; mi < g->m.size(); ++mi) {
+        Member& mb = g->m[mi];
         const bool staged = mb.rank != root || g->root_staging;
         int rc;
-        if (staged && (rc = ensure_stage(mb, (size_t)bpp * (size_t)width * (size_t)rows0 * (size_t)frames)))
+        if (staged && (rc = ensure_stage(mb, (size_t)bpp * (size_t)width * (size_t)rows0 * (size_t)frames,
+                                         slots ? slots[mi] : 1)))
             return rc;
     }
     return RTM_OK;
+}
+
+// Does any frame of one chunk overlap a frame of another chunk on a different lane
+// (chunk c on lane c % L)?  Such frames would be written side by side, so the later
+// frame might not land last.  Frames of equal size: sorting by address, any two
+// overlapping ones are joined by a chain of overlapping neighbours, so checking
+// sorted neighbours checks every pair (rtm_api.cpp frame_lanes).
+bool chunks_clash_across_lanes(const std::vector<std::pair<int32_t, int32_t>>& chunks, void* const* out_dev,
+                               uintptr_t frame_bytes, int L) {
+    if (L <= 1) return false;
+    std::vector<std::pair<uintptr_t, int>> r;
+    for (size_t c = 0; c < chunks.size(); ++c)
+        for (int32_t k = 0; k < chunks[c].second; ++k)
+            r.push_back({(uintptr_t)out_dev[chunks[c].first + k], (int)(c % (size_t)L)});
+    std::sort(r.begin(), r.end());
+    for (size_t i = 1; i < r.size(); ++i)
+        if (r[i].first < r[i - 1].first + frame_bytes && r[i].second != r[i - 1].second) return true;
+    return false;
 }
 
 int check_root_out(rtm_group* g, int32_t format, int32_t root, void* out) {
@@ -657,7 +691,50 @@ int rtm_group_render_frames_async(rtm_group* g, int32_t n_frames, const rtm_scen
     // chunk render in one launch per pass), the same on every rank
     const int32_t rows0 = part_of(height, g->n_ranks > 0 ? g->n_ranks : 1, group_stripe(g), 0).rows;
     const int32_t B = std::max(1, std::min<int32_t>(n_frames, rtm::internal::auto_frames_per_launch(width, rows0)));
-    int rc = group_begin(g, width, height, format, root, B);
+    if (root < 0 || root >= g->n_ranks) return set_error(RTM_ERR_INVALID, "root outside [0, n_ranks)");
+    const int32_t bpp = rtm::internal::bytes_per_pixel(format);
+    if (!bpp) return set_error(RTM_ERR_INVALID, "unknown output format");
+    bool holds_root = false;
+    for (const Member& mb : g->m) holds_root |= mb.rank == root;
+    const uintptr_t frame_bytes = (uintptr_t)bpp * (uintptr_t)width * height;
+    // The chunks: B frames each, except that on the root a chunk's frames need disjoint
+    // outputs (they render side by side), so a repeated output starts the next chunk
+    // and the later frame still lands last (chunking is local: every frame's gather is
+    // its own matched send/receive set).
+    std::vector<std::pair<int32_t, int32_t>> chunks;  // (first frame, frames)
+    for (int32_t i0 = 0; i0 < n_frames;) {
+        int nf = std::min<int32_t>(B, n_frames - i0);
+        if (holds_root)
+            for (int k = 1; k < nf; ++k) {
+                bool clash = false;
+                for (int q = 0; q < k && !clash; ++q) {
+                    const uintptr_t a = (uintptr_t)out_dev[i0 + k], b = (uintptr_t)out_dev[i0 + q];
+                    clash = a < b + frame_bytes && b < a + frame_bytes;
+                }
+                if (clash) {
+                    nf = k;
+                    break;
+                }
+            }
+        chunks.push_back({i0, nf});
+        i0 += nf;
+    }
+    const int32_t n_chunks = (int32_t)chunks.size();
+    // Every member spreads the chunks over its context's lanes, as rtm_render_frames_async
+    // spreads batches (chunk c on lane c % L).  A member rendering the root's rows in place
+    // writes the caller's frames from its lanes: where frames of chunks on different lanes
+    // overlap (one buffer reused across chunks) it keeps one lane, so they land in order.
+    std::vector<int> L(g->m.size(), 1), lane(g->m.size(), 0), cap(g->m.size(), 0), slots(g->m.size(), 1);
+    for (size_t mi = 0; mi < g->m.size(); ++mi) {
+        const Member& mb = g->m[mi];
+        const int32_t rows = part_of(height, g->n_ranks, group_stripe(g), mb.rank).rows;
+        if (rows <= 0) continue;
+        const int l = rtm::internal::lanes_plan(mb.ctx, width, rows, n_chunks);
+        const bool in_place = mb.rank == root && !g->root_staging;
+        cap[mi] = in_place && chunks_clash_across_lanes(chunks, out_dev, frame_bytes, l) ? 1 : 0;
+        slots[mi] = std::min(NSLOT, (cap[mi] ? 1 : l) + 1);
+    }
+    int rc = group_begin(g, width, height, format, root, B, slots.data());
     if (rc) return rc;
     // more than one band: each evaluates the shadow texels it reads (same image bits)
     const int32_t f = flags | (g->n_ranks > 1 ? RTM_FLAG_FUSED_SHADOW : 0);
@@ -674,19 +751,12 @@ int rtm_group_render_frames_async(rtm_group* g, int32_t n_frames, const rtm_scen
         if (!pf[(size_t)k]) return set_error(RTM_ERR_OOM, "host allocation failed");
         pp[(size_t)k] = pf[(size_t)k].get();
     }
-    bool holds_root = false;
-    for (const Member& mb : g->m) holds_root |= mb.rank == root;
-    const uintptr_t frame_bytes = (uintptr_t)rtm::internal::bytes_per_pixel(format) * (uintptr_t)width * height;
-    // every member spreads the call's chunks over its context's lanes, as
-    // rtm_render_frames_async spreads batches (chunk c on lane c % L); the lanes join
-    // the context stream at the end (rtm_group_synchronize waits on it)
-    const int32_t n_chunks = (n_frames + B - 1) / B;
-    std::vector<int> L(g->m.size(), 1), lane(g->m.size(), 0);
+    // the lanes join the context stream at the end (rtm_group_synchronize waits on it)
     for (size_t mi = 0; mi < g->m.size(); ++mi) {
         const int32_t rows = part_of(height, g->n_ranks, group_stripe(g), g->m[mi].rank).rows;
         if (rows <= 0) continue;
         Guard d(g->m[mi].device);
-        const int l = rtm::internal::lanes_begin(g->m[mi].ctx, width, rows, n_chunks);
+        const int l = rtm::internal::lanes_begin(g->m[mi].ctx, width, rows, n_chunks, cap[mi]);
         if (l < 0) {
             for (size_t q = 0; q < mi; ++q) (void)rtm::internal::lanes_end(g->m[q].ctx, L[q]);
             return l;
@@ -702,23 +772,8 @@ int rtm_group_render_frames_async(rtm_group* g, int32_t n_frames, const rtm_scen
         }
         return jr;
     };
-    for (int32_t i0 = 0, c = 0; i0 < n_frames; ++c) {
-        int nf = std::min<int32_t>(B, n_frames - i0);
-        // on the root, a chunk's frames need disjoint outputs (they render side by side);
-        // a repeated output starts the next chunk, so the later frame still lands last
-        // (chunking is local: every frame's gather is its own matched send/receive set)
-        if (holds_root)
-            for (int k = 1; k < nf; ++k) {
-                bool clash = false;
-                for (int q = 0; q < k && !clash; ++q) {
-                    const uintptr_t a = (uintptr_t)out_dev[i0 + k], b = (uintptr_t)out_dev[i0 + q];
-                    clash = a < b + frame_bytes && b < a + frame_bytes;
-                }
-                if (clash) {
-                    nf = k;
-                    break;
-                }
-            }
+    for (int32_t c = 0; c < n_chunks; ++c) {
+        const int32_t i0 = chunks[(size_t)c].first, nf = chunks[(size_t)c].second;
         for (int k = 0; k < nf && !rc; ++k)
             rc = rtm::internal::prepare_frame(pf[(size_t)k].get(), &scenes[i0 + k], eye, shadow, width, height,
                                               march_steps, f);
@@ -728,7 +783,6 @@ int rtm_group_render_frames_async(rtm_group* g, int32_t n_frames, const rtm_scen
             (void)join();  // the context streams still cover what was enqueued
             return rc;
         }
-        i0 += nf;
     }
     return join();
 }
@@ -754,7 +808,7 @@ int group_render_direct(rtm_group* g, const rtm_scene* scene, const rtm_camera* 
     if ((rc = rtm::internal::check_frame(scene, eye, shadow, width, height, march_steps, f))) return rc;
     const int32_t S = group_stripe(g);
     for (Member& mb : g->m)
-        if ((rc = ensure_stage(mb, row_bytes * (size_t)part_of(height, n, S, 0).rows))) return rc;
+        if ((rc = ensure_stage(mb, row_bytes * (size_t)part_of(height, n, S, 0).rows, 1))) return rc;
     std::unique_ptr<rtm::internal::PreparedFrame, PreparedDeleter> pf(rtm::internal::new_prepared());
     if (!pf) return set_error(RTM_ERR_OOM, "host allocation failed");
     if ((rc = rtm::internal::prepare_frame(pf.get(), scene, eye, shadow, width, height, march_steps, f))) return rc;

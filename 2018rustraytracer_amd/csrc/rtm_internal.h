@@ -42,7 +42,10 @@ int enqueue_prepared_batch(rtm_ctx* ctx, const PreparedFrame* const* fs, int n, 
 // Lanes for n_batches batches of width x rows frames (the rtm_render_frames_async
 // rule, rtm_ctx_set_lanes honoured): creates them and makes them start after ctx's
 // stream; returns the count (1: ctx's stream only) or a negative error.
-int lanes_begin(rtm_ctx* ctx, int32_t width, int32_t rows, int32_t n_batches);
+// max_lanes > 0 caps the count (1: the caller's batches must run in order).
+int lanes_begin(rtm_ctx* ctx, int32_t width, int32_t rows, int32_t n_batches, int32_t max_lanes = 0);
+// the count lanes_begin would return, without creating or forking anything
+int lanes_plan(const rtm_ctx* ctx, int32_t width, int32_t rows, int32_t n_batches);
 // ctx's stream waits for lanes 1..L-1 (every batch enqueued on them is then in its order)
 int lanes_end(rtm_ctx* ctx, int L);
 // the stream of ctx's lane (0: ctx's own)

@@ -105,14 +105,35 @@ __device__ __forceinline__ uint32_t wave_sphere_mask(const RasterSphereK* __rest
     return (uint32_t)__ballot(m);
 }
 
+// wave_sphere_mask for the eye pass, whose hits shade with the sphere's id: a
+// sphere whose id (the index into a.shade) is past the frame's sphere table is left out
+// of the set and flagged in `oob` (the host validated every id: see checked_id); its
+// id sits in the same 16 bytes as the range words.
+__device__ __forceinline__ uint32_t wave_sphere_mask_ids(const RasterSphereK* __restrict__ sph, int n, int xb, int xe,
+                                                         int ya, int ye, bool& oob) {
+    const int l = threadIdx.x & 63;
+    bool m = false, bad = false;
+    if (l < n) {
+        const RasterSphereK& s = sph[l];
+        m = (ye >= s.iy0) & (ya <= s.iy1) & (xe >= s.ix0) & (xb <= s.ix1);
+        bad = (unsigned)s.id >= (unsigned)n;
+    }
+    if (__builtin_expect(__ballot(bad) != 0, 0)) oob = true;
+    return (uint32_t)__ballot(m & !bad);
+}
+
 // Does the union of a viewport's sphere pixel ranges reach columns [xb, xe] of rows [ya, ye]?
 // An empty union (no sphere covers anything: x0 > x1, the host's (1, 0, 1, 0)) reaches
 // nothing -- without the emptiness test a range spanning row 0 and column 0 would
 // "meet" it, and the split shadow launch would leave that strip to a part it never runs.
 template <typename P>
 __device__ __forceinline__ bool union_may_cover(const P& a, int xb, int xe, int ya, int ye) {
+#if defined(RTM_TEST_REVERT_EMPTY_UNION)  // (tools/bounds_demo.sh only: the round-3 bug, no emptiness test)
+    return (ye >= a.cull_y0) & (ya <= a.cull_y1) & (xe >= a.cull_x0) & (xb <= a.cull_x1);
+#else
     return (a.cull_x0 <= a.cull_x1) & (a.cull_y0 <= a.cull_y1) & (ye >= a.cull_y0) & (ya <= a.cull_y1) &
            (xe >= a.cull_x0) & (xb <= a.cull_x1);
+#endif
 }
 
 // Coverage under a PERSPECTIVE camera (row f-3): the same test with the general
@@ -677,6 +698,18 @@ __device__ __forceinline__ double sdf_trace(const SdfK& g, const double ro[3], c
 // The ray-traced part of one eye pixel: planes, then cylinders, in scene order
 // (main.rs:573-638), then the row f-4 SDFs.  zb is the depth after the sphere
 // rasterize; kind/rid/t/n are updated in place when a primitive takes the pixel.
+// A hit's scene id indexes the frame's shading tables (a.shade, rt->pl / cy, sdf->s
+// by id, as renderColorImage indexes the scene's vectors, main.rs:748, 773, 791).  The
+// host validated every id against its table (rtm_api.cpp validate_scene), and the
+// kernels check it again where the id is taken -- a wave-uniform (scalar) id against
+// the frame's count: an id past the table is counted in `oob` (rtm_ctx_oob_reads) and
+// replaced by 0, so no id-indexed read can leave its table.
+__device__ __forceinline__ int checked_id(int id, int n, bool& oob) {
+    if ((unsigned)id < (unsigned)n) return id;
+    oob = true;
+    return 0;
+}
+
 struct RtHit {
     int kind;  // 0 none, 1 sphere, 2 circle plane, 3 capped cylinder, 4 SDF
     int id;
@@ -686,7 +719,7 @@ struct RtHit {
 
 template <bool NEAR = false>
 __device__ __forceinline__ void trace_sdfs(const SdfTabK* __restrict__ sdf, const double o[3], const double d[3],
-                                           double zb, RtHit& hit, uint32_t& evals) {
+                                           double zb, RtHit& hit, uint32_t& evals, bool& oob) {
     const int ns = sdf->n;
     const double m[3] = {1.0 / d[0], 1.0 / d[1], 1.0 / d[2]};
     const double am[3] = {fabs(m[0]), fabs(m[1]), fabs(m[2])};
@@ -695,7 +728,7 @@ __device__ __forceinline__ void trace_sdfs(const SdfTabK* __restrict__ sdf, cons
         const double t = sdf_trace<NEAR>(sdf->s[i], o, d, m, am, n, evals, zb);
         if (!(t > 0.0) || !(t < zb)) continue;  // the shader's acceptance (entry.frag:908-917)
         hit.kind = 4;
-        hit.id = sdf->s[i].id;
+        hit.id = checked_id(sdf->s[i].id, ns, oob);
         hit.t = t;
         hit.n[0] = n[0];
         hit.n[1] = n[1];
@@ -797,13 +830,26 @@ __device__ __forceinline__ uint32_t rt_wave_mask(const RtK* __restrict__ rt, con
     bool cullable;
     const int l = threadIdx.x & 63;
     rt_bound(rt, l, C, R, cullable);
+#if defined(RTM_TEST_REVERT_SLOT_MASKS)  // (tools/bounds_demo.sh only: the pre-dfafeba mask, every slot set)
+    return ~(uint32_t)__ballot(cone_culls(k, c, C, R, cullable));
+#else
     const bool exists = l < 16 ? l < rt->n_pl : l - 16 < rt->n_cy;
     return (uint32_t)__ballot(exists & !cone_culls(k, c, C, R, cullable));  // lane i < 16: plane i; 16 + i: cylinder i
+#endif
 }
 
-// The slot bits of a frame's existing primitives (bits 0-15 planes, 16-31 cylinders).
-__device__ __forceinline__ uint32_t rt_slots(int n_pl, int n_cy) {
+// The slot bits of a frame's existing primitives (bits 0-15 planes, 16-31 cylinders):
+// the masks' producers (rt_slots as the default, rt_wave_mask, rt_cull_wave) set no
+// other bit; rt_exist is the exact set trace_pixel checks them against.
+__device__ __forceinline__ uint32_t rt_exist(int n_pl, int n_cy) {
     return ((1u << n_pl) - 1u) | (((1u << n_cy) - 1u) << 16);
+}
+__device__ __forceinline__ uint32_t rt_slots(int n_pl, int n_cy) {
+#if defined(RTM_TEST_REVERT_SLOT_MASKS)
+    return ~0u;
+#else
+    return rt_exist(n_pl, n_cy);
+#endif
 }
 
 // The primitives of `mask` (wave-uniform; bits 0-15 planes, 16-31 cylinders, set only
@@ -814,9 +860,16 @@ __device__ __forceinline__ uint32_t rt_slots(int n_pl, int n_cy) {
 // PERSP: the rays start at the PERSPECTIVE camera position and rt holds its
 // origin-only constants (RtK::persp; a compile-time choice, so the kernel carries
 // one path).
+// A mask bit of a slot the frame does not fill (a producer's bug: no producer sets
+// one) is counted in `oob` and dropped, so the walk never visits an empty slot.
 template <bool PERSP>
 __device__ __forceinline__ void trace_pixel(const RtK* __restrict__ rt, const double o[3], const double d[3],
-                                            double& zb_io, RtHit& hit, uint32_t mask) {
+                                            double& zb_io, RtHit& hit, uint32_t mask, bool& oob) {
+    const uint32_t exist = rt_exist(rt->n_pl, rt->n_cy);
+    if (mask & ~exist) {  // (wave-uniform)
+        oob = true;
+        mask &= exist;
+    }
     double zb = zb_io;
     constexpr bool persp = PERSP;
     for (uint32_t m = mask & 0xFFFFu; m; m &= m - 1u) {
@@ -824,7 +877,7 @@ __device__ __forceinline__ void trace_pixel(const RtK* __restrict__ rt, const do
         double t;
         if (persp ? plane_hit_persp(rt->pl[i], o, d, zb, t) : plane_hit(rt->pl[i], o, d, zb, t)) {
             hit.kind = 2;
-            hit.id = rt->pl[i].id;
+            hit.id = checked_id(rt->pl[i].id, rt->n_pl, oob);
             hit.t = t;
             zb = t;
         }
@@ -837,7 +890,7 @@ __device__ __forceinline__ void trace_pixel(const RtK* __restrict__ rt, const do
         if (t < 0.0) continue;  // behind the camera (and misses)
         if (t > zb) continue;   // behind a known intersection
         hit.kind = 3;
-        hit.id = rt->cy[i].id;
+        hit.id = checked_id(rt->cy[i].id, rt->n_cy, oob);
         hit.t = t;
         cyi = i;
         cypart = part;
@@ -1644,7 +1697,7 @@ __device__ __forceinline__ void eye_tile(const EyePart& a, const ShadowPart& sh,
     int hit_kind = 0, hit_id = -1;
     uint32_t n_evals = 0;
     // the wave's spheres (all lanes active here); ascending bit order = scene order
-    uint32_t smask = um_ ? wave_sphere_mask(a.sph, ns_, xb, xb + TILE_X - 1, yi, yi) : 0u;
+    uint32_t smask = um_ ? wave_sphere_mask_ids(a.sph, ns_, xb, xb + TILE_X - 1, yi, yi, oob) : 0u;
     // the wave's ray-traced primitives (PERSPECTIVE eye; all lanes active here)
     uint32_t rmask = 0u;
 #if defined(RTM_TEST_REVERT_MASK_GUARD)  // (tools/bounds_demo.sh only: the round-3 over-read, to show tests/test_bounds.py catches it)
@@ -1653,8 +1706,8 @@ __device__ __forceinline__ void eye_tile(const EyePart& a, const ShadowPart& sh,
     if (RTP && rtm_ && rb_ + yl < re_) {  // (no mask word for rows past the part)
 #endif
         const int widx = yl * ((a.W + TILE_X - 1) / TILE_X) + (xb / TILE_X);  // (wave-uniform)
-        if (widx < tabs.rtmask_words) {
-            rmask = ((const __attribute__((address_space(4))) uint32_t*)tabs.rtmask)[widx];
+        if (widx < rtw_) {  // (the prologue's grouped copies of tabs.rtmask_words / tabs.rtmask)
+            rmask = ((const __attribute__((address_space(4))) uint32_t*)rtm_)[widx];
         } else {
             oob = true;
             rmask = rt_slots(rt->n_pl, rt->n_cy);  // (every primitive: the result stays exact)
@@ -1687,7 +1740,7 @@ __device__ __forceinline__ void eye_tile(const EyePart& a, const ShadowPart& sh,
                     best = depth;
                     bh = h;
                     bz = a.sph[i].z;
-                    bid = a.sph[i].id;
+                    bid = a.sph[i].id;  // (in range: wave_sphere_mask left out any sphere whose id is not)
                 }
             }
         }
@@ -1699,20 +1752,22 @@ __device__ __forceinline__ void eye_tile(const EyePart& a, const ShadowPart& sh,
             cam_ray(a.eye, x, y, o, d);
             double zb = best;
             if (rt) {
-                trace_pixel<RTP>(rt, o, d, zb, hit, rmask);
+                trace_pixel<RTP>(rt, o, d, zb, hit, rmask, oob);
                 if (COUNT) {
                     n_pl_tests = __builtin_popcount(rmask & ((1u << rt->n_pl) - 1u));
                     n_cy_tests = __builtin_popcount((rmask >> 16) & ((1u << rt->n_cy) - 1u));
                 }
             }
             // (a batch mixes frames with and without SDFs)
-            if (RT == 2 && sdf) trace_sdfs<!COUNT>(sdf, o, d, zb, hit, n_evals);
+            if (RT == 2 && sdf) trace_sdfs<!COUNT>(sdf, o, d, zb, hit, n_evals, oob);
         }
         if (hit.kind) {
             shaded = true;
             if (!RTB) cam_ray(a.eye, x, y, o, d);
             // world position and normal per surface kind (main.rs:729-796)
             double wx, wy, wz, nx, ny, nz, cr, cg, cb;
+            // (the tables below are indexed by the hit's scene id, checked where it was
+            // taken: checked_id)
             if (!RTB || hit.kind == 1) {
                 const ShadeSphereK& s = a.shade[bid];
                 const double depth = bz - bh * s.r;  // calcDepth (main.rs:160-162)
@@ -1729,8 +1784,9 @@ __device__ __forceinline__ void eye_tile(const EyePart& a, const ShadowPart& sh,
                 wx = o[0] + d[0] * hit.t;  // calcDepth = rayT (main.rs:166-171)
                 wy = o[1] + d[1] * hit.t;
                 wz = o[2] + d[2] * hit.t;
+                const int id = hit.id;
                 if (hit.kind == 2) {
-                    const PlaneK& p = rt->pl[hit.id];
+                    const PlaneK& p = rt->pl[id];
                     nx = p.nx;
                     ny = p.ny;
                     nz = p.nz;
@@ -1742,13 +1798,13 @@ __device__ __forceinline__ void eye_tile(const EyePart& a, const ShadowPart& sh,
                     ny = hit.n[1];
                     nz = hit.n[2];
                     if (RT != 2 || hit.kind == 3) {  // (kind 4, an SDF, only with RT 2)
-                        cr = rt->cy[hit.id].cr;
-                        cg = rt->cy[hit.id].cg;
-                        cb = rt->cy[hit.id].cb;
+                        cr = rt->cy[id].cr;
+                        cg = rt->cy[id].cg;
+                        cb = rt->cy[id].cb;
                     } else {
-                        cr = sdf->s[hit.id].cr;
-                        cg = sdf->s[hit.id].cg;
-                        cb = sdf->s[hit.id].cb;
+                        cr = sdf->s[id].cr;
+                        cg = sdf->s[id].cg;
+                        cb = sdf->s[id].cb;
                     }
                 }
             }
@@ -1912,6 +1968,18 @@ __global__ __launch_bounds__(BLOCK) void eye_batch_kernel(CBatch* __restrict__ f
                                     blockIdx.x, blockIdx.y, nullptr, tabs);
 }
 
+// eye_pass8_kernel for a batch (the headline kernel at config 3): the sphere-only pass
+// with the coded map's decode held to 8 waves per SIMD (64 VGPRs, no spills; unheld,
+// the id check of wave_sphere_mask_ids takes it from 62 to 70 VGPRs, 7 waves).
+template <int FMT>
+__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8))) void eye_batch8_kernel(
+    CBatch* __restrict__ fr) {
+    CBatch* f = fr + blockIdx.z;
+    const DevTabs tabs = *(const DevTabs*)&f->tabs;
+    eye_tile<false, false, 0, FMT>(*(const EyePart*)&f->a.ey, *(const ShadowPart*)&f->a.sh, f->smap, f->out,
+                                   blockIdx.x, blockIdx.y, nullptr, tabs);
+}
+
 template <int WPE, int FMT, bool NOSH = false>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8))) void eye_sdf_batch_kernel(
     CBatch* __restrict__ fr) {
@@ -2051,13 +2119,15 @@ __global__ __launch_bounds__(BLOCK) void vp_trace_kernel(const TraceArgs a, doub
     hit.kind = 0;
     hit.id = 0;
     double zb = zbuf[idx];
+    bool oob = false;
     if (a.rt) {
         const uint32_t slots = rt_slots(a.rt->n_pl, a.rt->n_cy);
-        if (a.rt->persp) trace_pixel<true>(a.rt, o, d, zb, hit, slots);
-        else trace_pixel<false>(a.rt, o, d, zb, hit, slots);
+        if (a.rt->persp) trace_pixel<true>(a.rt, o, d, zb, hit, slots, oob);
+        else trace_pixel<false>(a.rt, o, d, zb, hit, slots, oob);
     }
     uint32_t evals = 0;
-    if (a.sdf) trace_sdfs(a.sdf, o, d, zb, hit, evals);
+    if (a.sdf) trace_sdfs(a.sdf, o, d, zb, hit, evals, oob);
+    if (__builtin_expect(oob, 0)) note_oob();
     if (hit.kind) {
         zbuf[idx] = hit.t;
         gh[idx] = hit.t;
@@ -2078,8 +2148,16 @@ __global__ __launch_bounds__(BLOCK) void vp_shade_kernel(const ShadeArgs a, cons
     const int64_t idx = (int64_t)yi * a.W + xi;
     float4 c = make_float4(0.0f, 0.2f, 0.2f, 1.0f);
     const int32_t g = gid[idx];
-    if (g >= 0) {
-        const int32_t kind = g >> 16, id = g & 0xFFFF;
+    // the G-buffer id's table must hold it (the host checked the scene against what the
+    // viewport holds, rtm_render_color_image; checked again per pixel: an id past its
+    // table, or a null table, is counted and the pixel left as background)
+    const int32_t gk = g >> 16, gi = g & 0xFFFF;
+    const int32_t gn_ = gk == 0 ? a.n_spheres : gk == 1 ? (a.rt ? a.rt->n_pl : 0)
+                      : gk == 2 ? (a.rt ? a.rt->n_cy : 0) : gk == 3 ? (a.sdf ? a.sdf->n : 0) : 0;
+    const bool bad = g >= 0 && gi >= gn_;
+    if (__builtin_expect(bad, 0)) note_oob();
+    if (g >= 0 && !bad) {
+        const int32_t kind = gk, id = gi;
         const double s01 = ndc(xi, a.W), u01 = ndc(yi, a.H);
         double o[3], d[3];
         cam_ray(a.eye, s01, u01, o, d);
@@ -2305,7 +2383,7 @@ static void launch_eye_fmt(const FrameArgs& a, const double* smap, void* o, hipS
     } else if (fused) {
         RTM_EYE(true, 0, false);
     } else if (fr) {
-        RTM_EYE(false, 0, false);
+        hipLaunchKernelGGL((eye_batch8_kernel<FMT>), g, dim3(BLOCK), 0, s, fr);
     } else {
         hipLaunchKernelGGL((eye_pass8_kernel<FMT>), g, dim3(BLOCK), 0, s, a, smap, o, tabs);
     }

@@ -426,9 +426,16 @@ class Group:
                                             flags, fmt, out.ctypes.data_as(C.c_void_p)), "rtm_group_render")
         return out
 
-    def close(self):
+    # close() bounds the wait for queued group work: past it the communicators are
+    # aborted (a peer that died with a transfer unmatched cannot hang interpreter exit)
+    CLOSE_TIMEOUT_MS = 120_000
+
+    def close(self, timeout_ms: int | None = None):
         if self._h:
-            _lib().rtm_group_destroy(self._h)
+            lib = _lib()
+            # errors here (an aborted group, a peer lost) only decide how destroy frees
+            lib.rtm_group_synchronize(self._h, self.CLOSE_TIMEOUT_MS if timeout_ms is None else timeout_ms)
+            lib.rtm_group_destroy(self._h)
             self._h = C.c_void_p()
 
     def __del__(self):

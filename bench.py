@@ -313,26 +313,34 @@ def host_output(rtm, scene, eye, shadow, W, H, K, flags, frames=8, n_gpus=0):
     return res
 
 
+def librtm_build_id() -> str:
+    """sha256 (first 16 hex digits) of the librtm.so this run loads: the build a PMC
+    summary must have profiled for its counters to describe the benched code."""
+    import hashlib
+    with open(os.path.join(ROOT, "2018rustraytracer_amd", "librtm.so"), "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()[:16]
+
+
 def _latest_pmc(cfg_id: int, kernel: str, frames_per_launch: int = 1):
     """(file, per-launch counters) of `kernel` from the newest committed PMC summary
-    (tools/profile_pmc.sh) whose launches held `frames_per_launch` frames
-    (`frames_per_launch` in the summary, 1 when absent); (None, None) if none."""
-    import re
-
-    def key(f):  # newest round/version first: r01_v12 after r01_v9 (not lexicographic)
-        m = re.search(r"r(\d+)_v(\d+)", os.path.basename(f))
-        return (int(m.group(1)), int(m.group(2))) if m else (-1, -1)
-
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")), key=key)
-    for f in reversed(files):
+    (tools/profile_pmc.sh) of THIS librtm.so build (its `librtm_build_id` stamp,
+    tools/pmc_summary.py) whose launches held `frames_per_launch` frames
+    (`frames_per_launch` in the summary, 1 when absent); (None, None) if none: a
+    summary of another build is never cited."""
+    want = librtm_build_id()
+    cands = []
+    for f in glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")):
         try:
             d = json.load(open(f))
         except Exception:
             continue
-        if (d.get("config") == cfg_id and kernel in d.get("kernels", {})
+        if (d.get("librtm_build_id") == want and d.get("config") == cfg_id and kernel in d.get("kernels", {})
                 and d.get("frames_per_launch", 1) == frames_per_launch):
-            return os.path.relpath(f, ROOT), d["kernels"][kernel]
-    return None, None
+            cands.append((d.get("generated_unix", 0), f, d))
+    if not cands:
+        return None, None
+    _, f, d = max(cands, key=lambda c: c[0])  # newest by the summary's own time stamp
+    return os.path.relpath(f, ROOT), d["kernels"][kernel]
 
 
 def _latest_traffic(cfg_id: int, kernel: str, frames_per_launch: int = 1):
@@ -349,14 +357,16 @@ def pmc_fractions(cfg_id: int, kernel: str, frames_per_launch: int, alg_ops: int
     the VALU busy fraction with the f64 instructions at 4 cycles."""
     src, k = _latest_pmc(cfg_id, kernel, frames_per_launch)
     if not k or not k.get("avg_duration_ns_profiled"):
-        return None
+        return {"source": None, "librtm_build_id": librtm_build_id(),
+                "note": "no committed PMC summary of this librtm.so build for this config and frames per launch"}
     dur = k["avg_duration_ns_profiled"] * 1e-9
     f64 = 64.0 * sum(k.get(c, 0.0) for c in ("SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64",
                                               "SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_TRANS_F64"))
     valu = k.get("SQ_INSTS_VALU", 0.0)
     f64_wi = f64 / 64.0
     waves = k.get("SQ_WAVES", 0.0) or 1.0
-    return {"source": src, "kernel_name": k.get("kernel_name"), "duration_ns": round(k["avg_duration_ns_profiled"]),
+    return {"source": src, "librtm_build_id": librtm_build_id(), "kernel_name": k.get("kernel_name"),
+            "duration_ns": round(k["avg_duration_ns_profiled"]),
             "issued_f64_lane_ops": int(f64), "issued_f64_frac": round(f64 / dur / 39.3e12, 4),
             "valu_issue_frac": round(valu * 2 / (1024 * 2.4e9 * dur), 4),
             # f64 wave-instructions hold the SIMD 4 cycles (16 f64 lanes per clock), the rest 2
@@ -366,11 +376,35 @@ def pmc_fractions(cfg_id: int, kernel: str, frames_per_launch: int, alg_ops: int
             "note": "counters from the committed PMC summary of this config (same kernel, same frames per launch)"}
 
 
+def available_cores():
+    """The CPUs this process may actually run on, measured: the
+    scheduler affinity mask, capped by the cgroup v2 CPU quota (cpu.max) when one is
+    set, and by the job's CPU share in OMP_NUM_THREADS.  os.cpu_count() reports the
+    whole machine and is recorded beside it."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, period = f.read().split()[:2]
+        if q != "max":
+            quota = float(q) / float(period)
+    except (OSError, ValueError):
+        pass
+    # the GPU box grants each GPU job a CPU share through OMP_NUM_THREADS (16 there)
+    # without an affinity mask or quota: the share is honoured, and named as the limit
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    omp = int(omp) if omp.isdigit() and int(omp) > 0 else None
+    lims = {"sched_getaffinity": aff, "cgroup_cpu_max": int(quota) if quota else None, "OMP_NUM_THREADS": omp}
+    src, n = min(((k, v) for k, v in lims.items() if v), key=lambda kv: kv[1])
+    return max(1, n), {"sched_getaffinity": aff, "cgroup_cpu_max_cpus": quota, "OMP_NUM_THREADS": omp,
+                       "os_cpu_count": os.cpu_count(), "limited_by": src}
+
+
 def cpu_baseline(scene, eye, shadow, w, h, k, flags, threads, what):
     """The CPU oracle (f64 C restatement of main.rs) on the host cores, rank 0 only:
     `threads` threads (default 1, the reference's sequential loops), plus the
-    all-cores mode of BASELINE.md (OpenMP over row bands; the box's CPU share is
-    16 cores, os.cpu_count() reports the whole machine)."""
+    all-cores mode of BASELINE.md (OpenMP over row bands on every CPU the process
+    may run on: available_cores(), measured, not assumed)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle  # checker / CPU baseline only
 
@@ -388,7 +422,7 @@ def cpu_baseline(scene, eye, shadow, w, h, k, flags, threads, what):
     # a bounded sample, ~10 s of CPU work at config 3 (7 single-thread frames + 10 all-core frames)
     n_one, n_all = 7, 10
     best = best_of(n_one, threads)
-    all_cores = min(16, os.cpu_count() or 1)
+    all_cores, core_probe = available_cores()
     best_all = best_of(n_all, all_cores)
     model = None  # log the host CPU model and hardware concurrency
     try:
@@ -401,6 +435,7 @@ def cpu_baseline(scene, eye, shadow, w, h, k, flags, threads, what):
                 cpu_model=model, hardware_concurrency=os.cpu_count(),
                 seconds_per_frame=round(best, 3),
                 all_cores={"value": round(w * h / best_all / 1e6, 3), "cores": all_cores,
+                           "cores_probe": core_probe,
                            "seconds_per_frame": round(best_all, 4),
                            "sample": f"same frame, OpenMP over 8-row bands, best of {n_all}"})
 

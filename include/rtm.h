@@ -381,7 +381,10 @@ int rtm_group_unique_id(uint8_t id[128]);
 int rtm_group_create(int32_t n_devices, const int32_t* devices, rtm_group** out);
 int rtm_group_create_rank(int32_t device, int32_t n_ranks, int32_t rank, const uint8_t id[128],
                           rtm_group** out);
-/* Waits for the group's work, then frees it (communicators destroyed). */
+/* Waits for the group's work, then frees it (communicators destroyed).  The wait is
+ * bounded (600 s by default; RTM_GROUP_DESTROY_TIMEOUT_MS, 0 = none): past it the
+ * communicators are aborted instead, so a lost peer cannot hang the caller.  Bound
+ * it tighter with rtm_group_synchronize(g, timeout_ms) first. */
 void rtm_group_destroy(rtm_group* g);
 /* n_ranks in the group, members driven by this process, the first one's rank */
 int rtm_group_info(rtm_group* g, int32_t* n_ranks, int32_t* n_local, int32_t* first_rank);

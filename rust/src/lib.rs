@@ -24,9 +24,50 @@ pub fn check(rc: i32) -> Result<(), Error> {
     Err(Error { code: rc, message })
 }
 
+/// The reference's `Scene` (main.rs:404-410: spherePrimitives, circlePlanePrimitives,
+/// cappedCylinderPrimitives) plus the implicit patches its march takes as data
+/// (rayEntry_ShadowRay_testing's hard-coded one, main.rs:2024-2029) and the GL
+/// preview's SDFs.  Owns its primitives; `raw` borrows them for one call.
+#[derive(Clone, Default)]
+pub struct Scene {
+    pub spheres: Vec<rtm_sphere>,
+    pub patches: Vec<rtm_patch>,
+    pub circle_planes: Vec<rtm_circle_plane>,
+    pub capped_cylinders: Vec<rtm_capped_cylinder>,
+    pub sdfs: Vec<rtm_sdf>,
+}
+
+fn ptr_or_null<T>(v: &[T]) -> *const T {
+    if v.is_empty() { std::ptr::null() } else { v.as_ptr() }
+}
+
+impl Scene {
+    /// The C view of the scene (valid while `self` is borrowed and unchanged).
+    pub fn raw(&self) -> rtm_scene {
+        rtm_scene {
+            spheres: ptr_or_null(&self.spheres),
+            patches: ptr_or_null(&self.patches),
+            n_spheres: self.spheres.len() as i32,
+            n_patches: self.patches.len() as i32,
+            circle_planes: ptr_or_null(&self.circle_planes),
+            capped_cylinders: ptr_or_null(&self.capped_cylinders),
+            n_circle_planes: self.circle_planes.len() as i32,
+            n_capped_cylinders: self.capped_cylinders.len() as i32,
+            sdfs: ptr_or_null(&self.sdfs),
+            n_sdfs: self.sdfs.len() as i32,
+            reserved: 0,
+        }
+    }
+}
+
+/// The reference's `Camera` (main.rs:1887-1898; the resolution comes with the call).
+pub type Camera = rtm_camera;
+
 /// One device's context: its stream, shadow maps and lanes.
 pub struct Context {
     raw: *mut rtm_ctx,
+    // the device frame `render` renders into before its copy to the host (reused)
+    frame: std::cell::Cell<(*mut c_void, i64)>,
 }
 
 impl Context {
@@ -36,7 +77,45 @@ impl Context {
         }
         let mut raw = std::ptr::null_mut();
         check(unsafe { rtm_ctx_create(device, &mut raw) })?;
-        Ok(Context { raw })
+        Ok(Context { raw, frame: std::cell::Cell::new((std::ptr::null_mut(), 0)) })
+    }
+
+    /// The reference's whole frame -- shadow viewport rasterize + processRaymarchingRays,
+    /// eye viewport rasterize + processRaytracingRays, renderColorImage (main.rs:1568-1628)
+    /// -- as its `Map2d<Color32>`: width*height RGBA f32 in row order, in host memory.
+    /// Blocking.  The same frame as rtm_render, on this context's device and stream.
+    pub fn render(&self, scene: &Scene, eye: &Camera, shadow: &Camera, width: i32, height: i32,
+                  march_steps: i32, flags: i32) -> Result<Vec<f32>, Error> {
+        if width <= 0 || height <= 0 {
+            return Err(Error { code: RTM_ERR_INVALID, message: "image size must be positive".into() });
+        }
+        let n = width as usize * height as usize * 4;
+        let bytes = (n * 4) as i64;
+        let (mut dev, cap) = self.frame.get();
+        if cap < bytes {
+            if !dev.is_null() {
+                check(unsafe { rtm_ctx_free(self.raw, dev) })?;
+                self.frame.set((std::ptr::null_mut(), 0));
+            }
+            check(unsafe { rtm_ctx_alloc(self.raw, bytes, &mut dev) })?;
+            self.frame.set((dev, bytes));
+        }
+        let sc = scene.raw();
+        check(unsafe {
+            rtm_render_async(self.raw, &sc, eye, shadow, width, height, march_steps, flags, 0, height,
+                             dev as *mut f32)
+        })?;
+        let mut out = vec![0f32; n];
+        self.copy_to_host(dev as *const f32, &mut out)?;
+        Ok(out)
+    }
+
+    /// `Viewport{rasterized: None.., zBuffer: +INF, face, camera}` (main.rs:426-439) of
+    /// width x height on this context: the reference's per-seam calls.
+    pub fn viewport(&self, width: i32, height: i32, face: i32, camera: &Camera) -> Result<Viewport<'_>, Error> {
+        let mut raw = std::ptr::null_mut();
+        check(unsafe { rtm_viewport_create(self.raw, width, height, face, camera, &mut raw) })?;
+        Ok(Viewport { _ctx: self, raw, width, height })
     }
 
     pub fn raw(&self) -> *mut rtm_ctx {
@@ -103,8 +182,69 @@ impl Context {
 
 impl Drop for Context {
     fn drop(&mut self) {
+        let (dev, _) = self.frame.get();
+        if !dev.is_null() {
+            unsafe { rtm_ctx_free(self.raw, dev) };
+        }
         unsafe { rtm_ctx_destroy(self.raw) }
     }
+}
+
+/// The reference's `Viewport` (main.rs:426-643) on the device: its zBuffer and
+/// G-buffer stay in device memory between the seams.  Borrowing the context keeps
+/// the viewport from outliving it.
+pub struct Viewport<'a> {
+    _ctx: &'a Context,
+    raw: *mut rtm_viewport,
+    pub width: i32,
+    pub height: i32,
+}
+
+impl Viewport<'_> {
+    /// Viewport::rasterize (main.rs:445): every sphere projected and rasterized into
+    /// the zBuffer / G-buffer (face as created).
+    pub fn rasterize(&mut self, scene: &Scene) -> Result<(), Error> {
+        let sc = scene.raw();
+        check(unsafe { rtm_viewport_rasterize(self.raw, &sc) })
+    }
+
+    /// Viewport::processRaymarchingRays (main.rs:551): the patches marched in order,
+    /// `steps` steps of 0.03 (the reference hard-codes its patch and 500 steps,
+    /// main.rs:2024-2031: pass those for its frame).
+    pub fn process_raymarching_rays(&mut self, patches: &[rtm_patch], steps: i32) -> Result<(), Error> {
+        check(unsafe {
+            rtm_viewport_process_raymarching_rays(self.raw, ptr_or_null(patches), patches.len() as i32, steps)
+        })
+    }
+
+    /// Viewport::processRaytracingRays (main.rs:569): circle planes, then capped
+    /// cylinders, against every pixel's camera ray.
+    pub fn process_raytracing_rays(&mut self, scene: &Scene) -> Result<(), Error> {
+        let sc = scene.raw();
+        check(unsafe { rtm_viewport_process_raytracing_rays(self.raw, &sc) })
+    }
+
+    /// The zBuffer (width*height f64, row order).
+    pub fn z_buffer(&self) -> Result<Vec<f64>, Error> {
+        let mut z = vec![0f64; self.width as usize * self.height as usize];
+        check(unsafe { rtm_viewport_read_zbuffer(self.raw, z.as_mut_ptr()) })?;
+        Ok(z)
+    }
+}
+
+impl Drop for Viewport<'_> {
+    fn drop(&mut self) {
+        unsafe { rtm_viewport_destroy(self.raw) }
+    }
+}
+
+/// renderColorImage(&scene, &viewport, &shadowViewport) (main.rs:710): the shaded
+/// image, width*height RGBA f32 in host memory (its `Map2d<Color32>`).
+pub fn render_color_image(scene: &Scene, vp: &Viewport<'_>, shadow_vp: &Viewport<'_>) -> Result<Vec<f32>, Error> {
+    let mut out = vec![0f32; vp.width as usize * vp.height as usize * 4];
+    let sc = scene.raw();
+    check(unsafe { rtm_render_color_image(&sc, vp.raw, shadow_vp.raw, out.as_mut_ptr()) })?;
+    Ok(out)
 }
 
 /// Device frames owned through a context (freed after its stream drains).

@@ -228,9 +228,34 @@ def test_rust_layouts_equal_the_ctypes_mirror(parsed, rtm):
 
 def test_crate_calls_only_bound_functions(parsed):
     _, _, r_fns = parsed["rust"]
-    for f in ("rust/src/lib.rs", "rust/examples/closely_orbiting.rs"):
+    for f in ("rust/src/lib.rs", "rust/examples/closely_orbiting.rs", "rust/examples/closely_orbiting_seams.rs"):
         src = open(os.path.join(ROOT, f)).read()
         for n in set(re.findall(r"\b(rtm_[a-z0-9_]+)\s*\(", src)):
             assert n in r_fns, (f, n)
     ex = open(os.path.join(ROOT, "rust/examples/closely_orbiting.rs")).read()
     assert "render_frames" in ex  # the animation loop drives rtm_render_frames_async
+
+
+def test_safe_layer_is_the_reference_surface():
+    """The safe layer offers the reference's surface: the whole
+    frame into host memory (Context::render over rtm_render_async + the copy) and one
+    method per seam the reference's drivers call -- Viewport::rasterize (main.rs:445),
+    processRaymarchingRays (main.rs:551), processRaytracingRays (main.rs:569) and
+    renderColorImage (main.rs:710) -- each over its rtm_viewport_* call."""
+    lib = open(os.path.join(ROOT, "rust/src/lib.rs")).read()
+    seams = {"pub fn render(": "rtm_render_async(", "pub fn viewport(": "rtm_viewport_create(",
+             "pub fn rasterize(": "rtm_viewport_rasterize(",
+             "pub fn process_raymarching_rays(": "rtm_viewport_process_raymarching_rays(",
+             "pub fn process_raytracing_rays(": "rtm_viewport_process_raytracing_rays(",
+             "pub fn render_color_image(": "rtm_render_color_image(", "pub fn z_buffer(": "rtm_viewport_read_zbuffer("}
+    for method, call in seams.items():
+        i = lib.find(method)
+        assert i >= 0, method
+        body = lib[i:lib.find("\n    }", i) if method != "pub fn render_color_image(" else lib.find("\n}", i)]
+        assert call in body, (method, call)
+    assert "-> Result<Vec<f32>, Error>" in lib[lib.find("pub fn render("):lib.find("pub fn render(") + 300]
+    assert "impl Drop for Viewport" in lib  # rtm_viewport_destroy
+    ex = open(os.path.join(ROOT, "rust/examples/closely_orbiting_seams.rs")).read()
+    for m in ("ctx.viewport(", ".rasterize(&scene)", ".process_raymarching_rays(", "render_color_image(&scene",
+              "ctx.render(&scene"):
+        assert m in ex, m

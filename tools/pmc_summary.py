@@ -8,9 +8,11 @@ coalesced streaming reads (x2 applied, flagged), WRITE_SIZE is exact for
 import argparse
 import csv
 import glob
+import hashlib
 import json
 import os
 import re
+import time
 from collections import defaultdict
 
 
@@ -51,7 +53,12 @@ def main():
                 except ValueError:
                     pass
                 break
+    # the librtm.so the passes profiled (bench.py cites a summary only for the same build)
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    with open(os.path.join(root, "2018rustraytracer_amd", "librtm.so"), "rb") as f:
+        build_id = hashlib.sha256(f.read()).hexdigest()[:16]
     out = {"config": a.config, "tag": a.tag, "source": "rocprofv3 --pmc, one pass per counter group",
+           "librtm_build_id": build_id, "generated_unix": int(time.time()),
            "frames_per_launch": fpl, "kernels": {}}
     for k, cs in vals.items():
         d = {c: sum(v) / len(v) for c, v in cs.items()}
@@ -69,7 +76,8 @@ def main():
         timed_shadow = k.startswith("shadow_") and not k.startswith("shadow_pass_kernel<true")  # (<true>: stats)
         name = ("shadow_pass" if timed_shadow else
                 "eye_pass" if k.startswith(("eye_pass_kernel<false, false", "eye_batch_kernel<false",
-                                             "eye_sdf_kernel", "eye_sdf_batch_kernel", "eye_pass8_kernel")) else
+                                             "eye_sdf_kernel", "eye_sdf_batch_kernel", "eye_pass8_kernel",
+                                             "eye_batch8_kernel")) else
                 "eye_pass_fused" if k.startswith(("eye_pass_kernel<true, false", "eye_batch_kernel<true")) else k)
         if name in out["kernels"] and out["kernels"][name]["dispatches"] >= d["dispatches"]:
             out["kernels"][k] = d  # the timed kernel of this role is the one with the most dispatches
