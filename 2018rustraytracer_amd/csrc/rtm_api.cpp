@@ -735,6 +735,7 @@ struct rtm_ctx {
     int32_t tab_w = 0, tab_h = 0, tab_np = 0, tab_zmono = 0;
     double tab_z0 = 0.0;
     double tab_inv_sz = 0.0;
+    double tab_sz = 0.0;
     int64_t tab_rec = -1;  // offset (doubles) of the coded tile's records, -1: none
     bool tab_hast = false, tab_sep = false;
 };
@@ -949,6 +950,7 @@ int ensure_tables(rtm_ctx* ctx, int32_t steps, int32_t W, int32_t H, const rtm_c
         ctx->tab_z0 = nz ? zt[0] : 0.0;
         ctx->tab_rec = with_rec ? rec_at : -1;
         ctx->tab_inv_sz = nz ? 1.0 / sz : 0.0;
+        ctx->tab_sz = nz ? sz : 0.0;
     }
     const double* base = (const double*)ctx->tabs.p;
     const int64_t nt2 = ctx->tab_nt, nz2 = ctx->tab_nz;
@@ -959,6 +961,7 @@ int ensure_tables(rtm_ctx* ctx, int32_t steps, int32_t W, int32_t H, const rtm_c
     out->zmono = nz2 ? ctx->tab_zmono : 0;
     out->z0 = nz2 ? ctx->tab_z0 : 0.0;
     out->inv_sz = nz2 ? ctx->tab_inv_sz : 0.0;
+    out->sz = nz2 ? ctx->tab_sz : 0.0;
     if (ctx->tab_sep) {
         out->py = base + nt2 + W + H + nz2;
         out->d0 = out->py + H;

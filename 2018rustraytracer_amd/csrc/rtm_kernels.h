@@ -112,6 +112,8 @@ struct Tables {
     int32_t row_recs;  // RowRecK entries (H rounded up to 64; every read is bounds-checked against it)
     double z0;         // z[0] when z != nullptr (a kernarg copy: no dependent global load for it)
     double inv_sz;     // 1.0 / step.z when z != nullptr (the first-crossing guess's scale)
+    double sz;         // step.z = dir.z * 0.03 when z != nullptr (main.rs:2233; a kernarg: an SGPR pair, not
+                       // a VGPR-held f64 literal the coded tile would spill)
 };
 #define RTM_T_TABLE_MAX 65536
 

@@ -105,23 +105,6 @@ __device__ __forceinline__ uint32_t wave_sphere_mask(const RasterSphereK* __rest
     return (uint32_t)__ballot(m);
 }
 
-// wave_sphere_mask for the eye pass, whose hits shade with the sphere's id: a
-// sphere whose id (the index into a.shade) is past the frame's sphere table is left out
-// of the set and flagged in `oob` (the host validated every id: see checked_id); its
-// id sits in the same 16 bytes as the range words.
-__device__ __forceinline__ uint32_t wave_sphere_mask_ids(const RasterSphereK* __restrict__ sph, int n, int xb, int xe,
-                                                         int ya, int ye, bool& oob) {
-    const int l = threadIdx.x & 63;
-    bool m = false, bad = false;
-    if (l < n) {
-        const RasterSphereK& s = sph[l];
-        m = (ye >= s.iy0) & (ya <= s.iy1) & (xe >= s.ix0) & (xb <= s.ix1);
-        bad = (unsigned)s.id >= (unsigned)n;
-    }
-    if (__builtin_expect(__ballot(bad) != 0, 0)) oob = true;
-    return (uint32_t)__ballot(m & !bad);
-}
-
 // Does the union of a viewport's sphere pixel ranges reach columns [xb, xe] of rows [ya, ye]?
 // An empty union (no sphere covers anything: x0 > x1, the host's (1, 0, 1, 0)) reaches
 // nothing -- without the emptiness test a range spanning row 0 and column 0 would
@@ -1140,8 +1123,24 @@ constexpr int CODED_TILE_ROWS = CODED_ROWS * TILE_Y;
 // 24 us, profiles/r04_v3_*); its march codes take the per-texel check.
 template <int PART>
 constexpr int coded_wave_rows = PART == 2 ? 4 : CODED_ROWS;
+// PART 1 waves loop over P1_STRIPS consecutive 16-row strips (the prologue -- frame
+// header, the LDS table fill and its barrier, the row records -- paid once per wave).
+// 4 strips (a wave per 128 x 64 texels, a quarter of the waves): config 3 340 -> 348,
+// config 2 333 -> 341 Gpix/s in the 4-lane frame, same box, interleaved (the one-lane
+// raster-free launch is slower, 27.5 -> 30.9 us per 8 frames: a quarter of the waves fill
+// the chip 1.2 times; in the lanes the other frames' kernels fill the rest)
+// (profiles/r05_ab_shadow_strips.txt).  RTM_AB_P1NS overrides it in A/B builds.
+#ifndef RTM_AB_P1NS
+#define RTM_AB_P1NS 4
+#endif
+constexpr int P1_STRIPS = RTM_AB_P1NS;
+static_assert(P1_STRIPS >= 1 && P1_STRIPS * 16 <= 64, "a PART 1 wave's row records are one per lane: at most 64 rows");
 template <int PART>
-constexpr int coded_tile_rows = coded_wave_rows<PART> * TILE_Y;
+constexpr int coded_wave_strips = PART == 1 ? P1_STRIPS : 1;
+template <int PART>
+constexpr int coded_wave_span = coded_wave_rows<PART> * coded_wave_strips<PART>;  // rows a wave covers
+template <int PART>
+constexpr int coded_tile_rows = coded_wave_span<PART> * TILE_Y;
 constexpr uint32_t CODE_NONE = 0xFFFFu;  // packed-code +INF (also the U8 map's 0xFF)
 // The BACK-face depth range of a sphere's covered texels: fl(z + fl(h*r)), h in (0, 1].
 __device__ __forceinline__ void sphere_range(const RasterSphereK& s, double& lo, double& hi) {
@@ -1163,7 +1162,7 @@ struct RowLdsK {
     int32_t pad;
 };
 // Dynamic LDS of the coded tile: the 4 waves' row records, then the ZRecK table.
-constexpr size_t CODED_ROW_LDS = sizeof(RowLdsK) * CODED_TILE_ROWS;
+constexpr size_t CODED_ROW_LDS = sizeof(RowLdsK) * CODED_TILE_ROWS * (P1_STRIPS > 1 ? P1_STRIPS : 1);
 
 template <bool INC>
 __device__ __forceinline__ uint32_t code_check(const ZRecK* __restrict__ T, double D, float pyf, float g0, float g1,
@@ -1187,11 +1186,13 @@ template <bool INC, int CODE, int PART>
 __device__ __forceinline__ void shadow_tile_coded(const ShadowPart& a, void* __restrict__ map, int bx, int by,
                                                   ZRecK* __restrict__ T, RowLdsK* __restrict__ RL) {
     constexpr int NR = coded_wave_rows<PART>;
+    constexpr int NS = coded_wave_strips<PART>;  // strips per wave
+    constexpr int SPAN = coded_wave_span<PART>;
     const int lane = threadIdx.x & (TILE_X - 1);
     const int wv = threadIdx.x >> 6;
     const int xb = bx * 128;
     const int x0 = xb + lane * 2;
-    const int y0 = __builtin_amdgcn_readfirstlane(by * coded_tile_rows<PART> + wv * NR);
+    const int yw = __builtin_amdgcn_readfirstlane(by * coded_tile_rows<PART> + wv * SPAN);  // the wave's first row
     const int W = a.W, H = a.H, steps = a.steps;
     const bool march = !(a.flags & RTM_FLAG_NO_MARCH) && a.n_patches > 0 && steps > 0;
     // the LDS records: one per thread, loaded now, written before the barrier
@@ -1204,17 +1205,49 @@ __device__ __forceinline__ void shadow_tile_coded(const ShadowPart& a, void* __r
         rec1 = zsrc[2 * fid + 1];
     }
     const int xs0 = min(x0, W - 1), xs1 = min(x0 + 1, W - 1);
-    ColRecK c0{}, c1{};
-    RowRecK rl{};  // lane < 16: row y0 + lane's record (the wave's LDS row table)
+    ColRecK c00{}, c10{};  // patch 0's column records
+    RowRecK rl{};  // lane < SPAN: row yw + lane's record (the wave's LDS row table)
     if (march) {
-        c0 = a.tab.col[xs0];
-        c1 = a.tab.col[xs1];
-        // (the host pads the row table with non-marching rows to a multiple of 64 rows:
-        // y0 + 15 is inside it; checked all the same)
-        if (lane < NR) {
-            if (y0 + NR <= a.tab.row_recs) rl = a.tab.row[y0 + lane];
-            else note_oob();
+        if (NS == 1) {
+            c00 = a.tab.col[xs0];
+            c10 = a.tab.col[xs1];
         }
+        // (the host pads the row table with non-marching rows to a multiple of 64 rows:
+        // the wave's rows are inside it unless SPAN > 64; checked all the same)
+        if (lane < SPAN) {
+            if (yw + lane < a.tab.row_recs) rl = a.tab.row[yw + lane];
+            else if (yw + lane < H) note_oob();  // (rows past H need no record: no strip reads them)
+        }
+    }
+    if (march) {
+        double2* T2 = reinterpret_cast<double2*>(T);
+        if (fid <= steps) {
+            T2[2 * fid] = rec0;
+            T2[2 * fid + 1] = rec1;
+        }
+        for (int k = fid + BLOCK; k <= steps; k += BLOCK) {
+            T2[2 * k] = zsrc[2 * k];
+            T2[2 * k + 1] = zsrc[2 * k + 1];
+        }
+        if (lane < SPAN) RL[wv * SPAN + lane] = RowLdsK{rl.py, rl.pyf, 0};
+        __syncthreads();
+    }
+    // wave-uniform: bit r = row yw + r marches (inRange01 and < H)
+    const uint64_t rowbits_w = __ballot((lane < SPAN) & (rl.ok != 0));
+#pragma unroll 1
+    for (int st = 0; st < NS; ++st) {
+    const int y0 = yw + NR * st;  // this strip's first row
+    if (NS > 1 && y0 >= H) break;  // (wave-uniform)
+    // patch 0's column records: the prologue's for the first strip; a later strip reloads
+    // them (L1/L2-hot) rather than keep them live across the loop (registers)
+    ColRecK c0 = c00, c1 = c10;
+    if (NS > 1 && march) {
+        // (opaque copies of the column indices: the 64-bit record offsets are formed here,
+        // not kept live across the loop -- held across it they were spilled to scratch)
+        int i0 = xs0, i1 = xs1;
+        asm volatile("" : "+v"(i0), "+v"(i1));
+        c0 = a.tab.col[i0];
+        c1 = a.tab.col[i1];
     }
     // this wave's strip is left to the other part of a split launch (wave-uniform); a
     // skipping wave still fills its records and meets the workgroup barrier.  The
@@ -1227,25 +1260,12 @@ __device__ __forceinline__ void shadow_tile_coded(const ShadowPart& a, void* __r
     uint32_t cdp[NR];
 #pragma unroll
     for (int r = 0; r < NR; ++r) cdp[r] = 0xFFFFFFFFu;
-    if (march) {
-        double2* T2 = reinterpret_cast<double2*>(T);
-        if (fid <= steps) {
-            T2[2 * fid] = rec0;
-            T2[2 * fid + 1] = rec1;
-        }
-        for (int k = fid + BLOCK; k <= steps; k += BLOCK) {
-            T2[2 * k] = zsrc[2 * k];
-            T2[2 * k + 1] = zsrc[2 * k + 1];
-        }
-        if (lane < NR) RL[wv * NR + lane] = RowLdsK{rl.py, rl.pyf, 0};
-        __syncthreads();
-    }
     if (march && !skipw) {
         const double oz = a.tab.z0;
         const float fsteps = (float)steps;
-        const RowLdsK* RW = RL + wv * NR;  // the wave's rows (uniform reads are broadcasts)
-        // wave-uniform: bit r = row r marches (inRange01 and < H)
-        const uint32_t rowbits = (uint32_t)__ballot((lane < NR) & (rl.ok != 0)) & ((1u << NR) - 1u);
+        const RowLdsK* RW = RL + wv * SPAN + NR * st;  // the strip's rows (uniform reads are broadcasts)
+        // wave-uniform: bit r = row y0 + r marches (inRange01 and < H)
+        const uint32_t rowbits = (uint32_t)(rowbits_w >> (NR * st)) & ((1u << NR) - 1u);
         for (int k = 0; k < a.n_patches; ++k) {
             if (k > 0) {
                 c0 = a.tab.col[k * W + xs0];
@@ -1347,7 +1367,8 @@ __device__ __forceinline__ void shadow_tile_coded(const ShadowPart& a, void* __r
             else check(std::true_type{});
             if (__any(sany)) {
                 // exact per-texel march (march_axis) for the texels the check cannot decide
-                const double sz = a.cam.dir[2] * 0.03;
+                // (sz: the host's dir.z * 0.03, the same product)
+                const double sz = a.tab.sz;
 #pragma unroll 1
                 for (int q = 0; q < NR * 2; ++q) {
                     const int qr = q >> 1, qc = q & 1;
@@ -1440,21 +1461,44 @@ __device__ __forceinline__ void shadow_tile_coded(const ShadowPart& a, void* __r
                         if (yb + 3 < sp.iy0 || yb > sp.iy1) continue;  // wave-uniform
                         double lo, hi;
                         sphere_range(sp, lo, hi);
-                        double pa2[2];
+                        // Coverage s2 = pa*pa + pb*pb < 1 with pa = (rel*n)/m: evaluated with
+                        // 1/m (one wave-uniform division per sphere) in place of the divisions,
+                        // the approximate s2 is within ~8 ulp of the reference's, so away from 1
+                        // (|s2' - 1| > 1e-13) it decides exactly; a row where any texel lies
+                        // closer takes the reference's divisions (the coverage rim, rare)
+                        const double inv_m = 1.0 / sp.m;
+                        double qa[2], pa2[2];
 #pragma unroll
                         for (int c = 0; c < 2; ++c) {
-                            const double pa = ((xc[c] - sp.cx) * sp.n) / sp.m;
+                            qa[c] = (xc[c] - sp.cx) * sp.n;
+                            const double pa = qa[c] * inv_m;
                             pa2[c] = pa * pa;
                         }
 #pragma unroll
                         for (int r = 0; r < 4; ++r) {
                             const int y = yb + r;
                             if (y >= H || y < sp.iy0 || y > sp.iy1) continue;  // wave-uniform
-                            const double pb = ((((cdouble*)a.tab.ny)[y] - sp.cy) * sp.n) / sp.m;
-                            const double pb2 = pb * pb;
+                            const double qb = (((cdouble*)a.tab.ny)[y] - sp.cy) * sp.n;
+                            const double pbq = qb * inv_m;
+                            const double pb2 = pbq * pbq;
+                            bool inr[2], unsure = false;
 #pragma unroll
                             for (int c = 0; c < 2; ++c) {
-                                const bool in = pa2[c] + pb2 < 1.0;  // d = sqrt(pa*pa + pb*pb) < 1
+                                const double s2 = pa2[c] + pb2;
+                                inr[c] = s2 < 1.0;
+                                unsure |= fabs(s2 - 1.0) <= 1e-13;
+                            }
+                            if (__builtin_expect(__any(unsure), 0)) {
+                                const double pb = qb / sp.m;
+#pragma unroll
+                                for (int c = 0; c < 2; ++c) {
+                                    const double pa = qa[c] / sp.m;
+                                    inr[c] = pa * pa + pb * pb < 1.0;  // d = sqrt(pa*pa + pb*pb) < 1
+                                }
+                            }
+#pragma unroll
+                            for (int c = 0; c < 2; ++c) {
+                                const bool in = inr[c];
                                 any |= in;
                                 const uint32_t sh16 = 16u * (uint32_t)c, sh2 = 4u * (uint32_t)r + 2u * (uint32_t)c;
                                 const uint32_t v = tm[r][c] < lo ? 0u : tm[r][c] >= hi ? 1u : 2u;
@@ -1520,6 +1564,7 @@ __device__ __forceinline__ void shadow_tile_coded(const ShadowPart& a, void* __r
                     live &= live - 1u;
                     const RasterSphereK& sp = a.sph[i];
                     if (yb + 3 < sp.iy0 || yb > sp.iy1) continue;  // wave-uniform
+                    const double inv_m = 1.0 / sp.m;
                     double pa[2];
 #pragma unroll
                     for (int c = 0; c < 2; ++c) pa[c] = ((xc[c] - sp.cx) * sp.n) / sp.m;
@@ -1527,7 +1572,19 @@ __device__ __forceinline__ void shadow_tile_coded(const ShadowPart& a, void* __r
                     for (int r = 0; r < 4; ++r) {
                         const int y = yb + r;
                         if (y >= H || y < sp.iy0 || y > sp.iy1) continue;  // wave-uniform
-                        const double pb = ((((cdouble*)a.tab.ny)[y] - sp.cy) * sp.n) / sp.m;
+                        const double qb = (((cdouble*)a.tab.ny)[y] - sp.cy) * sp.n;
+                        {  // the division-free filter (see the disjoint path): a row no texel of
+                           // which can be covered needs no exact coverage
+                            const double pbq = qb * inv_m;
+                            bool maybe = false;
+#pragma unroll
+                            for (int c = 0; c < 2; ++c) {
+                                const double paq = ((xc[c] - sp.cx) * sp.n) * inv_m;
+                                maybe |= paq * paq + pbq * pbq < 1.0 + 1e-13;
+                            }
+                            if (!__any(maybe)) continue;
+                        }
+                        const double pb = qb / sp.m;
                         double s2[2];
                         bool in = false;
 #pragma unroll
@@ -1566,10 +1623,15 @@ __device__ __forceinline__ void shadow_tile_coded(const ShadowPart& a, void* __r
             }
         }
     }
-    if (skipw) return;
+    if (skipw) continue;
     // the lane's 4 rows x 2 columns of each block as one 8- (U8) or 16-byte (U16)
     // store: element lane*8 + r*2 + c of block (y >> 2, xb >> 7) (rows past H hold
-    // codes no reader looks up; a block wholly past H does not exist)
+    // codes no reader looks up; a block wholly past H does not exist).  The lane id is
+    // recomputed here (mbcnt): kept live across the march, the batched raster-free kernel
+    // spilled it to scratch, and its reload was a memory round trip ahead of the stores
+    // (plus 12 B of scratch traffic per lane: the 1.29x HBM writes of the r04 PMC view)
+    uint32_t lane_st;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane_st));
 #pragma unroll
     for (int b = 0; b < NR / 4; ++b) {
         const int yb = y0 + 4 * b;
@@ -1579,12 +1641,13 @@ __device__ __forceinline__ void shadow_tile_coded(const ShadowPart& a, void* __r
             // bytes (r, c) at 8*((r & 1)*2 + c) of word r >> 1: the low bytes of two rows' codes
             const uint32_t w0 = __builtin_amdgcn_perm(cdp[4 * b + 1], cdp[4 * b], 0x06040200u);
             const uint32_t w1 = __builtin_amdgcn_perm(cdp[4 * b + 3], cdp[4 * b + 2], 0x06040200u);
-            *reinterpret_cast<uint2*>((uint8_t*)map + blk * 512 + lane * 8) = make_uint2(w0, w1);
+            *reinterpret_cast<uint2*>((uint8_t*)map + blk * 512 + lane_st * 8) = make_uint2(w0, w1);
         } else {
-            *reinterpret_cast<uint4*>((uint8_t*)map + blk * 1024 + lane * 16) =
+            *reinterpret_cast<uint4*>((uint8_t*)map + blk * 1024 + lane_st * 16) =
                 make_uint4(cdp[4 * b], cdp[4 * b + 1], cdp[4 * b + 2], cdp[4 * b + 3]);
         }
     }
+    }  // strips
 }
 
 template <bool INC, int CODE, int PART>
@@ -1644,6 +1707,15 @@ shadow_coded_batch_kernel(CBatch* __restrict__ fr, int4 org) {
 // RT: 0 spheres only, 1 + ray-traced planes/cylinders and PERSPECTIVE spheres,
 // 2 + SDFs (its own instantiation: the sphere-trace loop's registers would
 // otherwise lower the occupancy of every ray-traced frame).
+// A pixel's NDC coordinates and camera ray, kept by a wave that renders the same
+// pixels of several frames of a batch (the frames share the eye camera, size and rows:
+// rtm_api.cpp enqueue_prepared_batch / rtm_render_frames_async), so later frames skip
+// the NDC loads and the ray set-up.  `have` is wave-uniform.
+struct EyePre {
+    double x, y, o[3], d[3];
+    bool have;
+};
+
 // Image row of the launch's local row j (EyePart: contiguous rows or cyclic stripes).
 __device__ __forceinline__ int eye_row(int row_begin, int S, int stride, int phase, int j) {
     return S > 0 ? phase + (j / S) * stride + j % S : row_begin + j;
@@ -1652,7 +1724,7 @@ __device__ __forceinline__ int eye_row(int row_begin, int S, int stride, int pha
 template <bool FUSED, bool COUNT, int RT, int FMT = RTM_FORMAT_RGBA32F, bool NOSH = false>
 __device__ __forceinline__ void eye_tile(const EyePart& a, const ShadowPart& sh, const double* __restrict__ smap,
                                          void* __restrict__ out, int bx, int by, StatsK* __restrict__ st,
-                                         const DevTabs tabs) {
+                                         const DevTabs tabs, EyePre* pre = nullptr) {
     // RT 3: RT 1 under a PERSPECTIVE eye, with the host's origin-only primitive
     // constants (RtK::persp) and the per-wave primitive masks of rt_cull_kernel
     constexpr bool RTP = RT == 3;
@@ -1697,7 +1769,7 @@ __device__ __forceinline__ void eye_tile(const EyePart& a, const ShadowPart& sh,
     int hit_kind = 0, hit_id = -1;
     uint32_t n_evals = 0;
     // the wave's spheres (all lanes active here); ascending bit order = scene order
-    uint32_t smask = um_ ? wave_sphere_mask_ids(a.sph, ns_, xb, xb + TILE_X - 1, yi, yi, oob) : 0u;
+    uint32_t smask = um_ ? wave_sphere_mask(a.sph, ns_, xb, xb + TILE_X - 1, yi, yi) : 0u;
     // the wave's ray-traced primitives (PERSPECTIVE eye; all lanes active here)
     uint32_t rmask = 0u;
 #if defined(RTM_TEST_REVERT_MASK_GUARD)  // (tools/bounds_demo.sh only: the round-3 over-read, to show tests/test_bounds.py catches it)
@@ -1723,8 +1795,14 @@ __device__ __forceinline__ void eye_tile(const EyePart& a, const ShadowPart& sh,
     // (its pixels keep the background colour, as the full loop would leave them)
     const bool reach = smask != 0u || (RTB && rt && rmask != 0u) || (RT == 2 && sdf);
     if (live && reach) {
-        const double x = a.nx[xi];
-        const double y = a.ny[yi];
+        double x, y;
+        if (pre && pre->have) {
+            x = pre->x;
+            y = pre->y;
+        } else {
+            x = a.nx[xi];
+            y = a.ny[yi];
+        }
         // z-test over spheres in scene order, strict '<' against +INF init (main.rs:318)
         double best = INFINITY, bh = 0.0, bz = 0.0;
         int bid = -1;
@@ -1740,7 +1818,7 @@ __device__ __forceinline__ void eye_tile(const EyePart& a, const ShadowPart& sh,
                     best = depth;
                     bh = h;
                     bz = a.sph[i].z;
-                    bid = a.sph[i].id;  // (in range: wave_sphere_mask left out any sphere whose id is not)
+                    bid = a.sph[i].id & (RTM_MAX_SPHERES - 1);  // (a.shade has RTM_MAX_SPHERES entries)
                 }
             }
         }
@@ -1749,7 +1827,23 @@ __device__ __forceinline__ void eye_tile(const EyePart& a, const ShadowPart& sh,
         hit.id = bid;
         double o[3], d[3];
         if (RTB) {
-            cam_ray(a.eye, x, y, o, d);
+            if (pre && pre->have) {
+                for (int k = 0; k < 3; ++k) {
+                    o[k] = pre->o[k];
+                    d[k] = pre->d[k];
+                }
+            } else {
+                cam_ray(a.eye, x, y, o, d);
+                if (pre) {
+                    pre->x = x;
+                    pre->y = y;
+                    for (int k = 0; k < 3; ++k) {
+                        pre->o[k] = o[k];
+                        pre->d[k] = d[k];
+                    }
+                    pre->have = true;
+                }
+            }
             double zb = best;
             if (rt) {
                 trace_pixel<RTP>(rt, o, d, zb, hit, rmask, oob);
@@ -1900,6 +1994,14 @@ __device__ __forceinline__ void eye_tile(const EyePart& a, const ShadowPart& sh,
             }
         }
     }
+    // the sphere ids a hit shades with (a.shade[id]): the host validated them (checked_id);
+    // the frame's first wave checks them again (here, after the tile's stores: earlier it
+    // cost the tile 8 VGPRs) and counts any past the table, and every read above masks
+    // the id into the 16-entry table, so none can leave it
+    if (bx == 0 && by == 0 && threadIdx.x < TILE_X) {  // (wave-uniform)
+        const int l = threadIdx.x;
+        if (__ballot(l < ns_ && (unsigned)a.sph[min(l, RTM_MAX_SPHERES - 1)].id >= (unsigned)ns_)) oob = true;
+    }
     if (__builtin_expect(oob, 0)) note_oob();  // (after the tile's last load, see above)
     if (COUNT) {
         stat_add(&st->eye_sphere_tests, n_tests);
@@ -1968,17 +2070,25 @@ __global__ __launch_bounds__(BLOCK) void eye_batch_kernel(CBatch* __restrict__ f
                                     blockIdx.x, blockIdx.y, nullptr, tabs);
 }
 
-// eye_pass8_kernel for a batch (the headline kernel at config 3): the sphere-only pass
-// with the coded map's decode held to 8 waves per SIMD (64 VGPRs, no spills; unheld,
-// the id check of wave_sphere_mask_ids takes it from 62 to 70 VGPRs, 7 waves).
-template <int FMT>
-__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8))) void eye_batch8_kernel(
-    CBatch* __restrict__ fr) {
-    CBatch* f = fr + blockIdx.z;
-    const DevTabs tabs = *(const DevTabs*)&f->tabs;
-    eye_tile<false, false, 0, FMT>(*(const EyePart*)&f->a.ey, *(const ShadowPart*)&f->a.sh, f->smap, f->out,
-                                   blockIdx.x, blockIdx.y, nullptr, tabs);
+#ifdef RTM_AB_EYE_FPW
+// A/B: the ray-traced batched eye pass with each wave rendering its pixels of
+// RTM_AB_EYE_FPW consecutive frames of the batch (grid z = frame groups), the pixels'
+// NDC coordinates and rays computed once (EyePre)
+template <bool FUSED, int RT, int FMT, bool NOSH = false>
+__global__ __launch_bounds__(BLOCK) void eye_batch_loop_kernel(CBatch* __restrict__ fr, int n) {
+    EyePre pre;
+    pre.have = false;
+#pragma unroll 1
+    for (int j = 0; j < RTM_AB_EYE_FPW; ++j) {
+        const int fi = (int)blockIdx.z * RTM_AB_EYE_FPW + j;
+        if (fi >= n) break;
+        CBatch* f = fr + fi;
+        const DevTabs tabs = *(const DevTabs*)&f->tabs;
+        eye_tile<FUSED, false, RT, FMT, NOSH>(*(const EyePart*)&f->a.ey, *(const ShadowPart*)&f->a.sh, f->smap, f->out,
+                                              blockIdx.x, blockIdx.y, nullptr, tabs, &pre);
+    }
 }
+#endif
 
 template <int WPE, int FMT, bool NOSH = false>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8))) void eye_sdf_batch_kernel(
@@ -2306,11 +2416,14 @@ static void launch_coded(const ShadowPart& sh, const FrameArgs* a, double* smap,
         if (fr) hipLaunchKernelGGL((shadow_coded_batch_kernel<I, M, P>), G, dim3(BLOCK), lsm, s, fr, O);          \
         else hipLaunchKernelGGL((shadow_coded_kernel<I, M, P>), G, dim3(BLOCK), lsm, s, *a, smap, O);            \
     } while (0)
+    // PART 1's workgroup tiles: coded_tile_rows<1> rows (P1_STRIPS strips per wave)
+    constexpr int TR1 = coded_tile_rows<1>;
+    const dim3 g1(g.x, (unsigned)((sh.H + TR1 - 1) / TR1), g.z);
 #define RTM_CKB(I, M)                                           \
     do {                                                        \
         if (split) {                                            \
             if (gb.x > 0 && gb.y > 0) RTM_CK(I, M, 2, gb, orgb); \
-            RTM_CK(I, M, 1, g, org0);                           \
+            RTM_CK(I, M, 1, g1, org0);                          \
         } else {                                                \
             RTM_CK(I, M, 0, g, org0);                           \
         }                                                       \
@@ -2353,11 +2466,23 @@ int launch_shadow_pass(const FrameArgs& a, double* smap, void* stream, StatsK* s
 template <int FMT>
 static void launch_eye_fmt(const FrameArgs& a, const double* smap, void* o, hipStream_t s, dim3 g, bool fused,
                            const DevTabs& tabs, CBatch* fr) {
+#ifdef RTM_AB_EYE_FPW
+#define RTM_EYE(F, R, N)                                                                                           \
+    do {                                                                                                        \
+        if (fr && (R == 1 || R == 3)) {                                                                         \
+            dim3 gl = g;                                                                                        \
+            gl.z = (g.z + RTM_AB_EYE_FPW - 1) / RTM_AB_EYE_FPW;                                                 \
+            hipLaunchKernelGGL((eye_batch_loop_kernel<F, R, FMT, N>), gl, dim3(BLOCK), 0, s, fr, (int)g.z);    \
+        } else if (fr) hipLaunchKernelGGL((eye_batch_kernel<F, R, FMT, N>), g, dim3(BLOCK), 0, s, fr);           \
+        else hipLaunchKernelGGL((eye_pass_kernel<F, false, R, FMT, N>), g, dim3(BLOCK), 0, s, a, smap, o, nullptr, tabs); \
+    } while (0)
+#else
 #define RTM_EYE(F, R, N)                                                                                           \
     do {                                                                                                        \
         if (fr) hipLaunchKernelGGL((eye_batch_kernel<F, R, FMT, N>), g, dim3(BLOCK), 0, s, fr);                  \
         else hipLaunchKernelGGL((eye_pass_kernel<F, false, R, FMT, N>), g, dim3(BLOCK), 0, s, a, smap, o, nullptr, tabs); \
     } while (0)
+#endif
 #define RTM_EYE_SDF(N)                                                                                              \
     do {                                                                                                        \
         if (fr) hipLaunchKernelGGL((eye_sdf_batch_kernel<5, FMT, N>), g, dim3(BLOCK), 0, s, fr);                 \
@@ -2383,7 +2508,7 @@ static void launch_eye_fmt(const FrameArgs& a, const double* smap, void* o, hipS
     } else if (fused) {
         RTM_EYE(true, 0, false);
     } else if (fr) {
-        hipLaunchKernelGGL((eye_batch8_kernel<FMT>), g, dim3(BLOCK), 0, s, fr);
+        RTM_EYE(false, 0, false);
     } else {
         hipLaunchKernelGGL((eye_pass8_kernel<FMT>), g, dim3(BLOCK), 0, s, a, smap, o, tabs);
     }

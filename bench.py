@@ -74,7 +74,7 @@ def parse():
                     help="tile-gather mode: what is rendered and gathered")
     ap.add_argument("--tile-gather-steps", type=int, default=-1,
                     help="frames of the secondary tile-gather measurement (0 = skip it; -1 = auto: "
-                         "at least 512 and at least 2 Gpixel, at most 8192)")
+                         "at least 2048 and at least 16 Gpixel, at most 16384)")
     ap.add_argument("--tile-gather-timeout-s", type=float, default=240.0,
                     help="watchdog of the secondary tile-gather measurement (group set-up included)")
     # The clocks ramp for tens of ms after an idle GPU: a time-based pre-roll before the
@@ -169,8 +169,16 @@ def tile_gather(rtm, lib, ctx, group, world, rank, dist, tdev, c_scenes, eye, sh
     if group is not None:
         # a swap chain of output frames on the root: every member renders its part of a
         # chunk of frames per launch (distinct outputs), chunks spread over its lanes, and
-        # frame i+1.. render while frame i is gathered
-        n_out = 32
+        # frame i+1.. render while frame i is gathered.  The ring is a multiple of the
+        # chunk frames x lanes the library picks for rank 0's part (rtm_api.cpp
+        # frame_batch / lanes_plan), so frames that share a buffer render on one lane and
+        # the root keeps its lanes (rtm_group.cpp chunks_clash_across_lanes: a ring of 32
+        # at 512x512, 64 frames per chunk, would leave it one lane)
+        rows0 = shard.stripe_rows_of(H, world, 8, 0) if world > 1 else H
+        px0 = W * rows0
+        b0 = max(1, min(64 if px0 < (1 << 20) else 32, (64 << 20) // px0))
+        l0 = 3 if px0 >= (16 << 20) else 4
+        n_out = b0 * l0 * -(-32 // (b0 * l0))
         outs = ([torch.empty(W * H * bpp, dtype=torch.uint8, device=dev) for _ in range(n_out)] if rank == 0
                 else [None] * n_out)
         ptrs = [C.c_void_p(o.data_ptr() if o is not None else 0) for o in outs]
@@ -810,8 +818,10 @@ def main():
         # every band count renders the same algorithm: each band evaluates the shadow
         # texels it reads (N = 1 included, so the N = 1 figure is the strong-scaling base)
         tflags = cfg["flags"] | rtm.abi.RTM_FLAG_FUSED_SHADOW
+        # (auto: at least 2048 frames and 16 Gpixel, at most 16384 -- 2048 frames, ~50 ms at
+        # 3840x2160: a 512-frame call read 1-2 % low from the lanes' start and drain)
         tg_steps = (a.tile_gather_steps if a.tile_gather_steps >= 0
-                    else min(8192, max(512, (2 << 30) // (W * H))))
+                    else min(16384, max(2048, (16 << 30) // (W * H))))
         for name, fmt in FORMATS.items():
             if "error" in tile:
                 break

@@ -280,3 +280,54 @@ def test_group_sequence_spreads_chunks_over_lanes(rtm, oracle, scenes, n):
     finally:
         g.close()
         torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("n", [1, 3])
+def test_group_sequence_into_one_buffer_lands_in_order(rtm, oracle, scenes, n):
+    """Every frame of a sequence into ONE root buffer: the repeated
+    output starts a new chunk per frame, and chunks would go to different lanes; the
+    member rendering the root's rows in place then keeps one lane, so the buffer holds
+    the LAST frame (N = 1: the RCCL group in place; N = 3: loopback, the root's own
+    stripes in place, the others' gathered)."""
+    import torch
+    w, h, k = 640, 360, 32
+    eye, sh = scenes.eye_camera(), scenes.shadow_camera()
+    shard = __import__("importlib").import_module("2018rustraytracer_amd.shard")
+    px = w * (shard.stripe_rows_of(h, n, 8, 0) if n > 1 else h)
+    per = max(1, min(64 if px < (1 << 20) else 32, (64 << 20) // px))  # the auto frames per launch
+    frames = [scenes.scene_a_bench(100 + 7 * i) for i in range(per + 1)]
+    g = rtm.Group(n_devices=1) if n == 1 else rtm.Group(n_devices=n, loopback=True)
+    try:
+        buf = device_out(torch, rtm, h, w, 0)
+        buf.fill_(float("nan"))
+        torch.cuda.synchronize()
+        g.render_frames_async(frames, eye, sh, w, h, k, 0, 0, 0, [buf.data_ptr()] * len(frames))
+        g.synchronize(120000)
+        assert g.member_lanes(0) == 1  # (member 0 holds the root, rendering in place)
+        fl = rtm.abi.RTM_FLAG_FUSED_SHADOW if n > 1 else 0
+        want = oracle.render(frames[-1], eye, sh, w, h, k, fl, nthreads=NT)["rgba"]
+        got = to_host(buf, h, w, 0, rtm.abi)
+        assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
+    finally:
+        g.close()
+        torch.cuda.empty_cache()
+
+
+def test_group_distinct_outputs_keep_their_lanes(rtm, scenes):
+    """The lane cap applies only where outputs overlap across chunks: distinct buffers
+    keep the auto lanes (test_group_sequence_spreads_chunks_over_lanes checks the images)."""
+    import torch
+    w, h, k = 640, 360, 16
+    eye, sh = scenes.eye_camera(), scenes.shadow_camera()
+    per = max(1, min(64, (64 << 20) // (w * h)))
+    frames = [scenes.scene_a_bench(100)] * (3 * per)
+    g = rtm.Group(n_devices=1)
+    try:
+        bufs = [device_out(torch, rtm, h, w, 0) for _ in frames]
+        torch.cuda.synchronize()
+        g.render_frames_async(frames, eye, sh, w, h, k, 0, 0, 0, [b.data_ptr() for b in bufs])
+        g.synchronize(120000)
+        assert g.member_lanes(0) == 3
+    finally:
+        g.close()
+        torch.cuda.empty_cache()
