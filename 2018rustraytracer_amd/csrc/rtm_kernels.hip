@@ -59,6 +59,25 @@ __device__ __forceinline__ void note_oob() {
     if ((threadIdx.x & 63) == __builtin_ctzll(__ballot(1))) atomicAdd(&g_oob_reads, 1ull);
 }
 
+#ifdef RTM_AB_PHASES
+// (A/B diagnostic builds only, tools/probes/phases.py) per-wave s_memtime stamps at
+// program points: wave w of kernel region r writes slot k of row r * PHASE_REGION + w.
+// Each stamp waits for the wave's outstanding memory operations first, so a phase
+// includes what it waited for.
+constexpr long long PHASE_REGION = 1 << 18;
+__device__ unsigned long long* g_phase;
+__device__ __forceinline__ void phase_stamp(int region, int k) {
+    __builtin_amdgcn_s_waitcnt(0);
+    const unsigned long long t = __builtin_amdgcn_s_memtime();
+    const long long w = (((long long)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x) * (blockDim.x >> 6) +
+                        (threadIdx.x >> 6);
+    if ((threadIdx.x & 63) == 0 && g_phase && w < PHASE_REGION) g_phase[(region * PHASE_REGION + w) * 8 + k] = t;
+}
+#define RTM_PHASE(r, k) phase_stamp(r, k)
+#else
+#define RTM_PHASE(r, k) ((void)0)
+#endif
+
 // main.rs:306-307 / 1903-1907: ((i as f64) / (res as f64)) * 2.0 - 1.0
 __device__ __forceinline__ double ndc(int i, int res) { return ((double)i / (double)res) * 2.0 - 1.0; }
 
@@ -1193,6 +1212,7 @@ __device__ __forceinline__ void shadow_tile_coded(const ShadowPart& a, void* __r
     const int xb = bx * 128;
     const int x0 = xb + lane * 2;
     const int yw = __builtin_amdgcn_readfirstlane(by * coded_tile_rows<PART> + wv * SPAN);  // the wave's first row
+    RTM_PHASE(PART, 0);
     const int W = a.W, H = a.H, steps = a.steps;
     const bool march = !(a.flags & RTM_FLAG_NO_MARCH) && a.n_patches > 0 && steps > 0;
     // the LDS records: one per thread, loaded now, written before the barrier
@@ -1232,6 +1252,7 @@ __device__ __forceinline__ void shadow_tile_coded(const ShadowPart& a, void* __r
         if (lane < SPAN) RL[wv * SPAN + lane] = RowLdsK{rl.py, rl.pyf, 0};
         __syncthreads();
     }
+    RTM_PHASE(PART, 1);  // (records loaded, LDS filled, past the barrier)
     // wave-uniform: bit r = row yw + r marches (inRange01 and < H)
     const uint64_t rowbits_w = __ballot((lane < SPAN) & (rl.ok != 0));
 #pragma unroll 1
@@ -1263,7 +1284,9 @@ __device__ __forceinline__ void shadow_tile_coded(const ShadowPart& a, void* __r
     if (march && !skipw) {
         const double oz = a.tab.z0;
         const float fsteps = (float)steps;
-        const RowLdsK* RW = RL + wv * SPAN + NR * st;  // the strip's rows (uniform reads are broadcasts)
+        // the strip's rows (uniform reads are broadcasts; the wave's base as a scalar: held in a
+        // VGPR across the strips it was spilled in the single-frame kernel)
+        const RowLdsK* RW = RL + __builtin_amdgcn_readfirstlane(wv * SPAN) + NR * st;
         // wave-uniform: bit r = row y0 + r marches (inRange01 and < H)
         const uint32_t rowbits = (uint32_t)(rowbits_w >> (NR * st)) & ((1u << NR) - 1u);
         for (int k = 0; k < a.n_patches; ++k) {
@@ -1397,6 +1420,7 @@ __device__ __forceinline__ void shadow_tile_coded(const ShadowPart& a, void* __r
             }
         }
     }
+    if (st == 0) RTM_PHASE(PART, 2);  // (strip 0's march codes)
     // shadow viewport rasterize, face BACK (main.rs:1569, 243), 4 rows at a time: the
     // strict minimum over the spheres in scene order, then the march code only where its
     // t is strictly below that minimum (main.rs:559).
@@ -1623,6 +1647,7 @@ __device__ __forceinline__ void shadow_tile_coded(const ShadowPart& a, void* __r
             }
         }
     }
+    if (st == 0) RTM_PHASE(PART, 3);  // (strip 0's raster)
     if (skipw) continue;
     // the lane's 4 rows x 2 columns of each block as one 8- (U8) or 16-byte (U16)
     // store: element lane*8 + r*2 + c of block (y >> 2, xb >> 7) (rows past H hold
@@ -1647,7 +1672,9 @@ __device__ __forceinline__ void shadow_tile_coded(const ShadowPart& a, void* __r
                 make_uint4(cdp[4 * b], cdp[4 * b + 1], cdp[4 * b + 2], cdp[4 * b + 3]);
         }
     }
+    if (st == 0) RTM_PHASE(PART, 4);  // (strip 0 stored)
     }  // strips
+    RTM_PHASE(PART, 5);  // (every strip stored and drained)
 }
 
 template <bool INC, int CODE, int PART>
@@ -1707,15 +1734,6 @@ shadow_coded_batch_kernel(CBatch* __restrict__ fr, int4 org) {
 // RT: 0 spheres only, 1 + ray-traced planes/cylinders and PERSPECTIVE spheres,
 // 2 + SDFs (its own instantiation: the sphere-trace loop's registers would
 // otherwise lower the occupancy of every ray-traced frame).
-// A pixel's NDC coordinates and camera ray, kept by a wave that renders the same
-// pixels of several frames of a batch (the frames share the eye camera, size and rows:
-// rtm_api.cpp enqueue_prepared_batch / rtm_render_frames_async), so later frames skip
-// the NDC loads and the ray set-up.  `have` is wave-uniform.
-struct EyePre {
-    double x, y, o[3], d[3];
-    bool have;
-};
-
 // Image row of the launch's local row j (EyePart: contiguous rows or cyclic stripes).
 __device__ __forceinline__ int eye_row(int row_begin, int S, int stride, int phase, int j) {
     return S > 0 ? phase + (j / S) * stride + j % S : row_begin + j;
@@ -1724,7 +1742,7 @@ __device__ __forceinline__ int eye_row(int row_begin, int S, int stride, int pha
 template <bool FUSED, bool COUNT, int RT, int FMT = RTM_FORMAT_RGBA32F, bool NOSH = false>
 __device__ __forceinline__ void eye_tile(const EyePart& a, const ShadowPart& sh, const double* __restrict__ smap,
                                          void* __restrict__ out, int bx, int by, StatsK* __restrict__ st,
-                                         const DevTabs tabs, EyePre* pre = nullptr) {
+                                         const DevTabs tabs) {
     // RT 3: RT 1 under a PERSPECTIVE eye, with the host's origin-only primitive
     // constants (RtK::persp) and the per-wave primitive masks of rt_cull_kernel
     constexpr bool RTP = RT == 3;
@@ -1736,6 +1754,7 @@ __device__ __forceinline__ void eye_tile(const EyePart& a, const ShadowPart& sh,
     const int xb = __builtin_amdgcn_readfirstlane(bx * TILE_X);
     const int xi = xb + (threadIdx.x & (TILE_X - 1));
     const int yl = __builtin_amdgcn_readfirstlane(by * TILE_Y + (int)(threadIdx.x >> 6));
+    if (!COUNT) RTM_PHASE(3, 0);
     // the header fields the prologue needs, read before any branch so their scalar loads
     // issue as one group: one wait instead of a chain of dependent round trips (the
     // short waves of small frames are latency-bound: config 7 +6 %, profiles/r04_ab_eye_prologue.txt)
@@ -1789,20 +1808,15 @@ __device__ __forceinline__ void eye_tile(const EyePart& a, const ShadowPart& sh,
     } else if (RTB && rt) {
         rmask = rt_slots(rt->n_pl, rt->n_cy);
     }
+    if (!COUNT) RTM_PHASE(3, 1);  // (masks ready)
     float4 c = make_float4(0.0f, 0.2f, 0.2f, 1.0f);  // (0.0, 0.2, 0.2) as f32 (main.rs:718-720)
     bool shaded = false;
     // a wave no sphere, primitive or SDF can reach is background: no NDC loads, no rays
     // (its pixels keep the background colour, as the full loop would leave them)
     const bool reach = smask != 0u || (RTB && rt && rmask != 0u) || (RT == 2 && sdf);
     if (live && reach) {
-        double x, y;
-        if (pre && pre->have) {
-            x = pre->x;
-            y = pre->y;
-        } else {
-            x = a.nx[xi];
-            y = a.ny[yi];
-        }
+        const double x = a.nx[xi];
+        const double y = a.ny[yi];
         // z-test over spheres in scene order, strict '<' against +INF init (main.rs:318)
         double best = INFINITY, bh = 0.0, bz = 0.0;
         int bid = -1;
@@ -1827,23 +1841,7 @@ __device__ __forceinline__ void eye_tile(const EyePart& a, const ShadowPart& sh,
         hit.id = bid;
         double o[3], d[3];
         if (RTB) {
-            if (pre && pre->have) {
-                for (int k = 0; k < 3; ++k) {
-                    o[k] = pre->o[k];
-                    d[k] = pre->d[k];
-                }
-            } else {
-                cam_ray(a.eye, x, y, o, d);
-                if (pre) {
-                    pre->x = x;
-                    pre->y = y;
-                    for (int k = 0; k < 3; ++k) {
-                        pre->o[k] = o[k];
-                        pre->d[k] = d[k];
-                    }
-                    pre->have = true;
-                }
-            }
+            cam_ray(a.eye, x, y, o, d);
             double zb = best;
             if (rt) {
                 trace_pixel<RTP>(rt, o, d, zb, hit, rmask, oob);
@@ -1956,6 +1954,7 @@ __device__ __forceinline__ void eye_tile(const EyePart& a, const ShadowPart& sh,
             }
         }
     }
+    if (!COUNT) RTM_PHASE(3, 2);  // (traced and shaded)
     // the frame store (all lanes converged): RGBA f32, or writeColorImage's bytes
     if (FMT == RTM_FORMAT_RGBA32F) {
         float4* o = reinterpret_cast<float4*>(out);
@@ -1994,6 +1993,7 @@ __device__ __forceinline__ void eye_tile(const EyePart& a, const ShadowPart& sh,
             }
         }
     }
+    if (!COUNT) RTM_PHASE(3, 3);  // (stored, drained)
     // the sphere ids a hit shades with (a.shade[id]): the host validated them (checked_id);
     // the frame's first wave checks them again (here, after the tile's stores: earlier it
     // cost the tile 8 VGPRs) and counts any past the table, and every read above masks
@@ -2069,26 +2069,6 @@ __global__ __launch_bounds__(BLOCK) void eye_batch_kernel(CBatch* __restrict__ f
     eye_tile<FUSED, false, RT, FMT, NOSH>(*(const EyePart*)&f->a.ey, *(const ShadowPart*)&f->a.sh, f->smap, f->out,
                                     blockIdx.x, blockIdx.y, nullptr, tabs);
 }
-
-#ifdef RTM_AB_EYE_FPW
-// A/B: the ray-traced batched eye pass with each wave rendering its pixels of
-// RTM_AB_EYE_FPW consecutive frames of the batch (grid z = frame groups), the pixels'
-// NDC coordinates and rays computed once (EyePre)
-template <bool FUSED, int RT, int FMT, bool NOSH = false>
-__global__ __launch_bounds__(BLOCK) void eye_batch_loop_kernel(CBatch* __restrict__ fr, int n) {
-    EyePre pre;
-    pre.have = false;
-#pragma unroll 1
-    for (int j = 0; j < RTM_AB_EYE_FPW; ++j) {
-        const int fi = (int)blockIdx.z * RTM_AB_EYE_FPW + j;
-        if (fi >= n) break;
-        CBatch* f = fr + fi;
-        const DevTabs tabs = *(const DevTabs*)&f->tabs;
-        eye_tile<FUSED, false, RT, FMT, NOSH>(*(const EyePart*)&f->a.ey, *(const ShadowPart*)&f->a.sh, f->smap, f->out,
-                                              blockIdx.x, blockIdx.y, nullptr, tabs, &pre);
-    }
-}
-#endif
 
 template <int WPE, int FMT, bool NOSH = false>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8))) void eye_sdf_batch_kernel(
@@ -2466,23 +2446,11 @@ int launch_shadow_pass(const FrameArgs& a, double* smap, void* stream, StatsK* s
 template <int FMT>
 static void launch_eye_fmt(const FrameArgs& a, const double* smap, void* o, hipStream_t s, dim3 g, bool fused,
                            const DevTabs& tabs, CBatch* fr) {
-#ifdef RTM_AB_EYE_FPW
-#define RTM_EYE(F, R, N)                                                                                           \
-    do {                                                                                                        \
-        if (fr && (R == 1 || R == 3)) {                                                                         \
-            dim3 gl = g;                                                                                        \
-            gl.z = (g.z + RTM_AB_EYE_FPW - 1) / RTM_AB_EYE_FPW;                                                 \
-            hipLaunchKernelGGL((eye_batch_loop_kernel<F, R, FMT, N>), gl, dim3(BLOCK), 0, s, fr, (int)g.z);    \
-        } else if (fr) hipLaunchKernelGGL((eye_batch_kernel<F, R, FMT, N>), g, dim3(BLOCK), 0, s, fr);           \
-        else hipLaunchKernelGGL((eye_pass_kernel<F, false, R, FMT, N>), g, dim3(BLOCK), 0, s, a, smap, o, nullptr, tabs); \
-    } while (0)
-#else
 #define RTM_EYE(F, R, N)                                                                                           \
     do {                                                                                                        \
         if (fr) hipLaunchKernelGGL((eye_batch_kernel<F, R, FMT, N>), g, dim3(BLOCK), 0, s, fr);                  \
         else hipLaunchKernelGGL((eye_pass_kernel<F, false, R, FMT, N>), g, dim3(BLOCK), 0, s, a, smap, o, nullptr, tabs); \
     } while (0)
-#endif
 #define RTM_EYE_SDF(N)                                                                                              \
     do {                                                                                                        \
         if (fr) hipLaunchKernelGGL((eye_sdf_batch_kernel<5, FMT, N>), g, dim3(BLOCK), 0, s, fr);                 \
@@ -2620,6 +2588,15 @@ int launch_eye_batch(const BatchFrame* dev, int n, const FrameArgs& a0, const De
     else launch_eye_fmt<RTM_FORMAT_RGBA32F>(a0, nullptr, nullptr, s, g, fused, t0, fr);
     return launched();
 }
+
+#ifdef RTM_AB_PHASES
+}  // namespace rtm
+extern "C" int rtm_diag_set_phase_buffer(void* dev) {
+    return hipMemcpyToSymbol(HIP_SYMBOL(rtm::g_phase), &dev, sizeof dev) == hipSuccess ? 0 : -3;
+}
+extern "C" long long rtm_diag_phase_region(void) { return rtm::PHASE_REGION; }
+namespace rtm {
+#endif
 
 int read_oob_reads(unsigned long long* count, void* stream) {
     const unsigned long long zero = 0ull;
