@@ -1148,7 +1148,9 @@ constexpr int coded_wave_rows = PART == 2 ? 4 : CODED_ROWS;
 // config 2 333 -> 341 Gpix/s in the 4-lane frame, same box, interleaved (the one-lane
 // raster-free launch is slower, 27.5 -> 30.9 us per 8 frames: a quarter of the waves fill
 // the chip 1.2 times; in the lanes the other frames' kernels fill the rest)
-// (profiles/r05_ab_shadow_strips.txt).  RTM_AB_P1NS overrides it in A/B builds.
+// (profiles/r05_ab_shadow_strips.txt).  The whole-span shortcut below then takes the
+// raster-free launch to 21.6 us one-lane and config 3 345 -> 359 Gpix/s in the lanes
+// (profiles/r05_ab_span.txt).  RTM_AB_P1NS overrides it in A/B builds.
 #ifndef RTM_AB_P1NS
 #define RTM_AB_P1NS 4
 #endif
@@ -1255,6 +1257,71 @@ __device__ __forceinline__ void shadow_tile_coded(const ShadowPart& a, void* __r
     RTM_PHASE(PART, 1);  // (records loaded, LDS filled, past the barrier)
     // wave-uniform: bit r = row yw + r marches (inRange01 and < H)
     const uint64_t rowbits_w = __ballot((lane < SPAN) & (rl.ok != 0));
+    // The whole span's shortcut (PART 1, one patch, every one of the wave's SPAN rows
+    // marching): a column's codes over the span are one monotone sequence by the strip
+    // argument (D is monotone down the whole column), so both ends, decided on one side of
+    // the entry threshold with D of one sign, and one binary search over the span locate
+    // its single boundary -- one chain of log2(SPAN) checks instead of one per strip.
+    // Any column it cannot decide sends the wave to the per-strip path.
+    bool span_ok = false;
+    uint32_t stop[2] = {CODE_NONE, CODE_NONE}, sbot[2] = {CODE_NONE, CODE_NONE};
+    int sbnd[2] = {SPAN, SPAN};
+    if (PART == 1 && NS > 1 && march && a.n_patches == 1 && rowbits_w == (SPAN == 64 ? ~0ull : ((1ull << SPAN) - 1))) {
+        int i0 = xs0, i1 = xs1;
+        asm volatile("" : "+v"(i0), "+v"(i1));
+        const ColRecK q0 = a.tab.col[i0], q1 = a.tab.col[i1];
+        const double d0[2] = {q0.d0, q1.d0};
+        const double dd[2] = {q0.dd, q1.dd};
+        const float g0[2] = {q0.g0, q1.g0};
+        const float g1[2] = {q0.g1, q1.g1};
+        const double oz = a.tab.z0;
+        const float fsteps = (float)steps;
+        const RowLdsK* RS = RL + __builtin_amdgcn_readfirstlane(wv * SPAN);
+        bool ok = true;
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            const RowLdsK rt = RS[0], rb = RS[SPAN - 1];
+            const double Dt = d0[c] + dd[c] * rt.py;
+            const double Db = d0[c] + dd[c] * rb.py;
+            bool st_, et, sb, eb;
+            stop[c] = code_check<INC>(T, Dt, rt.pyf, g0[c], g1[c], fsteps, oz, steps, st_, et);
+            sbot[c] = code_check<INC>(T, Db, rb.pyf, g0[c], g1[c], fsteps, oz, steps, sb, eb);
+            ok = ok & !st_ & !sb & (et == eb) & (__builtin_signbit(Dt) == __builtin_signbit(Db));
+        }
+        span_ok = __all(ok);
+        if (span_ok) {
+            const bool need[2] = {stop[0] != sbot[0], stop[1] != sbot[1]};
+            if (__any(need[0] | need[1])) {
+                int lo[2] = {0, 0}, hi[2] = {SPAN - 1, SPAN - 1};
+                uint32_t chi[2] = {sbot[0], sbot[1]};
+                bool bad = false;
+                constexpr int HALVINGS = SPAN <= 16 ? 4 : SPAN <= 32 ? 5 : 6;
+#pragma unroll
+                for (int it = 0; it < HALVINGS; ++it) {
+#pragma unroll
+                    for (int c = 0; c < 2; ++c) {
+                        const bool act = need[c] & (hi[c] - lo[c] > 1);
+                        const int mid = (lo[c] + hi[c]) >> 1;
+                        const RowLdsK rr = RS[act ? mid : 0];
+                        const double Dm = d0[c] + dd[c] * rr.py;
+                        bool sm, em;
+                        const uint32_t cm = code_check<INC>(T, Dm, rr.pyf, g0[c], g1[c], fsteps, oz, steps, sm, em);
+                        bad |= act & sm;
+                        const bool same = cm == stop[c];
+                        lo[c] = (act & same) ? mid : lo[c];
+                        hi[c] = (act & !same) ? mid : hi[c];
+                        chi[c] = (act & !same) ? cm : chi[c];
+                    }
+                }
+#pragma unroll
+                for (int c = 0; c < 2; ++c) {
+                    bad |= need[c] & (chi[c] != sbot[c]);
+                    sbnd[c] = need[c] ? hi[c] : SPAN;
+                }
+                span_ok = !__any(bad);
+            }
+        }
+    }
 #pragma unroll 1
     for (int st = 0; st < NS; ++st) {
     const int y0 = yw + NR * st;  // this strip's first row
@@ -1281,7 +1348,14 @@ __device__ __forceinline__ void shadow_tile_coded(const ShadowPart& a, void* __r
     uint32_t cdp[NR];
 #pragma unroll
     for (int r = 0; r < NR; ++r) cdp[r] = 0xFFFFFFFFu;
-    if (march && !skipw) {
+    if (span_ok && !skipw) {
+        // rows [0, sbnd) of the span hold the top code, [sbnd, SPAN) the bottom one
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {
+            const int row = NR * st + r;
+            cdp[r] = (row < sbnd[0] ? stop[0] : sbot[0]) | ((row < sbnd[1] ? stop[1] : sbot[1]) << 16);
+        }
+    } else if (march && !skipw) {
         const double oz = a.tab.z0;
         const float fsteps = (float)steps;
         // the strip's rows (uniform reads are broadcasts; the wave's base as a scalar: held in a
@@ -1706,10 +1780,15 @@ __device__ __forceinline__ void shadow_coded_block(const ShadowPart& sh, void* _
                                        reinterpret_cast<RowLdsK*>(lds));
 }
 
-// waves per SIMD the register allocator must keep: 7 for the raster-free part (round 3:
-// uncapped, fewer spilled SGPRs cost 90 VGPRs and 5 waves), else free
+// waves per SIMD the register allocator must keep: 6 for the raster-free part (round 3:
+// uncapped, fewer spilled SGPRs cost 90 VGPRs and 5 waves; round 5: the span shortcut's
+// registers spilled 16 B to scratch under 7, none under 6 -- 80 VGPRs, and 6 waves of
+// 4-strip waves still fill the chip), else free
+#ifndef RTM_AB_P1WAVES
+#define RTM_AB_P1WAVES 6
+#endif
 template <int PART>
-constexpr int CODED_MIN_WAVES = PART == 1 ? 7 : 1;
+constexpr int CODED_MIN_WAVES = PART == 1 ? RTM_AB_P1WAVES : 1;
 
 template <bool INC, int CODE, int PART>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(CODED_MIN_WAVES<PART>, 8))) void
