@@ -824,19 +824,95 @@ __device__ __forceinline__ bool cone_culls(const RayCone& k, const CamK& c, cons
     return cullable & (L > Ri) & (sb < 1.0) & (aw < thr * L);
 }
 
+// The capsule bound of a capped cone (pa, pb, R = max|r|: every point of its caps and
+// body lies within R of the segment pa-pb), against the wave's ray cone: no ray of the
+// cone meets the capsule when gamma, the least angle between the cone's axis and the
+// directions (from the apex) of the segment's points, exceeds theta + beta, beta =
+// asin(Ri / dmin) the angular radius of the capsule's cross-section at its least
+// distance dmin from the apex.  gamma: the nearer endpoint, or -- when the axis's
+// projection on the plane of the segment's directions falls on the arc between them
+// -- the angle to that plane.  The same inflation and margins as cone_culls; a long,
+// thin cylinder (main()'s scene: |ba| = 10, R = 0.3) is bounded 10x tighter than by
+// its sphere.  Non-finite data and a capsule holding the apex are kept.
+__device__ __forceinline__ bool capsule_culls(const RayCone& k, const CamK& c, const double pa[3], const double pb[3],
+                                              double R, bool cullable) {
+    const double Ri = R * 1.001 + 1e-7;
+    double p0[3], e[3], pe = 0.0, ee = 0.0;
+    for (int j = 0; j < 3; ++j) {
+        p0[j] = pa[j] - c.pos[j];
+        e[j] = pb[j] - pa[j];
+        pe += p0[j] * e[j];
+        ee += e[j] * e[j];
+    }
+    const double s = ee > 0.0 ? fmin(fmax(-pe / ee, 0.0), 1.0) : 0.0;
+    double q2 = 0.0, l0 = 0.0, l1 = 0.0, c0 = 0.0, c1 = 0.0, p1[3];
+    for (int j = 0; j < 3; ++j) {
+        p1[j] = p0[j] + e[j];
+        const double qj = p0[j] + e[j] * s;
+        q2 += qj * qj;
+        l0 += p0[j] * p0[j];
+        l1 += p1[j] * p1[j];
+        c0 += k.ax[j] * p0[j];
+        c1 += k.ax[j] * p1[j];
+    }
+    const double dmin = sqrt(q2);
+    if (!(dmin > Ri)) return false;  // (the apex inside the capsule; NaN)
+    const double sb = Ri / dmin;     // sin(beta)
+    const double cb = sqrt(fmax(1.0 - sb * sb, 0.0));
+    const double thr = k.ct * cb - k.st * sb - 1e-7;  // cos(theta + beta), less the margin
+    l0 = sqrt(l0);
+    l1 = sqrt(l1);
+    double u0[3], u1[3];
+    for (int j = 0; j < 3; ++j) {
+        u0[j] = p0[j] / l0;
+        u1[j] = p1[j] / l1;
+    }
+    double cg = fmax(c0 / l0, c1 / l1);  // cos of the angle to the nearer endpoint
+    double n[3] = {u0[1] * u1[2] - u0[2] * u1[1], u0[2] * u1[0] - u0[0] * u1[2], u0[0] * u1[1] - u0[1] * u1[0]};
+    const double nn = sqrt(n[0] * n[0] + n[1] * n[1] + n[2] * n[2]);
+    if (nn > 1e-12) {  // (else the arc is a point within 1e-12 rad: its endpoints decide)
+        double an = 0.0;
+        for (int j = 0; j < 3; ++j) {
+            n[j] /= nn;
+            an += k.ax[j] * n[j];
+        }
+        double ap[3];
+        for (int j = 0; j < 3; ++j) ap[j] = k.ax[j] - an * n[j];
+        // (u0 x ap).n and (ap x u1).n: the projection between the endpoints (a loose
+        // bound: counting a projection just outside the arc only raises cg)
+        const double w0 = (u0[1] * ap[2] - u0[2] * ap[1]) * n[0] + (u0[2] * ap[0] - u0[0] * ap[2]) * n[1] +
+                          (u0[0] * ap[1] - u0[1] * ap[0]) * n[2];
+        const double w1 = (ap[1] * u1[2] - ap[2] * u1[1]) * n[0] + (ap[2] * u1[0] - ap[0] * u1[2]) * n[1] +
+                          (ap[0] * u1[1] - ap[1] * u1[0]) * n[2];
+        if (!(w0 < -1e-6) && !(w1 < -1e-6)) cg = fmax(cg, sqrt(fmax(1.0 - an * an, 0.0)));
+    }
+    return cullable & (cg < thr);
+}
+
+// Slot l culled for the wave's cone: its bounding sphere, or (a cylinder) its capsule.
+__device__ __forceinline__ bool rt_culls(const RtK* __restrict__ rt, int l, const RayCone& k, const CamK& c) {
+    double C[3], R;
+    bool cullable;
+    rt_bound(rt, l, C, R, cullable);
+    if (cone_culls(k, c, C, R, cullable)) return true;
+    if (l >= 16 && l - 16 < rt->n_cy) {
+        const CylK& q = rt->cy[l - 16];
+        return capsule_culls(k, c, q.pa, q.pb, fmax(fabs(q.ra), fabs(q.rb)), cullable);
+    }
+    return false;
+}
+
 // Lane-parallel form inside a kernel (all lanes active): lane l tests slot l.
 __device__ __forceinline__ uint32_t rt_wave_mask(const RtK* __restrict__ rt, const CamK& c, int xb, int xe, int yi,
                                                  int W, int H) {
     const RayCone k = ray_cone(c, xb, xe, yi, W, H);
-    double C[3], R;
-    bool cullable;
     const int l = threadIdx.x & 63;
-    rt_bound(rt, l, C, R, cullable);
+    const bool culled = rt_culls(rt, l, k, c);
 #if defined(RTM_TEST_REVERT_SLOT_MASKS)  // (tools/bounds_demo.sh only: the pre-dfafeba mask, every slot set)
-    return ~(uint32_t)__ballot(cone_culls(k, c, C, R, cullable));
+    return ~(uint32_t)__ballot(culled);
 #else
     const bool exists = l < 16 ? l < rt->n_pl : l - 16 < rt->n_cy;
-    return (uint32_t)__ballot(exists & !cone_culls(k, c, C, R, cullable));  // lane i < 16: plane i; 16 + i: cylinder i
+    return (uint32_t)__ballot(exists & !culled);  // lane i < 16: plane i; 16 + i: cylinder i
 #endif
 }
 
@@ -1818,17 +1894,25 @@ __device__ __forceinline__ int eye_row(int row_begin, int S, int stride, int pha
     return S > 0 ? phase + (j / S) * stride + j % S : row_begin + j;
 }
 
+template <class T>
+__device__ __forceinline__ const T* const_table(const T* p) {
+    return (const T*)(const __attribute__((address_space(4))) T*)p;
+}
+
 template <bool FUSED, bool COUNT, int RT, int FMT = RTM_FORMAT_RGBA32F, bool NOSH = false>
 __device__ __forceinline__ void eye_tile(const EyePart& a, const ShadowPart& sh, const double* __restrict__ smap,
                                          void* __restrict__ out, int bx, int by, StatsK* __restrict__ st,
-                                         const DevTabs tabs) {
+                                         const DevTabs tabs, bool KMB = false, uint32_t kmw = 0u,
+                                         bool km_in = false) {
     // RT 3: RT 1 under a PERSPECTIVE eye, with the host's origin-only primitive
     // constants (RtK::persp) and the per-wave primitive masks of rt_cull_kernel
     constexpr bool RTP = RT == 3;
     constexpr int RTB = RTP ? 1 : RT;
-    const RtK* __restrict__ rt = tabs.rt;
-    const PerspK* __restrict__ psp = tabs.psp;
-    const SdfTabK* __restrict__ sdf = tabs.sdf;
+    // the frame's tables through constant-address-space pointers: their reads are scalar
+    // loads wherever the address is uniform, whatever the kernel stored before them
+    const RtK* rt_ = tabs.rt;
+    const PerspK* __restrict__ psp = const_table(tabs.psp);
+    const SdfTabK* __restrict__ sdf = const_table(tabs.sdf);
     // the workgroup's 4 waves stacked (64 x 4 pixels)
     const int xb = __builtin_amdgcn_readfirstlane(bx * TILE_X);
     const int xi = xb + (threadIdx.x & (TILE_X - 1));
@@ -1849,9 +1933,19 @@ __device__ __forceinline__ void eye_tile(const EyePart& a, const ShadowPart& sh,
     // -- makes every load complete here, together, under one wait; for the ray-traced
     // instantiations only: it pushes the SDF one to 155 spilled VGPRs and the sphere-only
     // one from 60 to 66 VGPRs, profiles/r04_ab_eye_prologue.txt)
+    // (with the batch kernel's mask word, the primitive table and the frame; the pointers
+    // pass as global-address-space ones: an asm's generic output pointer loses its address
+    // space, and the primitive table's reads became flat vector loads -- config 6 -29 %)
+    typedef const __attribute__((address_space(4))) RtK* RtG;
+    typedef __attribute__((address_space(1))) char* OutG;
+    RtG rtg = (RtG)rt_;
+    OutG outg = (OutG)out;
     if (RT == 1 || RT == 3)
         asm("" : "+s"(W_), "+s"(H_), "+s"(rb_), "+s"(re_), "+s"(og_), "+s"(S_), "+s"(ss_), "+s"(sp_), "+s"(rtm_),
-            "+s"(ns_), "+s"(cx0_), "+s"(cx1_), "+s"(cy0_), "+s"(cy1_), "+s"(nx_), "+s"(ny_), "+s"(rtw_));
+            "+s"(ns_), "+s"(cx0_), "+s"(cx1_), "+s"(cy0_), "+s"(cy1_), "+s"(nx_), "+s"(ny_), "+s"(rtw_), "+s"(kmw),
+            "+s"(rtg), "+s"(outg));
+    const RtK* __restrict__ rt = (const RtK*)rtg;
+    out = (void*)outg;
     const int yi = __builtin_amdgcn_readfirstlane(eye_row(rb_, S_, ss_, sp_, yl));
     const int yo = og_ ? yi : yl;  // the output row
     const bool live = (xi < W_) & (rb_ + yl < re_) & (yi < H_);
@@ -1873,7 +1967,15 @@ __device__ __forceinline__ void eye_tile(const EyePart& a, const ShadowPart& sh,
 #if defined(RTM_TEST_REVERT_MASK_GUARD)  // (tools/bounds_demo.sh only: the round-3 over-read, to show tests/test_bounds.py catches it)
     if (RTP && rtm_) {
 #else
-    if (RTP && rtm_ && rb_ + yl < re_) {  // (no mask word for rows past the part)
+    if (RTP && KMB) {
+        // (the batch kernel's word, loaded with the header; nw = gx * rows words, so
+        // km_in is the row guard; a frame without primitives has no word, and rt == null)
+        if (km_in) rmask = kmw;
+        else if (rb_ + yl < re_ && rt) {
+            oob = true;
+            rmask = rt_slots(rt->n_pl, rt->n_cy);
+        }
+    } else if (RTP && rtm_ && rb_ + yl < re_) {  // (no mask word for rows past the part)
 #endif
         const int widx = yl * ((a.W + TILE_X - 1) / TILE_X) + (xb / TILE_X);  // (wave-uniform)
         if (widx < rtw_) {  // (the prologue's grouped copies of tabs.rtmask_words / tabs.rtmask)
@@ -1892,7 +1994,11 @@ __device__ __forceinline__ void eye_tile(const EyePart& a, const ShadowPart& sh,
     bool shaded = false;
     // a wave no sphere, primitive or SDF can reach is background: no NDC loads, no rays
     // (its pixels keep the background colour, as the full loop would leave them)
+#ifdef RTM_AB_BGONLY  // (diagnostic A/B builds only: every wave stores the background -- not the image)
+    const bool reach = false;
+#else
     const bool reach = smask != 0u || (RTB && rt && rmask != 0u) || (RT == 2 && sdf);
+#endif
     if (live && reach) {
         const double x = a.nx[xi];
         const double y = a.ny[yi];
@@ -2141,12 +2247,49 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
 
 // NOSH: frames whose shadow viewport is all +INF (no shadow raster, no march): the
 // lookup is skipped (lit = +INF > qz, as the fused texel would give)
+// RT 3: the batch's per-wave primitive masks, addressed from the kernel arguments
+// (frame z's nw words at km + z * nw, nw = gx * rows) so that their load issues with the
+// frame header's, not after it
+// A RT 3 frame without shadows (main()'s scene and row f-1's bench, configs 6 and 7)
+// has short waves: its batched workgroups render RTM_AB_EYE_TILES_RT3 = 4 tiles one after
+// another, held to 8 waves per SIMD (62 VGPRs): configs 6 / 7 +1.5 % against one tile
+// (profiles/r05_ab_eye_tiles.txt).  The table reads stay scalar loads after a tile's
+// stores because the tables are read through constant-address-space pointers
+// (const_table); the frame pointer is opaque per tile, so the header is re-read from the
+// scalar cache rather than held in registers across the tiles (68 -> 62 VGPRs).
+#ifndef RTM_AB_EYE_TILES_RT3
+#define RTM_AB_EYE_TILES_RT3 4
+#endif
+template <int RT, bool NOSH>
+constexpr int eye_batch_tiles = RT == 3 && NOSH ? RTM_AB_EYE_TILES_RT3 : 1;
+// The sphere-only batched eye pass on the materialised map (the headline kernel) is held
+// to 8 waves per SIMD as well: 62 VGPRs, no scratch (the compiler's own allocation gave
+// 68, 7 waves): configs 3 / 2 / 4 +2 % (profiles/r05_ab_eye_tiles.txt).  The fused one
+// stays free: held to 8 it spills 20 B.
+#ifndef RTM_AB_EYE_WPE_RT0
+#define RTM_AB_EYE_WPE_RT0 8
+#endif
+template <bool FUSED, int RT, bool NOSH>
+constexpr int eye_batch_wpe = RT == 3 && NOSH ? 8 : RT == 0 && !FUSED ? RTM_AB_EYE_WPE_RT0 : 1;
 template <bool FUSED, int RT, int FMT, bool NOSH = false>
-__global__ __launch_bounds__(BLOCK) void eye_batch_kernel(CBatch* __restrict__ fr) {
-    CBatch* f = fr + blockIdx.z;
-    const DevTabs tabs = *(const DevTabs*)&f->tabs;
-    eye_tile<FUSED, false, RT, FMT, NOSH>(*(const EyePart*)&f->a.ey, *(const ShadowPart*)&f->a.sh, f->smap, f->out,
-                                    blockIdx.x, blockIdx.y, nullptr, tabs);
+__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(eye_batch_wpe<FUSED, RT, NOSH>, 8))) void eye_batch_kernel(
+    CBatch* __restrict__ fr, const uint32_t* __restrict__ km, int km_nw, int km_gx) {
+    constexpr int NT = eye_batch_tiles<RT, NOSH>;
+#pragma unroll 1
+    for (int t = 0; t < NT; ++t) {
+        CBatch* f = fr + blockIdx.z;
+        if (NT > 1) asm volatile("" : "+s"(f));
+        const int by = (int)blockIdx.y * NT + t;
+        const DevTabs tabs = *(const DevTabs*)&f->tabs;
+        uint32_t kmw = 0u;
+        int widx = 0;
+        if (RT == 3) {
+            widx = __builtin_amdgcn_readfirstlane((by * TILE_Y + (int)(threadIdx.x >> 6)) * km_gx + (int)blockIdx.x);
+            kmw = ((const __attribute__((address_space(4))) uint32_t*)km)[(size_t)blockIdx.z * km_nw + min(widx, km_nw - 1)];
+        }
+        eye_tile<FUSED, false, RT, FMT, NOSH>(*(const EyePart*)&f->a.ey, *(const ShadowPart*)&f->a.sh, f->smap, f->out,
+                                        blockIdx.x, by, nullptr, tabs, true, kmw, widx < km_nw);
+    }
 }
 
 template <int WPE, int FMT, bool NOSH = false>
@@ -2189,10 +2332,7 @@ __device__ __forceinline__ void rt_cull_wave(const CamK& c, const RtK* __restric
     uint32_t m = rt_slots(rt->n_pl, rt->n_cy);
     for (int l = 0; l < 32; ++l) {
         if (!((m >> l) & 1u)) continue;
-        double C[3], R;
-        bool cullable;
-        rt_bound(rt, l, C, R, cullable);
-        if (cone_culls(k, c, C, R, cullable)) m &= ~(1u << l);
+        if (rt_culls(rt, l, k, c)) m &= ~(1u << l);
     }
     masks[t] = m;
 }
@@ -2525,9 +2665,15 @@ int launch_shadow_pass(const FrameArgs& a, double* smap, void* stream, StatsK* s
 template <int FMT>
 static void launch_eye_fmt(const FrameArgs& a, const double* smap, void* o, hipStream_t s, dim3 g, bool fused,
                            const DevTabs& tabs, CBatch* fr) {
+    struct {
+        const uint32_t* p;
+        int nw, gx;
+    } km{nullptr, 1, 1};
+    if (fr && tabs.rtmask) km = {tabs.rtmask, tabs.rtmask_words, (int)g.x};
 #define RTM_EYE(F, R, N)                                                                                           \
     do {                                                                                                        \
-        if (fr) hipLaunchKernelGGL((eye_batch_kernel<F, R, FMT, N>), g, dim3(BLOCK), 0, s, fr);                  \
+        if (fr) hipLaunchKernelGGL((eye_batch_kernel<F, R, FMT, N>), dim3(g.x, (g.y + eye_batch_tiles<R, N> - 1) / eye_batch_tiles<R, N>, g.z), \
+                                   dim3(BLOCK), 0, s, fr, km.p, km.nw, km.gx);                                     \
         else hipLaunchKernelGGL((eye_pass_kernel<F, false, R, FMT, N>), g, dim3(BLOCK), 0, s, a, smap, o, nullptr, tabs); \
     } while (0)
 #define RTM_EYE_SDF(N)                                                                                              \

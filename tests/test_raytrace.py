@@ -316,6 +316,34 @@ def test_wave_cull_stress(rtm, oracle, scenes, seed):
            scenes.RAYTRACING_FLAGS)
 
 
+@pytest.mark.parametrize("seed", range(4))
+def test_capsule_cull_stress(rtm, oracle, scenes, seed):
+    """The cylinders' capsule cull (capsule_culls): long, thin capped cones in every
+    orientation -- along the view direction, across it, through the frustum's edges,
+    grazing wave rows, one passing next to the camera -- whose capsules the wave
+    cones just miss or just meet.  Bit-exact vs the oracle, which has no cull."""
+    rng = np.random.default_rng(0x2018 + 400 + seed)
+    S, C = scenes.Shading, scenes.PrimitiveCappedCylinder
+    cyls = []
+    for i in range(16):
+        z = float(rng.uniform(1.0, 14.0))
+        a = (float(rng.uniform(-1.2, 1.2) * z), float(rng.uniform(-1.2, 1.2) * z), z)
+        d = rng.normal(size=3)
+        d *= rng.uniform(1.0, 12.0) / np.linalg.norm(d)
+        if i % 4 == 0:  # along the view direction
+            d = np.array([0.0, 0.0, float(rng.uniform(2.0, 10.0))])
+        b = (a[0] + float(d[0]), a[1] + float(d[1]), a[2] + float(d[2]))
+        ra = float(rng.uniform(0.002, 0.15))
+        rb = float(rng.uniform(0.002, 0.15))
+        if i == 15:  # passes 0.2 from the camera origin
+            a, b, ra, rb = (-3.0, 0.2, 0.0), (3.0, 0.2, 0.5), 0.05, 0.12
+        cyls.append(C(i, S(*(float(v) for v in rng.uniform(0.05, 1.0, 3))), a, b, ra, rb))
+    scene = scenes.Scene([], [], [], cyls)
+    w, h = (640, 480) if seed % 2 == 0 else (1283, 97)
+    _check(rtm, oracle, scene, scenes.perspective_eye_camera(), scenes.shadow_camera(), w, h, 0,
+           scenes.RAYTRACING_FLAGS)
+
+
 def test_raytrace_error_codes(rtm, scenes, gpu_ctx):
     abi = rtm.abi
     # a perspective shadow camera: Camera::project asserts ORTHOGONAL (main.rs:1949)
