@@ -1216,8 +1216,11 @@ constexpr int CODED_TILE_ROWS = CODED_ROWS * TILE_Y;
 // workgroup: the sphere raster is most of its work and 16-row waves left it with too
 // few waves to hide its latency (2,800 per 8-frame launch at config 3: 37.9 instead of
 // 24 us, profiles/r04_v3_*); its march codes take the per-texel check.
+#ifndef RTM_AB_P2ROWS
+#define RTM_AB_P2ROWS 4
+#endif
 template <int PART>
-constexpr int coded_wave_rows = PART == 2 ? 4 : CODED_ROWS;
+constexpr int coded_wave_rows = PART == 2 ? RTM_AB_P2ROWS : CODED_ROWS;
 // PART 1 waves loop over P1_STRIPS consecutive 16-row strips (the prologue -- frame
 // header, the LDS table fill and its barrier, the row records -- paid once per wave).
 // 4 strips (a wave per 128 x 64 texels, a quarter of the waves): config 3 340 -> 348,

@@ -25,3 +25,7 @@ for grp in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_IN
   if [ $rc -eq 124 ] || [ $rc -eq 137 ] || [ $rc -gt 128 ]; then exit $rc; fi
 done
 python3 "$ROOT/tools/pmc_summary.py" "$OUT" --config "$CFG" --tag "$TAG" > "$OUT/summary.json" && cat "$OUT/summary.json"
+rc=$?
+# the raw passes stay on the box unless KEEP_RAW=1 (gpurun merges back at most 64 MiB)
+[ "${KEEP_RAW:-0}" = 1 ] || rm -rf "$OUT"/p[0-9]*
+exit $rc

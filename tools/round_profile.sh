@@ -21,6 +21,8 @@ step() {
   echo "$name rc=$rc" | tee -a "$OUT/status.txt"
   tail -3 "$OUT/$name.log"
   if fatal $rc; then echo "FATAL in $name, stopping"; exit $rc; fi
+  # (the per-dispatch traces stay on the box: gpurun merges back at most 64 MiB)
+  rm -f "$OUT/$name"/run_kernel_trace.csv
   return 0
 }
 [ "${SKIP_TESTS:-0}" = 1 ] || step pytest_gpu 900 python -m pytest tests -m gpu -q -p no:cacheprovider
