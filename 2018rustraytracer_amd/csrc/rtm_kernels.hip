@@ -834,72 +834,113 @@ __device__ __forceinline__ bool cone_culls(const RayCone& k, const CamK& c, cons
 // -- the angle to that plane.  The same inflation and margins as cone_culls; a long,
 // thin cylinder (main()'s scene: |ba| = 10, R = 0.3) is bounded 10x tighter than by
 // its sphere.  Non-finite data and a capsule holding the apex are kept.
-__device__ __forceinline__ bool capsule_culls(const RayCone& k, const CamK& c, const double pa[3], const double pb[3],
-                                              double R, bool cullable) {
-    const double Ri = R * 1.001 + 1e-7;
-    double p0[3], e[3], pe = 0.0, ee = 0.0;
-    for (int j = 0; j < 3; ++j) {
-        p0[j] = pa[j] - c.pos[j];
-        e[j] = pb[j] - pa[j];
-        pe += p0[j] * e[j];
-        ee += e[j] * e[j];
-    }
-    const double s = ee > 0.0 ? fmin(fmax(-pe / ee, 0.0), 1.0) : 0.0;
-    double q2 = 0.0, l0 = 0.0, l1 = 0.0, c0 = 0.0, c1 = 0.0, p1[3];
-    for (int j = 0; j < 3; ++j) {
-        p1[j] = p0[j] + e[j];
-        const double qj = p0[j] + e[j] * s;
-        q2 += qj * qj;
-        l0 += p0[j] * p0[j];
-        l1 += p1[j] * p1[j];
-        c0 += k.ax[j] * p0[j];
-        c1 += k.ax[j] * p1[j];
-    }
-    const double dmin = sqrt(q2);
-    if (!(dmin > Ri)) return false;  // (the apex inside the capsule; NaN)
-    const double sb = Ri / dmin;     // sin(beta)
-    const double cb = sqrt(fmax(1.0 - sb * sb, 0.0));
-    const double thr = k.ct * cb - k.st * sb - 1e-7;  // cos(theta + beta), less the margin
-    l0 = sqrt(l0);
-    l1 = sqrt(l1);
-    double u0[3], u1[3];
-    for (int j = 0; j < 3; ++j) {
-        u0[j] = p0[j] / l0;
-        u1[j] = p1[j] / l1;
-    }
-    double cg = fmax(c0 / l0, c1 / l1);  // cos of the angle to the nearer endpoint
-    double n[3] = {u0[1] * u1[2] - u0[2] * u1[1], u0[2] * u1[0] - u0[0] * u1[2], u0[0] * u1[1] - u0[1] * u1[0]};
-    const double nn = sqrt(n[0] * n[0] + n[1] * n[1] + n[2] * n[2]);
-    if (nn > 1e-12) {  // (else the arc is a point within 1e-12 rad: its endpoints decide)
-        double an = 0.0;
-        for (int j = 0; j < 3; ++j) {
-            n[j] /= nn;
-            an += k.ax[j] * n[j];
-        }
-        double ap[3];
-        for (int j = 0; j < 3; ++j) ap[j] = k.ax[j] - an * n[j];
-        // (u0 x ap).n and (ap x u1).n: the projection between the endpoints (a loose
-        // bound: counting a projection just outside the arc only raises cg)
-        const double w0 = (u0[1] * ap[2] - u0[2] * ap[1]) * n[0] + (u0[2] * ap[0] - u0[0] * ap[2]) * n[1] +
-                          (u0[0] * ap[1] - u0[1] * ap[0]) * n[2];
-        const double w1 = (ap[1] * u1[2] - ap[2] * u1[1]) * n[0] + (ap[2] * u1[0] - ap[0] * u1[2]) * n[1] +
-                          (ap[0] * u1[1] - ap[1] * u1[0]) * n[2];
-        if (!(w0 < -1e-6) && !(w1 < -1e-6)) cg = fmax(cg, sqrt(fmax(1.0 - an * an, 0.0)));
-    }
-    return cullable & (cg < thr);
-}
+//
+// Everything but the cone's axis and angle is the slot's own (the apex is the camera
+// position): CullK holds those terms, computed once per slot and frame (cull_prepare:
+// by 32 lanes into LDS in rt_cull_kernel), and cull_test is what remains per wave.
+struct CullK {
+    double w[3], L, sb, cb;      // bounding sphere: C - apex, |C - apex|, sin / cos of its angular radius
+    double u0[3], u1[3], nh[3];  // capsule: unit directions of its ends, the unit normal of their plane
+    double csb, ccb;             // sin / cos of the capsule's angular radius at dmin
+    int32_t sph, cap, has_n, pad;
+};
 
-// Slot l culled for the wave's cone: its bounding sphere, or (a cylinder) its capsule.
-__device__ __forceinline__ bool rt_culls(const RtK* __restrict__ rt, int l, const RayCone& k, const CamK& c) {
+__device__ __forceinline__ void cull_prepare(const RtK* __restrict__ rt, int l, const CamK& c, CullK& q) {
     double C[3], R;
     bool cullable;
     rt_bound(rt, l, C, R, cullable);
-    if (cone_culls(k, c, C, R, cullable)) return true;
-    if (l >= 16 && l - 16 < rt->n_cy) {
-        const CylK& q = rt->cy[l - 16];
-        return capsule_culls(k, c, q.pa, q.pb, fmax(fabs(q.ra), fabs(q.rb)), cullable);
+    const double Ri = R * 1.001 + 1e-7;
+    double L2 = 0.0;
+    for (int j = 0; j < 3; ++j) {
+        q.w[j] = C[j] - c.pos[j];
+        L2 += q.w[j] * q.w[j];
     }
-    return false;
+    q.L = sqrt(L2);
+    q.sb = Ri / q.L;  // sin(beta)
+    q.cb = sqrt(fmax(1.0 - q.sb * q.sb, 0.0));
+    q.sph = cullable & (q.L > Ri) & (q.sb < 1.0);
+    q.cap = 0;
+    q.has_n = 0;
+    q.csb = q.ccb = 0.0;
+    for (int j = 0; j < 3; ++j) q.u0[j] = q.u1[j] = q.nh[j] = 0.0;
+    if (l >= 16 && l - 16 < rt->n_cy) {
+        const CylK& cy = rt->cy[l - 16];
+        const double Rc = fmax(fabs(cy.ra), fabs(cy.rb)) * 1.001 + 1e-7;
+        double p0[3], p1[3], e[3], pe = 0.0, ee = 0.0;
+        for (int j = 0; j < 3; ++j) {
+            p0[j] = cy.pa[j] - c.pos[j];
+            e[j] = cy.pb[j] - cy.pa[j];
+            pe += p0[j] * e[j];
+            ee += e[j] * e[j];
+        }
+        const double t = ee > 0.0 ? fmin(fmax(-pe / ee, 0.0), 1.0) : 0.0;
+        double q2 = 0.0, l0 = 0.0, l1 = 0.0;
+        for (int j = 0; j < 3; ++j) {
+            p1[j] = p0[j] + e[j];
+            const double qj = p0[j] + e[j] * t;
+            q2 += qj * qj;
+            l0 += p0[j] * p0[j];
+            l1 += p1[j] * p1[j];
+        }
+        const double dmin = sqrt(q2);
+        l0 = sqrt(l0);
+        l1 = sqrt(l1);
+        // (the apex inside the capsule, and non-finite data, keep the slot)
+        if (dmin > Rc && __builtin_isfinite(dmin) && __builtin_isfinite(l0) && __builtin_isfinite(l1)) {
+            q.csb = Rc / dmin;
+            q.ccb = sqrt(fmax(1.0 - q.csb * q.csb, 0.0));
+            for (int j = 0; j < 3; ++j) {
+                q.u0[j] = p0[j] / l0;
+                q.u1[j] = p1[j] / l1;
+            }
+            double n[3] = {q.u0[1] * q.u1[2] - q.u0[2] * q.u1[1], q.u0[2] * q.u1[0] - q.u0[0] * q.u1[2],
+                           q.u0[0] * q.u1[1] - q.u0[1] * q.u1[0]};
+            const double nn = sqrt(n[0] * n[0] + n[1] * n[1] + n[2] * n[2]);
+            if (nn > 1e-12) {  // (else the arc is a point within 1e-12 rad: its endpoints decide)
+                for (int j = 0; j < 3; ++j) q.nh[j] = n[j] / nn;
+                q.has_n = 1;
+            }
+            q.cap = cullable;
+        }
+    }
+}
+
+// Slot culled for the wave's cone: its bounding sphere (cone_culls' test) or, a cylinder,
+// its capsule.  NaN anywhere compares false: kept.
+__device__ __forceinline__ bool cull_test(const RayCone& k, const CullK& q) {
+    if (q.sph) {
+        const double aw = k.ax[0] * q.w[0] + k.ax[1] * q.w[1] + k.ax[2] * q.w[2];
+        const double thr = k.ct * q.cb - k.st * q.sb - 1e-7;  // cos(theta + beta), less the margin
+        if (aw < thr * q.L) return true;
+    }
+    if (!q.cap) return false;
+    const double thr = k.ct * q.ccb - k.st * q.csb - 1e-7;
+    const double c0 = k.ax[0] * q.u0[0] + k.ax[1] * q.u0[1] + k.ax[2] * q.u0[2];
+    const double c1 = k.ax[0] * q.u1[0] + k.ax[1] * q.u1[1] + k.ax[2] * q.u1[2];
+    double cg = c0 > c1 ? c0 : c1;  // (cos of the angle to the nearer endpoint; a NaN axis: both NaN, kept)
+    if (q.has_n) {
+        const double an = k.ax[0] * q.nh[0] + k.ax[1] * q.nh[1] + k.ax[2] * q.nh[2];
+        double ap[3];
+        for (int j = 0; j < 3; ++j) ap[j] = k.ax[j] - an * q.nh[j];
+        // (u0 x ap).n and (ap x u1).n: the projection between the endpoints (a loose
+        // bound: counting a projection just outside the arc only raises cg)
+        const double w0 = (q.u0[1] * ap[2] - q.u0[2] * ap[1]) * q.nh[0] + (q.u0[2] * ap[0] - q.u0[0] * ap[2]) * q.nh[1] +
+                          (q.u0[0] * ap[1] - q.u0[1] * ap[0]) * q.nh[2];
+        const double w1 = (ap[1] * q.u1[2] - ap[2] * q.u1[1]) * q.nh[0] + (ap[2] * q.u1[0] - ap[0] * q.u1[2]) * q.nh[1] +
+                          (ap[0] * q.u1[1] - ap[1] * q.u1[0]) * q.nh[2];
+        if (!(w0 < -1e-6) && !(w1 < -1e-6)) {
+            const double cp = sqrt(fmax(1.0 - an * an, 0.0));
+            cg = cp > cg ? cp : cg;
+        }
+    }
+    return cg < thr;
+}
+
+// Slot l culled for the wave's cone (all terms per call: the lane-parallel cull below).
+__device__ __forceinline__ bool rt_culls(const RtK* __restrict__ rt, int l, const RayCone& k, const CamK& c) {
+    CullK q;
+    cull_prepare(rt, l, c, q);
+    return cull_test(k, q);
 }
 
 // Lane-parallel form inside a kernel (all lanes active): lane l tests slot l.
@@ -2328,14 +2369,19 @@ __global__ __launch_bounds__(BLOCK) void pull_kernel(const uint4* __restrict__ s
 // same operations, hence the same masks.
 __device__ __forceinline__ void rt_cull_wave(const CamK& c, const RtK* __restrict__ rt, int W, int H, int row_begin,
                                              int rows, int4 stripes, uint32_t* __restrict__ masks, int t) {
+    // the frame's slot terms, once per workgroup (lane l: slot l), then one wave per thread
+    __shared__ CullK cq[32];
+    const uint32_t slots = rt_slots(rt->n_pl, rt->n_cy);
+    if (threadIdx.x < 32 && ((slots >> threadIdx.x) & 1u)) cull_prepare(rt, (int)threadIdx.x, c, cq[threadIdx.x]);
+    __syncthreads();
     const int gx = (W + TILE_X - 1) / TILE_X;
     if (t >= gx * rows) return;
     const int xb = (t % gx) * TILE_X, yi = eye_row(row_begin, stripes.x, stripes.y, stripes.z, t / gx);
     const RayCone k = ray_cone(c, min(xb, W - 1), min(xb + TILE_X - 1, W - 1), min(yi, H - 1), W, H);
-    uint32_t m = rt_slots(rt->n_pl, rt->n_cy);
-    for (int l = 0; l < 32; ++l) {
-        if (!((m >> l) & 1u)) continue;
-        if (rt_culls(rt, l, k, c)) m &= ~(1u << l);
+    uint32_t m = slots;
+    for (uint32_t b = slots; b; b &= b - 1u) {
+        const int l = __builtin_ctz(b);
+        if (cull_test(k, cq[l])) m &= ~(1u << l);
     }
     masks[t] = m;
 }
