@@ -787,6 +787,36 @@ __device__ __forceinline__ RayCone ray_cone(const CamK& c, int xb, int xe, int y
     return k;
 }
 
+// The cone of an 8 x 8 pixel block's rays ([x0, x1] x [y0, y1]): the rays of a rectangle
+// of pixels lie in the convex hull of its four corner rays, so a cone (half-angle below
+// 90 degrees, a convex set) holding the four holds them all.  Axis: the normalised sum of
+// the corners' unit rays; half-angle: the largest angle to a corner.
+__device__ __forceinline__ RayCone ray_cone_block(const CamK& c, int x0, int x1, int y0, int y1, int W, int H) {
+    const double sx[2] = {ndc(x0, W), ndc(x1, W)}, uy[2] = {ndc(y0, H), ndc(y1, H)};
+    double n[4][3];
+    RayCone k;
+    double sum[3] = {0.0, 0.0, 0.0};
+    for (int q = 0; q < 4; ++q) {
+        double m = 0.0;
+        for (int j = 0; j < 3; ++j) {
+            n[q][j] = (c.dir[j] + c.side[j] * sx[q & 1]) + c.up[j] * uy[q >> 1];
+            m += n[q][j] * n[q][j];
+        }
+        m = 1.0 / sqrt(m);
+        for (int j = 0; j < 3; ++j) {
+            n[q][j] *= m;
+            sum[j] += n[q][j];
+        }
+    }
+    const double ma = 1.0 / sqrt(sum[0] * sum[0] + sum[1] * sum[1] + sum[2] * sum[2]);
+    for (int j = 0; j < 3; ++j) k.ax[j] = sum[j] * ma;
+    double ct = 1.0;
+    for (int q = 0; q < 4; ++q) ct = fmin(ct, k.ax[0] * n[q][0] + k.ax[1] * n[q][1] + k.ax[2] * n[q][2]);
+    k.ct = ct;
+    k.st = sqrt(1.0 - k.ct * k.ct);
+    return k;
+}
+
 // Bounding sphere of primitive slot l (l < 16: circle plane l; 16 + i: cylinder i);
 // cullable false for an empty slot and for near-cylinders.
 __device__ __forceinline__ void rt_bound(const RtK* __restrict__ rt, int l, double C[3], double& R, bool& cullable) {
@@ -1943,11 +1973,15 @@ __device__ __forceinline__ const T* const_table(const T* p) {
     return (const T*)(const __attribute__((address_space(4))) T*)p;
 }
 
-template <bool FUSED, bool COUNT, int RT, int FMT = RTM_FORMAT_RGBA32F, bool NOSH = false>
+// BLK: the waves are 8 x 8 pixel blocks (workgroup bx: 4 blocks side by side, block row
+// by: 8 rows), for the batched RT 3 frames without shadows and without stripes: a compact
+// primitive touches fewer blocks than 64 x 1 rows, and a block's cone is narrower.
+template <bool FUSED, bool COUNT, int RT, int FMT = RTM_FORMAT_RGBA32F, bool NOSH = false, bool BLK = false>
 __device__ __forceinline__ void eye_tile(const EyePart& a, const ShadowPart& sh, const double* __restrict__ smap,
                                          void* __restrict__ out, int bx, int by, StatsK* __restrict__ st,
                                          const DevTabs tabs, bool KMB = false, uint32_t kmw = 0u,
                                          bool km_in = false) {
+    static_assert(!BLK || (RT == 3 && FMT == RTM_FORMAT_RGBA32F && !COUNT), "8 x 8 blocks: RT 3, RGBA f32");
     // RT 3: RT 1 under a PERSPECTIVE eye, with the host's origin-only primitive
     // constants (RtK::persp) and the per-wave primitive masks of rt_cull_kernel
     constexpr bool RTP = RT == 3;
@@ -1958,9 +1992,12 @@ __device__ __forceinline__ void eye_tile(const EyePart& a, const ShadowPart& sh,
     const PerspK* __restrict__ psp = const_table(tabs.psp);
     const SdfTabK* __restrict__ sdf = const_table(tabs.sdf);
     // the workgroup's 4 waves stacked (64 x 4 pixels)
-    const int xb = __builtin_amdgcn_readfirstlane(bx * TILE_X);
-    const int xi = xb + (threadIdx.x & (TILE_X - 1));
-    const int yl = __builtin_amdgcn_readfirstlane(by * TILE_Y + (int)(threadIdx.x >> 6));
+    const int wv_ = (int)(threadIdx.x >> 6), ln_ = (int)(threadIdx.x & (TILE_X - 1));
+    const int xb = __builtin_amdgcn_readfirstlane(BLK ? bx * 32 + wv_ * 8 : bx * TILE_X);
+    const int xi = xb + (BLK ? (ln_ & 7) : ln_);
+    // (BLK: the lane's own row; else the wave's)
+    const int yl = BLK ? by * 8 + (ln_ >> 3) : __builtin_amdgcn_readfirstlane(by * TILE_Y + wv_);
+    const int yl0 = BLK ? __builtin_amdgcn_readfirstlane(by * 8) : yl;  // the wave's first row
     if (!COUNT) RTM_PHASE(3, 0);
     // the header fields the prologue needs, read before any branch so their scalar loads
     // issue as one group: one wait instead of a chain of dependent round trips (the
@@ -1990,11 +2027,14 @@ __device__ __forceinline__ void eye_tile(const EyePart& a, const ShadowPart& sh,
             "+s"(rtg), "+s"(outg));
     const RtK* __restrict__ rt = (const RtK*)rtg;
     out = (void*)outg;
-    const int yi = __builtin_amdgcn_readfirstlane(eye_row(rb_, S_, ss_, sp_, yl));
+    const int yi = BLK ? rb_ + yl : __builtin_amdgcn_readfirstlane(eye_row(rb_, S_, ss_, sp_, yl));
     const int yo = og_ ? yi : yl;  // the output row
     const bool live = (xi < W_) & (rb_ + yl < re_) & (yi < H_);
+    // the wave's image rows [ya, ye] and columns [xb, xe]
+    const int ya = BLK ? rb_ + yl0 : yi, ye = BLK ? ya + 7 : yi;
+    const int xe = xb + (BLK ? 7 : TILE_X - 1);
     // (union_may_cover on the loaded fields; an empty union (x0 > x1) meets nothing)
-    const bool um_ = (cx0_ <= cx1_) & (yi >= cy0_) & (yi <= cy1_) & (xb + TILE_X - 1 >= cx0_) & (xb <= cx1_);
+    const bool um_ = (cx0_ <= cx1_) & (ye >= cy0_) & (ya <= cy1_) & (xe >= cx0_) & (xb <= cx1_);
     // An out-of-range side-table read is counted once the tile's last load is done: the
     // counter's atomic is a global write, and one ahead of a load makes the compiler treat
     // the load as clobbered -- the primitive tables would go through vector instead of
@@ -2005,7 +2045,7 @@ __device__ __forceinline__ void eye_tile(const EyePart& a, const ShadowPart& sh,
     int hit_kind = 0, hit_id = -1;
     uint32_t n_evals = 0;
     // the wave's spheres (all lanes active here); ascending bit order = scene order
-    uint32_t smask = um_ ? wave_sphere_mask(a.sph, ns_, xb, xb + TILE_X - 1, yi, yi) : 0u;
+    uint32_t smask = um_ ? wave_sphere_mask(a.sph, ns_, xb, xe, ya, ye) : 0u;
     // the wave's ray-traced primitives (PERSPECTIVE eye; all lanes active here)
     uint32_t rmask = 0u;
 #if defined(RTM_TEST_REVERT_MASK_GUARD)  // (tools/bounds_demo.sh only: the round-3 over-read, to show tests/test_bounds.py catches it)
@@ -2315,9 +2355,22 @@ constexpr int eye_batch_tiles = RT == 3 && NOSH ? RTM_AB_EYE_TILES_RT3 : 1;
 #endif
 template <bool FUSED, int RT, bool NOSH>
 constexpr int eye_batch_wpe = RT == 3 && NOSH ? 8 : RT == 0 && !FUSED ? RTM_AB_EYE_WPE_RT0 : 1;
-template <bool FUSED, int RT, int FMT, bool NOSH = false>
+template <bool FUSED, int RT, int FMT, bool NOSH = false, bool BLK = false>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(eye_batch_wpe<FUSED, RT, NOSH>, 8))) void eye_batch_kernel(
     CBatch* __restrict__ fr, const uint32_t* __restrict__ km, int km_nw, int km_gx) {
+    if (BLK) {
+        // 8 x 8 blocks (eye_tile<BLK>): workgroup (bx, by) holds blocks 4 bx .. 4 bx + 3 of
+        // block row by; km_gx = blocks per row; every block of the frame has its word
+        const int col = (int)blockIdx.x * 4 + (int)(threadIdx.x >> 6);
+        if (col >= km_gx) return;  // (wave-uniform: a block past the frame's right edge; no barrier follows)
+        CBatch* f = fr + blockIdx.z;
+        const DevTabs tabs = *(const DevTabs*)&f->tabs;
+        const int widx = __builtin_amdgcn_readfirstlane((int)blockIdx.y * km_gx + col);
+        const uint32_t kmw = ((const __attribute__((address_space(4))) uint32_t*)km)[(size_t)blockIdx.z * km_nw + widx];
+        eye_tile<FUSED, false, RT, FMT, NOSH, BLK>(*(const EyePart*)&f->a.ey, *(const ShadowPart*)&f->a.sh, f->smap,
+                                                   f->out, blockIdx.x, blockIdx.y, nullptr, tabs, true, kmw, true);
+        return;
+    }
     constexpr int NT = eye_batch_tiles<RT, NOSH>;
 #pragma unroll 1
     for (int t = 0; t < NT; ++t) {
@@ -2367,6 +2420,8 @@ __global__ __launch_bounds__(BLOCK) void pull_kernel(const uint4* __restrict__ s
 // pixels bx*64 .. bx*64+63 of row row_begin + yl), so the cone set-up and the
 // bounding-sphere tests run once per wave instead of on every lane of it.  The
 // same operations, hence the same masks.
+// BLK: one thread per 8 x 8 pixel block of the eye pass (eye_batch_kernel<BLK>; no stripes)
+template <bool BLK = false>
 __device__ __forceinline__ void rt_cull_wave(const CamK& c, const RtK* __restrict__ rt, int W, int H, int row_begin,
                                              int rows, int4 stripes, uint32_t* __restrict__ masks, int t) {
     // the frame's slot terms, once per workgroup (lane l: slot l), then one wave per thread
@@ -2374,10 +2429,19 @@ __device__ __forceinline__ void rt_cull_wave(const CamK& c, const RtK* __restric
     const uint32_t slots = rt_slots(rt->n_pl, rt->n_cy);
     if (threadIdx.x < 32 && ((slots >> threadIdx.x) & 1u)) cull_prepare(rt, (int)threadIdx.x, c, cq[threadIdx.x]);
     __syncthreads();
-    const int gx = (W + TILE_X - 1) / TILE_X;
-    if (t >= gx * rows) return;
-    const int xb = (t % gx) * TILE_X, yi = eye_row(row_begin, stripes.x, stripes.y, stripes.z, t / gx);
-    const RayCone k = ray_cone(c, min(xb, W - 1), min(xb + TILE_X - 1, W - 1), min(yi, H - 1), W, H);
+    RayCone k;
+    if (BLK) {
+        const int gx8 = (W + 7) / 8, gy8 = (rows + 7) / 8;
+        if (t >= gx8 * gy8) return;
+        const int x0 = (t % gx8) * 8, y0 = row_begin + (t / gx8) * 8;
+        const int y1 = min(min(y0 + 7, row_begin + rows - 1), H - 1);
+        k = ray_cone_block(c, min(x0, W - 1), min(x0 + 7, W - 1), min(y0, H - 1), y1, W, H);
+    } else {
+        const int gx = (W + TILE_X - 1) / TILE_X;
+        if (t >= gx * rows) return;
+        const int xb = (t % gx) * TILE_X, yi = eye_row(row_begin, stripes.x, stripes.y, stripes.z, t / gx);
+        k = ray_cone(c, min(xb, W - 1), min(xb + TILE_X - 1, W - 1), min(yi, H - 1), W, H);
+    }
     uint32_t m = slots;
     for (uint32_t b = slots; b; b &= b - 1u) {
         const int l = __builtin_ctz(b);
@@ -2395,13 +2459,14 @@ __global__ __launch_bounds__(BLOCK) void rt_cull_kernel(const CamK c, const RtK*
 // rt_cull_kernel for a batch: frame blockIdx.z's masks (frames with ray-traced
 // primitives under a PERSPECTIVE eye get a mask buffer from the host; the others
 // have none and skip).
+template <bool BLK = false>
 __global__ __launch_bounds__(BLOCK) void rt_cull_batch_kernel(CBatch* __restrict__ fr) {
     CBatch* f = fr + blockIdx.z;
     uint32_t* masks = f->tabs.rtmask;
     const RtK* rt = f->tabs.rt;
     if (!masks || !rt) return;
     const EyePart& e = *(const EyePart*)&f->a.ey;
-    rt_cull_wave(e.eye, rt, e.W, e.H, e.row_begin, e.row_end - e.row_begin,
+    rt_cull_wave<BLK>(e.eye, rt, e.W, e.H, e.row_begin, e.row_end - e.row_begin,
                  make_int4(e.stripe_rows, e.stripe_stride, e.stripe_phase, 0), masks, blockIdx.x * BLOCK + threadIdx.x);
 }
 
@@ -2713,15 +2778,22 @@ int launch_shadow_pass(const FrameArgs& a, double* smap, void* stream, StatsK* s
 //     (eye_pass8_kernel); batched, the compiler's allocation (the headline kernel).
 template <int FMT>
 static void launch_eye_fmt(const FrameArgs& a, const double* smap, void* o, hipStream_t s, dim3 g, bool fused,
-                           const DevTabs& tabs, CBatch* fr) {
+                           const DevTabs& tabs, CBatch* fr, bool blk = false) {
     struct {
         const uint32_t* p;
         int nw, gx;
     } km{nullptr, 1, 1};
     if (fr && tabs.rtmask) km = {tabs.rtmask, tabs.rtmask_words, (int)g.x};
+    // 8 x 8 blocks (eye_block_mode): 4 blocks per workgroup across, 8 rows
+    const int rows_ = a.ey.row_end - a.ey.row_begin;
+    const int gx8 = (a.ey.W + 7) / 8;
+    const dim3 gblk((unsigned)((gx8 + 3) / 4), (unsigned)((rows_ + 7) / 8), g.z);
 #define RTM_EYE(F, R, N)                                                                                           \
     do {                                                                                                        \
-        if (fr) hipLaunchKernelGGL((eye_batch_kernel<F, R, FMT, N>), dim3(g.x, (g.y + eye_batch_tiles<R, N> - 1) / eye_batch_tiles<R, N>, g.z), \
+        constexpr bool B_ = R == 3 && N && FMT == RTM_FORMAT_RGBA32F;                                           \
+        if (fr && B_ && blk)                                                                                    \
+            hipLaunchKernelGGL((eye_batch_kernel<F, R, FMT, N, B_>), gblk, dim3(BLOCK), 0, s, fr, km.p, km.nw, gx8); \
+        else if (fr) hipLaunchKernelGGL((eye_batch_kernel<F, R, FMT, N>), dim3(g.x, (g.y + eye_batch_tiles<R, N> - 1) / eye_batch_tiles<R, N>, g.z), \
                                    dim3(BLOCK), 0, s, fr, km.p, km.nw, km.gx);                                     \
         else hipLaunchKernelGGL((eye_pass_kernel<F, false, R, FMT, N>), g, dim3(BLOCK), 0, s, a, smap, o, nullptr, tabs); \
     } while (0)
@@ -2843,23 +2915,47 @@ int launch_smap_decode(const ShadowPart& sh, const void* codes, double* out, voi
     return launched();
 }
 
+// The batch's eye pass in 8 x 8 pixel blocks (eye_tile<BLK>) for frames below 1 Mpixel:
+// RT 3 frames without shadows (the NOSH kernel), RGBA f32, no stripes, and every block's
+// mask word inside the frame's mask slot (ceil(W/8) * ceil(rows/8) <= ceil(W/64) * rows
+// words).  main()'s scene at 512 x 512 (config 7): its cylinder meets 2.4 % of the blocks
+// against 13.6 % of the 64 x 1 rows, and the eye kernel runs a 64-frame launch in 66 instead
+// of 113 us one lane: 234 -> 293 Gpix/s.  At 3840 x 2160 (config 6: 13 primitives, the
+// 64 x 1 rows at 4 tiles per workgroup) blocks were 3 % slower, so larger frames keep rows
+// (profiles/r05_ab_eye_blocks.txt).
+static bool eye_block_mode(const FrameArgs& a0, const DevTabs& t0, bool fused) {
+    const int both = RTM_FLAG_NO_MARCH | RTM_FLAG_NO_SHADOW_RASTER;
+    const bool nosh = fused && (a0.sh.flags & both) == both;
+    const int rows = a0.ey.row_end - a0.ey.row_begin;
+    const int64_t nw8 = (int64_t)((a0.ey.W + 7) / 8) * ((rows + 7) / 8);
+    return nosh && t0.rt && t0.rt_persp && !t0.sdf && t0.rtmask && (t0.fmt & FMT_MASK) == RTM_FORMAT_RGBA32F &&
+           a0.ey.stripe_rows == 0 && nw8 <= (int64_t)t0.rtmask_words && (int64_t)a0.ey.W * rows < (1 << 20);
+}
+
 int launch_eye_batch(const BatchFrame* dev, int n, const FrameArgs& a0, const DevTabs& t0, void* stream) {
     hipStream_t s = (hipStream_t)stream;
     CBatch* fr = (CBatch*)dev;
     const int rows = a0.ey.row_end - a0.ey.row_begin;
+    const bool fused = (a0.ey.flags & RTM_FLAG_FUSED_SHADOW) != 0;
+    const bool blk = eye_block_mode(a0, t0, fused);
     if (t0.rtmask) {  // the batch's per-wave primitive masks first (RT 3)
-        const int nw = ((a0.ey.W + TILE_X - 1) / TILE_X) * rows;
-        hipLaunchKernelGGL(rt_cull_batch_kernel, dim3((unsigned)((nw + BLOCK - 1) / BLOCK), 1, (unsigned)n),
-                           dim3(BLOCK), 0, s, fr);
+        if (blk) {
+            const int nw8 = ((a0.ey.W + 7) / 8) * ((rows + 7) / 8);
+            hipLaunchKernelGGL(rt_cull_batch_kernel<true>, dim3((unsigned)((nw8 + BLOCK - 1) / BLOCK), 1, (unsigned)n),
+                               dim3(BLOCK), 0, s, fr);
+        } else {
+            const int nw = ((a0.ey.W + TILE_X - 1) / TILE_X) * rows;
+            hipLaunchKernelGGL(rt_cull_batch_kernel<false>, dim3((unsigned)((nw + BLOCK - 1) / BLOCK), 1, (unsigned)n),
+                               dim3(BLOCK), 0, s, fr);
+        }
         if (launched()) return RTM_ERR_HIP;
     }
     dim3 g = grid_for(a0.ey.W, rows);
     g.z = (unsigned)n;
-    const bool fused = (a0.ey.flags & RTM_FLAG_FUSED_SHADOW) != 0;
     const int fmt = t0.fmt & FMT_MASK;
     if (fmt == RTM_FORMAT_RGBA8) launch_eye_fmt<RTM_FORMAT_RGBA8>(a0, nullptr, nullptr, s, g, fused, t0, fr);
     else if (fmt == RTM_FORMAT_RGB8) launch_eye_fmt<RTM_FORMAT_RGB8>(a0, nullptr, nullptr, s, g, fused, t0, fr);
-    else launch_eye_fmt<RTM_FORMAT_RGBA32F>(a0, nullptr, nullptr, s, g, fused, t0, fr);
+    else launch_eye_fmt<RTM_FORMAT_RGBA32F>(a0, nullptr, nullptr, s, g, fused, t0, fr, blk);
     return launched();
 }
 
