@@ -2353,6 +2353,12 @@ constexpr int eye_batch_tiles = RT == 3 && NOSH ? RTM_AB_EYE_TILES_RT3 : 1;
 #ifndef RTM_AB_EYE_WPE_RT0
 #define RTM_AB_EYE_WPE_RT0 8
 #endif
+// block rows per workgroup in the 8 x 8 mode, one after another: config 7 294 -> 317
+// Gpix/s against one (2: no gain; profiles/r05_ab_eye_blocks.txt)
+#ifndef RTM_AB_BLK_NT
+#define RTM_AB_BLK_NT 4
+#endif
+constexpr int EYE_BLK_NT = RTM_AB_BLK_NT;
 template <bool FUSED, int RT, bool NOSH>
 constexpr int eye_batch_wpe = RT == 3 && NOSH ? 8 : RT == 0 && !FUSED ? RTM_AB_EYE_WPE_RT0 : 1;
 template <bool FUSED, int RT, int FMT, bool NOSH = false, bool BLK = false>
@@ -2360,15 +2366,23 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(eye_batch
     CBatch* __restrict__ fr, const uint32_t* __restrict__ km, int km_nw, int km_gx) {
     if (BLK) {
         // 8 x 8 blocks (eye_tile<BLK>): workgroup (bx, by) holds blocks 4 bx .. 4 bx + 3 of
-        // block row by; km_gx = blocks per row; every block of the frame has its word
+        // block rows by * EYE_BLK_NT + t; km_gx = blocks per row; every block of the frame
+        // has its word
         const int col = (int)blockIdx.x * 4 + (int)(threadIdx.x >> 6);
         if (col >= km_gx) return;  // (wave-uniform: a block past the frame's right edge; no barrier follows)
-        CBatch* f = fr + blockIdx.z;
-        const DevTabs tabs = *(const DevTabs*)&f->tabs;
-        const int widx = __builtin_amdgcn_readfirstlane((int)blockIdx.y * km_gx + col);
-        const uint32_t kmw = ((const __attribute__((address_space(4))) uint32_t*)km)[(size_t)blockIdx.z * km_nw + widx];
-        eye_tile<FUSED, false, RT, FMT, NOSH, BLK>(*(const EyePart*)&f->a.ey, *(const ShadowPart*)&f->a.sh, f->smap,
-                                                   f->out, blockIdx.x, blockIdx.y, nullptr, tabs, true, kmw, true);
+        const int gy8 = (((const EyePart*)&fr[blockIdx.z].a.ey)->row_end - ((const EyePart*)&fr[blockIdx.z].a.ey)->row_begin + 7) / 8;
+#pragma unroll 1
+        for (int t = 0; t < EYE_BLK_NT; ++t) {
+            const int by = (int)blockIdx.y * EYE_BLK_NT + t;
+            if (by >= gy8) break;  // (wave-uniform)
+            CBatch* f = fr + blockIdx.z;
+            if (EYE_BLK_NT > 1) asm volatile("" : "+s"(f));
+            const DevTabs tabs = *(const DevTabs*)&f->tabs;
+            const int widx = __builtin_amdgcn_readfirstlane(by * km_gx + col);
+            const uint32_t kmw = ((const __attribute__((address_space(4))) uint32_t*)km)[(size_t)blockIdx.z * km_nw + widx];
+            eye_tile<FUSED, false, RT, FMT, NOSH, BLK>(*(const EyePart*)&f->a.ey, *(const ShadowPart*)&f->a.sh, f->smap,
+                                                       f->out, blockIdx.x, by, nullptr, tabs, true, kmw, true);
+        }
         return;
     }
     constexpr int NT = eye_batch_tiles<RT, NOSH>;
@@ -2787,7 +2801,7 @@ static void launch_eye_fmt(const FrameArgs& a, const double* smap, void* o, hipS
     // 8 x 8 blocks (eye_block_mode): 4 blocks per workgroup across, 8 rows
     const int rows_ = a.ey.row_end - a.ey.row_begin;
     const int gx8 = (a.ey.W + 7) / 8;
-    const dim3 gblk((unsigned)((gx8 + 3) / 4), (unsigned)((rows_ + 7) / 8), g.z);
+    const dim3 gblk((unsigned)((gx8 + 3) / 4), (unsigned)(((rows_ + 7) / 8 + EYE_BLK_NT - 1) / EYE_BLK_NT), g.z);
 #define RTM_EYE(F, R, N)                                                                                           \
     do {                                                                                                        \
         constexpr bool B_ = R == 3 && N && FMT == RTM_FORMAT_RGBA32F;                                           \
@@ -2920,16 +2934,21 @@ int launch_smap_decode(const ShadowPart& sh, const void* codes, double* out, voi
 // mask word inside the frame's mask slot (ceil(W/8) * ceil(rows/8) <= ceil(W/64) * rows
 // words).  main()'s scene at 512 x 512 (config 7): its cylinder meets 2.4 % of the blocks
 // against 13.6 % of the 64 x 1 rows, and the eye kernel runs a 64-frame launch in 66 instead
-// of 113 us one lane: 234 -> 293 Gpix/s.  At 3840 x 2160 (config 6: 13 primitives, the
-// 64 x 1 rows at 4 tiles per workgroup) blocks were 3 % slower, so larger frames keep rows
-// (profiles/r05_ab_eye_blocks.txt).
+// of 113 us one lane: 234 -> 293 Gpix/s, 317 with 4 block rows per workgroup.  At 3840 x
+// 2160 (config 6: 13 primitives) blocks at 4 rows per workgroup match the 64 x 1 rows (one
+// block row: 3 % slower); larger frames keep rows (profiles/r05_ab_eye_blocks.txt).
 static bool eye_block_mode(const FrameArgs& a0, const DevTabs& t0, bool fused) {
     const int both = RTM_FLAG_NO_MARCH | RTM_FLAG_NO_SHADOW_RASTER;
     const bool nosh = fused && (a0.sh.flags & both) == both;
     const int rows = a0.ey.row_end - a0.ey.row_begin;
     const int64_t nw8 = (int64_t)((a0.ey.W + 7) / 8) * ((rows + 7) / 8);
     return nosh && t0.rt && t0.rt_persp && !t0.sdf && t0.rtmask && (t0.fmt & FMT_MASK) == RTM_FORMAT_RGBA32F &&
-           a0.ey.stripe_rows == 0 && nw8 <= (int64_t)t0.rtmask_words && (int64_t)a0.ey.W * rows < (1 << 20);
+           a0.ey.stripe_rows == 0 && nw8 <= (int64_t)t0.rtmask_words &&
+#ifdef RTM_AB_BLK_ALL
+           true;
+#else
+           (int64_t)a0.ey.W * rows < (1 << 20);
+#endif
 }
 
 int launch_eye_batch(const BatchFrame* dev, int n, const FrameArgs& a0, const DevTabs& t0, void* stream) {
