@@ -975,8 +975,9 @@ __device__ __forceinline__ bool rt_culls(const RtK* __restrict__ rt, int l, cons
 
 // Lane-parallel form inside a kernel (all lanes active): lane l tests slot l.
 __device__ __forceinline__ uint32_t rt_wave_mask(const RtK* __restrict__ rt, const CamK& c, int xb, int xe, int yi,
-                                                 int W, int H) {
-    const RayCone k = ray_cone(c, xb, xe, yi, W, H);
+                                                 int W, int H, int ye = -1) {
+    // (ye >= 0: the wave is the block of rows [yi, ye])
+    const RayCone k = ye >= 0 ? ray_cone_block(c, xb, xe, yi, ye, W, H) : ray_cone(c, xb, xe, yi, W, H);
     const int l = threadIdx.x & 63;
     const bool culled = rt_culls(rt, l, k, c);
 #if defined(RTM_TEST_REVERT_SLOT_MASKS)  // (tools/bounds_demo.sh only: the pre-dfafeba mask, every slot set)
@@ -1981,7 +1982,7 @@ __device__ __forceinline__ void eye_tile(const EyePart& a, const ShadowPart& sh,
                                          void* __restrict__ out, int bx, int by, StatsK* __restrict__ st,
                                          const DevTabs tabs, bool KMB = false, uint32_t kmw = 0u,
                                          bool km_in = false) {
-    static_assert(!BLK || (RT == 3 && FMT == RTM_FORMAT_RGBA32F && !COUNT), "8 x 8 blocks: RT 3, RGBA f32");
+    static_assert(!BLK || ((RT == 3 || RT == 2) && FMT == RTM_FORMAT_RGBA32F && !COUNT), "8 x 8 blocks: RT 3 / 2, RGBA f32");
     // RT 3: RT 1 under a PERSPECTIVE eye, with the host's origin-only primitive
     // constants (RtK::persp) and the per-wave primitive masks of rt_cull_kernel
     constexpr bool RTP = RT == 3;
@@ -2069,7 +2070,9 @@ __device__ __forceinline__ void eye_tile(const EyePart& a, const ShadowPart& sh,
             rmask = rt_slots(rt->n_pl, rt->n_cy);  // (every primitive: the result stays exact)
         }
     } else if (RTB == 1 && rt && a.eye.type == RTM_CAMERA_PERSPECTIVE) {
-        rmask = rt_wave_mask(rt, a.eye, min(xb, a.W - 1), min(xb + TILE_X - 1, a.W - 1), min(yi, a.H - 1), a.W, a.H);
+        rmask = BLK ? rt_wave_mask(rt, a.eye, min(xb, a.W - 1), min(xe, a.W - 1), min(ya, a.H - 1), a.W, a.H,
+                                   min(ye, a.H - 1))
+                    : rt_wave_mask(rt, a.eye, min(xb, a.W - 1), min(xb + TILE_X - 1, a.W - 1), min(yi, a.H - 1), a.W, a.H);
     } else if (RTB && rt) {
         rmask = rt_slots(rt->n_pl, rt->n_cy);
     }
@@ -2403,9 +2406,18 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(eye_batch
     }
 }
 
-template <int WPE, int FMT, bool NOSH = false>
+template <int WPE, int FMT, bool NOSH = false, bool BLK = false>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8))) void eye_sdf_batch_kernel(
-    CBatch* __restrict__ fr) {
+    CBatch* __restrict__ fr, int gx8) {
+    if (BLK) {  // 8 x 8 blocks, 4 across per workgroup, one block row (a row loop spills 360 B)
+        const int col = (int)blockIdx.x * 4 + (int)(threadIdx.x >> 6);
+        if (col >= gx8) return;  // (wave-uniform; no barrier follows)
+        CBatch* f = fr + blockIdx.z;
+        const DevTabs tabs = *(const DevTabs*)&f->tabs;
+        eye_tile<false, false, 2, FMT, NOSH, BLK>(*(const EyePart*)&f->a.ey, *(const ShadowPart*)&f->a.sh, f->smap,
+                                                   f->out, blockIdx.x, blockIdx.y, nullptr, tabs);
+        return;
+    }
     CBatch* f = fr + blockIdx.z;
     const DevTabs tabs = *(const DevTabs*)&f->tabs;
     eye_tile<false, false, 2, FMT, NOSH>(*(const EyePart*)&f->a.ey, *(const ShadowPart*)&f->a.sh, f->smap, f->out,
@@ -2811,9 +2823,16 @@ static void launch_eye_fmt(const FrameArgs& a, const double* smap, void* o, hipS
                                    dim3(BLOCK), 0, s, fr, km.p, km.nw, km.gx);                                     \
         else hipLaunchKernelGGL((eye_pass_kernel<F, false, R, FMT, N>), g, dim3(BLOCK), 0, s, a, smap, o, nullptr, tabs); \
     } while (0)
+    // the SDF frames' batched eye pass in 8 x 8 pixel blocks as well (RGBA f32, no stripes):
+    // neighbouring rays in two dimensions march alike, config 8 21.5 -> 22.6 Gpix/s
+    // (profiles/r05_ab_eye_blocks.txt); one block row per workgroup (a row loop spills 360 B)
+    const bool sblk = fr && FMT == RTM_FORMAT_RGBA32F && a.ey.stripe_rows == 0;
 #define RTM_EYE_SDF(N)                                                                                              \
     do {                                                                                                        \
-        if (fr) hipLaunchKernelGGL((eye_sdf_batch_kernel<5, FMT, N>), g, dim3(BLOCK), 0, s, fr);                 \
+        constexpr bool SB_ = FMT == RTM_FORMAT_RGBA32F;                                                         \
+        if (fr && SB_ && sblk) hipLaunchKernelGGL((eye_sdf_batch_kernel<5, FMT, N, SB_>), dim3(gblk.x, (rows_ + 7) / 8, g.z), \
+                                                  dim3(BLOCK), 0, s, fr, gx8);                                   \
+        else if (fr) hipLaunchKernelGGL((eye_sdf_batch_kernel<5, FMT, N>), g, dim3(BLOCK), 0, s, fr, gx8);       \
         else hipLaunchKernelGGL((eye_sdf_kernel<5, FMT, N>), g, dim3(BLOCK), 0, s, a, smap, o, tabs);            \
     } while (0)
     const int both = RTM_FLAG_NO_MARCH | RTM_FLAG_NO_SHADOW_RASTER;
