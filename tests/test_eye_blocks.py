@@ -1,0 +1,87 @@
+"""The batched eye pass in 8 x 8 pixel blocks (rtm_kernels.hip `eye_block_mode`,
+`eye_tile<BLK>`, `ray_cone_block`): small ray-traced frames without shadows and SDF
+frames, at sizes that leave partial blocks and partial workgroups (W not a multiple of
+32, rows not a multiple of 8 where the block count still fits the mask slot), frames
+without primitives and with perspective spheres in the same batch, 4 block rows per
+workgroup past the frame's last block row.  Every frame against the oracle, bit for
+bit, with no out-of-range table read."""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import bits_equal, first_mismatch
+from test_bounds import oob
+
+pytestmark = pytest.mark.gpu
+
+NT = min(16, os.cpu_count() or 1)
+
+
+def _thin_cylinders(scenes, seed):
+    rng = np.random.default_rng(0x2018 + 500 + seed)
+    S, C, P = scenes.Shading, scenes.PrimitiveCappedCylinder, scenes.PrimitiveCirclePlane
+    cyls, planes = [], []
+    for i in range(6):
+        z = float(rng.uniform(2.0, 12.0))
+        a = (float(rng.uniform(-1.0, 1.0) * z), float(rng.uniform(-1.0, 1.0) * z), z)
+        d = rng.normal(size=3)
+        d *= rng.uniform(1.0, 8.0) / np.linalg.norm(d)
+        b = (a[0] + float(d[0]), a[1] + float(d[1]), a[2] + float(d[2]))
+        cyls.append(C(i, S(*(float(v) for v in rng.uniform(0.05, 1.0, 3))), a, b,
+                      float(rng.uniform(0.01, 0.2)), float(rng.uniform(0.01, 0.2))))
+    for i in range(2):
+        z = float(rng.uniform(3.0, 10.0))
+        n = rng.normal(size=3)
+        n /= np.linalg.norm(n)
+        planes.append(P(i, S(0.3, 0.6, 0.9), float(rng.uniform(0.2, 1.0)),
+                        (float(rng.uniform(-0.8, 0.8) * z), float(rng.uniform(-0.8, 0.8) * z), z),
+                        tuple(float(v) for v in n)))
+    return scenes.Scene([], [], planes, cyls)
+
+
+@pytest.mark.parametrize("w,h", [(200, 136), (517, 96), (640, 360), (72, 8)])
+def test_block_mode_ray_traced_batches(rtm, oracle, scenes, gpu_ctx, w, h):
+    import torch
+    eye, sh = scenes.perspective_eye_camera(), scenes.shadow_camera()
+    frames = [_thin_cylinders(scenes, 0), scenes.raytracing_plane0(), scenes.perspective_simple1(),
+              _thin_cylinders(scenes, 1), scenes.raytracing_plane0(True), _thin_cylinders(scenes, 2)]
+    outs = [torch.empty((h, w, 4), dtype=torch.float32, device="cuda") for _ in frames]
+    assert oob(rtm, gpu_ctx) >= 0  # clear
+    try:
+        gpu_ctx.set_batch(len(frames))
+        gpu_ctx.set_lanes(1)
+        torch.cuda.synchronize()
+        gpu_ctx.render_frames_async(frames, eye, sh, w, h, 0, scenes.RAYTRACING_FLAGS, [o.data_ptr() for o in outs])
+        gpu_ctx.synchronize()
+    finally:
+        gpu_ctx.set_lanes(0)
+        gpu_ctx.set_batch(0)
+    assert oob(rtm, gpu_ctx) == 0
+    for i, (s, o) in enumerate(zip(frames, outs)):
+        want = oracle.render(s, eye, sh, w, h, 0, scenes.RAYTRACING_FLAGS, nthreads=NT)["rgba"]
+        got = o.cpu().numpy()
+        assert bits_equal(got, want), f"frame {i}: {first_mismatch(got, want)}"
+
+
+@pytest.mark.parametrize("w,h", [(200, 136), (96, 72)])
+def test_block_mode_sdf_batches(rtm, oracle, scenes, gpu_ctx, w, h):
+    import torch
+    eye, sh = scenes.sdf_eye_camera(), scenes.shadow_camera()
+    frames = [scenes.sdf_preview_scene(), scenes.sdf_bench_scene(), scenes.sdf_preview_scene()]
+    outs = [torch.empty((h, w, 4), dtype=torch.float32, device="cuda") for _ in frames]
+    assert oob(rtm, gpu_ctx) >= 0
+    try:
+        gpu_ctx.set_batch(len(frames))
+        gpu_ctx.set_lanes(1)
+        torch.cuda.synchronize()
+        gpu_ctx.render_frames_async(frames, eye, sh, w, h, 0, scenes.RAYTRACING_FLAGS, [o.data_ptr() for o in outs])
+        gpu_ctx.synchronize()
+    finally:
+        gpu_ctx.set_lanes(0)
+        gpu_ctx.set_batch(0)
+    assert oob(rtm, gpu_ctx) == 0
+    for i, (s, o) in enumerate(zip(frames, outs)):
+        want = oracle.render(s, eye, sh, w, h, 0, scenes.RAYTRACING_FLAGS, nthreads=NT)["rgba"]
+        got = o.cpu().numpy()
+        assert bits_equal(got, want), f"frame {i}: {first_mismatch(got, want)}"
