@@ -12,9 +12,9 @@ _PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 # RTM_LIB: another build of the same library (A/B timing runs only, tools/ab_bench.py)
 LIB_PATH = os.environ.get("RTM_LIB") or os.path.join(_PKG_DIR, "librtm.so")
 
-RTM_ABI_VERSION = 10
+RTM_ABI_VERSION = 11
 # library versions whose public structs share this layout (an RTM_LIB A/B build may be one)
-RTM_ABI_LAYOUT_COMPATIBLE = frozenset({9, 10})
+RTM_ABI_LAYOUT_COMPATIBLE = frozenset({9, 10, 11})
 RTM_MAX_SPHERES = 16
 RTM_MAX_PATCHES = 4
 RTM_MAX_CIRCLE_PLANES = 16
@@ -141,6 +141,9 @@ ABI_SYMBOLS = [
                                           C.POINTER(rtm_camera), _I32, _I32, _I32, _I32, C.POINTER(_P)]),
     ("rtm_ctx_shadow_map", _P, [_P]),
     ("rtm_ctx_shadow_map_texel_bytes", C.c_int32, [_P]),
+    ("rtm_ctx_shadow_map_stored_bytes", C.c_int, [_P, C.POINTER(C.c_int64), C.POINTER(_I32)]),
+    ("rtm_ctx_frames_plan", C.c_int, [_P, _I32, _I32, _I32, C.POINTER(_I32), C.POINTER(_I32)]),
+    ("rtm_ctx_last_eye_blocks", C.c_int, [_P, C.POINTER(_I32)]),
     ("rtm_render_multi", C.c_int, [C.POINTER(rtm_scene), C.POINTER(rtm_camera), C.POINTER(rtm_camera),
                                    _I32, _I32, _I32, _I32, C.POINTER(C.c_float), _I32]),
     ("rtm_render_stats", C.c_int, [_P, C.POINTER(rtm_scene), C.POINTER(rtm_camera),
@@ -179,6 +182,7 @@ ABI_SYMBOLS = [
     ("rtm_group_set_host_direct", C.c_int, [_P, _I32]),
     ("rtm_group_set_partition", C.c_int, [_P, _I32]),
     ("rtm_group_partition", C.c_int32, [_P]),
+    ("rtm_group_frames_plan", C.c_int, [_P, _I32, _I32, _I32, _I32, C.POINTER(_I32), C.POINTER(_I32)]),
     ("rtm_render_stripes_async", C.c_int, [_P, C.POINTER(rtm_scene), C.POINTER(rtm_camera), C.POINTER(rtm_camera),
                                            _I32, _I32, _I32, _I32, _I32, _I32, _I32, _I32, _P]),
     ("rtm_stripe_rows", C.c_int32, [_I32, _I32, _I32, _I32]),

@@ -707,6 +707,7 @@ struct rtm_ctx {
     int32_t lanes_last = 0;                    // lanes of the last frame-sequence call
     int32_t batch_req = 0;                     // rtm_ctx_set_batch (0 = auto)
     int32_t batch_last = 1;                    // frames per launch of the last frame-sequence call
+    int32_t eye_blocks_last = 0;               // the last eye launch ran 8 x 8-pixel blocks (rtm_ctx_last_eye_blocks)
     std::unique_ptr<BatchRing> batch;          // lane 0's batch uploads
     std::vector<TimingSlot> ring;  // per-render kernel events (capacity = ring.size())
     int64_t renders = 0;           // renders recorded into the ring
@@ -1137,8 +1138,10 @@ int enqueue_frame(rtm_ctx* ctx, FrameArgs& a, const FrameExtra* x, void* out_dev
         // the map's storage: coded (1-2 B per texel) unless counting (f64)
         a.sh.smap_fmt = stats ? SMAP_F64 : shadow_map_format(a.sh);
         a.sh.smap_bw = (a.sh.W + 127) / 128;
+        a.sh.smap_spans = stats ? 0 : shadow_map_spans(a.sh);
         DevBuf& sb = l ? l->smap : ctx->smap;
-        if ((rc = sb.ensure((size_t)smap_bytes(a.sh.smap_fmt, a.sh.W, a.sh.H), ctx->device))) return rc;
+        if ((rc = sb.ensure((size_t)smap_bytes(a.sh.smap_fmt, a.sh.W, a.sh.H, a.sh.smap_spans), ctx->device)))
+            return rc;
         smap = (double*)sb.p;
         ctx->smap_w = a.sh.W;
         ctx->smap_h = a.sh.H;
@@ -1156,6 +1159,7 @@ int enqueue_frame(rtm_ctx* ctx, FrameArgs& a, const FrameExtra* x, void* out_dev
     }
     if (slot) HIP_TRY(hipEventRecord(slot->ev[2], s));
     if ((rc = launch_eye_pass(a, smap, out_dev, s, stats, tabs))) return fail(rc, "eye pass launch failed");
+    ctx->eye_blocks_last = 0;  // (single frames render 64 x 1 rows)
     if (slot) {
         HIP_TRY(hipEventRecord(slot->ev[3], s));
         slot->shadow = !fused;
@@ -1275,11 +1279,15 @@ int enqueue_batch(rtm_ctx* ctx, int lane, FrameArgs* fa, const FrameExtra* const
     ShadowPart widest = fa[0].sh;
     for (int k = 1; k < n; ++k) widest.n_spheres = std::max(widest.n_spheres, fa[k].sh.n_spheres);
     const int32_t sfmt = fused ? SMAP_F64 : shadow_map_format(widest);
+    // (the batch's shadow launch is frame 0's kernel: its span rule holds for every frame)
+    fa[0].sh.smap_fmt = sfmt;
+    const int32_t spans = fused ? 0 : shadow_map_spans(fa[0].sh);
     for (int k = 0; k < n; ++k) {
         fa[k].sh.smap_fmt = sfmt;
         fa[k].sh.smap_bw = (fa[k].sh.W + 127) / 128;
+        fa[k].sh.smap_spans = spans;
     }
-    const size_t map_bytes = ((size_t)smap_bytes(sfmt, fa[0].sh.W, fa[0].sh.H) + 255) & ~(size_t)255;
+    const size_t map_bytes = ((size_t)smap_bytes(sfmt, fa[0].sh.W, fa[0].sh.H, spans) + 255) & ~(size_t)255;
     if (!fused && (rc = br.smaps.ensure(map_bytes * (size_t)n, ctx->device))) return rc;
     // layout of the upload: the BatchFrame table, then each frame's device tables
     auto up = [](size_t v) { return (v + 255) & ~(size_t)255; };
@@ -1410,7 +1418,10 @@ int enqueue_batch(rtm_ctx* ctx, int lane, FrameArgs* fa, const FrameExtra* const
         ctx->have_shadow_pass = false;
     }
     if (slot) HIP_TRY(hipEventRecord(slot->ev[2], s));
-    if ((rc = launch_eye_batch((const BatchFrame*)db, n, fa[0], t0, s))) return fail(rc, "batched eye pass failed");
+    int blocks = 0;
+    if ((rc = launch_eye_batch((const BatchFrame*)db, n, fa[0], t0, s, &blocks)))
+        return fail(rc, "batched eye pass failed");
+    ctx->eye_blocks_last = blocks;
     if (slot) {
         HIP_TRY(hipEventRecord(slot->ev[3], s));
         slot->shadow = !fused;
@@ -1588,6 +1599,55 @@ int rtm_ctx_set_batch(rtm_ctx* ctx, int32_t frames) {
 int rtm_ctx_last_batch(rtm_ctx* ctx, int32_t* frames) {
     if (!ctx || !frames) return fail(RTM_ERR_INVALID, "bad arguments");
     *frames = ctx->batch_last;
+    return RTM_OK;
+}
+
+int rtm_ctx_last_eye_blocks(rtm_ctx* ctx, int32_t* blocks) {
+    if (!ctx || !blocks) return fail(RTM_ERR_INVALID, "bad arguments");
+    *blocks = ctx->eye_blocks_last;
+    return RTM_OK;
+}
+
+int rtm_ctx_frames_plan(rtm_ctx* ctx, int32_t width, int32_t rows, int32_t n_frames, int32_t* lanes,
+                        int32_t* frames_per_launch) {
+    if (!ctx || !lanes || !frames_per_launch || width < 1 || rows < 1 || n_frames < 1)
+        return fail(RTM_ERR_INVALID, "bad arguments");
+    // rtm_render_frames_async's own rules (frame_batch, frame_lanes) for distinct outputs
+    const int32_t B = std::min<int32_t>(frame_batch(ctx->batch_req, width, rows), n_frames);
+    std::vector<float*> outs((size_t)n_frames);
+    for (int32_t i = 0; i < n_frames; ++i) outs[(size_t)i] = (float*)(uintptr_t)(((uintptr_t)i + 1) << 40);
+    *frames_per_launch = B;
+    *lanes = frame_lanes(ctx->lanes_req, n_frames, width, rows, outs.data(), B);
+    return RTM_OK;
+}
+
+int rtm_ctx_shadow_map_stored_bytes(rtm_ctx* ctx, int64_t* bytes, int32_t* span_records) {
+    if (!ctx || !bytes) return fail(RTM_ERR_INVALID, "bad arguments");
+    *bytes = 0;
+    if (span_records) *span_records = 0;
+    const int32_t tb = rtm_ctx_shadow_map_texel_bytes(ctx);
+    if (tb == 0) return RTM_OK;
+    const ShadowPart& sh = ctx->last_sh;
+    if (!sh.smap_spans) {
+        *bytes = tb == 8 ? (int64_t)sh.W * sh.H * 8 : smap_bytes(sh.smap_fmt, sh.W, sh.H);
+        return RTM_OK;
+    }
+    if (span_records) *span_records = 1;
+    // the span records, then the block bytes of every span stored texel by texel (its
+    // rows of whole 4-row blocks, 128-column blocks wide as the tile stores them)
+    DeviceGuard g(ctx->device);
+    const int64_t pitch = (int64_t)sh.smap_bw * 128, nspan = (sh.H + SPAN_ROWS - 1) / SPAN_ROWS;
+    std::vector<uint32_t> rec((size_t)(pitch * nspan));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    HIP_TRY(hipMemcpy(rec.data(), (const char*)ctx->last_smap + smap_span_offset(sh.W, sh.H),
+                      rec.size() * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    const int32_t H4 = (sh.H + 3) & ~3;
+    int64_t n = (int64_t)rec.size() * 4;
+    for (int64_t sp = 0; sp < nspan; ++sp) {
+        const int64_t rows = std::min<int64_t>(SPAN_ROWS, H4 - sp * SPAN_ROWS);
+        for (int64_t x = 0; x < pitch; ++x) n += rec[(size_t)(sp * pitch + x)] == SPAN_DENSE ? rows : 0;
+    }
+    *bytes = n;
     return RTM_OK;
 }
 

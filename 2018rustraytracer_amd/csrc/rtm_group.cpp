@@ -865,6 +865,24 @@ int rtm_group_set_partition(rtm_group* g, int32_t stripe_rows) {
 
 int32_t rtm_group_partition(rtm_group* g) { return g ? group_stripe(g) : -1; }
 
+int rtm_group_frames_plan(rtm_group* g, int32_t width, int32_t height, int32_t n_frames, int32_t root,
+                          int32_t* frames_per_chunk, int32_t* lanes) {
+    if (!g || !frames_per_chunk || !lanes || width < 1 || height < 1 || n_frames < 1 || root < 0 ||
+        root >= g->n_ranks || g->m.empty())
+        return set_error(RTM_ERR_INVALID, "bad arguments");
+    // rtm_group_render_frames_async's rules: chunks of the auto frames per launch of part
+    // 0, and each member's lanes_plan over the chunks (distinct outputs: no clash cap)
+    const int32_t rows0 = part_of(height, g->n_ranks, group_stripe(g), 0).rows;
+    const int32_t B = std::max(1, std::min<int32_t>(n_frames, rtm::internal::auto_frames_per_launch(width, rows0)));
+    const Member* mb = &g->m[0];
+    for (const Member& m : g->m)
+        if (m.rank == root) mb = &m;
+    const int32_t rows = part_of(height, g->n_ranks, group_stripe(g), mb->rank).rows;
+    *frames_per_chunk = B;
+    *lanes = rows > 0 ? rtm::internal::lanes_plan(mb->ctx, width, rows, (n_frames + B - 1) / B) : 1;
+    return RTM_OK;
+}
+
 int rtm_group_set_host_direct(rtm_group* g, int32_t on) {
     if (!g) return set_error(RTM_ERR_INVALID, "group is NULL");
     if (on && (int32_t)g->m.size() != g->n_ranks)

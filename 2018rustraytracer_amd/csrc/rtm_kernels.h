@@ -129,6 +129,8 @@ struct ShadowPart {
     int32_t cull_x0, cull_x1, cull_y0, cull_y1;  // union of the spheres' pixel ranges (see EyePart)
     int32_t smap_fmt;  // SMAP_F64 / SMAP_U8 / SMAP_U16: how the shadow pass stores the map (shadow_map_format)
     int32_t smap_bw;   // coded maps: blocks per block row, ceil(W / 128)
+    int32_t smap_spans;  // 1: the U8 map carries span records after its codes (shadow_map_spans)
+    int32_t pad_;
 };
 
 // The shadow map's storage.  Every texel's value is one of +INF, a sphere's
@@ -144,9 +146,27 @@ constexpr int32_t SMAP_F64 = 0, SMAP_U8 = 1, SMAP_U16 = 2;
 constexpr int64_t smap_code_index(int x, int y, int bw) {
     return ((int64_t)(y >> 2) * bw + (x >> 7)) * 512 + ((x & 127) >> 1) * 8 + (y & 3) * 2 + (x & 1);
 }
-// bytes of a shadow map of W x H texels in format fmt
-inline int64_t smap_bytes(int32_t fmt, int32_t W, int32_t H) {
+// Span records (round 6; a U8 map written by the coded tile, ShadowPart::smap_spans).
+// Down a column of a strip that marches one patch and meets no sphere, the codes are one
+// monotone run (shadow_tile_coded): over a 64-row span they are a top code, a bottom code
+// and the row where the bottom code starts.  Such a span is stored as that record alone,
+// 4 bytes per column instead of 64 -- the raster-free waves, most of the map, then store
+// 1/16 of the bytes.  Every other span has the record SPAN_DENSE and its codes in the
+// blocks above.  Record of column x in span s = y >> 6: element s * (smap_bw * 128) + x of
+// the table that starts at smap_span_offset; value top | bottom << 8 | boundary << 16
+// (rows [0, boundary) of the span hold top).  A reader loads the record and the block
+// byte together and keeps the byte only for SPAN_DENSE: the same code, so the same bits.
+constexpr int SPAN_ROWS = 64;
+constexpr uint32_t SPAN_DENSE = 0xFFFFFFFFu;
+constexpr int64_t smap_span_index(int x, int y, int bw) { return (int64_t)(y >> 6) * bw * 128 + x; }
+constexpr int64_t smap_span_offset(int32_t W, int32_t H) {
+    return ((int64_t)((W + 127) / 128) * ((H + 3) / 4) * 512 + 255) & ~(int64_t)255;
+}
+// bytes of a shadow map of W x H texels in format fmt (spans: with span records)
+inline int64_t smap_bytes(int32_t fmt, int32_t W, int32_t H, int32_t spans = 0) {
     if (fmt == SMAP_F64) return (int64_t)W * H * 8;
+    if (fmt == SMAP_U8 && spans)
+        return smap_span_offset(W, H) + (int64_t)((H + SPAN_ROWS - 1) / SPAN_ROWS) * ((W + 127) / 128) * 128 * 4;
     return (int64_t)((W + 127) / 128) * ((H + 3) / 4) * 512 * (fmt == SMAP_U8 ? 1 : 2);
 }
 
@@ -348,6 +368,9 @@ int launch_shadow_pass(const FrameArgs& a, double* smap, void* stream, StatsK* s
 // coded map (SMAP_U8 when steps + n_spheres <= 254, SMAP_U16 up to 65534), else
 // f64 (and with RTM_SMAP=f64).  Set a.sh.smap_fmt / smap_bw before both passes launch.
 int32_t shadow_map_format(const ShadowPart& sh);
+// 1 when the shadow pass of sh (smap_fmt set) writes span records (a U8 map by the coded
+// tile): set a.sh.smap_spans from it and size the map with smap_bytes(..., spans).
+int32_t shadow_map_spans(const ShadowPart& sh);
 // f64 values of a coded map (rtm_ctx_shadow_map's view of it), async on stream.
 int launch_smap_decode(const ShadowPart& sh, const void* codes, double* out, void* stream);
 // rt / psp != nullptr: the frame has ray-traced primitives / a PERSPECTIVE eye
@@ -361,7 +384,9 @@ int launch_eye_pass(const FrameArgs& a, const double* smap, void* out, void* str
 // a batch shares the shapes, flags, tables and kernel variant).
 // box: the union of the batch's sphere pixel boxes (x0, x1, y0, y1) for the split coded launch
 int launch_shadow_batch(const BatchFrame* dev, int n, const FrameArgs& a0, void* stream, const int32_t* box = nullptr);
-int launch_eye_batch(const BatchFrame* dev, int n, const FrameArgs& a0, const DevTabs& t0, void* stream);
+// blocks (optional): set to 1 when the launch ran 8 x 8-pixel blocks (eye_block_mode), else 0
+int launch_eye_batch(const BatchFrame* dev, int n, const FrameArgs& a0, const DevTabs& t0, void* stream,
+                     int* blocks = nullptr);
 // Stream-ordered copy of host bytes into device memory by kernels whose
 // arguments carry the bytes (<= 3968 per launch), so the host copy is consumed
 // at launch: no pinned staging, no host synchronisation.  bytes % 8 == 0.

@@ -59,24 +59,6 @@ __device__ __forceinline__ void note_oob() {
     if ((threadIdx.x & 63) == __builtin_ctzll(__ballot(1))) atomicAdd(&g_oob_reads, 1ull);
 }
 
-#ifdef RTM_AB_PHASES
-// (A/B diagnostic builds only, tools/probes/phases.py) per-wave s_memtime stamps at
-// program points: wave w of kernel region r writes slot k of row r * PHASE_REGION + w.
-// Each stamp waits for the wave's outstanding memory operations first, so a phase
-// includes what it waited for.
-constexpr long long PHASE_REGION = 1 << 18;
-__device__ unsigned long long* g_phase;
-__device__ __forceinline__ void phase_stamp(int region, int k) {
-    __builtin_amdgcn_s_waitcnt(0);
-    const unsigned long long t = __builtin_amdgcn_s_memtime();
-    const long long w = (((long long)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x) * (blockDim.x >> 6) +
-                        (threadIdx.x >> 6);
-    if ((threadIdx.x & 63) == 0 && g_phase && w < PHASE_REGION) g_phase[(region * PHASE_REGION + w) * 8 + k] = t;
-}
-#define RTM_PHASE(r, k) phase_stamp(r, k)
-#else
-#define RTM_PHASE(r, k) ((void)0)
-#endif
 
 // main.rs:306-307 / 1903-1907: ((i as f64) / (res as f64)) * 2.0 - 1.0
 __device__ __forceinline__ double ndc(int i, int res) { return ((double)i / (double)res) * 2.0 - 1.0; }
@@ -1143,10 +1125,21 @@ __device__ __forceinline__ double shadow_texel(const ShadowPart& a, int xi, int 
 // shadow pass computed there, recomputed from its code with the writer's
 // operations (t_after; cover + the BACK-face depth of the lean and generic
 // tiles), so the same bits.
-__device__ __forceinline__ double smap_decode(const ShadowPart& sh, const void* __restrict__ map, int tx, int ty) {
+// The code of texel (tx, ty) of a coded map: its block byte, or with span records
+// (rtm_kernels.h) the span's record, both loaded together.
+__device__ __forceinline__ uint32_t smap_code(const ShadowPart& sh, const void* __restrict__ map, int tx, int ty) {
     const int64_t e = smap_code_index(tx, ty, sh.smap_bw);
-    const uint32_t code = sh.smap_fmt == SMAP_U8 ? (uint32_t)((const uint8_t*)map)[e]
-                                                 : (uint32_t)((const uint16_t*)map)[e];
+    if (sh.smap_fmt != SMAP_U8) return (uint32_t)((const uint16_t*)map)[e];
+    const uint32_t dense = (uint32_t)((const uint8_t*)map)[e];
+    if (!sh.smap_spans) return dense;
+    const uint32_t rec = ((const uint32_t*)((const uint8_t*)map + smap_span_offset(sh.W, sh.H)))
+        [smap_span_index(tx, ty, sh.smap_bw)];
+    const uint32_t run = (uint32_t)(ty & (SPAN_ROWS - 1)) < ((rec >> 16) & 0xFFu) ? rec & 0xFFu : (rec >> 8) & 0xFFu;
+    return rec == SPAN_DENSE ? dense : run;
+}
+
+__device__ __forceinline__ double smap_decode(const ShadowPart& sh, const void* __restrict__ map, int tx, int ty) {
+    const uint32_t code = smap_code(sh, map, tx, ty);
     const uint32_t inf = sh.smap_fmt == SMAP_U8 ? 0xFFu : 0xFFFFu;
     if (code == inf) return INFINITY;
     if ((int)code < sh.steps) return t_after(sh.tab, (int)code);
@@ -1171,9 +1164,8 @@ __device__ __forceinline__ double smap_decode(const ShadowPart& sh, const void* 
 // last load, see eye_tile).
 __device__ __forceinline__ double smap_decode_wave(const ShadowPart& sh, const void* __restrict__ map, int tx, int ty,
                                                    bool& oob) {
-    const int64_t e = smap_code_index(tx, ty, sh.smap_bw);
     const bool u8 = sh.smap_fmt == SMAP_U8;
-    const uint32_t code = u8 ? (uint32_t)((const uint8_t*)map)[e] : (uint32_t)((const uint16_t*)map)[e];
+    const uint32_t code = smap_code(sh, map, tx, ty);
     const double xs = sh.tab.nx[tx];
     const double ys = sh.tab.ny[ty];
     const uint32_t inf = u8 ? 0xFFu : 0xFFFFu;
@@ -1288,11 +1280,8 @@ constexpr int CODED_TILE_ROWS = CODED_ROWS * TILE_Y;
 // workgroup: the sphere raster is most of its work and 16-row waves left it with too
 // few waves to hide its latency (2,800 per 8-frame launch at config 3: 37.9 instead of
 // 24 us, profiles/r04_v3_*); its march codes take the per-texel check.
-#ifndef RTM_AB_P2ROWS
-#define RTM_AB_P2ROWS 4
-#endif
 template <int PART>
-constexpr int coded_wave_rows = PART == 2 ? RTM_AB_P2ROWS : CODED_ROWS;
+constexpr int coded_wave_rows = PART == 2 ? 4 : CODED_ROWS;
 // PART 1 waves loop over P1_STRIPS consecutive 16-row strips (the prologue -- frame
 // header, the LDS table fill and its barrier, the row records -- paid once per wave).
 // 4 strips (a wave per 128 x 64 texels, a quarter of the waves): config 3 340 -> 348,
@@ -1301,12 +1290,9 @@ constexpr int coded_wave_rows = PART == 2 ? RTM_AB_P2ROWS : CODED_ROWS;
 // the chip 1.2 times; in the lanes the other frames' kernels fill the rest)
 // (profiles/r05_ab_shadow_strips.txt).  The whole-span shortcut below then takes the
 // raster-free launch to 21.6 us one-lane and config 3 345 -> 359 Gpix/s in the lanes
-// (profiles/r05_ab_span.txt).  RTM_AB_P1NS overrides it in A/B builds.
-#ifndef RTM_AB_P1NS
-#define RTM_AB_P1NS 4
-#endif
-constexpr int P1_STRIPS = RTM_AB_P1NS;
-static_assert(P1_STRIPS >= 1 && P1_STRIPS * 16 <= 64, "a PART 1 wave's row records are one per lane: at most 64 rows");
+// (profiles/r05_ab_span.txt).
+constexpr int P1_STRIPS = 4;
+static_assert(P1_STRIPS * CODED_ROWS == SPAN_ROWS, "a PART 1 wave covers one span of the map's records (and its row records are one per lane)");
 template <int PART>
 constexpr int coded_wave_strips = PART == 1 ? P1_STRIPS : 1;
 template <int PART>
@@ -1352,8 +1338,31 @@ __device__ __forceinline__ uint32_t code_check(const ZRecK* __restrict__ T, doub
     return (fastD & okA & okB & (f < steps)) ? (uint32_t)f : CODE_NONE;
 }
 
-// PART (the split launch, launch_coded): 0 every strip; 1 only strips outside the
-// frame's sphere box (no raster code); 2 only strips meeting it.
+// Does a sphere of the frame cover a texel of the 128 x 16 strip of columns [xb, xb + 127]
+// and rows [s0, s0 + 15]?  A conservative test (wave-uniform): the sphere's exact pixel
+// ranges, then its disc -- coverage is pa^2 + pb^2 < 1 with |pa| = |x - cx| / |r| (n / m =
+// r / r^2, rtm_kernels.h), so no texel of the strip's NDC rectangle is covered when the
+// rectangle's nearest point lies farther than |r| from the centre; a 1e-6 relative margin
+// absorbs the rounding of both forms, and NaN / INF never reject.  The split launch gives
+// a strip to the raster part (PART 2) exactly when this holds, and both parts evaluate it
+// alike: round 5 used the union of the pixel ranges, which at config 3 also sent the empty
+// strips between the orbiting sphere and the other two to PART 2's per-texel path.
+__device__ __forceinline__ bool strip_rasters(const ShadowPart& a, int xb, int s0) {
+    const int xe = min(xb + 127, a.W - 1), ye = min(s0 + CODED_ROWS - 1, a.H - 1);
+    if ((a.flags & RTM_FLAG_NO_SHADOW_RASTER) || !union_may_cover(a, xb, xe, s0, ye)) return false;
+    uint32_t m = wave_sphere_mask(a.sph, a.n_spheres, xb, xe, s0, ye);
+    if (!m) return false;
+    const double X0 = a.tab.nx[xb], X1 = a.tab.nx[xe], Y0 = a.tab.ny[s0], Y1 = a.tab.ny[ye];
+    for (; m; m &= m - 1u) {
+        const RasterSphereK& s = a.sph[__builtin_ctz(m)];
+        const double dx = s.cx - fmin(fmax(s.cx, X0), X1), dy = s.cy - fmin(fmax(s.cy, Y0), Y1);
+        if (!(dx * dx + dy * dy > (s.r * s.r) * (1.0 + 1e-6))) return true;
+    }
+    return false;
+}
+
+// PART (the split launch, launch_coded): 0 every strip; 1 only strips no sphere covers
+// (strip_rasters; no raster code); 2 only the others.
 template <bool INC, int CODE, int PART>
 __device__ __forceinline__ void shadow_tile_coded(const ShadowPart& a, void* __restrict__ map, int bx, int by,
                                                   ZRecK* __restrict__ T, RowLdsK* __restrict__ RL) {
@@ -1365,7 +1374,6 @@ __device__ __forceinline__ void shadow_tile_coded(const ShadowPart& a, void* __r
     const int xb = bx * 128;
     const int x0 = xb + lane * 2;
     const int yw = __builtin_amdgcn_readfirstlane(by * coded_tile_rows<PART> + wv * SPAN);  // the wave's first row
-    RTM_PHASE(PART, 0);
     const int W = a.W, H = a.H, steps = a.steps;
     const bool march = !(a.flags & RTM_FLAG_NO_MARCH) && a.n_patches > 0 && steps > 0;
     // the LDS records: one per thread, loaded now, written before the barrier
@@ -1405,9 +1413,15 @@ __device__ __forceinline__ void shadow_tile_coded(const ShadowPart& a, void* __r
         if (lane < SPAN) RL[wv * SPAN + lane] = RowLdsK{rl.py, rl.pyf, 0};
         __syncthreads();
     }
-    RTM_PHASE(PART, 1);  // (records loaded, LDS filled, past the barrier)
     // wave-uniform: bit r = row yw + r marches (inRange01 and < H)
     const uint64_t rowbits_w = __ballot((lane < SPAN) & (rl.ok != 0));
+    // bit st: strip st of the wave is the raster part's (strip_rasters; wave-uniform)
+    uint32_t boxbits = 0u;
+#pragma unroll
+    for (int st = 0; st < NS; ++st) {
+        const int s0 = (yw + NR * st) & ~(CODED_ROWS - 1);
+        if (s0 < H && strip_rasters(a, xb, s0)) boxbits |= 1u << st;
+    }
     // The whole span's shortcut (PART 1, one patch, every one of the wave's SPAN rows
     // marching): a column's codes over the span are one monotone sequence by the strip
     // argument (D is monotone down the whole column), so both ends, decided on one side of
@@ -1473,6 +1487,23 @@ __device__ __forceinline__ void shadow_tile_coded(const ShadowPart& a, void* __r
             }
         }
     }
+    // The span records (rtm_kernels.h).  A span's record is written by the one wave that
+    // owns it: the PART 1 wave when no strip of its span is the raster part's (its codes
+    // then need no block bytes at all when span_ok), else wave 0 of each PART 2 workgroup
+    // of the span (the same SPAN_DENSE from each), or of the PART 0 workgroup (64 rows).
+    if (CODE == SMAP_U8 && a.smap_spans && yw < H) {
+        const bool own = PART == 1 ? boxbits == 0u : wv == 0;
+        if (own) {
+            const bool run = PART == 1 && span_ok;
+            const uint32_t r0 = run ? (stop[0] & 0xFFu) | ((sbot[0] & 0xFFu) << 8) | ((uint32_t)sbnd[0] << 16) : SPAN_DENSE;
+            const uint32_t r1 = run ? (stop[1] & 0xFFu) | ((sbot[1] & 0xFFu) << 8) | ((uint32_t)sbnd[1] << 16) : SPAN_DENSE;
+            uint32_t lane_r;
+            asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane_r));
+            uint32_t* rec = (uint32_t*)((uint8_t*)map + smap_span_offset(W, H)) + smap_span_index(xb, yw, a.smap_bw);
+            *reinterpret_cast<uint2*>(rec + 2 * lane_r) = make_uint2(r0, r1);
+            if (run) return;  // the record is the span's whole store
+        }
+    }
 #pragma unroll 1
     for (int st = 0; st < NS; ++st) {
     const int y0 = yw + NR * st;  // this strip's first row
@@ -1491,9 +1522,7 @@ __device__ __forceinline__ void shadow_tile_coded(const ShadowPart& a, void* __r
     // this wave's strip is left to the other part of a split launch (wave-uniform); a
     // skipping wave still fills its records and meets the workgroup barrier.  The
     // split is decided per 16-row strip (a PART 2 wave's 4 rows lie in one)
-    const int s0 = y0 & ~(CODED_ROWS - 1);
-    const bool strip_box =
-        !(a.flags & RTM_FLAG_NO_SHADOW_RASTER) && union_may_cover(a, xb, xb + 127, s0, s0 + CODED_ROWS - 1);
+    const bool strip_box = (boxbits >> st) & 1u;
     const bool skipw = (PART == 1 && strip_box) || (PART == 2 && !strip_box);
     // a row's two codes packed in one register (low: column 0), NONE = 0xFFFF
     uint32_t cdp[NR];
@@ -1645,7 +1674,6 @@ __device__ __forceinline__ void shadow_tile_coded(const ShadowPart& a, void* __r
             }
         }
     }
-    if (st == 0) RTM_PHASE(PART, 2);  // (strip 0's march codes)
     // shadow viewport rasterize, face BACK (main.rs:1569, 243), 4 rows at a time: the
     // strict minimum over the spheres in scene order, then the march code only where its
     // t is strictly below that minimum (main.rs:559).
@@ -1872,7 +1900,6 @@ __device__ __forceinline__ void shadow_tile_coded(const ShadowPart& a, void* __r
             }
         }
     }
-    if (st == 0) RTM_PHASE(PART, 3);  // (strip 0's raster)
     if (skipw) continue;
     // the lane's 4 rows x 2 columns of each block as one 8- (U8) or 16-byte (U16)
     // store: element lane*8 + r*2 + c of block (y >> 2, xb >> 7) (rows past H hold
@@ -1897,9 +1924,7 @@ __device__ __forceinline__ void shadow_tile_coded(const ShadowPart& a, void* __r
                 make_uint4(cdp[4 * b], cdp[4 * b + 1], cdp[4 * b + 2], cdp[4 * b + 3]);
         }
     }
-    if (st == 0) RTM_PHASE(PART, 4);  // (strip 0 stored)
     }  // strips
-    RTM_PHASE(PART, 5);  // (every strip stored and drained)
 }
 
 template <bool INC, int CODE, int PART>
@@ -1915,17 +1940,19 @@ __device__ __forceinline__ void shadow_coded_block(const ShadowPart& sh, void* _
         by = none ? (int)blockIdx.y : hot_rows_first((int)blockIdx.y, n, h0, h1);
     } else {
         // (workgroup-uniform: the whole workgroup leaves, before its barrier, when none of
-        // its 4 strips is this part's; the box is a rectangle, so its strips are a run)
+        // its strips is this part's, by the waves' own test, strip_rasters)
         bx += org.x;
         by = (int)blockIdx.y + org.y;
-        const bool rast = !(sh.flags & RTM_FLAG_NO_SHADOW_RASTER);
-        const int ya = by * TR;
-        const int sub = CODED_ROWS;  // (PART 1's waves; a PART 2 workgroup is one 16-row strip)
-        const int xa = bx * 128, xe = xa + 127;
-        if (PART == 2 ? !(rast && union_may_cover(sh, xa, xe, ya, ya + TR - 1))
-                      : (rast && union_may_cover(sh, xa, xe, ya, ya + sub - 1) &&
-                         union_may_cover(sh, xa, xe, ya + TR - sub, ya + TR - 1)))
-            return;
+        const int ya = by * TR, xa = bx * 128;
+        if (PART == 2) {  // (one 16-row strip per workgroup)
+            if (!strip_rasters(sh, xa, ya)) return;
+        } else if (!(sh.flags & RTM_FLAG_NO_SHADOW_RASTER) && union_may_cover(sh, xa, xa + 127, ya, ya + CODED_ROWS - 1) &&
+                   union_may_cover(sh, xa, xa + 127, ya + TR - CODED_ROWS, ya + TR - 1)) {
+            // (the union reaches both end strips: every strip may be PART 2's)
+            bool all = true;
+            for (int s0 = ya; s0 < ya + TR && s0 < sh.H && all; s0 += CODED_ROWS) all = strip_rasters(sh, xa, s0);
+            if (all) return;
+        }
     }
     shadow_tile_coded<INC, CODE, PART>(sh, map, bx, by, reinterpret_cast<ZRecK*>(lds + CODED_ROW_LDS),
                                        reinterpret_cast<RowLdsK*>(lds));
@@ -1935,11 +1962,8 @@ __device__ __forceinline__ void shadow_coded_block(const ShadowPart& sh, void* _
 // uncapped, fewer spilled SGPRs cost 90 VGPRs and 5 waves; round 5: the span shortcut's
 // registers spilled 16 B to scratch under 7, none under 6 -- 80 VGPRs, and 6 waves of
 // 4-strip waves still fill the chip), else free
-#ifndef RTM_AB_P1WAVES
-#define RTM_AB_P1WAVES 6
-#endif
 template <int PART>
-constexpr int CODED_MIN_WAVES = PART == 1 ? RTM_AB_P1WAVES : 1;
+constexpr int CODED_MIN_WAVES = PART == 1 ? 6 : 1;
 
 template <bool INC, int CODE, int PART>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(CODED_MIN_WAVES<PART>, 8))) void
@@ -1999,7 +2023,6 @@ __device__ __forceinline__ void eye_tile(const EyePart& a, const ShadowPart& sh,
     // (BLK: the lane's own row; else the wave's)
     const int yl = BLK ? by * 8 + (ln_ >> 3) : __builtin_amdgcn_readfirstlane(by * TILE_Y + wv_);
     const int yl0 = BLK ? __builtin_amdgcn_readfirstlane(by * 8) : yl;  // the wave's first row
-    if (!COUNT) RTM_PHASE(3, 0);
     // the header fields the prologue needs, read before any branch so their scalar loads
     // issue as one group: one wait instead of a chain of dependent round trips (the
     // short waves of small frames are latency-bound: config 7 +6 %, profiles/r04_ab_eye_prologue.txt)
@@ -2076,16 +2099,11 @@ __device__ __forceinline__ void eye_tile(const EyePart& a, const ShadowPart& sh,
     } else if (RTB && rt) {
         rmask = rt_slots(rt->n_pl, rt->n_cy);
     }
-    if (!COUNT) RTM_PHASE(3, 1);  // (masks ready)
     float4 c = make_float4(0.0f, 0.2f, 0.2f, 1.0f);  // (0.0, 0.2, 0.2) as f32 (main.rs:718-720)
     bool shaded = false;
     // a wave no sphere, primitive or SDF can reach is background: no NDC loads, no rays
     // (its pixels keep the background colour, as the full loop would leave them)
-#ifdef RTM_AB_BGONLY  // (diagnostic A/B builds only: every wave stores the background -- not the image)
-    const bool reach = false;
-#else
     const bool reach = smask != 0u || (RTB && rt && rmask != 0u) || (RT == 2 && sdf);
-#endif
     if (live && reach) {
         const double x = a.nx[xi];
         const double y = a.ny[yi];
@@ -2226,7 +2244,6 @@ __device__ __forceinline__ void eye_tile(const EyePart& a, const ShadowPart& sh,
             }
         }
     }
-    if (!COUNT) RTM_PHASE(3, 2);  // (traced and shaded)
     // the frame store (all lanes converged): RGBA f32, or writeColorImage's bytes
     if (FMT == RTM_FORMAT_RGBA32F) {
         float4* o = reinterpret_cast<float4*>(out);
@@ -2265,7 +2282,6 @@ __device__ __forceinline__ void eye_tile(const EyePart& a, const ShadowPart& sh,
             }
         }
     }
-    if (!COUNT) RTM_PHASE(3, 3);  // (stored, drained)
     // the sphere ids a hit shades with (a.shade[id]): the host validated them (checked_id);
     // the frame's first wave checks them again (here, after the tile's stores: earlier it
     // cost the tile 8 VGPRs) and counts any past the table, and every read above masks
@@ -2338,32 +2354,23 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
 // (frame z's nw words at km + z * nw, nw = gx * rows) so that their load issues with the
 // frame header's, not after it
 // A RT 3 frame without shadows (main()'s scene and row f-1's bench, configs 6 and 7)
-// has short waves: its batched workgroups render RTM_AB_EYE_TILES_RT3 = 4 tiles one after
+// has short waves: its batched workgroups render 4 tiles one after
 // another, held to 8 waves per SIMD (62 VGPRs): configs 6 / 7 +1.5 % against one tile
 // (profiles/r05_ab_eye_tiles.txt).  The table reads stay scalar loads after a tile's
 // stores because the tables are read through constant-address-space pointers
 // (const_table); the frame pointer is opaque per tile, so the header is re-read from the
 // scalar cache rather than held in registers across the tiles (68 -> 62 VGPRs).
-#ifndef RTM_AB_EYE_TILES_RT3
-#define RTM_AB_EYE_TILES_RT3 4
-#endif
 template <int RT, bool NOSH>
-constexpr int eye_batch_tiles = RT == 3 && NOSH ? RTM_AB_EYE_TILES_RT3 : 1;
+constexpr int eye_batch_tiles = RT == 3 && NOSH ? 4 : 1;
 // The sphere-only batched eye pass on the materialised map (the headline kernel) is held
 // to 8 waves per SIMD as well: 62 VGPRs, no scratch (the compiler's own allocation gave
 // 68, 7 waves): configs 3 / 2 / 4 +2 % (profiles/r05_ab_eye_tiles.txt).  The fused one
 // stays free: held to 8 it spills 20 B.
-#ifndef RTM_AB_EYE_WPE_RT0
-#define RTM_AB_EYE_WPE_RT0 8
-#endif
 // block rows per workgroup in the 8 x 8 mode, one after another: config 7 294 -> 317
 // Gpix/s against one (2: no gain; profiles/r05_ab_eye_blocks.txt)
-#ifndef RTM_AB_BLK_NT
-#define RTM_AB_BLK_NT 4
-#endif
-constexpr int EYE_BLK_NT = RTM_AB_BLK_NT;
+constexpr int EYE_BLK_NT = 4;
 template <bool FUSED, int RT, bool NOSH>
-constexpr int eye_batch_wpe = RT == 3 && NOSH ? 8 : RT == 0 && !FUSED ? RTM_AB_EYE_WPE_RT0 : 1;
+constexpr int eye_batch_wpe = RT == 3 && NOSH ? 8 : RT == 0 && !FUSED ? 8 : 1;
 template <bool FUSED, int RT, int FMT, bool NOSH = false, bool BLK = false>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(eye_batch_wpe<FUSED, RT, NOSH>, 8))) void eye_batch_kernel(
     CBatch* __restrict__ fr, const uint32_t* __restrict__ km, int km_nw, int km_gx) {
@@ -2934,6 +2941,10 @@ int32_t shadow_map_format(const ShadowPart& sh) {
     return SMAP_F64;
 }
 
+// Span records come with a U8 map whose shadow pass is the coded tile (launch_coded): its
+// waves write them (shadow_tile_coded); the generic tile writes block bytes only.
+int32_t shadow_map_spans(const ShadowPart& sh) { return sh.smap_fmt == SMAP_U8 && coded_ok(sh) ? 1 : 0; }
+
 __global__ __launch_bounds__(BLOCK) void smap_decode_kernel(const ShadowPart sh, const void* __restrict__ codes,
                                                             double* __restrict__ out) {
     const int x = blockIdx.x * BLOCK + threadIdx.x;
@@ -2963,19 +2974,21 @@ static bool eye_block_mode(const FrameArgs& a0, const DevTabs& t0, bool fused) {
     const int64_t nw8 = (int64_t)((a0.ey.W + 7) / 8) * ((rows + 7) / 8);
     return nosh && t0.rt && t0.rt_persp && !t0.sdf && t0.rtmask && (t0.fmt & FMT_MASK) == RTM_FORMAT_RGBA32F &&
            a0.ey.stripe_rows == 0 && nw8 <= (int64_t)t0.rtmask_words &&
-#ifdef RTM_AB_BLK_ALL
-           true;
-#else
            (int64_t)a0.ey.W * rows < (1 << 20);
-#endif
 }
 
-int launch_eye_batch(const BatchFrame* dev, int n, const FrameArgs& a0, const DevTabs& t0, void* stream) {
+int launch_eye_batch(const BatchFrame* dev, int n, const FrameArgs& a0, const DevTabs& t0, void* stream,
+                     int* blocks) {
     hipStream_t s = (hipStream_t)stream;
     CBatch* fr = (CBatch*)dev;
     const int rows = a0.ey.row_end - a0.ey.row_begin;
     const bool fused = (a0.ey.flags & RTM_FLAG_FUSED_SHADOW) != 0;
     const bool blk = eye_block_mode(a0, t0, fused);
+    // (the SDF batches take blocks under their own rule, launch_eye_fmt's sblk)
+    const bool sdf_blk = t0.sdf && (t0.fmt & FMT_MASK) == RTM_FORMAT_RGBA32F && a0.ey.stripe_rows == 0 &&
+                         !(fused && !((a0.sh.flags & (RTM_FLAG_NO_MARCH | RTM_FLAG_NO_SHADOW_RASTER)) ==
+                                      (RTM_FLAG_NO_MARCH | RTM_FLAG_NO_SHADOW_RASTER)));
+    if (blocks) *blocks = blk || sdf_blk;
     if (t0.rtmask) {  // the batch's per-wave primitive masks first (RT 3)
         if (blk) {
             const int nw8 = ((a0.ey.W + 7) / 8) * ((rows + 7) / 8);
@@ -2997,14 +3010,6 @@ int launch_eye_batch(const BatchFrame* dev, int n, const FrameArgs& a0, const De
     return launched();
 }
 
-#ifdef RTM_AB_PHASES
-}  // namespace rtm
-extern "C" int rtm_diag_set_phase_buffer(void* dev) {
-    return hipMemcpyToSymbol(HIP_SYMBOL(rtm::g_phase), &dev, sizeof dev) == hipSuccess ? 0 : -3;
-}
-extern "C" long long rtm_diag_phase_region(void) { return rtm::PHASE_REGION; }
-namespace rtm {
-#endif
 
 int read_oob_reads(unsigned long long* count, void* stream) {
     const unsigned long long zero = 0ull;

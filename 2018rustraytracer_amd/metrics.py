@@ -98,11 +98,15 @@ def shared_z_separable(shadow_cam) -> bool:
 def frame_work(stats: dict, width: int, height: int, n_spheres: int, n_patches: int, flags: int = 0,
                fused: bool = False, sep: bool = False, n_planes: int = 0, n_cyls: int = 0,
                perspective: bool = False, search: bool = False, n_sdfs: int = 0, map_texel_bytes: int = 8,
-               moving: bool = False) -> dict:
+               moving: bool = False, map_stored_bytes: int | None = None, span_records: bool = False) -> dict:
     """search: the march is the first-crossing search (monotone shared z table).
     map_texel_bytes: the shadow map's storage per texel (8: f64; 2 or 1: the coded
     map, rtm_ctx_shadow_map_texel_bytes) -- stored once per texel by the shadow
     pass, gathered once per hit pixel by the eye pass.
+    map_stored_bytes: what the shadow pass stored per frame when measured
+    (rtm_ctx_shadow_map_stored_bytes: with span records, the records plus the spans
+    stored texel by texel); span_records: an eye lookup reads the 4-byte record beside
+    the texel's byte.
     moving: the shadow rays move in x/y (the general march loop)."""
     px = width * height
     no_march = bool(flags & 0x1)
@@ -131,8 +135,9 @@ def frame_work(stats: dict, width: int, height: int, n_spheres: int, n_patches: 
                     + (RT_PER_PLANE_PERSP if hoisted else RT_PER_PLANE) * pl_tests
                     + (RT_PER_CYL_PERSP if hoisted else RT_PER_CYL) * cy_tests)
         eye_ops += SDF_PER_EVAL * stats.get("sdf_distance_evals", 0) + SDF_PER_HIT * stats.get("eye_sdf_pixels", 0)
-    sh_bytes = 0 if fused else map_texel_bytes * px
-    eye_bytes = 16 * px + (0 if fused else map_texel_bytes * stats["eye_hit_pixels"])
+    sh_bytes = 0 if fused else (map_stored_bytes if map_stored_bytes is not None else map_texel_bytes * px)
+    lookup = map_texel_bytes + (4 if span_records else 0)
+    eye_bytes = 16 * px + (0 if fused else lookup * stats["eye_hit_pixels"])
     return dict(shadow_pass=dict(ops=sh_ops, bytes=sh_bytes),
                 eye_pass=dict(ops=eye_ops + (sh_ops if fused else 0), bytes=eye_bytes))
 

@@ -87,6 +87,22 @@ class Context:
         abi.check(lib, lib.rtm_ctx_last_lanes(self._h, C.byref(n)), "rtm_ctx_last_lanes")
         return int(n.value)
 
+    def last_eye_blocks(self) -> bool:
+        """rtm_ctx_last_eye_blocks: the last eye launch ran 8 x 8-pixel blocks (else 64 x 1 rows)."""
+        n = C.c_int32()
+        lib = _lib()
+        abi.check(lib, lib.rtm_ctx_last_eye_blocks(self._h, C.byref(n)), "rtm_ctx_last_eye_blocks")
+        return bool(n.value)
+
+    def frames_plan(self, width: int, rows: int, n_frames: int):
+        """rtm_ctx_frames_plan: (lanes, frames per launch) render_frames_async picks for
+        n_frames frames of width x rows with distinct outputs on this context."""
+        ln, b = C.c_int32(), C.c_int32()
+        lib = _lib()
+        abi.check(lib, lib.rtm_ctx_frames_plan(self._h, width, rows, n_frames, C.byref(ln), C.byref(b)),
+                  "rtm_ctx_frames_plan")
+        return int(ln.value), int(b.value)
+
     def kernel_ms_history(self, n: int):
         """Per-render (shadow_pass_ms, eye_pass_ms) from HIP events, oldest first."""
         sm = (C.c_float * max(n, 1))()
@@ -171,6 +187,16 @@ class Context:
     def shadow_map_texel_bytes(self) -> int:
         """Bytes per texel of the last shadow pass's map: 8 (f64), 2 or 1 (coded)."""
         return int(_lib().rtm_ctx_shadow_map_texel_bytes(self._h))
+
+    def shadow_map_stored_bytes(self):
+        """rtm_ctx_shadow_map_stored_bytes: (bytes the last shadow pass stored -- span
+        records + the spans stored texel by texel for a 1-byte coded map, else the texel
+        bytes -- and whether the map carries span records)."""
+        n, sr = C.c_int64(), C.c_int32()
+        lib = _lib()
+        abi.check(lib, lib.rtm_ctx_shadow_map_stored_bytes(self._h, C.byref(n), C.byref(sr)),
+                  "rtm_ctx_shadow_map_stored_bytes")
+        return int(n.value), bool(sr.value)
 
     def stats(self, scene: Scene, eye: Camera, shadow: Camera, width: int, height: int, steps: int,
               flags: int = 0) -> dict:
@@ -350,6 +376,15 @@ class Group:
         abi.check(lib, lib.rtm_group_info(self._h, C.byref(n), C.byref(loc), C.byref(first)), "rtm_group_info")
         return int(n.value), int(loc.value), int(first.value)
 
+    def frames_plan(self, width: int, height: int, n_frames: int, root: int = 0):
+        """rtm_group_frames_plan: (frames per chunk, lanes of the root's member) that
+        render_frames_async uses for n_frames frames with distinct outputs."""
+        b, ln = C.c_int32(), C.c_int32()
+        lib = _lib()
+        abi.check(lib, lib.rtm_group_frames_plan(self._h, width, height, n_frames, root, C.byref(b), C.byref(ln)),
+                  "rtm_group_frames_plan")
+        return int(b.value), int(ln.value)
+
     def member_lanes(self, local: int = 0) -> int:
         """Lanes local member `local`'s context used for the last frame call."""
         lib = _lib()
@@ -426,21 +461,29 @@ class Group:
                                             flags, fmt, out.ctypes.data_as(C.c_void_p)), "rtm_group_render")
         return out
 
-    # close() bounds the wait for queued group work: past it the communicators are
-    # aborted (a peer that died with a transfer unmatched cannot hang interpreter exit)
-    CLOSE_TIMEOUT_MS = 120_000
+    # the garbage collector's and interpreter exit's bound on the wait for queued group work:
+    # past it the communicators are aborted (a peer that died with a transfer unmatched
+    # cannot hang interpreter exit)
+    DEL_TIMEOUT_MS = 120_000
 
-    def close(self, timeout_ms: int | None = None):
+    def close(self, timeout_ms: int = 0):
+        """Waits for the group's queued frames, then frees it.  timeout_ms <= 0 (default):
+        as long as they take; > 0: at most that long, then the communicators are aborted.
+        Raises RtmError when the wait failed or timed out (the group is freed all the same):
+        frames enqueued before close may then be incomplete."""
         if self._h:
             lib = _lib()
-            # errors here (an aborted group, a peer lost) only decide how destroy frees
-            lib.rtm_group_synchronize(self._h, self.CLOSE_TIMEOUT_MS if timeout_ms is None else timeout_ms)
+            rc = lib.rtm_group_synchronize(self._h, timeout_ms)
+            msg = lib.rtm_last_error() if rc != abi.RTM_OK else None
             lib.rtm_group_destroy(self._h)
             self._h = C.c_void_p()
+            if rc != abi.RTM_OK:
+                raise abi.RtmError(rc, "Group.close", (msg.decode() if msg else "") +
+                                   "; frames enqueued before close may be incomplete")
 
     def __del__(self):
         try:
-            self.close()
+            self.close(self.DEL_TIMEOUT_MS)
         except Exception:
             pass
 

@@ -88,10 +88,14 @@ def parse():
 FORMATS = {"rgba32f": 0, "rgba8": 1}
 
 
+WATCHDOG_EXIT = 3  # the status of a run whose secondary measurement stalled
+
+
 class _Watchdog:
     """Bounds a secondary measurement: if it has not finished after `seconds`, rank 0
-    prints the line it already holds (the secondary field marked as timed out) and
-    every rank leaves with status 0, so a stalled peer can never cost the headline."""
+    prints the line it already holds (the secondary field marked as timed out), and
+    every rank leaves with status WATCHDOG_EXIT: the headline line survives a stalled
+    peer, and the caller still sees that the run did not finish cleanly."""
 
     def __init__(self, seconds: float, res: dict | None, field: str):
         import threading
@@ -104,9 +108,10 @@ class _Watchdog:
         if res is not None:
             res[field] = {"error": f"watchdog: not finished after {seconds:.0f} s"}
             print(json.dumps(res), flush=True)
-        sys.stderr.write(f"bench.py: {field} watchdog fired after {seconds:.0f} s\n")
+        sys.stderr.write(f"bench.py: {field} watchdog fired after {seconds:.0f} s; exiting with status "
+                         f"{WATCHDOG_EXIT}\n")
         sys.stderr.flush()
-        os._exit(0)
+        os._exit(WATCHDOG_EXIT)
 
     def cancel(self):
         self._t.cancel()
@@ -174,10 +179,8 @@ def tile_gather(rtm, lib, ctx, group, world, rank, dist, tdev, c_scenes, eye, sh
         # frame_batch / lanes_plan), so frames that share a buffer render on one lane and
         # the root keeps its lanes (rtm_group.cpp chunks_clash_across_lanes: a ring of 32
         # at 512x512, 64 frames per chunk, would leave it one lane)
-        rows0 = shard.stripe_rows_of(H, world, 8, 0) if world > 1 else H
-        px0 = W * rows0
-        b0 = max(1, min(64 if px0 < (1 << 20) else 32, (64 << 20) // px0))
-        l0 = 3 if px0 >= (16 << 20) else 4
+        # (the library's own plan, rtm_group_frames_plan: VERDICT r05 ADVICE)
+        b0, l0 = group.frames_plan(W, H, max(steps, warmup, 1))
         n_out = b0 * l0 * -(-32 // (b0 * l0))
         outs = ([torch.empty(W * H * bpp, dtype=torch.uint8, device=dev) for _ in range(n_out)] if rank == 0
                 else [None] * n_out)
@@ -255,6 +258,11 @@ def tile_gather(rtm, lib, ctx, group, world, rank, dist, tdev, c_scenes, eye, sh
     stripe = group.partition if group is not None else 0
     extra = {"partition": (f"{stripe}-row cyclic stripes" if stripe > 0 and world > 1 else
                            f"contiguous bands of ceil(H/{world}) rows")}
+    if group is not None:
+        # the lanes the root's member actually used in the timed call, beside the plan the
+        # output ring was sized for (fewer: its frames clashed across lanes)
+        extra.update({"root_lanes_used": group.member_lanes(0), "root_lanes_planned": l0,
+                      "frames_per_chunk": b0, "output_ring": n_out})
     if bands:
         bt = band_times(rtm, lib, ctx, world, rank, dist, tdev, c_scenes[0], eye, shadow, W, H, K, flags, fmt,
                         stripe if group is not None else 0)
@@ -271,6 +279,27 @@ def tile_gather(rtm, lib, ctx, group, world, rank, dist, tdev, c_scenes, eye, sh
             "gather": gather,
             "shadow": ("fused: each band evaluates the shadow texels it reads" if world > 1 or flags & 4
                        else "two-pass (one band: the whole shadow map)"), **extra}
+
+
+def tile_scaling(tile: dict, res: dict, world: int) -> None:
+    """The assembled frame's strong-scaling figures, stated in the line itself (VERDICT r05
+    item 5): per format, `scaling_vs_n1` = the tile-gather frame rate over ONE GPU's fused
+    frame rate in the same run (alt_fused_shadow / N: every rank renders whole fused frames
+    there; without it the two-pass `value` / N), and `root_ingress_GBps` = the bytes the
+    root receives per frame over the time per frame.  The frames-mode `value` beside it is
+    the weak curve; these two read the strong one without DESIGN.md §7's model."""
+    alt = res.get("alt_fused_shadow") or {}
+    base, basis = (alt.get("value"), "alt_fused_shadow") if alt.get("value") else (res.get("value"), "value")
+    for name, t in tile.items():
+        if not isinstance(t, dict) or "value" not in t:
+            continue
+        if base:
+            t["scaling_vs_n1"] = round(t["value"] / (base / world), 6)
+            t["scaling_basis"] = (f"{name} tile-gather Mpix/s / ({basis} / {world}): the assembled frame's speed-up "
+                                  f"over one GPU's frame rate in this run ({'fused' if basis != 'value' else 'two-pass'})")
+        ms = t.get("ms_per_step")
+        if ms:
+            t["root_ingress_GBps"] = round(t["root_ingress_bytes_per_frame"] / (ms * 1e-3) / 1e9, 3)
 
 
 def make_group(rtm, world, rank, local, dist, backend):
@@ -532,12 +561,10 @@ def main():
     # multiple of frames-per-launch x lanes): 48 frames from 4 Mpixel up (the auto
     # batches of 2-8 frames on 2-3 lanes; 25 GB at 7680x4320, of 288 GB), 128 below
     # (batches of up to 64 frames on 2 lanes)
-    lanes_env = int(os.environ.get("RTM_LANES", "0") or 0)
     n_ring = 48 if W * H >= (4 << 20) else 128
-    # the library's auto rules (rtm_api.cpp frame_lanes / frame_batch), for overrides of one
-    lanes_auto = 3 if W * H >= (16 << 20) else 4
-    batch_auto = max(1, min(64 if W * H < (1 << 20) else 32, (64 << 20) // (W * H)))
-    m = (lanes_env if lanes_env > 0 else lanes_auto) * batch_auto
+    # the library's own plan for the timed call (rtm_ctx_frames_plan: its lanes and batch rules)
+    plan_lanes, plan_batch = ctx.frames_plan(W, H, max(nS, 1))
+    m = plan_lanes * plan_batch
     n_ring = n_ring if n_ring % m == 0 else m * ((n_ring + m - 1) // m)
     ring = ([torch.empty((H, W, 4), dtype=torch.float32, device=f"cuda:{local}") for _ in range(n_ring)]
             if not tile_mode else [])
@@ -586,6 +613,7 @@ def main():
         preroll["ms"], preroll["frames"] = round((time.perf_counter() - t_pre) * 1e3, 1), preroll_frames
         tg_primary = tile_gather(rtm, lib, ctx, group, world, rank, dist, tdev, c_scenes, eye, shadow, W, H, K,
                                  flags, fmt, nS, nW, bands=True)
+        tile_scaling({a.format: tg_primary}, {}, world)  # (root ingress; no one-GPU rate in this mode)
         elapsed = tg_primary["ms_per_step"] * nS / 1e3
     else:
         if sequence:
@@ -613,6 +641,8 @@ def main():
     # +INF texels on demand (rtm_api.cpp trivial_shadow), i.e. the fused frame's work
     trivial = (flags & 3) == 3 and not fused
     map_bytes = ctx.shadow_map_texel_bytes() or 8
+    # what the last timed frame's shadow pass stored (span records: DESIGN.md §5)
+    map_stored, span_records = ctx.shadow_map_stored_bytes() if not (fused or trivial) else (0, False)
     # per-kernel HIP-event durations over the timed region (ctx stream)
     n_launches = nS
     sh_ms, eye_ms = ctx.kernel_ms_history((n_launches + timing_stride - 1) // timing_stride)
@@ -715,6 +745,8 @@ def main():
                                       perspective=eye.type_ == sc.PERSPECTIVE,
                                       search=sep,
                                       n_sdfs=len(s0.sdfPrimitives), map_texel_bytes=map_bytes,
+                                      map_stored_bytes=map_stored if map_stored else None,
+                                      span_records=span_records,
                                       moving=(shadow.dirNormalized[0] * 0.03 != 0.0
                                               or shadow.dirNormalized[1] * 0.03 != 0.0))
 
@@ -789,6 +821,8 @@ def main():
             "roofline_other_kernel": roof_other,
             "roofline_frame": roof_frame,
             "shadow_map_texel_bytes": None if (fused or trivial) else map_bytes,
+            "shadow_map_stored_bytes_per_frame": None if (fused or trivial) else map_stored,
+            "shadow_map_span_records": None if (fused or trivial) else span_records,
             "lanes": lanes,
             "frames_per_launch": batch,
             "kernels_in_lanes": in_lanes,
@@ -836,9 +870,14 @@ def main():
                 break
         watchdog.cancel()
         if res is not None:
+            tile_scaling(tile, res, world)
             res["tile_gather"] = tile
     if group is not None:
-        group.close()
+        try:
+            group.close(120_000)  # (bounded: a stalled peer cannot hang the run's exit)
+        except Exception as ex:
+            if res is not None:
+                res["group_close_error"] = str(ex)[:300]
 
     if world > 1 and not a.no_host_output and a.config in (3, 4):
         # the N-link host frame: rank 0 drives all N devices while the others wait

@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define RTM_ABI_VERSION 10
+#define RTM_ABI_VERSION 11
 
 /* ---- limits: scene constants travel as kernel arguments (SGPR path) ---- */
 #define RTM_MAX_SPHERES 16
@@ -348,6 +348,22 @@ const double* rtm_ctx_shadow_map(rtm_ctx* ctx);
  * (the eye pass evaluates its +INF texels on demand; rtm_ctx_shadow_map still
  * returns the +INF map). */
 int32_t rtm_ctx_shadow_map_texel_bytes(rtm_ctx* ctx);
+/* ABI v11: bytes the last non-fused frame's shadow pass stored.  A 1-byte map written by
+ * the coded tile stores a span of 64 rows of a column whose march codes are one monotone
+ * run as a 4-byte record instead of 64 bytes (span records), so this is
+ * the span records plus the bytes of the spans stored texel by texel; other maps: their
+ * texel bytes.  *span_records (may be NULL): 1 when the map carries span records (an eye
+ * lookup then reads a record beside its byte).  Blocking (reads the records).  0 where
+ * rtm_ctx_shadow_map_texel_bytes is 0. */
+int rtm_ctx_shadow_map_stored_bytes(rtm_ctx* ctx, int64_t* bytes, int32_t* span_records);
+/* ABI v11: the plan rtm_render_frames_async makes for n_frames frames of width x rows with
+ * distinct outputs on this context (its rtm_ctx_set_lanes / rtm_ctx_set_batch, RTM_LANES):
+ * the lanes and the frames per launch.  Host only. */
+int rtm_ctx_frames_plan(rtm_ctx* ctx, int32_t width, int32_t rows, int32_t n_frames, int32_t* lanes,
+                        int32_t* frames_per_launch);
+/* ABI v11: the eye pass's wave shape in the last frame or batch this context launched:
+ * 0 = 64 x 1-pixel rows, 1 = 8 x 8-pixel blocks (small ray-traced frames). */
+int rtm_ctx_last_eye_blocks(rtm_ctx* ctx, int32_t* blocks);
 
 /* Counting variant of the frame (separate, untimed kernels): the per-pass
  * work counts behind the roofline's algorithmic flop count. */
@@ -439,6 +455,13 @@ int rtm_group_set_root_staging(rtm_group* g, int32_t on);
  * for the group's work first.  rtm_group_partition: the S in use. */
 int rtm_group_set_partition(rtm_group* g, int32_t stripe_rows);
 int32_t rtm_group_partition(rtm_group* g);
+/* ABI v11: the plan of rtm_group_render_frames_async for n_frames frames with distinct
+ * outputs: frames per chunk (one launch per pass per chunk on every member) and the lanes
+ * of the member that holds rank `root` (local member 0 if this process does not).  An
+ * output ring that is a multiple of chunk x lanes frames keeps the root on its lanes.
+ * Host only. */
+int rtm_group_frames_plan(rtm_group* g, int32_t width, int32_t height, int32_t n_frames, int32_t root,
+                          int32_t* frames_per_chunk, int32_t* lanes);
 /* ABI v9: part `part` of n_parts of the frame under stripe_rows-row cyclic stripes
  * (the rows a group rank renders), compact rows into out_dev (rtm_stripe_rows(...)
  * rows), on ctx's stream; rtm_stripe_rows: that row count (-1: bad arguments). */

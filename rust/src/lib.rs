@@ -261,3 +261,95 @@ impl Drop for FrameRing<'_> {
         }
     }
 }
+
+/// The north star's multi-GPU frame: N devices of this process
+/// joined by one RCCL communicator (rtm_group_create: ncclCommInitAll).  Each frame is
+/// tile-partitioned over the devices (8-row cyclic stripes by default), every device
+/// renders its part -- evaluating the shadow texels it reads, so the image is the same
+/// bits -- and ONE gather over xGMI assembles it on device 0, from where it is copied into
+/// the caller's host buffer.  It replaces the reference's per-frame render in its
+/// animation loop (main.rs:1469-1633).
+pub struct Group {
+    raw: *mut rtm_group,
+    /// bound on the wait in `Drop` before the communicators are aborted
+    pub drop_timeout_ms: i32,
+}
+
+impl Group {
+    /// A group over `devices` (empty: every device, 0..rtm_device_count()).
+    pub fn new(devices: &[i32]) -> Result<Group, Error> {
+        if unsafe { rtm_abi_version() } != RTM_ABI_VERSION {
+            return Err(Error { code: RTM_ERR_INVALID, message: "librtm ABI version mismatch".into() });
+        }
+        let n = if devices.is_empty() { unsafe { rtm_device_count() } } else { devices.len() as i32 };
+        let mut raw = std::ptr::null_mut();
+        check(unsafe { rtm_group_create(n, ptr_or_null(devices), &mut raw) })?;
+        Ok(Group { raw, drop_timeout_ms: 120_000 })
+    }
+
+    /// Devices (ranks) in the group.
+    pub fn len(&self) -> Result<i32, Error> {
+        let (mut n, mut local, mut first) = (0i32, 0i32, 0i32);
+        check(unsafe { rtm_group_info(self.raw, &mut n, &mut local, &mut first) })?;
+        Ok(n)
+    }
+
+    /// One frame of the animation as `format` pixels (RTM_FORMAT_RGBA32F: the reference's
+    /// Map2d<Color32> + alpha; RGBA8 / RGB8: writeColorImage's bytes), width*height pixels
+    /// in row order, in host memory.  Blocking: rtm_group_render.
+    pub fn render(&self, scene: &Scene, eye: &Camera, shadow: &Camera, width: i32, height: i32, march_steps: i32,
+                  flags: i32, format: i32) -> Result<Vec<u8>, Error> {
+        let mut out = Vec::new();
+        self.render_into(scene, eye, shadow, width, height, march_steps, flags, format, &mut out)?;
+        Ok(out)
+    }
+
+    /// `render` into a caller-owned buffer (resized to the frame), e.g. one registered once
+    /// with rtm_host_register for direct DMA and reused by every frame of the loop.
+    pub fn render_into(&self, scene: &Scene, eye: &Camera, shadow: &Camera, width: i32, height: i32,
+                       march_steps: i32, flags: i32, format: i32, out: &mut Vec<u8>) -> Result<(), Error> {
+        let bpp = unsafe { rtm_format_bytes(format) };
+        if bpp <= 0 || width <= 0 || height <= 0 {
+            return Err(Error { code: RTM_ERR_INVALID, message: "bad format or image size".into() });
+        }
+        out.resize(width as usize * height as usize * bpp as usize, 0);
+        let sc = scene.raw();
+        check(unsafe {
+            rtm_group_render(self.raw, &sc, eye, shadow, width, height, march_steps, flags, format,
+                             out.as_mut_ptr() as *mut c_void)
+        })
+    }
+
+    /// true: every device copies its part straight into its rows of the host frame (N PCIe
+    /// links, no gather); false: gather on device 0, then one copy (the default).
+    pub fn set_host_direct(&self, on: bool) -> Result<(), Error> {
+        check(unsafe { rtm_group_set_host_direct(self.raw, on as i32) })
+    }
+
+    /// The partition: stripe_rows > 0 cyclic stripes of that many rows, 0 contiguous
+    /// bands of ceil(H/N) rows, -1 the default (8-row stripes).
+    pub fn set_partition(&self, stripe_rows: i32) -> Result<(), Error> {
+        check(unsafe { rtm_group_set_partition(self.raw, stripe_rows) })
+    }
+
+    /// Wait for every device's work; timeout_ms > 0 bounds the wait (RTM_ERR_COMM past it,
+    /// with the communicators aborted).
+    pub fn synchronize(&self, timeout_ms: i32) -> Result<(), Error> {
+        check(unsafe { rtm_group_synchronize(self.raw, timeout_ms) })
+    }
+
+    pub fn raw(&self) -> *mut rtm_group {
+        self.raw
+    }
+}
+
+impl Drop for Group {
+    fn drop(&mut self) {
+        // a bounded wait first: a lost device cannot hang the drop (rtm_group_destroy then
+        // aborts the communicators instead of waiting on them)
+        unsafe {
+            let _ = rtm_group_synchronize(self.raw, self.drop_timeout_ms);
+            rtm_group_destroy(self.raw)
+        }
+    }
+}

@@ -1,4 +1,4 @@
-//! Raw bindings of `include/rtm.h` (librtm.so, RTM_ABI_VERSION 10) for the
+//! Raw bindings of `include/rtm.h` (librtm.so, RTM_ABI_VERSION 11) for the
 //! PtrMan/2018RustRayTracer crate.  Every function and struct of the header is
 //! bound here, in header order; `tests/test_rust_ffi.py` parses this file and the
 //! header and fails on any drift (names, argument counts and C types, return types,
@@ -9,7 +9,7 @@
 
 use std::os::raw::{c_char, c_void};
 
-pub const RTM_ABI_VERSION: i32 = 10;
+pub const RTM_ABI_VERSION: i32 = 11;
 
 // limits: scene constants travel as kernel arguments
 pub const RTM_MAX_SPHERES: i32 = 16;
@@ -215,6 +215,10 @@ extern "C" {
                                    march_steps: i32, flags: i32, out_rgba_dev: *const *mut f32) -> i32;
     pub fn rtm_ctx_shadow_map(ctx: *mut rtm_ctx) -> *const f64;
     pub fn rtm_ctx_shadow_map_texel_bytes(ctx: *mut rtm_ctx) -> i32;
+    pub fn rtm_ctx_shadow_map_stored_bytes(ctx: *mut rtm_ctx, bytes: *mut i64, span_records: *mut i32) -> i32;
+    pub fn rtm_ctx_frames_plan(ctx: *mut rtm_ctx, width: i32, rows: i32, n_frames: i32, lanes: *mut i32,
+                               frames_per_launch: *mut i32) -> i32;
+    pub fn rtm_ctx_last_eye_blocks(ctx: *mut rtm_ctx, blocks: *mut i32) -> i32;
     pub fn rtm_render_stats(ctx: *mut rtm_ctx, scene: *const rtm_scene, eye: *const rtm_camera,
                             shadow: *const rtm_camera, width: i32, height: i32, march_steps: i32, flags: i32,
                             out: *mut rtm_stats) -> i32;
@@ -242,6 +246,8 @@ extern "C" {
     pub fn rtm_group_set_root_staging(g: *mut rtm_group, on: i32) -> i32;
     pub fn rtm_group_set_partition(g: *mut rtm_group, stripe_rows: i32) -> i32;
     pub fn rtm_group_partition(g: *mut rtm_group) -> i32;
+    pub fn rtm_group_frames_plan(g: *mut rtm_group, width: i32, height: i32, n_frames: i32, root: i32,
+                                 frames_per_chunk: *mut i32, lanes: *mut i32) -> i32;
     pub fn rtm_render_stripes_async(ctx: *mut rtm_ctx, scene: *const rtm_scene, eye: *const rtm_camera,
                                     shadow: *const rtm_camera, width: i32, height: i32, march_steps: i32,
                                     flags: i32, format: i32, stripe_rows: i32, n_parts: i32, part: i32,

@@ -63,3 +63,16 @@ def first_mismatch(a, b):
         return None
     i = tuple(idx[0])
     return f"{len(idx)} mismatches, first at {i}: got {a[i]!r} want {b[i]!r}"
+
+
+def device_smap(ctx, w, h):
+    """The context's last shadow map as f64 values (rtm_ctx_shadow_map: decoded from the
+    coded map on the device), copied to the host."""
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so")
+    hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    m = np.empty((h, w), np.float64)
+    p = ctx.shadow_map_ptr()
+    assert p, "no shadow map"
+    assert hip.hipMemcpy(m.ctypes.data, p, w * h * 8, 2) == 0
+    return m

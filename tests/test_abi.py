@@ -119,3 +119,18 @@ def test_product_package_does_not_import_oracle():
                     assert bad not in txt, (f, bad)
     so = open(os.path.join(pkg, "librtm.so"), "rb").read()
     assert b"rtmo_" not in so and b"librtm_oracle" not in so
+
+
+def test_package_ships_only_the_product_library():
+    """The product package holds one shared library, librtm.so:
+    A/B variants and the bounds demos' revert builds go to build/ (tools/ab_lib.sh,
+    tools/bounds_demo.sh), and the product source defines no A/B switch."""
+    pkg = os.path.join(ROOT, "2018rustraytracer_amd")
+    libs = sorted(f for f in os.listdir(pkg) if f.endswith(".so"))
+    assert libs == ["librtm.so"], libs
+    csrc = os.path.join(pkg, "csrc")
+    for f in os.listdir(csrc):
+        if f.endswith((".hip", ".cpp", ".h")):
+            assert "RTM_AB_" not in open(os.path.join(csrc, f)).read(), f
+    for tool in ("ab_lib.sh", "bounds_demo.sh"):
+        assert "build/" in open(os.path.join(ROOT, "tools", tool)).read(), tool

@@ -125,18 +125,44 @@ def test_bench_frames_gloo_rehearsal_world2_carries_tile_gather():
     assert F >= 8 and res["value"] == pytest.approx(2 * F * 1920 * 1080 / (res["ms_per_step"] * 1e-3) / 1e6, rel=1e-2)
     assert set(res["tile_gather"]) == {"rgba32f", "rgba8"}
     assert all(v["value"] > 0 for v in res["tile_gather"].values())
+    # the strong curve in the line itself: speed-up over one GPU's frame rate, root ingress
+    for name, v in res["tile_gather"].items():
+        assert v["scaling_vs_n1"] == pytest.approx(v["value"] / (res["value"] / 2), rel=1e-3)
+        assert v["root_ingress_GBps"] == pytest.approx(v["root_ingress_bytes_per_frame"] / v["ms_per_step"] / 1e6,
+                                                       rel=1e-3)
 
 
-def test_bench_watchdog_prints_the_line_and_exits_cleanly():
+def test_tile_scaling_fields():
+    """bench.tile_scaling: the tile-gather figures against one GPU's rate of the same
+    run (alt_fused_shadow when measured, else the two-pass value), per format."""
+    import sys
+    sys.path.insert(0, ROOT)
+    import bench
+    tile = {"rgba32f": {"value": 1000.0, "ms_per_step": 2.0, "root_ingress_bytes_per_frame": 4_000_000},
+            "rgba8": {"error": "x"}}
+    bench.tile_scaling(tile, {"value": 3000.0, "alt_fused_shadow": {"value": 4000.0}}, 8)
+    t = tile["rgba32f"]
+    assert t["scaling_vs_n1"] == 2.0 and "alt_fused_shadow" in t["scaling_basis"]
+    assert t["root_ingress_GBps"] == 2.0 and "scaling_vs_n1" not in tile["rgba8"]
+    tile = {"rgba8": {"value": 600.0, "ms_per_step": 1.0, "root_ingress_bytes_per_frame": 0}}
+    bench.tile_scaling(tile, {"value": 300.0, "alt_fused_shadow": None}, 2)
+    assert tile["rgba8"]["scaling_vs_n1"] == 4.0 and tile["rgba8"]["root_ingress_GBps"] == 0.0
+
+
+def test_bench_watchdog_prints_the_line_and_exits_nonzero():
     """bench.py's secondary-measurement watchdog: when it fires, rank 0 prints the
-    line it holds (the secondary field marked) and the process exits with status 0."""
+    line it holds (the secondary field marked), exactly once, and the process exits with
+    a non-zero status (bench.WATCHDOG_EXIT): a stalled run never reads as a clean one."""
     import json
     import subprocess
     import sys
     code = ("import sys, time; sys.path.insert(0, %r); import bench; "
             "bench._Watchdog(0.2, {'value': 1.0, 'tile_gather': None}, 'tile_gather'); time.sleep(30)" % ROOT)
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60)
-    assert r.returncode == 0, r.stderr
+    sys.path.insert(0, ROOT)
+    import bench
+    assert r.returncode == bench.WATCHDOG_EXIT != 0, (r.returncode, r.stderr)
+    assert "watchdog fired" in r.stderr
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1
     d = json.loads(lines[0])

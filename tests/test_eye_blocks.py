@@ -10,7 +10,7 @@ import os
 import numpy as np
 import pytest
 
-from conftest import bits_equal, first_mismatch
+from conftest import bits_equal, device_smap, first_mismatch
 from test_bounds import oob
 
 pytestmark = pytest.mark.gpu
@@ -57,6 +57,8 @@ def test_block_mode_ray_traced_batches(rtm, oracle, scenes, gpu_ctx, w, h):
     finally:
         gpu_ctx.set_lanes(0)
         gpu_ctx.set_batch(0)
+    # the batch really ran the 8 x 8 kernels (rtm_ctx_last_eye_blocks), not the 64 x 1 rows
+    assert gpu_ctx.last_eye_blocks()
     assert oob(rtm, gpu_ctx) == 0
     for i, (s, o) in enumerate(zip(frames, outs)):
         want = oracle.render(s, eye, sh, w, h, 0, scenes.RAYTRACING_FLAGS, nthreads=NT)["rgba"]
@@ -80,8 +82,41 @@ def test_block_mode_sdf_batches(rtm, oracle, scenes, gpu_ctx, w, h):
     finally:
         gpu_ctx.set_lanes(0)
         gpu_ctx.set_batch(0)
+    assert gpu_ctx.last_eye_blocks()
     assert oob(rtm, gpu_ctx) == 0
     for i, (s, o) in enumerate(zip(frames, outs)):
         want = oracle.render(s, eye, sh, w, h, 0, scenes.RAYTRACING_FLAGS, nthreads=NT)["rgba"]
         got = o.cpu().numpy()
         assert bits_equal(got, want), f"frame {i}: {first_mismatch(got, want)}"
+
+
+@pytest.mark.parametrize("w,h", [(200, 136), (136, 200)])
+def test_block_mode_shadowed_sdf_batches(rtm, oracle, scenes, gpu_ctx, w, h):
+    """Shadowed, non-fused SDF batches (flags 0, march steps > 0: the materialised coded
+    map, decoded by the SDF block kernel's lookups) at sizes with partial blocks and
+    workgroups: the SDF beside Scene A-bench's spheres and patch, under the
+    orthographic eye, with the sun's map; every frame and the last map == the oracle."""
+    import torch
+    eye, sh = scenes.eye_camera(), scenes.shadow_camera()
+    frames = [scenes.mixed_sdf(100 + 7 * i) for i in range(4)]
+    k = 64
+    outs = [torch.empty((h, w, 4), dtype=torch.float32, device="cuda") for _ in frames]
+    assert oob(rtm, gpu_ctx) >= 0
+    try:
+        gpu_ctx.set_batch(len(frames))
+        gpu_ctx.set_lanes(1)
+        torch.cuda.synchronize()
+        gpu_ctx.render_frames_async(frames, eye, sh, w, h, k, 0, [o.data_ptr() for o in outs])
+        gpu_ctx.synchronize()
+    finally:
+        gpu_ctx.set_lanes(0)
+        gpu_ctx.set_batch(0)
+    assert gpu_ctx.last_batch() == len(frames) and gpu_ctx.last_eye_blocks()
+    assert gpu_ctx.shadow_map_texel_bytes() == 1
+    assert oob(rtm, gpu_ctx) == 0
+    for i, (s, o) in enumerate(zip(frames, outs)):
+        want = oracle.render(s, eye, sh, w, h, k, 0, nthreads=NT, want_shadow=i == len(frames) - 1)
+        got = o.cpu().numpy()
+        assert bits_equal(got, want["rgba"]), f"frame {i}: {first_mismatch(got, want['rgba'])}"
+    m = device_smap(gpu_ctx, w, h)
+    assert bits_equal(m, want["shadow"]), first_mismatch(m, want["shadow"])

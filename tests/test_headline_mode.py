@@ -7,7 +7,12 @@ with their own shadow maps) x 8 frames per launch (batched kernels, one pulled
 frame table per launch) and the 1-byte coded shadow map.  These tests run that
 same call shape and compare every frame, and the last frame's shadow map,
 with oracle.render bit for bit -- not with the library's own single-frame path.
-The 8K configs (4, 5) run on 3 lanes x 2 frames per launch.
+The 8K configs (4, 5) run on 3 lanes x 2 frames per launch.  Configs 2, 6, 7 and 8
+run their bench shapes too: 1920x1080 at 4 lanes x 32 frames per
+launch, main()'s own scene (raytracingPlane0, config 7) at 512x512 in the 8 x 8-block
+eye kernel at 4 lanes x 64 frames per launch, and rows f-1 / f-4 at 3840x2160 (configs
+6 and 8) at 4 lanes x 8 -- every frame against oracle.render, with no out-of-range
+side-table read.
 """
 import os
 
@@ -15,6 +20,7 @@ import numpy as np
 import pytest
 
 from conftest import bits_equal, first_mismatch
+from test_bounds import oob
 
 pytestmark = pytest.mark.gpu
 
@@ -32,7 +38,7 @@ def _smap(ctx, w, h):
     return m
 
 
-def _sequence_vs_oracle(rtm, oracle, scenes, frames, w, h, k, lanes, batch, map_bytes):
+def _sequence_vs_oracle(rtm, oracle, scenes, frames, w, h, k, lanes, batch, map_bytes, compressed=True):
     """Render `frames` in one auto-ruled sequence call on a fresh context and
     compare every frame and the last shadow map with the oracle."""
     import torch
@@ -46,6 +52,12 @@ def _sequence_vs_oracle(rtm, oracle, scenes, frames, w, h, k, lanes, batch, map_
         assert ctx.last_lanes() == lanes, ctx.last_lanes()
         assert ctx.last_batch() == batch, ctx.last_batch()
         assert ctx.shadow_map_texel_bytes() == map_bytes
+        # the coded tile's 1-byte map carries span records; every span of a
+        # sphere-free 64-row column run stored as its record makes the map far smaller
+        stored, spans = ctx.shadow_map_stored_bytes()
+        assert spans == (map_bytes == 1)
+        if spans and compressed:
+            assert 0 < stored < w * h, (stored, w * h)
         for i, (s, o) in enumerate(zip(frames, outs)):
             want = oracle.render(s, eye, sh, w, h, k, 0, nthreads=NT,
                                  want_shadow=(i == len(frames) - 1))
@@ -76,8 +88,10 @@ def test_8k_sequence_three_lanes_batched(rtm, oracle, scenes, cfg):
         frames = [scenes.scene_a_bench(100 + 3 * i) for i in range(6)]
     else:
         frames = [c["scene"]() for _ in range(6)]
+    # (config 5's 16 spheres cover more than the split launch's bound: one launch, every
+    # span stored texel by texel)
     _sequence_vs_oracle(rtm, oracle, scenes, frames, c["width"], c["height"], c["steps"], lanes=3, batch=2,
-                        map_bytes=1)
+                        map_bytes=1, compressed=cfg == 4)
 
 
 def test_batched_mixed_sphere_counts_pick_the_widest_code(rtm, oracle, scenes):
@@ -115,3 +129,58 @@ def test_batched_mixed_sphere_counts_pick_the_widest_code(rtm, oracle, scenes):
             assert bits_equal(o.cpu().numpy(), oracle.render(s, eye, sh, w, h, k, 0, nthreads=NT)["rgba"])
     finally:
         ctx.close()
+
+
+def _bench_shape_vs_oracle(rtm, oracle, scenes, cfg, frames, lanes, batch, blocks, static):
+    """bench.py's call for config `cfg`: one rtm_render_frames_async over `frames` with
+    the auto rules on a fresh context, its flags and cameras; asserts the plan (lanes,
+    frames per launch, the eye kernel's wave shape) and compares every frame with
+    oracle.render (a static scene: one oracle frame for all)."""
+    import torch
+    c = scenes.CONFIGS[cfg]
+    w, h, k, fl = c["width"], c["height"], c["steps"], c["flags"]
+    eye = c.get("eye", scenes.eye_camera)()
+    sh = c.get("shadow", scenes.shadow_camera)()
+    ctx = rtm.Context(0)
+    outs = [torch.empty((h, w, 4), dtype=torch.float32, device="cuda") for _ in frames]
+    try:
+        assert ctx.frames_plan(w, h, len(frames)) == (lanes, batch)
+        assert oob(rtm, ctx) >= 0  # clear
+        torch.cuda.synchronize()
+        ctx.render_frames_async(frames, eye, sh, w, h, k, fl, [o.data_ptr() for o in outs])
+        ctx.synchronize()
+        assert (ctx.last_lanes(), ctx.last_batch(), ctx.last_eye_blocks()) == (lanes, batch, blocks)
+        assert oob(rtm, ctx) == 0
+        want = oracle.render(frames[0], eye, sh, w, h, k, fl, nthreads=NT)["rgba"] if static else None
+        for i, (s, o) in enumerate(zip(frames, outs)):
+            if not static:
+                want = oracle.render(s, eye, sh, w, h, k, fl, nthreads=NT)["rgba"]
+            got = o.cpu().numpy()
+            assert bits_equal(got, want), (i, first_mismatch(got, want))
+    finally:
+        del outs
+        ctx.close()
+        torch.cuda.empty_cache()
+
+
+def test_config2_bench_shape(rtm, oracle, scenes):
+    """Config 2 as timed: 1920x1080, K = 32, 4 lanes x 32 frames per launch; 128
+    animation frames = one batch per lane."""
+    frames = [scenes.scene_a_bench(100 + i) for i in range(128)]
+    _bench_shape_vs_oracle(rtm, oracle, scenes, 2, frames, lanes=4, batch=32, blocks=False, static=False)
+
+
+def test_config7_main_scene_bench_shape(rtm, oracle, scenes):
+    """Config 7, main()'s own frame (testscene_raytracingPlane0, main.rs:910-1046) as
+    benched: 512x512, flags 3 (no shadow pass), the 8 x 8-block eye kernel, 4 lanes x 64
+    frames per launch (256 frames)."""
+    frames = [scenes.raytracing_plane0() for _ in range(256)]
+    _bench_shape_vs_oracle(rtm, oracle, scenes, 7, frames, lanes=4, batch=64, blocks=True, static=True)
+
+
+@pytest.mark.parametrize("cfg,blocks", [(6, False), (8, True)])
+def test_config6_config8_bench_shape(rtm, oracle, scenes, cfg, blocks):
+    """Rows f-1 (config 6, R-bench: 64 x 1-row waves at 4K) and f-4 (config 8,
+    S-bench: the SDF kernel's 8 x 8 blocks) at their bench batch: 4 lanes x 8 frames."""
+    frames = [scenes.CONFIGS[cfg]["scene"]() for _ in range(32)]
+    _bench_shape_vs_oracle(rtm, oracle, scenes, cfg, frames, lanes=4, batch=8, blocks=blocks, static=True)

@@ -259,3 +259,22 @@ def test_safe_layer_is_the_reference_surface():
     for m in ("ctx.viewport(", ".rasterize(&scene)", ".process_raymarching_rays(", "render_color_image(&scene",
               "ctx.render(&scene"):
         assert m in ex, m
+    # the north star's multi-GPU frame: Group over rtm_group_*, its
+    # Drop bounding the wait before the communicators are destroyed
+    group = {"pub fn new(": "rtm_group_create(", "pub fn render_into(": "rtm_group_render(",
+             "pub fn set_host_direct(": "rtm_group_set_host_direct(",
+             "pub fn set_partition(": "rtm_group_set_partition(", "pub fn synchronize(": "rtm_group_synchronize("}
+    g0 = lib.find("impl Group {")
+    assert g0 >= 0 and "pub struct Group" in lib
+    for method, call in group.items():
+        i = lib.find(method, g0)
+        assert i >= 0, method
+        assert call in lib[i:lib.find("\n    }", i)], (method, call)
+    i = lib.find("pub fn render(", g0)
+    assert "-> Result<Vec<u8>, Error>" in lib[i:i + 300] and "self.render_into(" in lib[i:lib.find("\n    }", i)]
+    d = lib[lib.find("impl Drop for Group"):]
+    d = d[:d.find("\n}")]
+    assert d.find("rtm_group_synchronize(self.raw, self.drop_timeout_ms)") < d.find("rtm_group_destroy(self.raw)")
+    ex = open(os.path.join(ROOT, "rust/examples/closely_orbiting_group.rs")).read()
+    for m in ("Group::new(", "group.render_into(&scene", "RTM_FORMAT_RGB8", "for frame in 0..300"):
+        assert m in ex, m
