@@ -1137,8 +1137,8 @@ int enqueue_frame(rtm_ctx* ctx, FrameArgs& a, const FrameExtra* x, void* out_dev
     if (!fused) {
         // the map's storage: coded (1-2 B per texel) unless counting (f64)
         a.sh.smap_fmt = stats ? SMAP_F64 : shadow_map_format(a.sh);
-        a.sh.smap_bw = (a.sh.W + 127) / 128;
-        a.sh.smap_spans = stats ? 0 : shadow_map_spans(a.sh);
+        a.sh.smap_bw = (int16_t)((a.sh.W + 127) / 128);
+        a.sh.smap_spans = (int16_t)(stats ? 0 : shadow_map_spans(a.sh));
         DevBuf& sb = l ? l->smap : ctx->smap;
         if ((rc = sb.ensure((size_t)smap_bytes(a.sh.smap_fmt, a.sh.W, a.sh.H, a.sh.smap_spans), ctx->device)))
             return rc;
@@ -1284,8 +1284,8 @@ int enqueue_batch(rtm_ctx* ctx, int lane, FrameArgs* fa, const FrameExtra* const
     const int32_t spans = fused ? 0 : shadow_map_spans(fa[0].sh);
     for (int k = 0; k < n; ++k) {
         fa[k].sh.smap_fmt = sfmt;
-        fa[k].sh.smap_bw = (fa[k].sh.W + 127) / 128;
-        fa[k].sh.smap_spans = spans;
+        fa[k].sh.smap_bw = (int16_t)((fa[k].sh.W + 127) / 128);
+        fa[k].sh.smap_spans = (int16_t)spans;
     }
     const size_t map_bytes = ((size_t)smap_bytes(sfmt, fa[0].sh.W, fa[0].sh.H, spans) + 255) & ~(size_t)255;
     if (!fused && (rc = br.smaps.ensure(map_bytes * (size_t)n, ctx->device))) return rc;

@@ -128,9 +128,9 @@ struct ShadowPart {
     int32_t steps, flags;
     int32_t cull_x0, cull_x1, cull_y0, cull_y1;  // union of the spheres' pixel ranges (see EyePart)
     int32_t smap_fmt;  // SMAP_F64 / SMAP_U8 / SMAP_U16: how the shadow pass stores the map (shadow_map_format)
-    int32_t smap_bw;   // coded maps: blocks per block row, ceil(W / 128)
-    int32_t smap_spans;  // 1: the U8 map carries span records after its codes (shadow_map_spans)
-    int32_t pad_;
+    // (two 16-bit fields: FrameArgs must not grow, see the kernarg check below)
+    int16_t smap_bw;     // coded maps: blocks per block row, ceil(W / 128) <= 256
+    int16_t smap_spans;  // 1: the U8 map carries span records after its codes (shadow_map_spans)
 };
 
 // The shadow map's storage.  Every texel's value is one of +INF, a sphere's
@@ -300,6 +300,12 @@ struct DevTabs {
     uint32_t* rtmask;
     int32_t rt_persp, rtmask_words;
 };
+// eye_pass_kernel's explicit arguments (FrameArgs, smap, out, stats, DevTabs) share the
+// 4 KiB kernarg segment: past it the launch reads arguments the runtime never copied
+// (round 6: ShadowPart grew by 8 bytes and the single-frame eye pass read a stale tail of
+// DevTabs -- an illegal memory access in the RGB8 stripes test)
+static_assert(sizeof(FrameArgs) + 3 * sizeof(void*) + sizeof(DevTabs) <= 4096,
+              "eye_pass_kernel's explicit kernel arguments must fit the 4 KiB kernarg segment");
 constexpr int32_t FMT_MASK = 0xff;
 constexpr int32_t FMT_RGB8_DWORDS = 0x100;
 

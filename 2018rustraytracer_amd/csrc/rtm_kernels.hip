@@ -1416,9 +1416,10 @@ __device__ __forceinline__ void shadow_tile_coded(const ShadowPart& a, void* __r
     // wave-uniform: bit r = row yw + r marches (inRange01 and < H)
     const uint64_t rowbits_w = __ballot((lane < SPAN) & (rl.ok != 0));
     // bit st: strip st of the wave is the raster part's (strip_rasters; wave-uniform)
-    uint32_t boxbits = 0u;
+    // (a PART 2 workgroup runs only when its strip rasterizes: shadow_coded_block tested it)
+    uint32_t boxbits = PART == 2 ? 1u : 0u;
 #pragma unroll
-    for (int st = 0; st < NS; ++st) {
+    for (int st = 0; st < NS && PART != 2; ++st) {
         const int s0 = (yw + NR * st) & ~(CODED_ROWS - 1);
         if (s0 < H && strip_rasters(a, xb, s0)) boxbits |= 1u << st;
     }
@@ -2001,7 +2002,10 @@ __device__ __forceinline__ const T* const_table(const T* p) {
 // BLK: the waves are 8 x 8 pixel blocks (workgroup bx: 4 blocks side by side, block row
 // by: 8 rows), for the batched RT 3 frames without shadows and without stripes: a compact
 // primitive touches fewer blocks than 64 x 1 rows, and a block's cone is narrower.
-template <bool FUSED, bool COUNT, int RT, int FMT = RTM_FORMAT_RGBA32F, bool NOSH = false, bool BLK = false>
+// WIDE: the workgroup's 4 waves side by side in one row (256 x 1 pixels: 4 KB of RGBA f32
+// stored contiguously per workgroup) instead of stacked (64 x 4).
+template <bool FUSED, bool COUNT, int RT, int FMT = RTM_FORMAT_RGBA32F, bool NOSH = false, bool BLK = false,
+          bool WIDE = false>
 __device__ __forceinline__ void eye_tile(const EyePart& a, const ShadowPart& sh, const double* __restrict__ smap,
                                          void* __restrict__ out, int bx, int by, StatsK* __restrict__ st,
                                          const DevTabs tabs, bool KMB = false, uint32_t kmw = 0u,
@@ -2018,10 +2022,11 @@ __device__ __forceinline__ void eye_tile(const EyePart& a, const ShadowPart& sh,
     const SdfTabK* __restrict__ sdf = const_table(tabs.sdf);
     // the workgroup's 4 waves stacked (64 x 4 pixels)
     const int wv_ = (int)(threadIdx.x >> 6), ln_ = (int)(threadIdx.x & (TILE_X - 1));
-    const int xb = __builtin_amdgcn_readfirstlane(BLK ? bx * 32 + wv_ * 8 : bx * TILE_X);
+    static_assert(!WIDE || (!BLK && RT == 0), "256 x 1 workgroups: the sphere-only tile");
+    const int xb = __builtin_amdgcn_readfirstlane(BLK ? bx * 32 + wv_ * 8 : WIDE ? (bx * TILE_Y + wv_) * TILE_X : bx * TILE_X);
     const int xi = xb + (BLK ? (ln_ & 7) : ln_);
     // (BLK: the lane's own row; else the wave's)
-    const int yl = BLK ? by * 8 + (ln_ >> 3) : __builtin_amdgcn_readfirstlane(by * TILE_Y + wv_);
+    const int yl = BLK ? by * 8 + (ln_ >> 3) : __builtin_amdgcn_readfirstlane(WIDE ? by : by * TILE_Y + wv_);
     const int yl0 = BLK ? __builtin_amdgcn_readfirstlane(by * 8) : yl;  // the wave's first row
     // the header fields the prologue needs, read before any branch so their scalar loads
     // issue as one group: one wait instead of a chain of dependent round trips (the
@@ -2369,9 +2374,11 @@ constexpr int eye_batch_tiles = RT == 3 && NOSH ? 4 : 1;
 // block rows per workgroup in the 8 x 8 mode, one after another: config 7 294 -> 317
 // Gpix/s against one (2: no gain; profiles/r05_ab_eye_blocks.txt)
 constexpr int EYE_BLK_NT = 4;
+// the sphere-only batched eye pass (RT 0, RGBA f32: the headline's) in 256 x 1 workgroups
+constexpr bool EYE_WIDE_RT0 = false;
 template <bool FUSED, int RT, bool NOSH>
 constexpr int eye_batch_wpe = RT == 3 && NOSH ? 8 : RT == 0 && !FUSED ? 8 : 1;
-template <bool FUSED, int RT, int FMT, bool NOSH = false, bool BLK = false>
+template <bool FUSED, int RT, int FMT, bool NOSH = false, bool BLK = false, bool WIDE = false>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(eye_batch_wpe<FUSED, RT, NOSH>, 8))) void eye_batch_kernel(
     CBatch* __restrict__ fr, const uint32_t* __restrict__ km, int km_nw, int km_gx) {
     if (BLK) {
@@ -2408,8 +2415,8 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(eye_batch
             widx = __builtin_amdgcn_readfirstlane((by * TILE_Y + (int)(threadIdx.x >> 6)) * km_gx + (int)blockIdx.x);
             kmw = ((const __attribute__((address_space(4))) uint32_t*)km)[(size_t)blockIdx.z * km_nw + min(widx, km_nw - 1)];
         }
-        eye_tile<FUSED, false, RT, FMT, NOSH>(*(const EyePart*)&f->a.ey, *(const ShadowPart*)&f->a.sh, f->smap, f->out,
-                                        blockIdx.x, by, nullptr, tabs, true, kmw, widx < km_nw);
+        eye_tile<FUSED, false, RT, FMT, NOSH, false, WIDE>(*(const EyePart*)&f->a.ey, *(const ShadowPart*)&f->a.sh, f->smap,
+                                                           f->out, blockIdx.x, by, nullptr, tabs, true, kmw, widx < km_nw);
     }
 }
 
@@ -2824,8 +2831,12 @@ static void launch_eye_fmt(const FrameArgs& a, const double* smap, void* o, hipS
 #define RTM_EYE(F, R, N)                                                                                           \
     do {                                                                                                        \
         constexpr bool B_ = R == 3 && N && FMT == RTM_FORMAT_RGBA32F;                                           \
+        constexpr bool W_ = EYE_WIDE_RT0 && R == 0 && FMT == RTM_FORMAT_RGBA32F;                                \
         if (fr && B_ && blk)                                                                                    \
             hipLaunchKernelGGL((eye_batch_kernel<F, R, FMT, N, B_>), gblk, dim3(BLOCK), 0, s, fr, km.p, km.nw, gx8); \
+        else if (fr && W_)                                                                                      \
+            hipLaunchKernelGGL((eye_batch_kernel<F, R, FMT, N, false, W_>), dim3((g.x + 3) / 4, (unsigned)rows_, g.z), \
+                               dim3(BLOCK), 0, s, fr, km.p, km.nw, km.gx);                                     \
         else if (fr) hipLaunchKernelGGL((eye_batch_kernel<F, R, FMT, N>), dim3(g.x, (g.y + eye_batch_tiles<R, N> - 1) / eye_batch_tiles<R, N>, g.z), \
                                    dim3(BLOCK), 0, s, fr, km.p, km.nw, km.gx);                                     \
         else hipLaunchKernelGGL((eye_pass_kernel<F, false, R, FMT, N>), g, dim3(BLOCK), 0, s, a, smap, o, nullptr, tabs); \
