@@ -100,3 +100,46 @@ def test_capsule_cull_keeps_degenerate_and_non_finite():
     assert not capsule_test(mid / np.linalg.norm(mid), math.cos(0.05), math.sin(0.05), t)
     side = np.array([math.sin(math.radians(10)), 0.0, math.cos(math.radians(10))])
     assert capsule_test(side, math.cos(0.05), math.sin(0.05), t)
+
+
+def _strip_rasters_disc(nx, ny, xb, xe, s0, ye, cx, cy, r):
+    """rtm_kernels.hip strip_rasters' disc test (its pixel-range test aside): False = no
+    texel of the strip's NDC rectangle can be covered."""
+    X0, X1, Y0, Y1 = nx[xb], nx[xe], ny[s0], ny[ye]
+    dx = cx - np.fmin(np.fmax(cx, X0), X1)
+    dy = cy - np.fmin(np.fmax(cy, Y0), Y1)
+    return not (dx * dx + dy * dy > (r * r) * (1.0 + 1e-6))
+
+
+def test_strip_split_disc_test_is_conservative():
+    """The split shadow launch gives a 128 x 16 strip to the raster-free part only when
+    strip_rasters says no sphere covers a texel of it (round 6: per sphere disc, not the
+    union box).  Against the kernels' own coverage -- pa = ((x - cx) * n) / m with n =
+    r * (1/m), m = sqrt(r*r + 0*0), covered iff sqrt(pa^2 + pb^2) < 1 -- on random spheres
+    (both signs of r, tiny and large, centres off the map) and map sizes: no rejected strip
+    holds a covered texel, and the test rejects most strips the spheres do not reach."""
+    rng = np.random.default_rng(0x5EED)
+    rejected = reachable_rejects = 0
+    for _ in range(60):
+        W, H = int(rng.integers(130, 900)), int(rng.integers(17, 700))
+        nx = (np.arange(W, dtype=np.float64) / np.float64(W)) * 2.0 - 1.0
+        ny = (np.arange(H, dtype=np.float64) / np.float64(H)) * 2.0 - 1.0
+        cx, cy = float(rng.uniform(-1.3, 1.3)), float(rng.uniform(-1.3, 1.3))
+        r = float(rng.choice([-1.0, 1.0]) * 10.0 ** rng.uniform(-3.5, -0.3))
+        m = math.sqrt(r * r + 0.0 * 0.0)
+        n = r * (1.0 / m)
+        pa = ((nx - cx) * n) / m
+        pb = ((ny - cy) * n) / m
+        cov = np.sqrt(pa[None, :] * pa[None, :] + pb[:, None] * pb[:, None]) < 1.0  # [y, x]
+        for xb in range(0, W, 128):
+            xe = min(xb + 127, W - 1)
+            for s0 in range(0, H, 16):
+                ye = min(s0 + 15, H - 1)
+                hit = bool(cov[s0:ye + 1, xb:xe + 1].any())
+                if not _strip_rasters_disc(nx, ny, xb, xe, s0, ye, cx, cy, r):
+                    rejected += 1
+                    assert not hit, (W, H, cx, cy, r, xb, s0)
+                elif not hit:
+                    reachable_rejects += 1
+    # (the bound is tight: strips it keeps without a covered texel graze the disc)
+    assert rejected > 10 * max(reachable_rejects, 1)

@@ -296,7 +296,7 @@ def test_group_frame_sequence_batched(rtm, oracle, scenes, fmt, staging):
 
 
 @pytest.mark.parametrize("fmt", [0, 2])
-def test_group_frame_sequence_raytraced_perspective(rtm, scenes, fmt):
+def test_group_frame_sequence_raytraced_perspective(rtm, scenes, gpu_ctx, fmt):
     """The group's batched bands with ray-traced primitives under a PERSPECTIVE eye
     (the batched per-wave primitive cull) and perspective spheres, in one chunk:
     every frame equals the single-device rtm_render_ex bytes."""
@@ -310,9 +310,12 @@ def test_group_frame_sequence_raytraced_perspective(rtm, scenes, fmt):
               scenes.raytracing_plane0(True), scenes.scene_r_bench(), scenes.perspective_simple2()]
     bufs = [(torch.empty((h, w, 4), dtype=torch.float32, device="cuda") if fmt == 0 else
              torch.empty(h * w * rtm.abi.FORMAT_BYTES[fmt], dtype=torch.uint8, device="cuda")) for _ in frames]
+    from test_bounds import oob
+    assert oob(rtm, gpu_ctx) >= 0  # clear (the count is the device's, every context's)
     torch.cuda.synchronize()
     g.render_frames_async(frames, eye, sh, w, h, 0, fl, fmt, 0, [b.data_ptr() for b in bufs])
     g.synchronize(60000)
+    assert oob(rtm, gpu_ctx) == 0  # (RGBA f32: the listed-block eye pass, its list in range)
     for s, b in zip(frames, bufs):
         want = rtm.render_frame_ex(s, eye, sh, w, h, 0, fl, fmt)
         got = to_host(b, h, w, fmt, rtm.abi)
