@@ -1317,9 +1317,6 @@ int enqueue_batch(rtm_ctx* ctx, int lane, FrameArgs* fa, const FrameExtra* const
             } else { o_sdf[(size_t)k] = off; off = up(off + sizeof(SdfTabK)); }
         }
     }
-    // the listed-block eye pass's entry counter, zeroed by every upload (launch_eye_batch)
-    const size_t o_cnt = off;
-    off = up(off + sizeof(uint32_t));
     const size_t bytes = off;
     const int j = br.next;
     br.next = (br.next + 1) % BatchRing::R;
@@ -1340,7 +1337,6 @@ int enqueue_batch(rtm_ctx* ctx, int lane, FrameArgs* fa, const FrameExtra* const
         if ((rc = br.dev[j].ensure(bytes, ctx->device))) return rc;
     }
     char* hb = (char*)br.host[j];
-    *(uint32_t*)(hb + o_cnt) = 0u;
     char* db = (char*)br.dev[j].p;
     DevTabs t0{};
     for (int k = 0; k < n; ++k) {
@@ -1378,10 +1374,8 @@ int enqueue_batch(rtm_ctx* ctx, int lane, FrameArgs* fa, const FrameExtra* const
     if (t0.rt && t0.rt_persp && !t0.sdf) {
         // per-wave primitive masks (rt_cull_batch_kernel) for every frame with primitives,
         // ceil(W/64) * rows words each; stream-ordered reuse on this lane
-        // (and as many words again for the listed-block eye pass's list: ceil(W/8) * ceil(rows/8)
-        // <= nw entries per frame when it runs, eye_block_mode)
         const size_t nw = (size_t)((fa[0].ey.W + 63) / 64) * (size_t)(fa[0].ey.row_end - fa[0].ey.row_begin);
-        if ((rc = br.rtmask.ensure(sizeof(uint32_t) * nw * (size_t)n * 2, ctx->device))) return rc;
+        if ((rc = br.rtmask.ensure(sizeof(uint32_t) * nw * (size_t)n, ctx->device))) return rc;
         for (int k = 0; k < n; ++k)
             if (exs[k]->has_rt) {
                 BatchFrame& bf = *(BatchFrame*)(hb + sizeof(BatchFrame) * (size_t)k);
@@ -1425,13 +1419,7 @@ int enqueue_batch(rtm_ctx* ctx, int lane, FrameArgs* fa, const FrameExtra* const
     }
     if (slot) HIP_TRY(hipEventRecord(slot->ev[2], s));
     int blocks = 0;
-    uint32_t* list = nullptr;
-    uint32_t* count = nullptr;
-    if (t0.rtmask && eye_batch_blocks(fa[0], t0)) {
-        list = (uint32_t*)br.rtmask.p + (size_t)t0.rtmask_words * (size_t)n;
-        count = (uint32_t*)(db + o_cnt);
-    }
-    if ((rc = launch_eye_batch((const BatchFrame*)db, n, fa[0], t0, s, &blocks, list, count)))
+    if ((rc = launch_eye_batch((const BatchFrame*)db, n, fa[0], t0, s, &blocks)))
         return fail(rc, "batched eye pass failed");
     ctx->eye_blocks_last = blocks;
     if (slot) {

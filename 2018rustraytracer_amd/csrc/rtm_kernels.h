@@ -390,13 +390,9 @@ int launch_eye_pass(const FrameArgs& a, const double* smap, void* out, void* str
 // a batch shares the shapes, flags, tables and kernel variant).
 // box: the union of the batch's sphere pixel boxes (x0, x1, y0, y1) for the split coded launch
 int launch_shadow_batch(const BatchFrame* dev, int n, const FrameArgs& a0, void* stream, const int32_t* box = nullptr);
-// blocks (optional): set to 1 when the launch ran 8 x 8-pixel blocks (eye_block_mode), else 0.
-// list / count: scratch for the listed-block mode of such a batch (n * ceil(W/8) *
-// ceil(rows/8) entries; *count zero when the launch starts), else nullptr (one kernel).
+// blocks (optional): set to 1 when the launch ran 8 x 8-pixel blocks (eye_block_mode), else 0
 int launch_eye_batch(const BatchFrame* dev, int n, const FrameArgs& a0, const DevTabs& t0, void* stream,
-                     int* blocks = nullptr, uint32_t* list = nullptr, uint32_t* count = nullptr);
-// The batch's eye pass runs 8 x 8-pixel blocks (t0: the batch's DevTabs as launch_eye_batch gets them).
-bool eye_batch_blocks(const FrameArgs& a0, const DevTabs& t0);
+                     int* blocks = nullptr);
 // Stream-ordered copy of host bytes into device memory by kernels whose
 // arguments carry the bytes (<= 3968 per launch), so the host copy is consumed
 // at launch: no pinned staging, no host synchronisation.  bytes % 8 == 0.

@@ -2002,10 +2002,7 @@ __device__ __forceinline__ const T* const_table(const T* p) {
 // BLK: the waves are 8 x 8 pixel blocks (workgroup bx: 4 blocks side by side, block row
 // by: 8 rows), for the batched RT 3 frames without shadows and without stripes: a compact
 // primitive touches fewer blocks than 64 x 1 rows, and a block's cone is narrower.
-// WIDE: the workgroup's 4 waves side by side in one row (256 x 1 pixels: 4 KB of RGBA f32
-// stored contiguously per workgroup) instead of stacked (64 x 4).
-template <bool FUSED, bool COUNT, int RT, int FMT = RTM_FORMAT_RGBA32F, bool NOSH = false, bool BLK = false,
-          bool WIDE = false>
+template <bool FUSED, bool COUNT, int RT, int FMT = RTM_FORMAT_RGBA32F, bool NOSH = false, bool BLK = false>
 __device__ __forceinline__ void eye_tile(const EyePart& a, const ShadowPart& sh, const double* __restrict__ smap,
                                          void* __restrict__ out, int bx, int by, StatsK* __restrict__ st,
                                          const DevTabs tabs, bool KMB = false, uint32_t kmw = 0u,
@@ -2022,12 +2019,11 @@ __device__ __forceinline__ void eye_tile(const EyePart& a, const ShadowPart& sh,
     const SdfTabK* __restrict__ sdf = const_table(tabs.sdf);
     // the workgroup's 4 waves stacked (64 x 4 pixels)
     const int wv_ = (int)(threadIdx.x >> 6), ln_ = (int)(threadIdx.x & (TILE_X - 1));
-    static_assert(!WIDE || (!BLK && RT == 0), "256 x 1 workgroups: the sphere-only tile");
     // (BLK: bx is the wave's block column)
-    const int xb = __builtin_amdgcn_readfirstlane(BLK ? bx * 8 : WIDE ? (bx * TILE_Y + wv_) * TILE_X : bx * TILE_X);
+    const int xb = __builtin_amdgcn_readfirstlane(BLK ? bx * 8 : bx * TILE_X);
     const int xi = xb + (BLK ? (ln_ & 7) : ln_);
     // (BLK: the lane's own row; else the wave's)
-    const int yl = BLK ? by * 8 + (ln_ >> 3) : __builtin_amdgcn_readfirstlane(WIDE ? by : by * TILE_Y + wv_);
+    const int yl = BLK ? by * 8 + (ln_ >> 3) : __builtin_amdgcn_readfirstlane(by * TILE_Y + wv_);
     const int yl0 = BLK ? __builtin_amdgcn_readfirstlane(by * 8) : yl;  // the wave's first row
     // the header fields the prologue needs, read before any branch so their scalar loads
     // issue as one group: one wait instead of a chain of dependent round trips (the
@@ -2375,11 +2371,9 @@ constexpr int eye_batch_tiles = RT == 3 && NOSH ? 4 : 1;
 // block rows per workgroup in the 8 x 8 mode, one after another: config 7 294 -> 317
 // Gpix/s against one (2: no gain; profiles/r05_ab_eye_blocks.txt)
 constexpr int EYE_BLK_NT = 4;
-// the sphere-only batched eye pass (RT 0, RGBA f32: the headline's) in 256 x 1 workgroups
-constexpr bool EYE_WIDE_RT0 = false;
 template <bool FUSED, int RT, bool NOSH>
 constexpr int eye_batch_wpe = RT == 3 && NOSH ? 8 : RT == 0 && !FUSED ? 8 : 1;
-template <bool FUSED, int RT, int FMT, bool NOSH = false, bool BLK = false, bool WIDE = false>
+template <bool FUSED, int RT, int FMT, bool NOSH = false, bool BLK = false>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(eye_batch_wpe<FUSED, RT, NOSH>, 8))) void eye_batch_kernel(
     CBatch* __restrict__ fr, const uint32_t* __restrict__ km, int km_nw, int km_gx) {
     if (BLK) {
@@ -2416,8 +2410,8 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(eye_batch
             widx = __builtin_amdgcn_readfirstlane((by * TILE_Y + (int)(threadIdx.x >> 6)) * km_gx + (int)blockIdx.x);
             kmw = ((const __attribute__((address_space(4))) uint32_t*)km)[(size_t)blockIdx.z * km_nw + min(widx, km_nw - 1)];
         }
-        eye_tile<FUSED, false, RT, FMT, NOSH, false, WIDE>(*(const EyePart*)&f->a.ey, *(const ShadowPart*)&f->a.sh, f->smap,
-                                                           f->out, blockIdx.x, by, nullptr, tabs, true, kmw, widx < km_nw);
+        eye_tile<FUSED, false, RT, FMT, NOSH>(*(const EyePart*)&f->a.ey, *(const ShadowPart*)&f->a.sh, f->smap, f->out,
+                                              blockIdx.x, by, nullptr, tabs, true, kmw, widx < km_nw);
     }
 }
 
@@ -2509,110 +2503,6 @@ __global__ __launch_bounds__(BLOCK) void rt_cull_batch_kernel(CBatch* __restrict
     const EyePart& e = *(const EyePart*)&f->a.ey;
     rt_cull_wave<BLK>(e.eye, rt, e.W, e.H, e.row_begin, e.row_end - e.row_begin,
                  make_int4(e.stripe_rows, e.stripe_stride, e.stripe_phase, 0), masks, blockIdx.x * BLOCK + threadIdx.x);
-}
-
-constexpr bool EYE_LISTED = true;  // (the listed-block mode below; false: one kernel, eye_batch_kernel<BLK>)
-// Listed blocks (round 6): the batched 8 x 8-block eye pass of small ray-traced frames
-// without shadows (eye_block_mode) in three launches instead of one.  Most of such a frame
-// is background -- main()'s scene (config 7): 2.4 % of its blocks meet the cylinder -- and
-// the one-kernel pass paid a wave per block, prologue and mask load included, just to store
-// the background.  Now:
-//   * rt_cull_list_kernel: per block its primitive mask (as rt_cull_batch_kernel) and, for
-//     every block a sphere's pixel range or a primitive can reach (exactly eye_tile's
-//     `reach`), an entry (frame << 16 | block) appended to the batch's list;
-//   * eye_bg_fill_kernel: every frame's output rows stored with the background colour,
-//     4 KB per workgroup-store, the pure-store pattern;
-//   * eye_list_kernel: eye_tile<BLK> over the listed blocks only (a fixed grid, each wave
-//     taking entries i, i + waves, ... of the list), overwriting the fill.
-// A block left out of the list is one eye_tile would have stored as background (its
-// `reach` is false), so the image is the same bits.
-__global__ __launch_bounds__(BLOCK) void rt_cull_list_kernel(CBatch* __restrict__ fr, uint32_t* __restrict__ list,
-                                                             uint32_t* __restrict__ count, uint32_t cap) {
-    CBatch* f = fr + blockIdx.z;
-    const EyePart& e = *(const EyePart*)&f->a.ey;
-    uint32_t* masks = f->tabs.rtmask;
-    const RtK* rt = f->tabs.rt;
-    const int t = blockIdx.x * BLOCK + threadIdx.x;
-    const int rows = e.row_end - e.row_begin;
-    const int gx8 = (e.W + 7) / 8, nb = gx8 * ((rows + 7) / 8);
-    if (masks && rt) {
-        rt_cull_wave<true>(e.eye, rt, e.W, e.H, e.row_begin, rows, make_int4(0, 0, 0, 0), masks, t);
-    }
-    // (eye_tile's check of the sphere ids, made by the frame's first wave there: block (0, 0)
-    // may not be listed here)
-    if (t == 0)
-        for (int l = 0; l < e.n_spheres; ++l)
-            if ((unsigned)e.sph[l].id >= (unsigned)e.n_spheres) atomicAdd(&g_oob_reads, 1ull);
-    if (t >= nb) return;
-    const uint32_t m = masks && rt ? masks[t] : 0u;
-    // eye_tile's wave sphere set for the block's columns [x0, x0 + 7] and image rows [y0, y0 + 7]
-    const int x0 = (t % gx8) * 8, y0 = e.row_begin + (t / gx8) * 8;
-    const int x1 = x0 + 7, y1 = y0 + 7;
-    bool sph = (e.cull_x0 <= e.cull_x1) & (y1 >= e.cull_y0) & (y0 <= e.cull_y1) & (x1 >= e.cull_x0) & (x0 <= e.cull_x1);
-    if (sph) {
-        bool any = false;
-        for (int i = 0; i < e.n_spheres; ++i) {
-            const RasterSphereK& q = e.sph[i];
-            any |= (y1 >= q.iy0) & (y0 <= q.iy1) & (x1 >= q.ix0) & (x0 <= q.ix1);
-        }
-        sph = any;
-    }
-    const bool reach = sph || m != 0u;
-    // one atomic per wave: the wave's listed blocks take consecutive entries
-    const unsigned long long b = __ballot(reach);
-    if (b == 0ull) return;
-    const int lane = threadIdx.x & 63;
-    const int leader = __builtin_ctzll(b);
-    uint32_t base = 0u;
-    if (lane == leader) base = atomicAdd(count, (uint32_t)__popcll(b));
-    base = (uint32_t)__shfl((int)base, leader);
-    const uint32_t at = base + (uint32_t)__popcll(b & ((1ull << lane) - 1ull));
-    // (the list holds every block of every frame: an entry past it is counted, not written)
-    if (reach && at < cap) list[at] = ((uint32_t)blockIdx.z << 16) | (uint32_t)t;
-    else if (reach) atomicAdd(&g_oob_reads, 1ull);
-}
-
-// the background of every frame's output rows (RGBA f32), 4 pixels per thread
-constexpr int BG_FILL_PX = 4;
-__global__ __launch_bounds__(BLOCK) void eye_bg_fill_kernel(CBatch* __restrict__ fr) {
-    CBatch* f = fr + blockIdx.z;
-    const EyePart& e = *(const EyePart*)&f->a.ey;
-    const int64_t n = (int64_t)(e.row_end - e.row_begin) * e.W;
-    float4* o = reinterpret_cast<float4*>(f->out) + (e.out_global ? (int64_t)e.row_begin * e.W : 0);
-    const f32x4 bg = {0.0f, 0.2f, 0.2f, 1.0f};
-#pragma unroll
-    for (int k = 0; k < BG_FILL_PX; ++k) {
-        const int64_t i = ((int64_t)blockIdx.x * BG_FILL_PX + k) * BLOCK + threadIdx.x;
-        if (i < n) __builtin_nontemporal_store(bg, reinterpret_cast<f32x4*>(o + i));
-    }
-}
-
-// eye_tile<BLK> over the listed blocks; every wave leaves once the list is exhausted
-__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(8, 8))) void eye_list_kernel(
-    CBatch* __restrict__ fr, const uint32_t* __restrict__ km, int km_nw, const uint32_t* __restrict__ list,
-    const uint32_t* __restrict__ count, int n_frames, int nb) {
-    typedef const __attribute__((address_space(4))) uint32_t CU32;
-    const uint32_t c = *(CU32*)count, cap = (uint32_t)n_frames * (uint32_t)nb;
-    if (c > cap && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&g_oob_reads, 1ull);
-    const uint32_t n = min(c, cap);
-    const uint32_t waves = gridDim.x * (BLOCK / TILE_X);
-#pragma unroll 1
-    for (uint32_t i = blockIdx.x * (BLOCK / TILE_X) + (threadIdx.x >> 6); i < n; i += waves) {
-        const uint32_t ent = ((CU32*)list)[__builtin_amdgcn_readfirstlane(i)];
-        const int z = (int)(ent >> 16), t = (int)(ent & 0xFFFFu);
-        if (z >= n_frames || t >= nb) {  // (no cull writes such an entry: counted, skipped)
-            if ((threadIdx.x & 63) == 0) atomicAdd(&g_oob_reads, 1ull);
-            continue;
-        }
-        CBatch* f = fr + z;
-        asm volatile("" : "+s"(f));
-        const int gx8 = (((const EyePart*)&f->a.ey)->W + 7) / 8;
-        const DevTabs tabs = *(const DevTabs*)&f->tabs;
-        const uint32_t kmw = ((CU32*)km)[(size_t)z * km_nw + t];
-        eye_tile<false, false, 3, RTM_FORMAT_RGBA32F, true, true>(*(const EyePart*)&f->a.ey, *(const ShadowPart*)&f->a.sh,
-                                                                  f->smap, f->out, t % gx8, t / gx8, nullptr, tabs, true,
-                                                                  kmw, true);
-    }
 }
 
 // ---- reference-seam kernels ----
@@ -2936,12 +2826,8 @@ static void launch_eye_fmt(const FrameArgs& a, const double* smap, void* o, hipS
 #define RTM_EYE(F, R, N)                                                                                           \
     do {                                                                                                        \
         constexpr bool B_ = R == 3 && N && FMT == RTM_FORMAT_RGBA32F;                                           \
-        constexpr bool W_ = EYE_WIDE_RT0 && R == 0 && FMT == RTM_FORMAT_RGBA32F;                                \
         if (fr && B_ && blk)                                                                                    \
             hipLaunchKernelGGL((eye_batch_kernel<F, R, FMT, N, B_>), gblk, dim3(BLOCK), 0, s, fr, km.p, km.nw, gx8); \
-        else if (fr && W_)                                                                                      \
-            hipLaunchKernelGGL((eye_batch_kernel<F, R, FMT, N, false, W_>), dim3((g.x + 3) / 4, (unsigned)rows_, g.z), \
-                               dim3(BLOCK), 0, s, fr, km.p, km.nw, km.gx);                                     \
         else if (fr) hipLaunchKernelGGL((eye_batch_kernel<F, R, FMT, N>), dim3(g.x, (g.y + eye_batch_tiles<R, N> - 1) / eye_batch_tiles<R, N>, g.z), \
                                    dim3(BLOCK), 0, s, fr, km.p, km.nw, km.gx);                                     \
         else hipLaunchKernelGGL((eye_pass_kernel<F, false, R, FMT, N>), g, dim3(BLOCK), 0, s, a, smap, o, nullptr, tabs); \
@@ -3093,33 +2979,13 @@ static bool eye_block_mode(const FrameArgs& a0, const DevTabs& t0, bool fused) {
            (int64_t)a0.ey.W * rows < (1 << 20);
 }
 
-bool eye_batch_blocks(const FrameArgs& a0, const DevTabs& t0) {
-    return eye_block_mode(a0, t0, (a0.ey.flags & RTM_FLAG_FUSED_SHADOW) != 0);
-}
-
 int launch_eye_batch(const BatchFrame* dev, int n, const FrameArgs& a0, const DevTabs& t0, void* stream,
-                     int* blocks, uint32_t* list, uint32_t* count) {
+                     int* blocks) {
     hipStream_t s = (hipStream_t)stream;
     CBatch* fr = (CBatch*)dev;
     const int rows = a0.ey.row_end - a0.ey.row_begin;
     const bool fused = (a0.ey.flags & RTM_FLAG_FUSED_SHADOW) != 0;
     const bool blk = eye_block_mode(a0, t0, fused);
-    if (EYE_LISTED && blk && list && count) {  // listed blocks: cull + list, background fill, the listed blocks
-        const int nw8 = ((a0.ey.W + 7) / 8) * ((rows + 7) / 8);
-        if (blocks) *blocks = 1;
-        hipLaunchKernelGGL(rt_cull_list_kernel, dim3((unsigned)((nw8 + BLOCK - 1) / BLOCK), 1, (unsigned)n),
-                           dim3(BLOCK), 0, s, fr, list, count, (uint32_t)nw8 * (uint32_t)n);
-        const int64_t px = (int64_t)rows * a0.ey.W;
-        hipLaunchKernelGGL(eye_bg_fill_kernel,
-                           dim3((unsigned)((px + BLOCK * BG_FILL_PX - 1) / (BLOCK * BG_FILL_PX)), 1, (unsigned)n),
-                           dim3(BLOCK), 0, s, fr);
-        // (waves to fill the chip; each takes entries i, i + waves, ... of the list)
-        const int64_t need = ((int64_t)nw8 * n + 3) / 4;
-        const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>(need, 2048));
-        hipLaunchKernelGGL(eye_list_kernel, dim3(g), dim3(BLOCK), 0, s, fr, t0.rtmask, t0.rtmask_words, list, count,
-                           n, nw8);
-        return launched();
-    }
     // (the SDF batches take blocks under their own rule, launch_eye_fmt's sblk)
     const bool sdf_blk = t0.sdf && (t0.fmt & FMT_MASK) == RTM_FORMAT_RGBA32F && a0.ey.stripe_rows == 0 &&
                          !(fused && !((a0.sh.flags & (RTM_FLAG_NO_MARCH | RTM_FLAG_NO_SHADOW_RASTER)) ==

@@ -303,13 +303,17 @@ def tile_scaling(tile: dict, res: dict, world: int) -> None:
 
 
 def make_group(rtm, world, rank, local, dist, backend):
-    """librtm's RCCL group: ncclCommInitAll at N = 1, one rank per process otherwise
-    (the 128-byte id from rank 0, handed over by torch.distributed)."""
+    """librtm's group: one rank per process over RCCL (ncclCommInitRank, the 128-byte id
+    from rank 0 handed over by torch.distributed).  At N = 1 there is nothing to gather
+    (the one band renders in place), so no communicator is formed: the one-member group
+    of the device-copy transport runs the same render path (a process that formed and
+    destroyed one-device RCCL communicators later met illegal memory accesses on this
+    pool, tests/test_zz_rccl_groups.py)."""
     import torch
     if backend != "nccl":
         return None
     if world == 1:
-        return rtm.Group(n_devices=1, devices=[local])
+        return rtm.Group(n_devices=1, devices=[local], loopback=True)
     uid = torch.zeros(128, dtype=torch.uint8, device=f"cuda:{local}")
     if rank == 0:
         uid.copy_(torch.frombuffer(bytearray(rtm.Group.unique_id()), dtype=torch.uint8))

@@ -172,6 +172,7 @@ def group_frames(rtm, torch, g, frames, eye, sh, w, h, k, flags, fmt):
     return [to_host(t, h, w, fmt, rtm.abi) for t in outs]
 
 
+@pytest.mark.rccl
 @pytest.mark.parametrize("staging", [False, True], ids=["in-place", "rccl-self-gather"])
 @pytest.mark.parametrize("fmt", [0, 1, 2])
 def test_group_comm_init_all_one_device(rtm, oracle, scenes, fmt, staging):
@@ -191,6 +192,7 @@ def test_group_comm_init_all_one_device(rtm, oracle, scenes, fmt, staging):
     g.close()
 
 
+@pytest.mark.rccl
 def test_group_rank_form_one_rank(rtm, oracle, scenes):
     """ncclCommInitRank with a unique id (the one-process-per-GPU form bench.py uses)."""
     import torch
@@ -207,6 +209,7 @@ def test_group_rank_form_one_rank(rtm, oracle, scenes):
     g.close()
 
 
+@pytest.mark.rccl
 def test_group_full_size_config3(rtm, scenes, gpu_ctx):
     """Config 3 at full size through the group (RCCL self-gather, RGBA32F): equal to
     the single-context frame bit for bit."""
@@ -228,6 +231,7 @@ def test_group_full_size_config3(rtm, scenes, gpu_ctx):
     g.close()
 
 
+@pytest.mark.rccl
 def test_group_rejects_bad_input_before_enqueue(rtm, scenes):
     import torch
     g = rtm.Group(n_devices=1)
@@ -245,6 +249,7 @@ def test_group_rejects_bad_input_before_enqueue(rtm, scenes):
     g.close()
 
 
+@pytest.mark.rccl
 @pytest.mark.parametrize("staging", [False, True], ids=["in-place", "rccl-self-gather"])
 @pytest.mark.parametrize("fmt", [0, 1, 2])
 def test_group_render_host_output(rtm, oracle, scenes, fmt, staging):
@@ -268,6 +273,7 @@ def test_group_render_host_output(rtm, oracle, scenes, fmt, staging):
     g.close()
 
 
+@pytest.mark.rccl
 @pytest.mark.parametrize("staging", [False, True], ids=["in-place", "rccl-self-gather"])
 @pytest.mark.parametrize("fmt", [0, 1])
 def test_group_frame_sequence_batched(rtm, oracle, scenes, fmt, staging):
@@ -295,6 +301,7 @@ def test_group_frame_sequence_batched(rtm, oracle, scenes, fmt, staging):
     g.close()
 
 
+@pytest.mark.rccl
 @pytest.mark.parametrize("fmt", [0, 2])
 def test_group_frame_sequence_raytraced_perspective(rtm, scenes, gpu_ctx, fmt):
     """The group's batched bands with ray-traced primitives under a PERSPECTIVE eye

@@ -139,6 +139,7 @@ def test_group_render_host_direct(rtm, oracle, scenes, n, fmt):
         g.close()
 
 
+@pytest.mark.rccl
 def test_group_host_direct_rccl_one_device(rtm, oracle, scenes):
     """The RCCL group (ncclCommInitAll over the one device) in direct mode."""
     g = rtm.Group(n_devices=1)
@@ -252,7 +253,7 @@ def test_loopback_root_moves_between_calls(rtm, oracle, scenes):
         g.close()
 
 
-@pytest.mark.parametrize("n", [1, 3])
+@pytest.mark.parametrize("n", [pytest.param(1, marks=pytest.mark.rccl), 3])
 def test_group_sequence_spreads_chunks_over_lanes(rtm, oracle, scenes, n):
     """A long sequence: every member's chunks (frames per launch of its part) go to its
     context's lanes (4 below 16 Mpixel), as rtm_render_frames_async's batches do; frames
@@ -282,7 +283,7 @@ def test_group_sequence_spreads_chunks_over_lanes(rtm, oracle, scenes, n):
         torch.cuda.empty_cache()
 
 
-@pytest.mark.parametrize("n", [1, 3])
+@pytest.mark.parametrize("n", [pytest.param(1, marks=pytest.mark.rccl), 3])
 def test_group_sequence_into_one_buffer_lands_in_order(rtm, oracle, scenes, n):
     """Every frame of a sequence into ONE root buffer: the repeated
     output starts a new chunk per frame, and chunks would go to different lanes; the
@@ -313,6 +314,7 @@ def test_group_sequence_into_one_buffer_lands_in_order(rtm, oracle, scenes, n):
         torch.cuda.empty_cache()
 
 
+@pytest.mark.rccl
 def test_group_distinct_outputs_keep_their_lanes(rtm, scenes):
     """The lane cap applies only where outputs overlap across chunks: distinct buffers
     keep the auto lanes (test_group_sequence_spreads_chunks_over_lanes checks the images)."""

@@ -16,7 +16,7 @@ if [ -n "${PATCH:-}" ]; then (cd "$B" && patch -s -p3 < "$PATCH"); fi
 /opt/rocm/bin/hipcc -O3 -fPIC -std=c++17 -ffp-contract=off -fno-fast-math -Wall -Wno-unused-function \
     -I"$PWD" --offload-arch=gfx950 $FLAGS -c "$B/rtm_kernels.hip" -o "$B/rtm_kernels.o"
 API=rtm_api.o
-if [ -n "$API_FLAGS" ]; then
+if [ -n "$API_FLAGS" ] || { [ -n "${PATCH:-}" ] && grep -q "rtm_api.cpp" "$PATCH"; }; then
   /opt/rocm/bin/hipcc -O3 -fPIC -std=c++17 -ffp-contract=off -fno-fast-math -Wall -Wno-unused-function \
       -I"$PWD" $API_FLAGS -c "$B/rtm_api.cpp" -o "$B/rtm_api.o"
   API="$B/rtm_api.o"
