@@ -1458,30 +1458,68 @@ __device__ __forceinline__ void shadow_tile_coded(const ShadowPart& a, void* __r
         if (span_ok) {
             const bool need[2] = {stop[0] != sbot[0], stop[1] != sbot[1]};
             if (__any(need[0] | need[1])) {
-                int lo[2] = {0, 0}, hi[2] = {SPAN - 1, SPAN - 1};
-                uint32_t chi[2] = {sbot[0], sbot[1]};
-                bool bad = false;
+                // The boundary as a threshold on D (no code evaluation per step).  With entry
+                // alike over the span, a row's code is the first k with P(z_k) (NONE = steps:
+                // none before `steps`; P monotone over the table), so "code != top" is one
+                // compare: !P(z_top) when the codes rise down the column, P(z_{top-1}) when they
+                // fall -- monotone in D, hence in the row.  The first such row hi: a guess
+                // from the ends' D (interpolated, f32), confirmed by rows hi - 1 and hi, else
+                // a binary search on the same compare.  Row hi's code is the bottom code when
+                // the two codes are adjacent (monotone codes strictly between none); otherwise
+                // one check at hi confirms it (any other code: the span is no single run).
+                const double Dt0 = d0[0] + dd[0] * RS[0].py, Db0 = d0[0] + dd[0] * RS[SPAN - 1].py;
+                const double Dt1 = d0[1] + dd[1] * RS[0].py, Db1 = d0[1] + dd[1] * RS[SPAN - 1].py;
+                const double Dt[2] = {Dt0, Dt1}, Db[2] = {Db0, Db1};
+                int lo[2], hi[2];
+                double zt[2];
+                bool rise[2];
+#pragma unroll
+                for (int c = 0; c < 2; ++c) {
+                    const int ct = stop[c] == CODE_NONE ? steps : (int)stop[c];
+                    const int cb = sbot[c] == CODE_NONE ? steps : (int)sbot[c];
+                    rise[c] = cb > ct;
+                    zt[c] = T[rise[c] ? ct : ct - 1].z;  // (need: ct != cb, so ct < steps when rising, >= 1 falling)
+                    // the guess: D runs from Dt to Db over rows 0 .. SPAN - 1
+                    float fr = (float)(zt[c] - Dt[c]) * __builtin_amdgcn_rcpf((float)(Db[c] - Dt[c]));
+                    fr = fr == fr ? fr * (float)(SPAN - 1) : 1.0f;
+                    const int g = (int)ceilf(__builtin_amdgcn_fmed3f(fr, 1.0f, (float)(SPAN - 1)));
+                    const double Da = d0[c] + dd[c] * RS[g - 1].py, Dg = d0[c] + dd[c] * RS[g].py;
+                    // differs(D): the row's code is not the top code
+                    const bool pa = INC ? !(zt[c] < Da) : (zt[c] < Da), pg = INC ? !(zt[c] < Dg) : (zt[c] < Dg);
+                    const bool da = rise[c] ? !pa : pa, dg = rise[c] ? !pg : pg;
+                    const bool hitg = need[c] & !da & dg;
+                    lo[c] = hitg ? g - 1 : 0;
+                    hi[c] = hitg ? g : SPAN - 1;
+                }
                 constexpr int HALVINGS = SPAN <= 16 ? 4 : SPAN <= 32 ? 5 : 6;
 #pragma unroll
                 for (int it = 0; it < HALVINGS; ++it) {
+                    const bool act0 = need[0] & (hi[0] - lo[0] > 1), act1 = need[1] & (hi[1] - lo[1] > 1);
+                    if (!__any(act0 | act1)) break;
 #pragma unroll
                     for (int c = 0; c < 2; ++c) {
-                        const bool act = need[c] & (hi[c] - lo[c] > 1);
+                        const bool act = c ? act1 : act0;
                         const int mid = (lo[c] + hi[c]) >> 1;
-                        const RowLdsK rr = RS[act ? mid : 0];
-                        const double Dm = d0[c] + dd[c] * rr.py;
-                        bool sm, em;
-                        const uint32_t cm = code_check<INC>(T, Dm, rr.pyf, g0[c], g1[c], fsteps, oz, steps, sm, em);
-                        bad |= act & sm;
-                        const bool same = cm == stop[c];
-                        lo[c] = (act & same) ? mid : lo[c];
-                        hi[c] = (act & !same) ? mid : hi[c];
-                        chi[c] = (act & !same) ? cm : chi[c];
+                        const double Dm = d0[c] + dd[c] * RS[act ? mid : 0].py;
+                        const bool pm = INC ? !(zt[c] < Dm) : (zt[c] < Dm);
+                        const bool dm = rise[c] ? !pm : pm;
+                        lo[c] = (act & !dm) ? mid : lo[c];
+                        hi[c] = (act & dm) ? mid : hi[c];
                     }
                 }
+                bool bad = false;
 #pragma unroll
                 for (int c = 0; c < 2; ++c) {
-                    bad |= need[c] & (chi[c] != sbot[c]);
+                    const int ct = stop[c] == CODE_NONE ? steps : (int)stop[c];
+                    const int cb = sbot[c] == CODE_NONE ? steps : (int)sbot[c];
+                    const bool adj = (cb - ct == 1) | (ct - cb == 1);
+                    if (__any(need[c] & !adj)) {
+                        const RowLdsK rr = RS[hi[c]];
+                        bool sm, em;
+                        const uint32_t cm = code_check<INC>(T, d0[c] + dd[c] * rr.py, rr.pyf, g0[c], g1[c], fsteps, oz,
+                                                            steps, sm, em);
+                        bad |= need[c] & !adj & (sm | (cm != sbot[c]));
+                    }
                     sbnd[c] = need[c] ? hi[c] : SPAN;
                 }
                 span_ok = !__any(bad);
