@@ -1246,8 +1246,10 @@ int frame_batch(int32_t req, int32_t W, int32_t H) {
 
 // Enqueue frames [0, n) of `fa` (same tables, flags and sizes) as ONE batched
 // launch per pass on `lane`; a frame's output is outs[k] (RGBA f32).
+// alone: no other lane of the call runs beside this one (the shadow pass's split launch
+// then runs as one launch, launch_shadow_batch).
 int enqueue_batch(rtm_ctx* ctx, int lane, FrameArgs* fa, const FrameExtra* const* exs, void* const* outs, int n,
-                  int32_t fmt = RTM_FORMAT_RGBA32F) {
+                  int32_t fmt = RTM_FORMAT_RGBA32F, bool alone = false) {
     int rc;
     if ((rc = frame_tables(ctx, fa[0]))) return rc;
     for (int k = 1; k < n; ++k) {
@@ -1404,7 +1406,8 @@ int enqueue_batch(rtm_ctx* ctx, int lane, FrameArgs* fa, const FrameExtra* const
             box[2] = std::min(box[2], q.cull_y0);
             box[3] = std::max(box[3], q.cull_y1);
         }
-        if ((rc = launch_shadow_batch((const BatchFrame*)db, n, fa[0], s, box))) return fail(rc, "batched shadow pass failed");
+        if ((rc = launch_shadow_batch((const BatchFrame*)db, n, fa[0], s, box, alone)))
+            return fail(rc, "batched shadow pass failed");
         if (slot) HIP_TRY(hipEventRecord(slot->ev[1], s));
         ctx->have_shadow_pass = true;
         ctx->last_trivial = false;
@@ -1781,7 +1784,8 @@ int rtm_render_frames_async(rtm_ctx* ctx, int32_t n_frames, const rtm_scene* sce
                 std::vector<const FrameExtra*> xp((size_t)(e - k));
                 for (int32_t q = k; q < e; ++q) xp[(size_t)(q - k)] = &fx[(size_t)q];
                 rc = enqueue_batch(ctx, lane, &fa[(size_t)k], xp.data(),
-                                   reinterpret_cast<void* const*>(out_rgba_dev + i0 + k), e - k);
+                                   reinterpret_cast<void* const*>(out_rgba_dev + i0 + k), e - k, RTM_FORMAT_RGBA32F,
+                                   L == 1);
             } else {
                 rc = enqueue_frame(ctx, fa[(size_t)k], &fx[(size_t)k], out_rgba_dev[i0 + k], nullptr, lane);
             }

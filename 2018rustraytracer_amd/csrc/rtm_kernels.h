@@ -389,7 +389,10 @@ int launch_eye_pass(const FrameArgs& a, const double* smap, void* out, void* str
 // (device memory); a0 / t0: the host copy of frame 0's arguments (every frame of
 // a batch shares the shapes, flags, tables and kernel variant).
 // box: the union of the batch's sphere pixel boxes (x0, x1, y0, y1) for the split coded launch
-int launch_shadow_batch(const BatchFrame* dev, int n, const FrameArgs& a0, void* stream, const int32_t* box = nullptr);
+// one_launch: a split coded pass as one launch of both parts (shadow_split_batch_kernel; the
+// caller's choice when the batch's lane runs alone, rtm_api.cpp enqueue_batch)
+int launch_shadow_batch(const BatchFrame* dev, int n, const FrameArgs& a0, void* stream, const int32_t* box = nullptr,
+                        bool one_launch = false);
 // blocks (optional): set to 1 when the launch ran 8 x 8-pixel blocks (eye_block_mode), else 0
 int launch_eye_batch(const BatchFrame* dev, int n, const FrameArgs& a0, const DevTabs& t0, void* stream,
                      int* blocks = nullptr);

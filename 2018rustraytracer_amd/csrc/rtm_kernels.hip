@@ -1966,6 +1966,27 @@ __device__ __forceinline__ void shadow_tile_coded(const ShadowPart& a, void* __r
     }  // strips
 }
 
+// One workgroup tile (bx, by) of a split launch's part: it leaves at once (workgroup-
+// uniform, before its barrier) when none of its strips is this part's, by the waves' own
+// test, strip_rasters.
+template <bool INC, int CODE, int PART>
+__device__ __forceinline__ void shadow_split_block(const ShadowPart& sh, void* __restrict__ map, char* __restrict__ lds,
+                                                   int bx, int by) {
+    constexpr int TR = coded_tile_rows<PART>;
+    const int ya = by * TR, xa = bx * 128;
+    if (PART == 2) {  // (one 16-row strip per workgroup)
+        if (!strip_rasters(sh, xa, ya)) return;
+    } else if (!(sh.flags & RTM_FLAG_NO_SHADOW_RASTER) && union_may_cover(sh, xa, xa + 127, ya, ya + CODED_ROWS - 1) &&
+               union_may_cover(sh, xa, xa + 127, ya + TR - CODED_ROWS, ya + TR - 1)) {
+        // (the union reaches both end strips: every strip may be PART 2's)
+        bool all = true;
+        for (int s0 = ya; s0 < ya + TR && s0 < sh.H && all; s0 += CODED_ROWS) all = strip_rasters(sh, xa, s0);
+        if (all) return;
+    }
+    shadow_tile_coded<INC, CODE, PART>(sh, map, bx, by, reinterpret_cast<ZRecK*>(lds + CODED_ROW_LDS),
+                                       reinterpret_cast<RowLdsK*>(lds));
+}
+
 template <bool INC, int CODE, int PART>
 __device__ __forceinline__ void shadow_coded_block(const ShadowPart& sh, void* __restrict__ map, char* __restrict__ lds,
                                                    int4 org) {
@@ -1978,20 +1999,8 @@ __device__ __forceinline__ void shadow_coded_block(const ShadowPart& sh, void* _
         const bool none = sh.cull_x0 > sh.cull_x1 || sh.cull_y0 > sh.cull_y1 || sh.cull_y1 < 0;
         by = none ? (int)blockIdx.y : hot_rows_first((int)blockIdx.y, n, h0, h1);
     } else {
-        // (workgroup-uniform: the whole workgroup leaves, before its barrier, when none of
-        // its strips is this part's, by the waves' own test, strip_rasters)
-        bx += org.x;
-        by = (int)blockIdx.y + org.y;
-        const int ya = by * TR, xa = bx * 128;
-        if (PART == 2) {  // (one 16-row strip per workgroup)
-            if (!strip_rasters(sh, xa, ya)) return;
-        } else if (!(sh.flags & RTM_FLAG_NO_SHADOW_RASTER) && union_may_cover(sh, xa, xa + 127, ya, ya + CODED_ROWS - 1) &&
-                   union_may_cover(sh, xa, xa + 127, ya + TR - CODED_ROWS, ya + TR - 1)) {
-            // (the union reaches both end strips: every strip may be PART 2's)
-            bool all = true;
-            for (int s0 = ya; s0 < ya + TR && s0 < sh.H && all; s0 += CODED_ROWS) all = strip_rasters(sh, xa, s0);
-            if (all) return;
-        }
+        shadow_split_block<INC, CODE, PART>(sh, map, lds, bx + org.x, (int)blockIdx.y + org.y);
+        return;
     }
     shadow_tile_coded<INC, CODE, PART>(sh, map, bx, by, reinterpret_cast<ZRecK*>(lds + CODED_ROW_LDS),
                                        reinterpret_cast<RowLdsK*>(lds));
@@ -2017,6 +2026,27 @@ shadow_coded_batch_kernel(CBatch* __restrict__ fr, int4 org) {
     extern __shared__ char lds_coded[];
     CBatch* f = fr + blockIdx.z;
     shadow_coded_block<INC, CODE, PART>(*(const ShadowPart*)&f->a.sh, f->smap, lds_coded, org);
+}
+
+constexpr int SPLIT_MIN_WAVES = 5;
+// Both parts of a batch's split launch as ONE launch (round 6): workgroups [0, org.w) of a
+// frame are PART 2's tiles over the box (org.z of them per row, from (org.x, org.y)), the
+// rest PART 1's over the whole map, row-major.  One launch's fixed cost instead of two
+// (an empty launch of either part took ~4.2 us one-lane at config 3, profiles/r06_ab_shadow.txt);
+// the sphere tiles come first, so their longer waves start first.
+template <bool INC, int CODE>
+__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(SPLIT_MIN_WAVES, 8))) void
+shadow_split_batch_kernel(CBatch* __restrict__ fr, int4 org) {
+    extern __shared__ char lds_coded[];
+    CBatch* f = fr + blockIdx.z;
+    const ShadowPart& sh = *(const ShadowPart*)&f->a.sh;
+    const int id = (int)blockIdx.x;
+    if (id < org.w) {
+        shadow_split_block<INC, CODE, 2>(sh, f->smap, lds_coded, org.x + id % org.z, org.y + id / org.z);
+    } else {
+        const int j = id - org.w, gx = (sh.W + 127) >> 7;
+        shadow_split_block<INC, CODE, 1>(sh, f->smap, lds_coded, j % gx, j / gx);
+    }
 }
 
 
@@ -2767,7 +2797,7 @@ static bool coded_ok(const ShadowPart& sh) {
 // (configs 2-4 split; config 5's 16 spheres span more: one launch there, measured as
 // fast in the 4-lane frame and faster one-lane, profiles/r03_ab_coded_split.txt).
 static void launch_coded(const ShadowPart& sh, const FrameArgs* a, double* smap, CBatch* fr, int n, hipStream_t s,
-                         const int32_t* box = nullptr) {
+                         const int32_t* box = nullptr, bool one_launch = false) {
     const bool march = !(sh.flags & RTM_FLAG_NO_MARCH) && sh.n_patches > 0 && sh.steps > 0;
     const size_t lsm = march ? CODED_ROW_LDS + sizeof(ZRecK) * (size_t)(sh.steps + 1) : 0;
     constexpr int TR = CODED_TILE_ROWS;
@@ -2805,14 +2835,24 @@ static void launch_coded(const ShadowPart& sh, const FrameArgs* a, double* smap,
     // PART 1's workgroup tiles: coded_tile_rows<1> rows (P1_STRIPS strips per wave)
     constexpr int TR1 = coded_tile_rows<1>;
     const dim3 g1(g.x, (unsigned)((sh.H + TR1 - 1) / TR1), g.z);
-#define RTM_CKB(I, M)                                           \
-    do {                                                        \
-        if (split) {                                            \
-            if (gb.x > 0 && gb.y > 0) RTM_CK(I, M, 2, gb, orgb); \
-            RTM_CK(I, M, 1, g1, org0);                          \
-        } else {                                                \
-            RTM_CK(I, M, 0, g, org0);                           \
-        }                                                       \
+    // a batch whose lane runs alone: one launch of both parts (shadow_split_batch_kernel).
+    // One-lane at config 3 it takes 29.7 us per 8-frame launch against 17.8 + 16.8 us for
+    // the two launches; with 4 lanes the other lanes' kernels fill the gap between the two
+    // launches and the merged kernel's registers (84 VGPRs for PART 2's waves, 62 alone)
+    // cost 1-4 % of the frame rate, so lanes keep two (profiles/r06_ab_shadow.txt)
+    const int n2 = (int)(gb.x * gb.y);
+    const dim3 gs((unsigned)(n2 + (int)(g1.x * g1.y)), 1u, g.z);
+    const int4 orgs = make_int4(bx0, c0, (int)gb.x, n2);
+#define RTM_CKB(I, M)                                                                                        \
+    do {                                                                                                     \
+        if (split && fr && one_launch) {                                                                                \
+            hipLaunchKernelGGL((shadow_split_batch_kernel<I, M>), gs, dim3(BLOCK), lsm, s, fr, orgs);         \
+        } else if (split) {                                                                                  \
+            if (gb.x > 0 && gb.y > 0) RTM_CK(I, M, 2, gb, orgb);                                             \
+            RTM_CK(I, M, 1, g1, org0);                                                                       \
+        } else {                                                                                             \
+            RTM_CK(I, M, 0, g, org0);                                                                        \
+        }                                                                                                    \
     } while (0)
     if (sh.smap_fmt == SMAP_U8) {
         if (inc) RTM_CKB(true, SMAP_U8);
@@ -2951,12 +2991,13 @@ int launch_eye_pass(const FrameArgs& a, const double* smap, void* out, void* str
     return launched();
 }
 
-int launch_shadow_batch(const BatchFrame* dev, int n, const FrameArgs& a0, void* stream, const int32_t* box) {
+int launch_shadow_batch(const BatchFrame* dev, int n, const FrameArgs& a0, void* stream, const int32_t* box,
+                        bool one_launch) {
     hipStream_t s = (hipStream_t)stream;
     CBatch* fr = (CBatch*)dev;
     const ShadowPart& sh = a0.sh;
     if (coded_ok(sh)) {
-        launch_coded(sh, nullptr, nullptr, fr, n, s, box);
+        launch_coded(sh, nullptr, nullptr, fr, n, s, box, one_launch);
         return launched();
     }
     dim3 g = grid_for(sh.W, sh.H);

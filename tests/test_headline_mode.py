@@ -79,6 +79,40 @@ def test_headline_sequence_4k_four_lanes_eight_per_launch(rtm, oracle, scenes):
     _sequence_vs_oracle(rtm, oracle, scenes, frames, 3840, 2160, 64, lanes=4, batch=8, map_bytes=1)
 
 
+def test_headline_frames_one_lane_one_launch(rtm, oracle, scenes):
+    """Config 3's frames on ONE lane (8 per launch): a lone lane's split shadow pass is one
+    launch of both parts (shadow_split_batch_kernel, round 6); every frame and the last
+    map against the oracle, and no out-of-range side-table read."""
+    import torch
+    from test_bounds import oob
+    frames = [scenes.scene_a_bench(200 + 3 * i) for i in range(8)]
+    w, h, k = 3840, 2160, 64
+    eye, sh = scenes.eye_camera(), scenes.shadow_camera()
+    ctx = rtm.Context(0)
+    outs = [torch.empty((h, w, 4), dtype=torch.float32, device="cuda") for _ in frames]
+    try:
+        ctx.set_lanes(1)
+        ctx.set_batch(8)
+        assert oob(rtm, ctx) >= 0
+        torch.cuda.synchronize()
+        ctx.render_frames_async(frames, eye, sh, w, h, k, 0, [o.data_ptr() for o in outs])
+        ctx.synchronize()
+        assert (ctx.last_lanes(), ctx.last_batch()) == (1, 8)
+        assert oob(rtm, ctx) == 0
+        stored, spans = ctx.shadow_map_stored_bytes()
+        assert spans and 0 < stored < w * h
+        for i, (s, o) in enumerate(zip(frames, outs)):
+            want = oracle.render(s, eye, sh, w, h, k, 0, nthreads=NT, want_shadow=(i == len(frames) - 1))
+            got = o.cpu().numpy()
+            assert bits_equal(got, want["rgba"]), (i, first_mismatch(got, want["rgba"]))
+        got_map = _smap(ctx, w, h)
+        assert bits_equal(got_map, want["shadow"]), first_mismatch(got_map, want["shadow"])
+    finally:
+        del outs
+        ctx.close()
+        torch.cuda.empty_cache()
+
+
 @pytest.mark.parametrize("cfg", [4, 5])
 def test_8k_sequence_three_lanes_batched(rtm, oracle, scenes, cfg):
     """Configs 4 / 5 under the auto rule from 16 Mpixel: 3 lanes x 2 frames per
