@@ -393,9 +393,11 @@ int launch_eye_pass(const FrameArgs& a, const double* smap, void* out, void* str
 // caller's choice when the batch's lane runs alone, rtm_api.cpp enqueue_batch)
 int launch_shadow_batch(const BatchFrame* dev, int n, const FrameArgs& a0, void* stream, const int32_t* box = nullptr,
                         bool one_launch = false);
-// blocks (optional): set to 1 when the launch ran 8 x 8-pixel blocks (eye_block_mode), else 0
+// blocks (optional): set to 1 when the launch ran 8 x 8-pixel blocks (eye_block_mode), else 0.
+// mask_shared: the frames' primitive masks are one set, frame 0's (its words at t0.rtmask;
+// every frame has frame 0's eye camera, rows and primitive table: rtm_api.cpp enqueue_batch)
 int launch_eye_batch(const BatchFrame* dev, int n, const FrameArgs& a0, const DevTabs& t0, void* stream,
-                     int* blocks = nullptr);
+                     int* blocks = nullptr, bool mask_shared = false);
 // Stream-ordered copy of host bytes into device memory by kernels whose
 // arguments carry the bytes (<= 3968 per launch), so the host copy is consumed
 // at launch: no pinned staging, no host synchronisation.  bytes % 8 == 0.

@@ -2443,7 +2443,7 @@ template <bool FUSED, int RT, bool NOSH>
 constexpr int eye_batch_wpe = RT == 3 && NOSH ? 8 : RT == 0 && !FUSED ? 8 : 1;
 template <bool FUSED, int RT, int FMT, bool NOSH = false, bool BLK = false>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(eye_batch_wpe<FUSED, RT, NOSH>, 8))) void eye_batch_kernel(
-    CBatch* __restrict__ fr, const uint32_t* __restrict__ km, int km_nw, int km_gx) {
+    CBatch* __restrict__ fr, const uint32_t* __restrict__ km, int km_nw, int km_gx, int km_fs) {
     if (BLK) {
         // 8 x 8 blocks (eye_tile<BLK>): workgroup (bx, by) holds blocks 4 bx .. 4 bx + 3 of
         // block rows by * EYE_BLK_NT + t; km_gx = blocks per row; every block of the frame
@@ -2459,7 +2459,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(eye_batch
             if (EYE_BLK_NT > 1) asm volatile("" : "+s"(f));
             const DevTabs tabs = *(const DevTabs*)&f->tabs;
             const int widx = __builtin_amdgcn_readfirstlane(by * km_gx + col);
-            const uint32_t kmw = ((const __attribute__((address_space(4))) uint32_t*)km)[(size_t)blockIdx.z * km_nw + widx];
+            const uint32_t kmw = ((const __attribute__((address_space(4))) uint32_t*)km)[(size_t)blockIdx.z * km_fs + widx];
             eye_tile<FUSED, false, RT, FMT, NOSH, BLK>(*(const EyePart*)&f->a.ey, *(const ShadowPart*)&f->a.sh, f->smap,
                                                        f->out, col, by, nullptr, tabs, true, kmw, true);
         }
@@ -2476,7 +2476,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(eye_batch
         int widx = 0;
         if (RT == 3) {
             widx = __builtin_amdgcn_readfirstlane((by * TILE_Y + (int)(threadIdx.x >> 6)) * km_gx + (int)blockIdx.x);
-            kmw = ((const __attribute__((address_space(4))) uint32_t*)km)[(size_t)blockIdx.z * km_nw + min(widx, km_nw - 1)];
+            kmw = ((const __attribute__((address_space(4))) uint32_t*)km)[(size_t)blockIdx.z * km_fs + min(widx, km_nw - 1)];
         }
         eye_tile<FUSED, false, RT, FMT, NOSH>(*(const EyePart*)&f->a.ey, *(const ShadowPart*)&f->a.sh, f->smap, f->out,
                                               blockIdx.x, by, nullptr, tabs, true, kmw, widx < km_nw);
@@ -2891,12 +2891,13 @@ int launch_shadow_pass(const FrameArgs& a, double* smap, void* stream, StatsK* s
 //     (eye_pass8_kernel); batched, the compiler's allocation (the headline kernel).
 template <int FMT>
 static void launch_eye_fmt(const FrameArgs& a, const double* smap, void* o, hipStream_t s, dim3 g, bool fused,
-                           const DevTabs& tabs, CBatch* fr, bool blk = false) {
+                           const DevTabs& tabs, CBatch* fr, bool blk = false, bool mask_shared = false) {
     struct {
         const uint32_t* p;
-        int nw, gx;
-    } km{nullptr, 1, 1};
-    if (fr && tabs.rtmask) km = {tabs.rtmask, tabs.rtmask_words, (int)g.x};
+        int nw, gx, fs;
+    } km{nullptr, 1, 1, 0};
+    // (fs: frame z's words at z * fs; 0 when the batch's frames share one set, launch_eye_batch)
+    if (fr && tabs.rtmask) km = {tabs.rtmask, tabs.rtmask_words, (int)g.x, mask_shared ? 0 : tabs.rtmask_words};
     // 8 x 8 blocks (eye_block_mode): 4 blocks per workgroup across, 8 rows
     const int rows_ = a.ey.row_end - a.ey.row_begin;
     const int gx8 = (a.ey.W + 7) / 8;
@@ -2905,9 +2906,9 @@ static void launch_eye_fmt(const FrameArgs& a, const double* smap, void* o, hipS
     do {                                                                                                        \
         constexpr bool B_ = R == 3 && N && FMT == RTM_FORMAT_RGBA32F;                                           \
         if (fr && B_ && blk)                                                                                    \
-            hipLaunchKernelGGL((eye_batch_kernel<F, R, FMT, N, B_>), gblk, dim3(BLOCK), 0, s, fr, km.p, km.nw, gx8); \
+            hipLaunchKernelGGL((eye_batch_kernel<F, R, FMT, N, B_>), gblk, dim3(BLOCK), 0, s, fr, km.p, km.nw, gx8, km.fs); \
         else if (fr) hipLaunchKernelGGL((eye_batch_kernel<F, R, FMT, N>), dim3(g.x, (g.y + eye_batch_tiles<R, N> - 1) / eye_batch_tiles<R, N>, g.z), \
-                                   dim3(BLOCK), 0, s, fr, km.p, km.nw, km.gx);                                     \
+                                   dim3(BLOCK), 0, s, fr, km.p, km.nw, km.gx, km.fs);                              \
         else hipLaunchKernelGGL((eye_pass_kernel<F, false, R, FMT, N>), g, dim3(BLOCK), 0, s, a, smap, o, nullptr, tabs); \
     } while (0)
     // the SDF frames' batched eye pass in 8 x 8 pixel blocks as well (RGBA f32, no stripes):
@@ -3059,7 +3060,7 @@ static bool eye_block_mode(const FrameArgs& a0, const DevTabs& t0, bool fused) {
 }
 
 int launch_eye_batch(const BatchFrame* dev, int n, const FrameArgs& a0, const DevTabs& t0, void* stream,
-                     int* blocks) {
+                     int* blocks, bool mask_shared) {
     hipStream_t s = (hipStream_t)stream;
     CBatch* fr = (CBatch*)dev;
     const int rows = a0.ey.row_end - a0.ey.row_begin;
@@ -3071,13 +3072,16 @@ int launch_eye_batch(const BatchFrame* dev, int n, const FrameArgs& a0, const De
                                       (RTM_FLAG_NO_MARCH | RTM_FLAG_NO_SHADOW_RASTER)));
     if (blocks) *blocks = blk || sdf_blk;
     if (t0.rtmask) {  // the batch's per-wave primitive masks first (RT 3)
+        // (mask_shared: every frame has frame 0's camera and primitive table, so frame 0's
+        // masks are every frame's: one frame's cull)
+        const int nm = mask_shared ? 1 : n;
         if (blk) {
             const int nw8 = ((a0.ey.W + 7) / 8) * ((rows + 7) / 8);
-            hipLaunchKernelGGL(rt_cull_batch_kernel<true>, dim3((unsigned)((nw8 + BLOCK - 1) / BLOCK), 1, (unsigned)n),
+            hipLaunchKernelGGL(rt_cull_batch_kernel<true>, dim3((unsigned)((nw8 + BLOCK - 1) / BLOCK), 1, (unsigned)nm),
                                dim3(BLOCK), 0, s, fr);
         } else {
             const int nw = ((a0.ey.W + TILE_X - 1) / TILE_X) * rows;
-            hipLaunchKernelGGL(rt_cull_batch_kernel<false>, dim3((unsigned)((nw + BLOCK - 1) / BLOCK), 1, (unsigned)n),
+            hipLaunchKernelGGL(rt_cull_batch_kernel<false>, dim3((unsigned)((nw + BLOCK - 1) / BLOCK), 1, (unsigned)nm),
                                dim3(BLOCK), 0, s, fr);
         }
         if (launched()) return RTM_ERR_HIP;
@@ -3085,9 +3089,9 @@ int launch_eye_batch(const BatchFrame* dev, int n, const FrameArgs& a0, const De
     dim3 g = grid_for(a0.ey.W, rows);
     g.z = (unsigned)n;
     const int fmt = t0.fmt & FMT_MASK;
-    if (fmt == RTM_FORMAT_RGBA8) launch_eye_fmt<RTM_FORMAT_RGBA8>(a0, nullptr, nullptr, s, g, fused, t0, fr);
-    else if (fmt == RTM_FORMAT_RGB8) launch_eye_fmt<RTM_FORMAT_RGB8>(a0, nullptr, nullptr, s, g, fused, t0, fr);
-    else launch_eye_fmt<RTM_FORMAT_RGBA32F>(a0, nullptr, nullptr, s, g, fused, t0, fr, blk);
+    if (fmt == RTM_FORMAT_RGBA8) launch_eye_fmt<RTM_FORMAT_RGBA8>(a0, nullptr, nullptr, s, g, fused, t0, fr, false, mask_shared);
+    else if (fmt == RTM_FORMAT_RGB8) launch_eye_fmt<RTM_FORMAT_RGB8>(a0, nullptr, nullptr, s, g, fused, t0, fr, false, mask_shared);
+    else launch_eye_fmt<RTM_FORMAT_RGBA32F>(a0, nullptr, nullptr, s, g, fused, t0, fr, blk, mask_shared);
     return launched();
 }
 

@@ -120,3 +120,34 @@ def test_block_mode_shadowed_sdf_batches(rtm, oracle, scenes, gpu_ctx, w, h):
         assert bits_equal(got, want["rgba"]), f"frame {i}: {first_mismatch(got, want['rgba'])}"
     m = device_smap(gpu_ctx, w, h)
     assert bits_equal(m, want["shadow"]), first_mismatch(m, want["shadow"])
+
+
+@pytest.mark.parametrize("w,h", [(200, 136), (1280, 832)])
+def test_shared_primitive_masks(rtm, oracle, scenes, gpu_ctx, w, h):
+    """A batch whose frames all hold frame 0's primitive table shares frame 0's masks (one
+    frame's cull, rtm_api.cpp enqueue_batch); one differing frame anywhere in the batch
+    makes every frame cull its own.  Blocks (200 x 136) and rows (1280 x 832, above 1
+    Mpixel), a shared batch right after an unshared one and back on one context (stale
+    mask words would show), every frame against the oracle, no out-of-range read."""
+    import torch
+    eye, sh = scenes.perspective_eye_camera(), scenes.shadow_camera()
+    a, b = scenes.raytracing_plane0(True), _thin_cylinders(scenes, 3)
+    seqs = [[a] * 6, [a, a, a, b, a, a], [b] * 6, [a] * 6]
+    outs = [torch.empty((h, w, 4), dtype=torch.float32, device="cuda") for _ in range(6)]
+    want = {id(s): oracle.render(s, eye, sh, w, h, 0, scenes.RAYTRACING_FLAGS, nthreads=NT)["rgba"] for s in (a, b)}
+    assert oob(rtm, gpu_ctx) >= 0  # clear
+    try:
+        gpu_ctx.set_batch(6)
+        gpu_ctx.set_lanes(1)
+        for frames in seqs:
+            torch.cuda.synchronize()
+            gpu_ctx.render_frames_async(frames, eye, sh, w, h, 0, scenes.RAYTRACING_FLAGS, [o.data_ptr() for o in outs])
+            gpu_ctx.synchronize()
+            assert gpu_ctx.last_eye_blocks() == (w * h < (1 << 20))
+            for i, (s, o) in enumerate(zip(frames, outs)):
+                got = o.cpu().numpy()
+                assert bits_equal(got, want[id(s)]), (i, first_mismatch(got, want[id(s)]))
+    finally:
+        gpu_ctx.set_lanes(0)
+        gpu_ctx.set_batch(0)
+    assert oob(rtm, gpu_ctx) == 0
