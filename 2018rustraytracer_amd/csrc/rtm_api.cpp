@@ -673,6 +673,10 @@ struct BatchRing {
     int next = 0;
     DevBuf smaps;  // the batch's shadow maps, B x W x H f64
     DevBuf rtmask; // per-wave primitive masks of the batch's PERSPECTIVE eye passes (row f-1)
+    // what the shared masks in rtmask were culled for (enqueue_batch's mask key), valid while
+    // no unshared batch has written the buffer since
+    std::vector<char> mask_key;
+    const void* mask_buf = nullptr;
     int device = 0;
     ~BatchRing() {
         int cur = 0;
@@ -1373,7 +1377,7 @@ int enqueue_batch(rtm_ctx* ctx, int lane, FrameArgs* fa, const FrameExtra* const
     }
     // a frame without ray-traced primitives in a RT 3 batch: every frame shares the eye camera
     t0.rt_persp = t0.rt ? t0.rt_persp : 0;
-    bool mask_shared = false;
+    bool mask_shared = false, cull = true;
     if (t0.rt && t0.rt_persp && !t0.sdf) {
         // per-wave primitive masks (rt_cull_batch_kernel) for every frame with primitives,
         // ceil(W/64) * rows words each; stream-ordered reuse on this lane.  A mask depends on
@@ -1385,6 +1389,24 @@ int enqueue_batch(rtm_ctx* ctx, int lane, FrameArgs* fa, const FrameExtra* const
         for (int k = 0; k < n && mask_shared; ++k) mask_shared = exs[k]->has_rt && (k == 0 || !fresh_rt[(size_t)k]);
         const size_t nw = (size_t)((fa[0].ey.W + 63) / 64) * (size_t)(fa[0].ey.row_end - fa[0].ey.row_begin);
         if ((rc = br.rtmask.ensure(sizeof(uint32_t) * nw * (size_t)(mask_shared ? 1 : n), ctx->device))) return rc;
+        // Shared masks are a pure function of (primitive table, eye camera, sizes, rows,
+        // stripes, format, flags): the same key as the lane's last shared cull, with the
+        // buffer untouched since, finds the words already there (stream order: that cull ran
+        // before this batch's eye pass).  main()'s scene, a static camera and cylinder, is
+        // culled once per lane instead of once per launch.
+        std::vector<char> key;
+        if (mask_shared) {
+            const EyePart& e = fa[0].ey;
+            const int32_t sz[9] = {e.W, e.H, e.row_begin, e.row_end, e.stripe_rows, e.stripe_stride, e.stripe_phase,
+                                   fmt, e.flags};
+            key.resize(sizeof(RtK) + sizeof(CamK) + sizeof(sz));
+            std::memcpy(key.data(), &exs[0]->rt, sizeof(RtK));
+            std::memcpy(key.data() + sizeof(RtK), &e.eye, sizeof(CamK));
+            std::memcpy(key.data() + sizeof(RtK) + sizeof(CamK), sz, sizeof(sz));
+        }
+        cull = !(mask_shared && br.mask_buf == br.rtmask.p && br.mask_key == key);
+        br.mask_key = std::move(key);
+        br.mask_buf = mask_shared ? br.rtmask.p : nullptr;
         for (int k = 0; k < n; ++k)
             if (exs[k]->has_rt) {
                 BatchFrame& bf = *(BatchFrame*)(hb + sizeof(BatchFrame) * (size_t)k);
@@ -1429,7 +1451,7 @@ int enqueue_batch(rtm_ctx* ctx, int lane, FrameArgs* fa, const FrameExtra* const
     }
     if (slot) HIP_TRY(hipEventRecord(slot->ev[2], s));
     int blocks = 0;
-    if ((rc = launch_eye_batch((const BatchFrame*)db, n, fa[0], t0, s, &blocks, mask_shared)))
+    if ((rc = launch_eye_batch((const BatchFrame*)db, n, fa[0], t0, s, &blocks, mask_shared, cull)))
         return fail(rc, "batched eye pass failed");
     ctx->eye_blocks_last = blocks;
     if (slot) {

@@ -396,8 +396,9 @@ int launch_shadow_batch(const BatchFrame* dev, int n, const FrameArgs& a0, void*
 // blocks (optional): set to 1 when the launch ran 8 x 8-pixel blocks (eye_block_mode), else 0.
 // mask_shared: the frames' primitive masks are one set, frame 0's (its words at t0.rtmask;
 // every frame has frame 0's eye camera, rows and primitive table: rtm_api.cpp enqueue_batch)
+// cull false: the shared masks are in place already (the lane's last cull had the same inputs).
 int launch_eye_batch(const BatchFrame* dev, int n, const FrameArgs& a0, const DevTabs& t0, void* stream,
-                     int* blocks = nullptr, bool mask_shared = false);
+                     int* blocks = nullptr, bool mask_shared = false, bool cull = true);
 // Stream-ordered copy of host bytes into device memory by kernels whose
 // arguments carry the bytes (<= 3968 per launch), so the host copy is consumed
 // at launch: no pinned staging, no host synchronisation.  bytes % 8 == 0.

@@ -3060,7 +3060,7 @@ static bool eye_block_mode(const FrameArgs& a0, const DevTabs& t0, bool fused) {
 }
 
 int launch_eye_batch(const BatchFrame* dev, int n, const FrameArgs& a0, const DevTabs& t0, void* stream,
-                     int* blocks, bool mask_shared) {
+                     int* blocks, bool mask_shared, bool cull) {
     hipStream_t s = (hipStream_t)stream;
     CBatch* fr = (CBatch*)dev;
     const int rows = a0.ey.row_end - a0.ey.row_begin;
@@ -3071,7 +3071,7 @@ int launch_eye_batch(const BatchFrame* dev, int n, const FrameArgs& a0, const De
                          !(fused && !((a0.sh.flags & (RTM_FLAG_NO_MARCH | RTM_FLAG_NO_SHADOW_RASTER)) ==
                                       (RTM_FLAG_NO_MARCH | RTM_FLAG_NO_SHADOW_RASTER)));
     if (blocks) *blocks = blk || sdf_blk;
-    if (t0.rtmask) {  // the batch's per-wave primitive masks first (RT 3)
+    if (t0.rtmask && cull) {  // the batch's per-wave primitive masks first (RT 3)
         // (mask_shared: every frame has frame 0's camera and primitive table, so frame 0's
         // masks are every frame's: one frame's cull)
         const int nm = mask_shared ? 1 : n;

@@ -125,28 +125,39 @@ def test_block_mode_shadowed_sdf_batches(rtm, oracle, scenes, gpu_ctx, w, h):
 @pytest.mark.parametrize("w,h", [(200, 136), (1280, 832)])
 def test_shared_primitive_masks(rtm, oracle, scenes, gpu_ctx, w, h):
     """A batch whose frames all hold frame 0's primitive table shares frame 0's masks (one
-    frame's cull, rtm_api.cpp enqueue_batch); one differing frame anywhere in the batch
-    makes every frame cull its own.  Blocks (200 x 136) and rows (1280 x 832, above 1
-    Mpixel), a shared batch right after an unshared one and back on one context (stale
-    mask words would show), every frame against the oracle, no out-of-range read."""
+    frame's cull, rtm_api.cpp enqueue_batch), and a lane whose last shared cull had the same
+    table, camera and sizes reuses its words without culling again; one differing frame
+    anywhere in the batch makes every frame cull its own (and drops the lane's shared words).
+    Blocks (200 x 136) and rows (1280 x 832, above 1 Mpixel) on one context: shared, shared
+    again (reuse), unshared, another table shared twice, the first table again, then the
+    first table under a moved camera (same table: must cull again).  Every frame against
+    the oracle, no out-of-range read."""
     import torch
     eye, sh = scenes.perspective_eye_camera(), scenes.shadow_camera()
+    eye2 = scenes.Camera(eye.type_, (0.3, -0.2, 0.5), eye.dirNormalized, eye.upNormalized, eye.sideNormalized)
     a, b = scenes.raytracing_plane0(True), _thin_cylinders(scenes, 3)
-    seqs = [[a] * 6, [a, a, a, b, a, a], [b] * 6, [a] * 6]
+    seqs = [(eye, [a] * 6), (eye, [a] * 6), (eye, [a, a, a, b, a, a]), (eye, [b] * 6), (eye, [b] * 6),
+            (eye, [a] * 6), (eye2, [a] * 6), (eye, [a] * 6)]
     outs = [torch.empty((h, w, 4), dtype=torch.float32, device="cuda") for _ in range(6)]
-    want = {id(s): oracle.render(s, eye, sh, w, h, 0, scenes.RAYTRACING_FLAGS, nthreads=NT)["rgba"] for s in (a, b)}
+    want = {}
+    for e, frames in seqs:
+        for s_ in frames:
+            if (id(e), id(s_)) not in want:
+                want[(id(e), id(s_))] = oracle.render(s_, e, sh, w, h, 0, scenes.RAYTRACING_FLAGS, nthreads=NT)["rgba"]
     assert oob(rtm, gpu_ctx) >= 0  # clear
     try:
         gpu_ctx.set_batch(6)
         gpu_ctx.set_lanes(1)
-        for frames in seqs:
+        for q, (e, frames) in enumerate(seqs):
+            for o in outs:
+                o.fill_(-1.0)
             torch.cuda.synchronize()
-            gpu_ctx.render_frames_async(frames, eye, sh, w, h, 0, scenes.RAYTRACING_FLAGS, [o.data_ptr() for o in outs])
+            gpu_ctx.render_frames_async(frames, e, sh, w, h, 0, scenes.RAYTRACING_FLAGS, [o.data_ptr() for o in outs])
             gpu_ctx.synchronize()
             assert gpu_ctx.last_eye_blocks() == (w * h < (1 << 20))
-            for i, (s, o) in enumerate(zip(frames, outs)):
-                got = o.cpu().numpy()
-                assert bits_equal(got, want[id(s)]), (i, first_mismatch(got, want[id(s)]))
+            for i, (s_, o) in enumerate(zip(frames, outs)):
+                got, ref = o.cpu().numpy(), want[(id(e), id(s_))]
+                assert bits_equal(got, ref), (q, i, first_mismatch(got, ref))
     finally:
         gpu_ctx.set_lanes(0)
         gpu_ctx.set_batch(0)
