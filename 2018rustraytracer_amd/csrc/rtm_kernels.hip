@@ -2446,14 +2446,17 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(eye_batch
     CBatch* __restrict__ fr, const uint32_t* __restrict__ km, int km_nw, int km_gx, int km_fs) {
     if (BLK) {
         // 8 x 8 blocks (eye_tile<BLK>): workgroup (bx, by) holds blocks 4 bx .. 4 bx + 3 of
-        // block rows by * EYE_BLK_NT + t; km_gx = blocks per row; every block of the frame
-        // has its word
+        // block rows by + t * gridDim.y; km_gx = blocks per row; every block of the frame
+        // has its word.  (Strided rows, not EYE_BLK_NT adjacent ones: a compact primitive's
+        // blocks -- main()'s vertical cylinder -- no longer fall to the same wave one after
+        // another, whose 4 traced tiles made the launch's tail: config 7's eye pass 0.97 ->
+        // 0.90 us per frame one-lane, profiles/r06_ab_eye_variants.txt)
         const int col = (int)blockIdx.x * 4 + (int)(threadIdx.x >> 6);
         if (col >= km_gx) return;  // (wave-uniform: a block past the frame's right edge; no barrier follows)
         const int gy8 = (((const EyePart*)&fr[blockIdx.z].a.ey)->row_end - ((const EyePart*)&fr[blockIdx.z].a.ey)->row_begin + 7) / 8;
 #pragma unroll 1
         for (int t = 0; t < EYE_BLK_NT; ++t) {
-            const int by = (int)blockIdx.y * EYE_BLK_NT + t;
+            const int by = (int)blockIdx.y + t * (int)gridDim.y;
             if (by >= gy8) break;  // (wave-uniform)
             CBatch* f = fr + blockIdx.z;
             if (EYE_BLK_NT > 1) asm volatile("" : "+s"(f));
