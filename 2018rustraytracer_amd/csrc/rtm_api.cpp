@@ -1378,6 +1378,7 @@ int enqueue_batch(rtm_ctx* ctx, int lane, FrameArgs* fa, const FrameExtra* const
     // a frame without ray-traced primitives in a RT 3 batch: every frame shares the eye camera
     t0.rt_persp = t0.rt ? t0.rt_persp : 0;
     bool mask_shared = false, cull = true;
+    const void* new_buf = nullptr;  // the shared masks' buffer once this batch's eye launch is in
     if (t0.rt && t0.rt_persp && !t0.sdf) {
         // per-wave primitive masks (rt_cull_batch_kernel) for every frame with primitives,
         // ceil(W/64) * rows words each; stream-ordered reuse on this lane.  A mask depends on
@@ -1405,8 +1406,11 @@ int enqueue_batch(rtm_ctx* ctx, int lane, FrameArgs* fa, const FrameExtra* const
             std::memcpy(key.data() + sizeof(RtK) + sizeof(CamK), sz, sizeof(sz));
         }
         cull = !(mask_shared && br.mask_buf == br.rtmask.p && br.mask_key == key);
+        // (the buffer's words count as this key's only once the batch's launches are in:
+        // until then, and after any failure on the way, they count as nobody's)
+        if (mask_shared) new_buf = br.rtmask.p;
         br.mask_key = std::move(key);
-        br.mask_buf = mask_shared ? br.rtmask.p : nullptr;
+        br.mask_buf = nullptr;
         for (int k = 0; k < n; ++k)
             if (exs[k]->has_rt) {
                 BatchFrame& bf = *(BatchFrame*)(hb + sizeof(BatchFrame) * (size_t)k);
@@ -1453,6 +1457,7 @@ int enqueue_batch(rtm_ctx* ctx, int lane, FrameArgs* fa, const FrameExtra* const
     int blocks = 0;
     if ((rc = launch_eye_batch((const BatchFrame*)db, n, fa[0], t0, s, &blocks, mask_shared, cull)))
         return fail(rc, "batched eye pass failed");
+    if (t0.rtmask) br.mask_buf = new_buf;  // (a batch without masks leaves the lane's words as they were)
     ctx->eye_blocks_last = blocks;
     if (slot) {
         HIP_TRY(hipEventRecord(slot->ev[3], s));
